@@ -1,0 +1,29 @@
+# Build libnst_hip.so (gfx950) in-tree.  `make -j4`.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := neuralstyletransferv1_amd
+CSRC := $(PKG)/csrc
+BUILD := build/obj
+CXXFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+            -Iinclude -I$(CSRC)
+SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
+OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
+LIB := $(PKG)/libnst_hip.so
+
+all: $(LIB)
+
+$(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/nst_internal.h include/nst_hip.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/%.cpp.o: $(CSRC)/%.cpp $(CSRC)/nst_internal.h include/nst_hip.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(CXXFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+clean:
+	rm -rf $(BUILD) $(LIB)
+
+.PHONY: all clean

@@ -1,0 +1,160 @@
+/*
+ * nst_hip.h — C ABI of libnst_hip.so, the MI355X (gfx950) stylization engine.
+ *
+ * Drop-in boundary for the reference's per-frame stylization hot path
+ * (TrentMahaffey/NeuralStyleTransferV1).  The reference is pure Python/PyTorch;
+ * the interfaces these entry points replace are Python call sites, cited per
+ * function below.  Plain pointers and sizes only: no torch types cross this ABI.
+ * Device pointers are HIP device pointers (e.g. a PyTorch-ROCm tensor's
+ * data_ptr()); `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *
+ * Ownership: the caller owns every input/output/workspace buffer; a handle owns
+ * its packed weights (device) and nothing else.  No entry point allocates device
+ * memory except nst_create / nst_lab_create (one-time packing/uploads).
+ * Threading: calls on one handle must be serialised on one stream; handles on
+ * different devices may be used concurrently from different threads/processes.
+ * Errors: every int-returning function returns NST_OK (0) or a negative NST_E*
+ * code; nst_last_error() returns the calling thread's last message.
+ */
+#ifndef NST_HIP_H
+#define NST_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define NST_OK 0
+#define NST_E_INVALID (-1)   /* bad argument / unknown enum */
+#define NST_E_PARAM (-2)     /* missing or mis-shaped checkpoint tensor */
+#define NST_E_SHAPE (-3)     /* unsupported input/output geometry */
+#define NST_E_HIP (-4)       /* HIP runtime error */
+#define NST_E_WORKSPACE (-5) /* workspace too small */
+
+/* ---- architectures (pipeline.py:72-79 _detect_transformer_type, :598-603 reconet) ---- */
+#define NST_ARCH_JOHNSON 0 /* transformer_net.py:4-41 */
+#define NST_ARCH_NST 1     /* transformer_net_nst.py:62-127 */
+#define NST_ARCH_RECONET 2 /* model.py:107-116 (frn=False, as pipeline.py:602 builds it) */
+
+/* ---- compute dtypes ---- */
+#define NST_DT_F32 0  /* fp32 "parity" mode: exact-f32 MFMA (v_mfma_f32_16x16x4_f32) */
+#define NST_DT_BF16 1 /* bf16 "throughput" mode: bf16 MFMA, fp32 accumulate/statistics */
+
+/* ---- I/O formats for nst_forward ---- */
+#define NST_IO_F32_NCHW 0 /* raw model tensor [n,3,h,w] fp32 (TransformerNet.forward(X) surface) */
+#define NST_IO_U8_NHWC 1  /* frames [n,h,w,3] uint8 RGB; io_preset encode/decode + clamp + ToPILImage truncation fused */
+
+/* ---- io presets (pipeline.py:1445-1486; auto table :2518-2523) ---- */
+#define NST_PRESET_NONE 0 /* only valid with NST_IO_F32_NCHW on both sides */
+#define NST_PRESET_TANH 1
+#define NST_PRESET_IMAGENET_01 2
+#define NST_PRESET_IMAGENET_255 3
+#define NST_PRESET_CAFFE_BGR 4
+#define NST_PRESET_RAW_255 5
+#define NST_PRESET_RAW_01 6
+
+typedef struct nst_handle nst_handle;
+typedef struct nst_lab nst_lab;
+
+/* One checkpoint tensor, by its reference state_dict name (e.g. "res1.conv1.conv2d.weight"). */
+typedef struct nst_param {
+  const char* name;
+  const float* data; /* host fp32, contiguous in the reference's PyTorch layout */
+  int64_t numel;
+} nst_param;
+
+/* Last error message of the calling thread ("" if none). */
+const char* nst_last_error(void);
+
+/* Library version string. */
+const char* nst_version(void);
+
+/*
+ * Pack a checkpoint for one device.  Replaces model construction + load:
+ * `TransformerNet().to(device)` + `_load_checkpoint_compat` (pipeline.py:554-569, 597-619).
+ * Every parameter of the architecture must be present (missing -> NST_E_PARAM);
+ * unknown names are ignored (load_state_dict(strict=False) semantics).
+ */
+int nst_create(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
+               nst_handle** out);
+void nst_destroy(nst_handle* h);
+
+/* Output spatial size the architecture produces for an h x w input
+ * (Johnson/ReCoNet: 4*ceil(ceil(h/2)/2); NST: centre-cropped back to h x w). */
+int nst_output_hw(const nst_handle* h, int in_h, int in_w, int* out_h, int* out_w);
+
+/* Device workspace nst_forward needs for a batch of n frames of h x w. */
+int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* out);
+
+/*
+ * Stylize a batch.  Replaces `model(x_in)` with its io_preset pre/post arithmetic
+ * (pipeline.py:1445-1486: preset encode -> .to(device) -> model -> .cpu() -> decode -> clamp(0,1))
+ * and, for NST_IO_U8_NHWC output, the ToPILImage truncation `pic.mul(255).byte()`
+ * (pipeline.py:1943/2094).  x: [n,3,h,w] f32 or [n,h,w,3] u8; y: [n,3,oh,ow] f32 (raw
+ * model output, no preset) or [n,oh,ow,3] u8 (decoded).  U8 output requires
+ * nst_output_hw(h,w) == (h,w) (otherwise use F32 output + nst_resize_bilinear_u8).
+ */
+int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset,
+                void* y, int y_fmt, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Decode a raw model output (f32 NCHW [n,3,h,w]) with `preset` + clamp(0,1), resize
+ * bilinearly (align_corners=False) to out_h x out_w, truncate to u8 NHWC.
+ * Replaces pipeline.py:1512-1516 (F.interpolate to content size) + :1943 ToPILImage.
+ */
+int nst_decode_resize_u8(const float* y, int n, int h, int w, int preset, uint8_t* out, int out_h,
+                         int out_w, void* stream);
+
+/* ---- LAB temporal smoothing (pipeline.py:1942-1978) ---- */
+
+/* Upload the two 2^24-entry LittleCMS (Pillow) LUTs: rgb2lab[(r<<16)|(g<<8)|b] = {L,a,b}
+ * bytes and lab2rgb[(L<<16)|(a<<8)|b] = {r,g,b} bytes (3*2^24 bytes each, host). */
+int nst_lab_create(const uint8_t* rgb2lab, const uint8_t* lab2rgb, int device, nst_lab** out);
+void nst_lab_destroy(nst_lab* lab);
+
+/*
+ * One frame (or a batch processed in frame order) of the LAB EMA:
+ * L' = alpha*L + (1-alpha)*prev_L (fp32), prev_L = L', L byte = trunc(clip(L',0,255));
+ * optional same EMA on a/b bytes with chroma_alpha.  `state` is a caller-owned device
+ * buffer of 3*h*w floats (prev_L, prev_a, prev_b); `first` != 0 seeds it from the frame
+ * (pipeline.py:1951-1952 `prev_L = L.copy()`).  rgb in/out: [n,h,w,3] u8 (may alias).
+ * alpha/chroma_alpha are the fp32 values of the Python float coefficients.
+ */
+int nst_lab_ema_u8(const nst_lab* lab, const uint8_t* rgb_in, uint8_t* rgb_out, int n, int h, int w,
+                   int smooth_lightness, float alpha, float one_minus_alpha, int smooth_chroma,
+                   float chroma_alpha, float one_minus_chroma_alpha, float* state, int first,
+                   void* stream);
+
+/*
+ * Uniform / masked blend with the original frame (pipeline.py:1984-2092):
+ *   mask (optional, [n,h,w] f32 alpha in [0,1]): keep: C = a*S + (1-a)*O; replace: (1-a)*S + a*O; clip
+ *   then if 0 <= blend < 1: out = clamp(blend*C + (1-blend)*O, 0, 1); truncate to u8.
+ * S and O are u8 NHWC frames read as x/255 (to_tensor).  composite_mode: 0 keep, 1 replace.
+ */
+int nst_blend_u8(const uint8_t* styled, const uint8_t* orig, const float* mask, int composite_mode,
+                 float blend, float one_minus_blend, uint8_t* out, int n, int h, int w,
+                 void* stream);
+
+/*
+ * Live per-layer kernel timing (bench.py roofline): between nst_profile_begin and
+ * nst_profile_end every conv launch of nst_forward on this handle is bracketed by a pair of
+ * HIP events recorded on the forward's stream.  Call nst_profile_end after synchronising
+ * that stream; it returns, per layer index (0..n_layers-1, program order), the summed
+ * kernel milliseconds and the launch count, and releases the events.
+ */
+int nst_profile_begin(nst_handle* h);
+int nst_profile_end(nst_handle* h, int n_layers, float* total_ms, int* launches);
+/* Number of conv layers of the handle's architecture and a layer's state_dict prefix. */
+int nst_num_layers(const nst_handle* h);
+const char* nst_layer_name(const nst_handle* h, int layer);
+
+/* Gram matrix G[b] = F[b] F[b]^T / (c*hw) (utils.py:80-83), F [n,c,hw] f32 or bf16. fp32 out. */
+int nst_gram(const void* F, int dtype, int n, int c, int hw, float* G, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NST_HIP_H */

@@ -1,0 +1,106 @@
+"""ctypes binding of libnst_hip.so (C ABI declared in include/nst_hip.h).
+
+The product path has no fallback: if the library is missing or cannot be loaded,
+`lib()` raises, and every stylization entry point fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (load torch's HIP runtime first so libnst_hip binds to the same one)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NST_HIP_LIB", os.path.join(_HERE, "libnst_hip.so"))
+
+NST_OK = 0
+NST_ARCH_JOHNSON, NST_ARCH_NST, NST_ARCH_RECONET = 0, 1, 2
+NST_DT_F32, NST_DT_BF16 = 0, 1
+NST_IO_F32_NCHW, NST_IO_U8_NHWC = 0, 1
+PRESETS = {
+    "none": 0,
+    "tanh": 1,
+    "imagenet_01": 2,
+    "imagenet_255": 3,
+    "caffe_bgr": 4,
+    "raw_255": 5,
+    "raw_01": 6,
+}
+
+# every symbol include/nst_hip.h declares (tests check the library exports all of them)
+EXPORTED_SYMBOLS = (
+    "nst_last_error", "nst_version", "nst_create", "nst_destroy", "nst_output_hw",
+    "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8", "nst_lab_create",
+    "nst_lab_destroy", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
+    "nst_profile_end", "nst_num_layers", "nst_layer_name",
+)
+
+
+class NstParam(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.POINTER(ctypes.c_float)), ("numel", ctypes.c_int64)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NstError(RuntimeError):
+    """Raised for any non-zero status from libnst_hip (message from nst_last_error)."""
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NstError(
+                f"libnst_hip.so not found at {LIB_PATH}: build it with `make` (or __graft_entry__.build()); "
+                "there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+        L.nst_last_error.restype = ctypes.c_char_p
+        L.nst_version.restype = ctypes.c_char_p
+        L.nst_create.argtypes = [i, ctypes.POINTER(NstParam), i, i, i, ctypes.POINTER(vp)]
+        L.nst_destroy.argtypes = [vp]
+        L.nst_destroy.restype = None
+        L.nst_output_hw.argtypes = [vp, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.nst_workspace_bytes.argtypes = [vp, i, i, i, ctypes.POINTER(sz)]
+        L.nst_forward.argtypes = [vp, vp, i, i, i, i, i, vp, i, vp, sz, vp]
+        L.nst_decode_resize_u8.argtypes = [vp, i, i, i, i, vp, i, i, vp]
+        L.nst_lab_create.argtypes = [vp, vp, i, ctypes.POINTER(vp)]
+        L.nst_lab_destroy.argtypes = [vp]
+        L.nst_lab_destroy.restype = None
+        L.nst_lab_ema_u8.argtypes = [vp, vp, vp, i, i, i, i, f, f, i, f, f, vp, i, vp]
+        L.nst_blend_u8.argtypes = [vp, vp, vp, i, f, f, vp, i, i, i, vp]
+        L.nst_gram.argtypes = [vp, i, i, i, i, vp, vp]
+        L.nst_profile_begin.argtypes = [vp]
+        L.nst_profile_end.argtypes = [vp, i, ctypes.POINTER(f), ctypes.POINTER(i)]
+        L.nst_num_layers.argtypes = [vp]
+        L.nst_num_layers.restype = i
+        L.nst_layer_name.argtypes = [vp, i]
+        L.nst_layer_name.restype = ctypes.c_char_p
+        for name in ("nst_create", "nst_output_hw", "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8",
+                     "nst_lab_create", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
+                     "nst_profile_end"):
+            getattr(L, name).restype = i
+        _lib = L
+        return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != NST_OK:
+        msg = lib().nst_last_error().decode(errors="replace")
+        raise NstError(f"{what} failed ({rc}): {msg}")
+
+
+def require_gpu_tensor(t: torch.Tensor, what: str) -> None:
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise NstError(f"{what} must be a tensor on an MI355X (cuda) device; there is no CPU path")
+
+
+def stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,689 @@
+// nst_api.cpp — C ABI of libnst_hip.so (declared in include/nst_hip.h).
+//
+// Host side of the engine: per-architecture layer programs (the reference's module graphs
+// transformer_net.py:29-41, transformer_net_nst.py:95-127, model.py:69-116 restated as a
+// flat list of conv / residual-add steps), one-time weight packing into MFMA fragment order,
+// workspace planning, and kernel sequencing on the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "nst_hip.h"
+#include "nst_internal.h"
+
+namespace nst {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+const ConvKernelInfo* conv_table_bf16(int* count);
+const ConvKernelInfo* conv_table_f32(int* count);
+
+const ConvKernelInfo* find_conv_kernel(int dtype, int ks, int stride, int cinp, int bn, int in_kind,
+                                       int out_kind) {
+  int count = 0;
+  const ConvKernelInfo* t = dtype == NST_DT_BF16 ? conv_table_bf16(&count) : conv_table_f32(&count);
+  for (int i = 0; i < count; ++i) {
+    const ConvKernelInfo& k = t[i];
+    if (k.ks == ks && k.stride == stride && k.cinp == cinp && k.bn == bn && k.in_kind == in_kind &&
+        k.out_kind == out_kind)
+      return &k;
+  }
+  return nullptr;
+}
+
+// ---------------------------------------------------------------------------------------
+// Layer descriptions
+enum Role { ROLE_IN = 0, ROLE_FINAL = 1 };  // conv followed by InstanceNorm, or the output conv
+
+struct LayerDef {
+  std::string conv;  // state_dict prefix of the conv ("conv1.conv2d")
+  std::string norm;  // prefix of the InstanceNorm2d, "" for the output conv
+  int cin, cout, ks, stride, axis_mode, pad, pre;
+  bool convT;
+};
+
+struct Layer {
+  LayerDef d;
+  int cinp, coutp;
+  const ConvKernelInfo* k_main = nullptr;  // in/out kind of the activation path
+  const ConvKernelInfo* k_alt = nullptr;   // image layer: F32 NCHW input; final: F32 NCHW output
+  void* wpk = nullptr;
+  float* bias = nullptr;
+  float* gamma = nullptr;
+  float* beta = nullptr;
+};
+
+// Program steps
+enum OpKind { OP_CONV = 0, OP_RESADD = 1 };
+enum Buf { B_IMG = -1, B_OUT = -2, B_A = 0, B_B = 1, B_C = 2, B_D = 3, B_E = 4, NBUF = 5 };
+struct Op {
+  int kind;
+  int layer;     // OP_CONV: layer to run; OP_RESADD: layer whose IN applies to y
+  int src, dst;  // buffers
+  int in_norm;   // OP_CONV: layer whose IN+ReLU the prologue applies (-1: identity)
+  int r_buf, r_norm, r_relu, relu_out;  // OP_RESADD
+};
+
+static int round_up(int v, int a) { return (v + a - 1) / a * a; }
+
+static void build_program(int arch, std::vector<LayerDef>& L, std::vector<Op>& P) {
+  auto conv = [&](int layer, int src, int dst, int in_norm) {
+    P.push_back(Op{OP_CONV, layer, src, dst, in_norm, 0, 0, 0, 0});
+  };
+  auto resadd = [&](int layer, int y, int dst, int r_buf, int r_norm, int relu_out) {
+    P.push_back(Op{OP_RESADD, layer, y, dst, -1, r_buf, r_norm, r_norm >= 0 ? 1 : 0, relu_out});
+  };
+  if (arch == NST_ARCH_JOHNSON) {
+    // transformer_net.py:4-41
+    L.push_back({"conv1.conv2d", "in1", 3, 32, 9, 1, AX_REFLECT, 4, 0, false});
+    L.push_back({"conv2.conv2d", "in2", 32, 64, 3, 2, AX_REFLECT, 1, 0, false});
+    L.push_back({"conv3.conv2d", "in3", 64, 128, 3, 2, AX_REFLECT, 1, 0, false});
+    for (int r = 1; r <= 5; ++r) {
+      const std::string p = "res" + std::to_string(r);
+      L.push_back({p + ".conv1.conv2d", p + ".in1", 128, 128, 3, 1, AX_REFLECT, 1, 0, false});
+      L.push_back({p + ".conv2.conv2d", p + ".in2", 128, 128, 3, 1, AX_REFLECT, 1, 0, false});
+    }
+    L.push_back({"deconv1.conv2d", "in4", 128, 64, 3, 1, AX_REFLECT_UP2, 1, 0, false});
+    L.push_back({"deconv2.conv2d", "in5", 64, 32, 3, 1, AX_REFLECT_UP2, 1, 0, false});
+    L.push_back({"deconv3.conv2d", "", 32, 3, 9, 1, AX_REFLECT, 4, 0, false});
+  } else if (arch == NST_ARCH_NST) {
+    // transformer_net_nst.py:62-127 (zero-padded convs after ReflectionPad2d(40); ConvTranspose ups)
+    L.push_back({"down1.conv", "down1.norm", 3, 32, 9, 1, AX_ZERO_PREREFLECT, 4, 40, false});
+    L.push_back({"down2.conv", "down2.norm", 32, 64, 3, 2, AX_ZERO, 1, 0, false});
+    L.push_back({"down3.conv", "down3.norm", 64, 128, 3, 2, AX_ZERO, 1, 0, false});
+    for (int r = 1; r <= 5; ++r) {
+      const std::string p = "res" + std::to_string(r);
+      L.push_back({p + ".conv1", p + ".norm1", 128, 128, 3, 1, AX_ZERO, 1, 0, false});
+      L.push_back({p + ".conv2", p + ".norm2", 128, 128, 3, 1, AX_ZERO, 1, 0, false});
+    }
+    L.push_back({"up1.conv", "up1.norm", 128, 64, 3, 1, AX_ZINSERT, 1, 0, true});
+    L.push_back({"up2.conv", "up2.norm", 64, 32, 3, 1, AX_ZINSERT, 1, 0, true});
+    L.push_back({"final", "", 32, 3, 9, 1, AX_ZERO, 4, 0, false});
+  } else {
+    // model.py:69-116, frn=False
+    L.push_back({"encoder.layers.0.layers.0.layers.1", "encoder.layers.0.layers.1", 3, 48, 9, 1, AX_REFLECT, 4, 0, false});
+    L.push_back({"encoder.layers.1.layers.0.layers.1", "encoder.layers.1.layers.1", 48, 96, 3, 2, AX_REFLECT, 1, 0, false});
+    L.push_back({"encoder.layers.2.layers.0.layers.1", "encoder.layers.2.layers.1", 96, 192, 3, 2, AX_REFLECT, 1, 0, false});
+    for (int r = 3; r <= 6; ++r) {
+      const std::string p = "encoder.layers." + std::to_string(r) + ".branch.";
+      L.push_back({p + "0.layers.0.layers.1", p + "0.layers.1", 192, 192, 3, 1, AX_REFLECT, 1, 0, false});
+      L.push_back({p + "1.layers.0.layers.1", p + "1.layers.1", 192, 192, 3, 1, AX_REFLECT, 1, 0, false});
+    }
+    L.push_back({"decoder.layers.1.layers.0.layers.1", "decoder.layers.1.layers.1", 192, 96, 3, 1, AX_REFLECT_UP2, 1, 0, false});
+    L.push_back({"decoder.layers.3.layers.0.layers.1", "decoder.layers.3.layers.1", 96, 48, 3, 1, AX_REFLECT_UP2, 1, 0, false});
+    L.push_back({"decoder.layers.4.layers.0.layers.1", "", 48, 3, 9, 1, AX_REFLECT, 4, 0, false});
+  }
+  const int nres = arch == NST_ARCH_RECONET ? 4 : 5;
+  const int relu_out = arch == NST_ARCH_RECONET ? 1 : 0;  // ReCoNet ResLayer: ReLU after the add
+  conv(0, B_IMG, B_A, -1);
+  conv(1, B_A, B_B, 0);
+  conv(2, B_B, B_C, 1);
+  // residual stream lives in B_C; block k's input is C (block 1: IN+ReLU of layer 2, lazily)
+  for (int r = 0; r < nres; ++r) {
+    const int l1 = 3 + 2 * r, l2 = 4 + 2 * r;
+    conv(l1, B_C, B_D, r == 0 ? 2 : -1);
+    conv(l2, B_D, B_E, l1);
+    resadd(l2, B_E, B_C, B_C, r == 0 ? 2 : -1, relu_out);
+  }
+  const int u1 = 3 + 2 * nres, u2 = u1 + 1, fin = u1 + 2;
+  conv(u1, B_C, B_A, -1);
+  conv(u2, B_A, B_B, u1);
+  conv(fin, B_B, B_OUT, u2);
+}
+
+}  // namespace nst
+
+using namespace nst;
+
+struct nst_handle {
+  int arch, dtype, device;
+  std::vector<Layer> layers;
+  std::vector<Op> prog;
+  // live profiling (nst_profile_begin/end)
+  bool profiling = false;
+  struct Rec { int layer; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+};
+
+struct nst_lab {
+  int device;
+  uint8_t* rgb2lab = nullptr;
+  uint8_t* lab2rgb = nullptr;
+};
+
+namespace {
+
+uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// Pack conv weights into MFMA A-fragment order: [cblk][step (nstep+1, last zero)][n-subtile][lane][cpc]
+// lane l = (g = l>>4, q = l&15): output channel of row q in subtile t (wave wn, local t):
+//   cb*bn + wn*nsub*16 + 4*nsub*(q>>2) + 4*t + (q&3);  K chunk 4*step+g -> (tap, channel chunk).
+std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W, int coutp) {
+  const int ncblk = coutp / k.bn;
+  const size_t per_frag = 64 * (size_t)k.cpc;
+  std::vector<float> out((size_t)ncblk * (k.nstep + 1) * k.nsubt * per_frag, 0.f);
+  auto w_at = [&](int co, int ci, int dy, int dx) -> float {
+    if (d.convT)  // ConvTranspose2d weight [cin][cout][kh][kw], flipped
+      return W[(((size_t)ci * d.cout + co) * d.ks + (d.ks - 1 - dy)) * d.ks + (d.ks - 1 - dx)];
+    return W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
+  };
+  for (int cb = 0; cb < ncblk; ++cb)
+    for (int s = 0; s < k.nstep; ++s)
+      for (int tg = 0; tg < k.nsubt; ++tg)
+        for (int lane = 0; lane < 64; ++lane) {
+          const int wn = tg / k.nsub, t = tg % k.nsub, q = lane & 15, g = lane >> 4;
+          const int co = cb * k.bn + wn * k.nsub * 16 + 4 * k.nsub * (q >> 2) + 4 * t + (q & 3);
+          const int i = 4 * s + g;
+          float* dst = &out[((((size_t)cb * (k.nstep + 1) + s) * k.nsubt + tg) * 64 + lane) * k.cpc];
+          if (i >= k.nchunk || co >= d.cout) continue;
+          const int tap = i / k.nch, c = i % k.nch;
+          const int dy = tap / k.kp, dxp = tap % k.kp;
+          for (int j = 0; j < k.cpc; ++j) {
+            int dx, ci;
+            if (k.pair) { dx = 2 * dxp + (j >= 4 ? 1 : 0); ci = j & 3; }
+            else { dx = dxp; ci = c * k.cpc + j; }
+            if (dx < d.ks && ci < d.cin) dst[j] = w_at(co, ci, dy, dx);
+          }
+        }
+  return out;
+}
+
+int upload(const void* host, size_t bytes, void** dev) {
+  NST_HIP_CHECK(hipMalloc(dev, bytes));
+  NST_HIP_CHECK(hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice));
+  return NST_OK;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  bool changed = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+      changed = hipSetDevice(dev) == hipSuccess;
+    }
+  }
+  ~DeviceGuard() {
+    if (changed) (void)hipSetDevice(prev);
+  }
+};
+
+// conv output extent along one axis for an input extent L
+int conv_out_dim(const LayerDef& d, int L) {
+  switch (d.axis_mode) {
+    case AX_REFLECT_UP2: return (2 * L + 2 * d.pad - d.ks) / d.stride + 1;
+    case AX_ZERO_PREREFLECT: return (L + 2 * d.pre + 2 * d.pad - d.ks) / d.stride + 1;
+    case AX_ZINSERT: return 2 * L;  // ConvTranspose2d(k3, s2, p1, output_padding 1)
+    default: return (L + 2 * d.pad - d.ks) / d.stride + 1;
+  }
+}
+
+// minimum input extent for which the reference's padding is legal
+bool layer_input_ok(const LayerDef& d, int L) {
+  if (d.axis_mode == AX_REFLECT) return L > d.pad;
+  if (d.axis_mode == AX_REFLECT_UP2) return 2 * L > d.pad;
+  if (d.axis_mode == AX_ZERO_PREREFLECT) return L > d.pre;
+  return L >= 1;
+}
+
+struct Plan {
+  bool ok = false;
+  std::string err;
+  // per op: input and output dims
+  std::vector<int> ih, iw, oh, ow, ch, cw;  // ch/cw: conv extent (before crop)
+  size_t buf_bytes[NBUF] = {0, 0, 0, 0, 0};
+  size_t partial_floats = 0;
+  int out_h = 0, out_w = 0;
+  size_t ws_bytes = 0;
+  size_t off_buf[NBUF], off_partial, off_stats;
+};
+
+size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+
+Plan make_plan(const nst_handle* h, int n, int H, int W) {
+  Plan P;
+  const size_t esz = h->dtype == NST_DT_BF16 ? 2 : 4;
+  int bh[NBUF], bw[NBUF];
+  const size_t nops = h->prog.size();
+  P.ih.resize(nops); P.iw.resize(nops); P.oh.resize(nops); P.ow.resize(nops); P.ch.resize(nops); P.cw.resize(nops);
+  for (size_t i = 0; i < nops; ++i) {
+    const Op& op = h->prog[i];
+    const Layer& Ly = h->layers[op.layer];
+    if (op.kind == OP_CONV) {
+      const int sh = op.src == B_IMG ? H : bh[op.src];
+      const int sw = op.src == B_IMG ? W : bw[op.src];
+      if (!layer_input_ok(Ly.d, sh) || !layer_input_ok(Ly.d, sw)) {
+        P.err = "input " + std::to_string(H) + "x" + std::to_string(W) + " too small for layer " + Ly.d.conv +
+                " (padding must be smaller than its input " + std::to_string(sh) + "x" + std::to_string(sw) + ")";
+        return P;
+      }
+      const int ch = conv_out_dim(Ly.d, sh), cw = conv_out_dim(Ly.d, sw);
+      P.ih[i] = sh; P.iw[i] = sw; P.ch[i] = ch; P.cw[i] = cw;
+      if (op.dst == B_OUT) {
+        if (h->arch == NST_ARCH_NST) {  // centre crop back to the input size (transformer_net_nst.py:121-125)
+          P.oh[i] = H; P.ow[i] = W;
+        } else {
+          P.oh[i] = ch; P.ow[i] = cw;
+        }
+        P.out_h = P.oh[i]; P.out_w = P.ow[i];
+      } else {
+        P.oh[i] = ch; P.ow[i] = cw;
+        bh[op.dst] = ch; bw[op.dst] = cw;
+        const size_t bytes = (size_t)n * ch * cw * Ly.coutp * esz;
+        if (bytes > P.buf_bytes[op.dst]) P.buf_bytes[op.dst] = bytes;
+        const int tiles = ((ch + Ly.k_main->th - 1) / Ly.k_main->th) * ((cw + Ly.k_main->tw - 1) / Ly.k_main->tw);
+        const size_t pf = (size_t)n * tiles * Ly.coutp * 2;
+        if (pf > P.partial_floats) P.partial_floats = pf;
+      }
+    } else {
+      P.ih[i] = P.oh[i] = bh[op.src];
+      P.iw[i] = P.ow[i] = bw[op.src];
+      bh[op.dst] = bh[op.src];
+      bw[op.dst] = bw[op.src];
+    }
+  }
+  size_t off = 0;
+  for (int b = 0; b < NBUF; ++b) { P.off_buf[b] = off; off += align256(P.buf_bytes[b]); }
+  P.off_partial = off;
+  off += align256(P.partial_floats * 4);
+  P.off_stats = off;
+  for (const Layer& Ly : h->layers) off += align256((size_t)n * Ly.coutp * 8);
+  P.ws_bytes = off;
+  P.ok = true;
+  return P;
+}
+
+struct PresetConsts {
+  float ea[3], eb[3], ed[3];
+  int eperm[3];
+  float dp[3], dq[3], dr[3], ds[3];
+  int dperm[3];
+};
+
+// fp32 constants exactly as the reference's torch expressions round them (pipeline.py:272-273, 1445-1486)
+bool preset_consts(int preset, PresetConsts& c) {
+  const float mean[3] = {0.485f, 0.456f, 0.406f}, stdv[3] = {0.229f, 0.224f, 0.225f};
+  const float caffe[3] = {103.939f, 116.779f, 123.68f};
+  for (int i = 0; i < 3; ++i) {
+    c.ea[i] = 1.f; c.eb[i] = 0.f; c.ed[i] = 1.f; c.eperm[i] = i;
+    c.dp[i] = 0.f; c.dq[i] = 1.f; c.dr[i] = 1.f; c.ds[i] = 0.f; c.dperm[i] = i;
+  }
+  switch (preset) {
+    case NST_PRESET_NONE: case NST_PRESET_RAW_01: return true;
+    case NST_PRESET_TANH:
+      for (int i = 0; i < 3; ++i) { c.ea[i] = 2.f; c.eb[i] = 1.f; c.dp[i] = 1.f; c.dq[i] = 0.5f; }
+      return true;
+    case NST_PRESET_IMAGENET_01:
+      for (int i = 0; i < 3; ++i) { c.eb[i] = mean[i]; c.ed[i] = stdv[i]; c.dq[i] = stdv[i]; c.ds[i] = mean[i]; }
+      return true;
+    case NST_PRESET_IMAGENET_255:
+      for (int i = 0; i < 3; ++i) {
+        volatile float m = mean[i] * 255.0f, s = stdv[i] * 255.0f;
+        c.ea[i] = 255.f; c.eb[i] = m; c.ed[i] = s; c.dr[i] = 255.f;
+      }
+      return true;
+    case NST_PRESET_CAFFE_BGR:
+      for (int i = 0; i < 3; ++i) {
+        c.ea[i] = 255.f; c.eb[i] = caffe[i]; c.eperm[i] = 2 - i; c.dr[i] = 255.f; c.dperm[i] = 2 - i;
+      }
+      return true;
+    case NST_PRESET_RAW_255:
+      for (int i = 0; i < 3; ++i) { c.ea[i] = 255.f; c.dr[i] = 255.f; }
+      return true;
+    default: return false;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nst_last_error(void) { return g_last_error.c_str(); }
+const char* nst_version(void) { return "nst_hip 0.1.0 (gfx950)"; }
+
+int nst_create(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
+               nst_handle** out) {
+  if (!out || arch < 0 || arch > 2 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16)) {
+    set_error("nst_create: invalid arguments");
+    return NST_E_INVALID;
+  }
+  *out = nullptr;
+  std::map<std::string, const nst_param*> byname;
+  for (int i = 0; i < n_params; ++i)
+    if (params[i].name) byname[params[i].name] = &params[i];
+  auto get = [&](const std::string& name, int64_t numel, const float** p) -> int {
+    auto it = byname.find(name);
+    if (it == byname.end()) { set_error("missing checkpoint tensor: " + name); return NST_E_PARAM; }
+    if (it->second->numel != numel) {
+      set_error("checkpoint tensor " + name + " has " + std::to_string(it->second->numel) +
+                " elements, expected " + std::to_string(numel));
+      return NST_E_PARAM;
+    }
+    *p = it->second->data;
+    return NST_OK;
+  };
+  DeviceGuard guard(device);
+  auto* h = new nst_handle();
+  h->arch = arch; h->dtype = compute_dtype; h->device = device;
+  std::vector<LayerDef> defs;
+  build_program(arch, defs, h->prog);
+  const int align = compute_dtype == NST_DT_BF16 ? 32 : 16;
+  int rc = NST_OK;
+  for (size_t li = 0; li < defs.size() && rc == NST_OK; ++li) {
+    Layer Ly;
+    Ly.d = defs[li];
+    const LayerDef& d = Ly.d;
+    const bool image_in = li == 0;
+    const bool final_layer = d.norm.empty();
+    Ly.cinp = image_in ? 4 : round_up(d.cin, align);
+    Ly.coutp = final_layer ? 16 : round_up(d.cout, align);
+    const int ink = image_in ? IN_U8_NHWC : IN_ACT;
+    const int outk = final_layer ? OUT_U8_NHWC : OUT_ACT;
+    Ly.k_main = find_conv_kernel(compute_dtype, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk);
+    if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk);
+    if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW);
+    if (!Ly.k_main || ((image_in || final_layer) && !Ly.k_alt)) {
+      set_error("no compiled conv kernel for layer " + d.conv + " (ks " + std::to_string(d.ks) + " stride " +
+                std::to_string(d.stride) + " cin " + std::to_string(Ly.cinp) + " cout " + std::to_string(Ly.coutp) + ")");
+      rc = NST_E_SHAPE;
+      break;
+    }
+    const float *W = nullptr, *b = nullptr, *gm = nullptr, *bt = nullptr;
+    const int64_t wn = (int64_t)d.cout * d.cin * d.ks * d.ks;
+    if ((rc = get(d.conv + ".weight", wn, &W)) != NST_OK) break;
+    if ((rc = get(d.conv + ".bias", d.cout, &b)) != NST_OK) break;
+    if (!final_layer) {
+      if ((rc = get(d.norm + ".weight", d.cout, &gm)) != NST_OK) break;
+      if ((rc = get(d.norm + ".bias", d.cout, &bt)) != NST_OK) break;
+    }
+    std::vector<float> pk = pack_weights(*Ly.k_main, d, W, Ly.coutp);
+    if (compute_dtype == NST_DT_BF16) {
+      std::vector<uint16_t> pb(pk.size());
+      for (size_t i = 0; i < pk.size(); ++i) pb[i] = f32_to_bf16_rne(pk[i]);
+      rc = upload(pb.data(), pb.size() * 2, &Ly.wpk);
+    } else {
+      rc = upload(pk.data(), pk.size() * 4, &Ly.wpk);
+    }
+    if (rc != NST_OK) break;
+    std::vector<float> bp(Ly.coutp, 0.f), gp(Ly.coutp, 0.f), btp(Ly.coutp, 0.f);
+    for (int c = 0; c < d.cout; ++c) {
+      bp[c] = b[c];
+      if (gm) { gp[c] = gm[c]; btp[c] = bt[c]; }
+    }
+    if ((rc = upload(bp.data(), bp.size() * 4, (void**)&Ly.bias)) != NST_OK) break;
+    if (!final_layer) {
+      if ((rc = upload(gp.data(), gp.size() * 4, (void**)&Ly.gamma)) != NST_OK) break;
+      if ((rc = upload(btp.data(), btp.size() * 4, (void**)&Ly.beta)) != NST_OK) break;
+    }
+    h->layers.push_back(Ly);
+  }
+  if (rc != NST_OK) {
+    nst_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return NST_OK;
+}
+
+void nst_destroy(nst_handle* h) {
+  if (!h) return;
+  DeviceGuard guard(h->device);
+  for (Layer& Ly : h->layers) {
+    if (Ly.wpk) (void)hipFree(Ly.wpk);
+    if (Ly.bias) (void)hipFree(Ly.bias);
+    if (Ly.gamma) (void)hipFree(Ly.gamma);
+    if (Ly.beta) (void)hipFree(Ly.beta);
+  }
+  delete h;
+}
+
+int nst_output_hw(const nst_handle* h, int in_h, int in_w, int* out_h, int* out_w) {
+  if (!h || !out_h || !out_w || in_h <= 0 || in_w <= 0) { set_error("nst_output_hw: invalid arguments"); return NST_E_INVALID; }
+  Plan P = make_plan(h, 1, in_h, in_w);
+  if (!P.ok) { set_error(P.err); return NST_E_SHAPE; }
+  *out_h = P.out_h;
+  *out_w = P.out_w;
+  return NST_OK;
+}
+
+int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* out) {
+  if (!h || !out || n <= 0 || in_h <= 0 || in_w <= 0) { set_error("nst_workspace_bytes: invalid arguments"); return NST_E_INVALID; }
+  Plan P = make_plan(h, n, in_h, in_w);
+  if (!P.ok) { set_error(P.err); return NST_E_SHAPE; }
+  *out = P.ws_bytes;
+  return NST_OK;
+}
+
+int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset, void* y,
+                int y_fmt, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!h || !x || !y || n <= 0 || in_h <= 0 || in_w <= 0 ||
+      (x_fmt != NST_IO_F32_NCHW && x_fmt != NST_IO_U8_NHWC) || (y_fmt != NST_IO_F32_NCHW && y_fmt != NST_IO_U8_NHWC)) {
+    set_error("nst_forward: invalid arguments");
+    return NST_E_INVALID;
+  }
+  PresetConsts pc;
+  if (!preset_consts(preset, pc)) { set_error("nst_forward: unknown preset " + std::to_string(preset)); return NST_E_INVALID; }
+  if (preset == NST_PRESET_NONE && (x_fmt == NST_IO_U8_NHWC || y_fmt == NST_IO_U8_NHWC)) {
+    set_error("nst_forward: uint8 frames need an io_preset");
+    return NST_E_INVALID;
+  }
+  Plan P = make_plan(h, n, in_h, in_w);
+  if (!P.ok) { set_error(P.err); return NST_E_SHAPE; }
+  if (y_fmt == NST_IO_U8_NHWC && (P.out_h != in_h || P.out_w != in_w)) {
+    set_error("nst_forward: model output " + std::to_string(P.out_h) + "x" + std::to_string(P.out_w) +
+              " differs from the input; request F32 output and use nst_decode_resize_u8");
+    return NST_E_SHAPE;
+  }
+  if (!workspace || workspace_bytes < P.ws_bytes) {
+    set_error("nst_forward: workspace too small (" + std::to_string(workspace_bytes) + " < " + std::to_string(P.ws_bytes) + ")");
+    return NST_E_WORKSPACE;
+  }
+  DeviceGuard guard(h->device);
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  void* bufs[NBUF];
+  for (int b = 0; b < NBUF; ++b) bufs[b] = ws + P.off_buf[b];
+  float* partial = (float*)(ws + P.off_partial);
+  std::vector<float2*> stats(h->layers.size());
+  {
+    size_t off = P.off_stats;
+    for (size_t li = 0; li < h->layers.size(); ++li) {
+      stats[li] = (float2*)(ws + off);
+      off += align256((size_t)n * h->layers[li].coutp * 8);
+    }
+  }
+  for (size_t i = 0; i < h->prog.size(); ++i) {
+    const Op& op = h->prog[i];
+    const Layer& Ly = h->layers[op.layer];
+    if (op.kind == OP_RESADD) {
+      const int hw = P.oh[i] * P.ow[i];
+      hipError_t e = launch_residual(h->dtype, bufs[op.src], stats[op.layer], bufs[op.r_buf],
+                                     op.r_norm >= 0 ? stats[op.r_norm] : nullptr, op.r_relu, op.relu_out,
+                                     bufs[op.dst], n, hw, Ly.coutp, st);
+      if (e != hipSuccess) { set_error(std::string("residual launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+      continue;
+    }
+    const bool image_in = op.src == B_IMG, final_out = op.dst == B_OUT;
+    const ConvKernelInfo* k = Ly.k_main;
+    if (image_in && x_fmt == NST_IO_F32_NCHW) k = Ly.k_alt;
+    if (final_out && y_fmt == NST_IO_F32_NCHW) k = Ly.k_alt;
+    ConvParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.in = image_in ? x : bufs[op.src];
+    p.hs = P.ih[i];
+    p.ws = P.iw[i];
+    p.cs = image_in ? 3 : Ly.cinp;
+    p.axis_mode = Ly.d.axis_mode;
+    p.pad = Ly.d.axis_mode == AX_ZINSERT ? 1 : Ly.d.pad;
+    p.pre = Ly.d.pre;
+    p.in_norm = op.in_norm >= 0 ? stats[op.in_norm] : nullptr;
+    p.in_relu = op.in_norm >= 0 ? 1 : 0;
+    for (int c = 0; c < 3; ++c) {
+      p.enc_a[c] = pc.ea[c]; p.enc_b[c] = pc.eb[c]; p.enc_d[c] = pc.ed[c]; p.enc_perm[c] = pc.eperm[c];
+      p.dec_p[c] = pc.dp[c]; p.dec_q[c] = pc.dq[c]; p.dec_r[c] = pc.dr[c]; p.dec_s[c] = pc.ds[c]; p.dec_perm[c] = pc.dperm[c];
+    }
+    if (image_in && x_fmt == NST_IO_F32_NCHW && preset == NST_PRESET_NONE) {
+      for (int c = 0; c < 3; ++c) { p.enc_a[c] = 1.f; p.enc_b[c] = 0.f; p.enc_d[c] = 1.f; p.enc_perm[c] = c; }
+    }
+    p.dec_tanh = (h->arch == NST_ARCH_RECONET && final_out) ? 1 : 0;
+    p.wpk = Ly.wpk;
+    p.bias = Ly.bias;
+    p.hconv = P.ch[i];
+    p.wconv = P.cw[i];
+    p.oh = P.oh[i];
+    p.ow = P.ow[i];
+    p.crop_y = (P.ch[i] - P.oh[i]) / 2;
+    p.crop_x = (P.cw[i] - P.ow[i]) / 2;
+    p.out = final_out ? y : bufs[op.dst];
+    p.cout_real = Ly.d.cout;
+    p.cout_stride = Ly.coutp;
+    p.tiles_x = (p.ow + k->tw - 1) / k->tw;
+    p.tiles_y = (p.oh + k->th - 1) / k->th;
+    p.n_cblk = Ly.coutp / k->bn;
+    p.partial = final_out ? nullptr : partial;
+    dim3 grid(p.tiles_x * p.tiles_y, n * p.n_cblk);
+    nst_handle::Rec rec{op.layer, nullptr, nullptr};
+    if (h->profiling) {
+      NST_HIP_CHECK(hipEventCreate(&rec.a));
+      NST_HIP_CHECK(hipEventCreate(&rec.b));
+      NST_HIP_CHECK(hipEventRecord(rec.a, st));
+    }
+    k->launch(p, grid, st);
+    hipError_t e = hipGetLastError();
+    if (h->profiling && e == hipSuccess) {
+      NST_HIP_CHECK(hipEventRecord(rec.b, st));
+      h->recs.push_back(rec);
+    }
+    if (e != hipSuccess) { set_error("conv " + Ly.d.conv + " launch: " + hipGetErrorString(e)); return NST_E_HIP; }
+    if (!final_out) {
+      e = launch_in_finalize(partial, n, p.tiles_x * p.tiles_y, Ly.coutp, (double)p.hconv * (double)p.wconv,
+                             Ly.gamma, Ly.beta, 1e-5f, stats[op.layer], st);
+      if (e != hipSuccess) { set_error(std::string("finalize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+    }
+  }
+  return NST_OK;
+}
+
+int nst_profile_begin(nst_handle* h) {
+  if (!h) { set_error("nst_profile_begin: null handle"); return NST_E_INVALID; }
+  h->profiling = true;
+  return NST_OK;
+}
+
+int nst_profile_end(nst_handle* h, int n_layers, float* total_ms, int* launches) {
+  if (!h || n_layers < 0 || (n_layers > 0 && (!total_ms || !launches))) {
+    set_error("nst_profile_end: invalid arguments");
+    return NST_E_INVALID;
+  }
+  DeviceGuard guard(h->device);
+  for (int i = 0; i < n_layers; ++i) { total_ms[i] = 0.f; launches[i] = 0; }
+  int rc = NST_OK;
+  for (auto& r : h->recs) {
+    float ms = 0.f;
+    hipError_t e = hipEventElapsedTime(&ms, r.a, r.b);
+    if (e != hipSuccess && rc == NST_OK) {
+      set_error(std::string("hipEventElapsedTime: ") + hipGetErrorString(e));
+      rc = NST_E_HIP;
+    }
+    if (r.layer < n_layers) { total_ms[r.layer] += ms; launches[r.layer] += 1; }
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  h->recs.clear();
+  h->profiling = false;
+  return rc;
+}
+
+int nst_num_layers(const nst_handle* h) { return h ? (int)h->layers.size() : 0; }
+
+const char* nst_layer_name(const nst_handle* h, int layer) {
+  if (!h || layer < 0 || layer >= (int)h->layers.size()) return "";
+  return h->layers[layer].d.conv.c_str();
+}
+
+int nst_decode_resize_u8(const float* y, int n, int h, int w, int preset, uint8_t* out, int out_h, int out_w,
+                         void* stream) {
+  PresetConsts pc;
+  if (!y || !out || n <= 0 || h <= 0 || w <= 0 || out_h <= 0 || out_w <= 0 || !preset_consts(preset, pc)) {
+    set_error("nst_decode_resize_u8: invalid arguments");
+    return NST_E_INVALID;
+  }
+  hipError_t e = launch_decode_resize_u8(y, n, h, w, pc.dp, pc.dq, pc.dr, pc.ds, pc.dperm, out, out_h, out_w,
+                                         (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("decode_resize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+int nst_lab_create(const uint8_t* rgb2lab, const uint8_t* lab2rgb, int device, nst_lab** out) {
+  if (!rgb2lab || !lab2rgb || !out) { set_error("nst_lab_create: invalid arguments"); return NST_E_INVALID; }
+  DeviceGuard guard(device);
+  auto* l = new nst_lab();
+  l->device = device;
+  const size_t bytes = (size_t)3 << 24;
+  int rc = upload(rgb2lab, bytes, (void**)&l->rgb2lab);
+  if (rc == NST_OK) rc = upload(lab2rgb, bytes, (void**)&l->lab2rgb);
+  if (rc != NST_OK) { nst_lab_destroy(l); return rc; }
+  *out = l;
+  return NST_OK;
+}
+
+void nst_lab_destroy(nst_lab* l) {
+  if (!l) return;
+  DeviceGuard guard(l->device);
+  if (l->rgb2lab) (void)hipFree(l->rgb2lab);
+  if (l->lab2rgb) (void)hipFree(l->lab2rgb);
+  delete l;
+}
+
+int nst_lab_ema_u8(const nst_lab* lab, const uint8_t* rgb_in, uint8_t* rgb_out, int n, int h, int w,
+                   int smooth_lightness, float alpha, float one_minus_alpha, int smooth_chroma, float chroma_alpha,
+                   float one_minus_chroma_alpha, float* state, int first, void* stream) {
+  if (!lab || !rgb_in || !rgb_out || !state || n <= 0 || h <= 0 || w <= 0) {
+    set_error("nst_lab_ema_u8: invalid arguments");
+    return NST_E_INVALID;
+  }
+  hipError_t e = launch_lab_ema(lab->rgb2lab, lab->lab2rgb, rgb_in, rgb_out, n, h * w, smooth_lightness, alpha,
+                                one_minus_alpha, smooth_chroma, chroma_alpha, one_minus_chroma_alpha, state, first,
+                                (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("lab_ema launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+int nst_blend_u8(const uint8_t* styled, const uint8_t* orig, const float* mask, int composite_mode, float blend,
+                 float one_minus_blend, uint8_t* out, int n, int h, int w, void* stream) {
+  if (!styled || !orig || !out || n <= 0 || h <= 0 || w <= 0 || composite_mode < 0 || composite_mode > 1) {
+    set_error("nst_blend_u8: invalid arguments");
+    return NST_E_INVALID;
+  }
+  hipError_t e = launch_blend(styled, orig, mask, composite_mode, blend, one_minus_blend, out, n, h * w,
+                              (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("blend launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+int nst_gram(const void* F, int dtype, int n, int c, int hw, float* G, void* stream) {
+  if (!F || !G || n <= 0 || c <= 0 || hw <= 0 || (dtype != NST_DT_F32 && dtype != NST_DT_BF16)) {
+    set_error("nst_gram: invalid arguments");
+    return NST_E_INVALID;
+  }
+  const int vec = dtype == NST_DT_BF16 ? 8 : 4;
+  if (hw % vec != 0 || ((uintptr_t)F % 16) != 0) {
+    set_error("nst_gram: h*w must be a multiple of " + std::to_string(vec) + " and F 16-byte aligned");
+    return NST_E_SHAPE;
+  }
+  hipError_t e = launch_gram(F, dtype, n, c, hw, G, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("gram launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+}  // extern "C"

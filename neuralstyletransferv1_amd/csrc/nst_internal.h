@@ -1,0 +1,96 @@
+// nst_internal.h — shared declarations between the HIP translation units of libnst_hip.so.
+// Not part of the public ABI (that is include/nst_hip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+
+namespace nst {
+
+// ---- error plumbing (thread-local last error, see nst_last_error) ----
+void set_error(const std::string& msg);
+#define NST_HIP_CHECK(expr)                                                               \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      ::nst::set_error(std::string(#expr) + " failed: " + hipGetErrorString(_e));         \
+      return NST_E_HIP;                                                                   \
+    }                                                                                     \
+  } while (0)
+
+// ---- how a conv layer's input tile is sourced ----
+enum InKind { IN_ACT = 0, IN_U8_NHWC = 1, IN_F32_NCHW = 2 };
+// ---- what a conv layer's epilogue writes ----
+enum OutKind { OUT_ACT = 0, OUT_U8_NHWC = 1, OUT_F32_NCHW = 2 };
+
+// Virtual-coordinate -> source-pixel mapping of the conv input along one axis.
+//   AX_REFLECT          ReflectionPad2d(pad)                       transformer_net.py:47-48, model.py:10
+//   AX_REFLECT_UP2      interpolate(nearest, x2) then reflect pad  transformer_net.py:95-97, model.py:92-96
+//   AX_ZERO             Conv2d(padding=pad)                        transformer_net_nst.py:19,32-34
+//   AX_ZERO_PREREFLECT  ReflectionPad2d(pre) then Conv2d(padding)  transformer_net_nst.py:74,99,76
+//   AX_ZINSERT          ConvTranspose2d(3, s2, p1, op1) as a conv over the zero-inserted grid
+//                                                                  transformer_net_nst.py:50-53
+enum AxisMode { AX_REFLECT = 0, AX_REFLECT_UP2 = 1, AX_ZERO = 2, AX_ZERO_PREREFLECT = 3, AX_ZINSERT = 4 };
+
+struct ConvParams {
+  // input
+  const void* in;
+  int hs, ws;   // source spatial dims
+  int cs;       // source channel stride (elements) for IN_ACT
+  int axis_mode, pad, pre;
+  const float2* in_norm;  // [n][cs] {scale, shift} of the producer's InstanceNorm, or nullptr
+  int in_relu;            // apply ReLU after in_norm
+  // image-input preset encode: x_in[c] = ((x01[perm[c]] * a[c]) - b[c]) / d[c]
+  float enc_a[3], enc_b[3], enc_d[3];
+  int enc_perm[3];
+  // weights
+  const void* wpk;     // packed fragments (see pack_conv_weights)
+  const float* bias;   // [cout_pad]
+  // output geometry
+  int hconv, wconv;    // conv output extent (statistics count)
+  int crop_y, crop_x;  // stored (oy,ox) -> conv coordinate (oy+crop_y, ox+crop_x)
+  int oh, ow;          // stored output extent
+  void* out;
+  int cout_real;
+  int cout_stride;     // channel stride of OUT_ACT buffers (= padded cout)
+  float* partial;      // [n][tiles][cout_stride][2] InstanceNorm partial sums (OUT_ACT), or nullptr
+  int tiles_x, tiles_y, n_cblk;
+  // output decode: v[c] = (((y[perm[c]] + p[c]) * q[c]) / r[c]) + s[c]; clamp(0,1)
+  float dec_p[3], dec_q[3], dec_r[3], dec_s[3];
+  int dec_perm[3];
+  int dec_tanh;  // apply tanh to the raw output first (ReCoNet ConvTanhLayer, model.py:77-80)
+};
+
+// Static description of one compiled conv kernel instantiation.
+struct ConvKernelInfo {
+  int dtype;  // NST_DT_*
+  int ks, stride, cinp, bn, th, tw, wm, wn, in_kind, out_kind;
+  // derived
+  int pair, nch, cpc, kp, nchunk, nstep, nsubt, nsub, lds_bytes;
+  void (*launch)(const ConvParams&, dim3 grid, hipStream_t);
+};
+
+// Look up a compiled instantiation; nullptr if the combination was not built.
+const ConvKernelInfo* find_conv_kernel(int dtype, int ks, int stride, int cinp, int bn, int in_kind,
+                                       int out_kind);
+
+// ---- elementwise / reduction launchers (nst_ops.hip) ----
+hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
+                              const float* gamma, const float* beta, float eps, float2* out,
+                              hipStream_t st);
+hipError_t launch_residual(int dtype, const void* y, const float2* ys, const void* r,
+                           const float2* rs, int r_relu, int relu_out, void* out, int n, int hw,
+                           int c, hipStream_t st);
+hipError_t launch_decode_resize_u8(const float* y, int n, int h, int w, const float* p,
+                                   const float* q, const float* r, const float* s, const int* perm,
+                                   uint8_t* out, int oh, int ow, hipStream_t st);
+hipError_t launch_lab_ema(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* in,
+                          uint8_t* out, int n, int hw, int sl, float a, float oma, int sc, float ca,
+                          float coma, float* state, int first, hipStream_t st);
+hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,
+                        float omb, uint8_t* out, int n, int hw, hipStream_t st);
+hipError_t launch_gram(const void* F, int dtype, int n, int c, int hw, float* G, hipStream_t st);
+
+}  // namespace nst

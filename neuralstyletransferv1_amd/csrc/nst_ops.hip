@@ -1,0 +1,389 @@
+// nst_ops.hip — the non-conv kernels of the hot path: InstanceNorm finalize, residual add,
+// output decode + bilinear fit, LAB temporal smoothing, original/mask blend, Gram matrix.
+// All fp32 elementwise arithmetic is written op-by-op in the reference's order and the
+// library is built with -ffp-contract=off, so no FMA contraction changes a rounding.
+#include "nst_internal.h"
+#include "nst_hip.h"
+
+namespace nst {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------
+// InstanceNorm2d(affine=True, eps=1e-5, track_running_stats=False) statistics:
+// per-(n,c) mean and BIASED variance over H*W (transformer_net.py:9 etc; frozen eval
+// semantics identical to train for IN).  Reduces the conv epilogue's per-tile partial sums
+// in fp64 and emits the affine {scale, shift} the consumer's prologue applies:
+//   y = x*scale + shift, scale = gamma/sqrt(var+eps), shift = beta - mean*scale.
+// grid (n, cstride/64), block 256 = 64 channels x 4 tile phases.
+__global__ __launch_bounds__(256) void in_finalize_kernel(const float* __restrict__ partial, int tiles,
+                                                          int cstride, double count,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          float2* __restrict__ out) {
+  __shared__ double red[4][64][2];
+  const int n = blockIdx.x;
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < cstride) {
+    const float2* p = (const float2*)partial + (size_t)n * tiles * cstride + c;
+    int t = q;
+    for (; t + 12 < tiles; t += 16) {
+      const float2 a = p[(size_t)t * cstride], b = p[(size_t)(t + 4) * cstride];
+      const float2 d = p[(size_t)(t + 8) * cstride], e = p[(size_t)(t + 12) * cstride];
+      s1 += (double)a.x + (double)b.x + (double)d.x + (double)e.x;
+      s2 += (double)a.y + (double)b.y + (double)d.y + (double)e.y;
+    }
+    for (; t < tiles; t += 4) {
+      const float2 a = p[(size_t)t * cstride];
+      s1 += a.x;
+      s2 += a.y;
+    }
+  }
+  red[q][cl][0] = s1;
+  red[q][cl][1] = s2;
+  __syncthreads();
+  if (q == 0 && c < cstride) {
+    s1 = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    s2 = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+    const double mean = s1 / count;
+    double var = s2 / count - mean * mean;
+    var = var < 0.0 ? 0.0 : var;
+    const double rstd = 1.0 / sqrt(var + (double)eps);
+    const double scale = (double)gamma[c] * rstd;
+    out[(size_t)n * cstride + c] = make_float2((float)scale, (float)((double)beta[c] - mean * scale));
+  }
+}
+
+hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
+                              const float* gamma, const float* beta, float eps, float2* out,
+                              hipStream_t st) {
+  dim3 grid(n, (cstride + 63) / 64);
+  hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(256), 0, st, partial, tiles, cstride, count, gamma,
+                     beta, eps, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Residual add:  out = IN(y) + r  (ResidualBlock.forward, transformer_net.py:71-76 /
+// transformer_net_nst.py:138-142), r either materialised or itself IN+ReLU of a raw conv
+// output (the first block's input, never materialised); ReCoNet ResLayer applies ReLU after
+// the add (model.py:55-60).  16 bytes per thread, NHWC.
+template <typename T>
+__global__ __launch_bounds__(256) void residual_kernel(const T* __restrict__ y, const float2* __restrict__ ys,
+                                                       const T* r, const float2* __restrict__ rs,
+                                                       int r_relu, int relu_out, T* out, int hw, int c,
+                                                       size_t nvec) {
+  constexpr int CPC = 16 / (int)sizeof(T);
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nvec) return;
+  const size_t e0 = i * CPC;
+  const int ch0 = (int)(e0 % (size_t)c);
+  const int n = (int)(e0 / ((size_t)c * hw));
+  const float2* ysn = ys + (size_t)n * c + ch0;
+  const float2* rsn = rs ? rs + (size_t)n * c + ch0 : nullptr;
+  float vy[CPC], vr[CPC];
+  if constexpr (sizeof(T) == 2) {
+    const uint4 a = *(const uint4*)(y + e0), b = *(const uint4*)(r + e0);
+    const uint32_t wa[4] = {a.x, a.y, a.z, a.w}, wb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      vy[2 * j] = __uint_as_float(wa[j] << 16);
+      vy[2 * j + 1] = __uint_as_float(wa[j] & 0xffff0000u);
+      vr[2 * j] = __uint_as_float(wb[j] << 16);
+      vr[2 * j + 1] = __uint_as_float(wb[j] & 0xffff0000u);
+    }
+  } else {
+    const float4 a = *(const float4*)(y + e0), b = *(const float4*)(r + e0);
+    vy[0] = a.x; vy[1] = a.y; vy[2] = a.z; vy[3] = a.w;
+    vr[0] = b.x; vr[1] = b.y; vr[2] = b.z; vr[3] = b.w;
+  }
+  float o[CPC];
+#pragma unroll
+  for (int j = 0; j < CPC; ++j) {
+    float rr = vr[j];
+    if (rsn) {
+      rr = rr * rsn[j].x + rsn[j].y;
+      if (r_relu) rr = fmaxf(rr, 0.f);
+    }
+    float v = vy[j] * ysn[j].x + ysn[j].y;
+    v = rr + v;
+    if (relu_out) v = fmaxf(v, 0.f);
+    o[j] = v;
+  }
+  if constexpr (sizeof(T) == 2) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __bf16 lo = (__bf16)o[2 * j], hi = (__bf16)o[2 * j + 1];
+      w[j] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    }
+    *(uint4*)(out + e0) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    *(float4*)(out + e0) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+hipError_t launch_residual(int dtype, const void* y, const float2* ys, const void* r, const float2* rs,
+                           int r_relu, int relu_out, void* out, int n, int hw, int c, hipStream_t st) {
+  const int cpc = dtype == NST_DT_BF16 ? 8 : 4;
+  const size_t nvec = (size_t)n * hw * c / cpc;
+  const unsigned blocks = (unsigned)((nvec + 255) / 256);
+  if (dtype == NST_DT_BF16)
+    hipLaunchKernelGGL(residual_kernel<__bf16>, dim3(blocks), dim3(256), 0, st, (const __bf16*)y, ys,
+                       (const __bf16*)r, rs, r_relu, relu_out, (__bf16*)out, hw, c, nvec);
+  else
+    hipLaunchKernelGGL(residual_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)y, ys,
+                       (const float*)r, rs, r_relu, relu_out, (float*)out, hw, c, nvec);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Output fit: preset decode + clamp(0,1) of the raw model output (pipeline.py:1445-1486),
+// bilinear resize to the content size with align_corners=False (pipeline.py:1512-1516,
+// PyTorch upsample_bilinear2d index math), ToPILImage truncation to uint8 NHWC.
+struct DecodeConsts {
+  float p[3], q[3], r[3], s[3];
+  int perm[3];
+};
+
+__device__ __forceinline__ float decode01(const float* y, int ch, const DecodeConsts& d) {
+  float v = (((y[d.perm[ch]] + d.p[ch]) * d.q[ch]) / d.r[ch]) + d.s[ch];
+  return fminf(fmaxf(v, 0.f), 1.f);
+}
+
+__global__ __launch_bounds__(256) void decode_resize_kernel(const float* __restrict__ y, int n, int h, int w,
+                                                            DecodeConsts d, uint8_t* __restrict__ out,
+                                                            int oh, int ow) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)n * oh * ow;
+  if (i >= total) return;
+  const int ox = (int)(i % ow);
+  const int oy = (int)((i / ow) % oh);
+  const int b = (int)(i / ((size_t)ow * oh));
+  const size_t plane = (size_t)h * w;
+  const float* yb = y + (size_t)b * 3 * plane;
+  uint8_t* o = out + i * 3;
+  if (oh == h && ow == w) {
+    const float yy[3] = {yb[(size_t)oy * w + ox], yb[plane + (size_t)oy * w + ox], yb[2 * plane + (size_t)oy * w + ox]};
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) o[ch] = (uint8_t)(decode01(yy, ch, d) * 255.0f);
+    return;
+  }
+  const float sh = (float)h / (float)oh, sw = (float)w / (float)ow;
+  float fy = sh * ((float)oy + 0.5f) - 0.5f;
+  fy = fy < 0.f ? 0.f : fy;
+  float fx = sw * ((float)ox + 0.5f) - 0.5f;
+  fx = fx < 0.f ? 0.f : fx;
+  const int y0 = (int)fy, x0 = (int)fx;
+  const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
+  const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+  float c00[3], c01[3], c10[3], c11[3];
+  const size_t i00 = (size_t)y0 * w + x0, i01 = (size_t)y0 * w + x1, i10 = (size_t)y1 * w + x0,
+               i11 = (size_t)y1 * w + x1;
+  float t00[3], t01[3], t10[3], t11[3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    t00[ch] = yb[ch * plane + i00];
+    t01[ch] = yb[ch * plane + i01];
+    t10[ch] = yb[ch * plane + i10];
+    t11[ch] = yb[ch * plane + i11];
+  }
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    c00[ch] = decode01(t00, ch, d);
+    c01[ch] = decode01(t01, ch, d);
+    c10[ch] = decode01(t10, ch, d);
+    c11[ch] = decode01(t11, ch, d);
+  }
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float v = ly0 * (lx0 * c00[ch] + lx1 * c01[ch]) + ly1 * (lx0 * c10[ch] + lx1 * c11[ch]);
+    o[ch] = (uint8_t)(v * 255.0f);
+  }
+}
+
+hipError_t launch_decode_resize_u8(const float* y, int n, int h, int w, const float* p, const float* q,
+                                   const float* r, const float* s, const int* perm, uint8_t* out, int oh,
+                                   int ow, hipStream_t st) {
+  DecodeConsts d;
+  for (int c = 0; c < 3; ++c) {
+    d.p[c] = p[c]; d.q[c] = q[c]; d.r[c] = r[c]; d.s[c] = s[c]; d.perm[c] = perm[c];
+  }
+  const size_t total = (size_t)n * oh * ow;
+  hipLaunchKernelGGL(decode_resize_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, y, n, h,
+                     w, d, out, oh, ow);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// LAB temporal smoothing (pipeline.py:1942-1978): Pillow RGB->LAB, float32 EMA of L (and
+// optionally a/b bytes), np.clip(0,255), astype(uint8) truncation, LAB->RGB.  The two
+// LittleCMS transforms are exact 2^24-entry LUT gathers (tables made from Pillow itself).
+// One thread per pixel walks the batch in frame order (the EMA state is per pixel).
+__global__ __launch_bounds__(256) void lab_ema_kernel(const uint8_t* __restrict__ rgb2lab,
+                                                      const uint8_t* __restrict__ lab2rgb,
+                                                      const uint8_t* in, uint8_t* out, int n, int hw,
+                                                      int sl, float a, float oma, int sc, float ca,
+                                                      float coma, float* __restrict__ state, int first) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= hw) return;
+  float pL = state[p], pa = state[hw + p], pb = state[2 * hw + p];
+  for (int f = 0; f < n; ++f) {
+    const size_t idx = ((size_t)f * hw + p) * 3;
+    const uint32_t rgb = ((uint32_t)in[idx] << 16) | ((uint32_t)in[idx + 1] << 8) | in[idx + 2];
+    const uint8_t* lab = rgb2lab + (size_t)rgb * 3;
+    float L = (float)lab[0], A = (float)lab[1], Bc = (float)lab[2];
+    if (sl) {
+      if (first && f == 0) pL = L;
+      const float t0 = a * L;
+      const float t1 = oma * pL;
+      const float Ls = t0 + t1;
+      pL = Ls;
+      L = fminf(fmaxf(Ls, 0.f), 255.f);
+    }
+    if (sc) {
+      if (first && f == 0) { pa = A; pb = Bc; }
+      const float as = ca * A + coma * pa;
+      const float bs = ca * Bc + coma * pb;
+      pa = as;
+      pb = bs;
+      A = fminf(fmaxf(as, 0.f), 255.f);
+      Bc = fminf(fmaxf(bs, 0.f), 255.f);
+    }
+    const uint32_t li = ((uint32_t)(uint8_t)L << 16) | ((uint32_t)(uint8_t)A << 8) | (uint32_t)(uint8_t)Bc;
+    const uint8_t* o = lab2rgb + (size_t)li * 3;
+    out[idx] = o[0];
+    out[idx + 1] = o[1];
+    out[idx + 2] = o[2];
+  }
+  state[p] = pL;
+  state[hw + p] = pa;
+  state[2 * hw + p] = pb;
+}
+
+hipError_t launch_lab_ema(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* in, uint8_t* out,
+                          int n, int hw, int sl, float a, float oma, int sc, float ca, float coma,
+                          float* state, int first, hipStream_t st) {
+  hipLaunchKernelGGL(lab_ema_kernel, dim3((unsigned)((hw + 255) / 256)), dim3(256), 0, st, rgb2lab, lab2rgb,
+                     in, out, n, hw, sl, a, oma, sc, ca, coma, state, first);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Mask composite (pipeline.py:2040-2043) + uniform blend with the original (pipeline.py:2087-2092)
+// + ToPILImage truncation.  S = styled/255, O = original/255 (to_tensor).
+__global__ __launch_bounds__(256) void blend_kernel(const uint8_t* __restrict__ s, const uint8_t* __restrict__ o,
+                                                    const float* __restrict__ mask, int mode, float b, float omb,
+                                                    uint8_t* out, size_t npix) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float S = (float)s[p * 3 + ch] / 255.0f;
+    const float O = (float)o[p * 3 + ch] / 255.0f;
+    float C = S;
+    if (mask) {
+      const float al = mask[p];
+      const float oal = 1.0f - al;
+      const float v = mode == 0 ? (al * S + oal * O) : (oal * S + al * O);
+      C = fminf(fmaxf(v, 0.f), 1.f);
+    }
+    float v = C;
+    if (b >= 0.f && b < 1.f) {
+      const float t0 = b * C;
+      const float t1 = omb * O;
+      v = fminf(fmaxf(t0 + t1, 0.f), 1.f);
+    }
+    out[p * 3 + ch] = (uint8_t)(v * 255.0f);
+  }
+}
+
+hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b, float omb,
+                        uint8_t* out, int n, int hw, hipStream_t st) {
+  const size_t npix = (size_t)n * hw;
+  hipLaunchKernelGGL(blend_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, s, o, mask, mode, b,
+                     omb, out, npix);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Gram matrix G = F F^T / (c*h*w)  (utils.py:80-83) on MFMA.
+// F [n][c][hw] row-major.  One workgroup = one 32x32 tile of G (4 waves = 2x2 16x16 tiles)
+// over a KCH-long slice of hw; slices accumulate with fp32 atomics into G (zeroed first),
+// then a scale pass divides by c*hw.
+template <typename T>
+__global__ __launch_bounds__(256) void gram_kernel(const T* __restrict__ F, int c, int hw, int kchunk,
+                                                   float* __restrict__ G) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.z;
+  const int ti = blockIdx.x / ((c + 31) / 32), tj = blockIdx.x % ((c + 31) / 32);
+  const int i0 = ti * 32 + (wave >> 1) * 16, j0 = tj * 32 + (wave & 1) * 16;
+  const int row = lane & 15, g = lane >> 4;
+  const int ri = min(i0 + row, c - 1), rj = min(j0 + row, c - 1);
+  const T* Fi = F + ((size_t)b * c + ri) * hw;
+  const T* Fj = F + ((size_t)b * c + rj) * hw;
+  const int k0 = blockIdx.y * kchunk, k1 = min(hw, k0 + kchunk);
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (sizeof(T) == 2) {
+    int k = k0;
+    for (; k + 32 <= k1; k += 32) {
+      const uint4 a = *(const uint4*)(Fi + k + 8 * g), bb = *(const uint4*)(Fj + k + 8 * g);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, bb), acc, 0, 0, 0);
+    }
+    for (; k < k1; k += 4) {  // tail (hw % 32): 4 at a time through the f32 MFMA
+      const int kk = k + g;
+      const float av = kk < k1 ? (float)Fi[kk] : 0.f, bv = kk < k1 ? (float)Fj[kk] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+  } else {
+    int k = k0;
+    for (; k + 16 <= k1; k += 16) {
+      const float4 a = *(const float4*)(Fi + k + 4 * g), bb = *(const float4*)(Fj + k + 4 * g);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bb.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bb.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bb.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bb.w, acc, 0, 0, 0);
+    }
+    for (; k < k1; k += 4) {
+      const int kk = k + g;
+      const float av = kk < k1 ? Fi[kk] : 0.f, bv = kk < k1 ? Fj[kk] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+  }
+  // C[row = 4g + r][col = lane&15]: row -> i, col -> j
+  const int j = j0 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * g + r;
+    if (i < c && j < c) atomicAdd(&G[((size_t)b * c + i) * c + j], acc[r]);
+  }
+}
+
+__global__ void gram_scale_kernel(float* G, size_t total, float denom) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < total) G[i] = G[i] / denom;
+}
+
+hipError_t launch_gram(const void* F, int dtype, int n, int c, int hw, float* G, hipStream_t st) {
+  const size_t total = (size_t)n * c * c;
+  hipError_t e = hipMemsetAsync(G, 0, total * sizeof(float), st);
+  if (e != hipSuccess) return e;
+  const int tiles = ((c + 31) / 32) * ((c + 31) / 32);
+  const int kchunk = 2048;
+  dim3 grid(tiles, (hw + kchunk - 1) / kchunk, n);
+  if (dtype == NST_DT_BF16)
+    hipLaunchKernelGGL(gram_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)F, c, hw, kchunk, G);
+  else
+    hipLaunchKernelGGL(gram_kernel<float>, grid, dim3(256), 0, st, (const float*)F, c, hw, kchunk, G);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gram_scale_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, G, total,
+                     (float)((double)c * (double)hw));
+  return hipGetLastError();
+}
+
+}  // namespace nst

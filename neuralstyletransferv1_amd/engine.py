@@ -1,0 +1,177 @@
+"""Engine handle + the nn.Module base class shared by the three stylization nets.
+
+`StylizationNet` keeps the reference's Module surface (`Net()`, `.to(device)`,
+`.load_state_dict(sd, strict=False)`, `.eval()`, `net(X)`), so the reference's callers
+(pipeline.py:597-619 model load, :1449-1485 `model(x_in)`) work unchanged, but its
+parameters are only containers: `forward` packs them once into a libnst_hip handle and
+runs the whole network as hand-written HIP kernels on the caller's stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Tuple
+
+import torch
+from torch import nn
+
+from . import _lib
+from ._lib import NstError, NstParam, check, lib
+
+_DTYPES = {"fp32": _lib.NST_DT_F32, "float32": _lib.NST_DT_F32, "bf16": _lib.NST_DT_BF16, "bfloat16": _lib.NST_DT_BF16}
+
+
+class Engine:
+    """One packed checkpoint on one device (owns an nst_handle and a reusable workspace)."""
+
+    def __init__(self, arch: int, state: Dict[str, torch.Tensor], dtype: str, device: torch.device):
+        if device.type != "cuda":
+            raise NstError("libnst_hip runs on MI355X (cuda) devices only; there is no CPU path")
+        self.arch = arch
+        self.dtype = _DTYPES[dtype]
+        self.device = device
+        host = {k: v.detach().to("cpu", torch.float32).contiguous() for k, v in state.items()}
+        names = list(host.keys())
+        arr = (NstParam * len(names))()
+        self._keep = []
+        for i, k in enumerate(names):
+            b = k.encode()
+            self._keep.append(b)
+            arr[i].name = b
+            arr[i].data = ctypes.cast(host[k].data_ptr(), ctypes.POINTER(ctypes.c_float))
+            arr[i].numel = host[k].numel()
+        h = ctypes.c_void_p()
+        dev_index = device.index if device.index is not None else torch.cuda.current_device()
+        check(lib().nst_create(arch, arr, len(names), self.dtype, dev_index, ctypes.byref(h)), "nst_create")
+        self._h = h
+        self._keep = None
+        self._ws: Optional[torch.Tensor] = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().nst_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def layer_names(self):
+        return [lib().nst_layer_name(self._h, i).decode() for i in range(lib().nst_num_layers(self._h))]
+
+    def profile_begin(self) -> None:
+        check(lib().nst_profile_begin(self._h), "nst_profile_begin")
+
+    def profile_end(self):
+        """-> list of (layer_name, total_ms, launches); call after synchronising the stream."""
+        names = self.layer_names()
+        n = len(names)
+        ms = (ctypes.c_float * n)()
+        cnt = (ctypes.c_int * n)()
+        check(lib().nst_profile_end(self._h, n, ms, cnt), "nst_profile_end")
+        return [(names[i], float(ms[i]), int(cnt[i])) for i in range(n)]
+
+    def output_hw(self, h: int, w: int) -> Tuple[int, int]:
+        oh, ow = ctypes.c_int(), ctypes.c_int()
+        check(lib().nst_output_hw(self._h, h, w, ctypes.byref(oh), ctypes.byref(ow)), "nst_output_hw")
+        return oh.value, ow.value
+
+    def workspace(self, n: int, h: int, w: int) -> torch.Tensor:
+        need = ctypes.c_size_t()
+        check(lib().nst_workspace_bytes(self._h, n, h, w, ctypes.byref(need)), "nst_workspace_bytes")
+        if self._ws is None or self._ws.numel() < need.value:
+            self._ws = torch.empty(max(need.value, 256), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def forward_tensor(self, x: torch.Tensor) -> torch.Tensor:
+        """Raw model tensor in, raw model tensor out: [n,3,h,w] fp32 -> [n,3,oh,ow] fp32."""
+        _lib.require_gpu_tensor(x, "input")
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise NstError(f"expected [N,3,H,W] input, got {tuple(x.shape)}")
+        x = x.to(self.device, torch.float32).contiguous()
+        n, _, h, w = x.shape
+        oh, ow = self.output_hw(h, w)
+        y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=self.device)
+        ws = self.workspace(n, h, w)
+        check(lib().nst_forward(self._h, x.data_ptr(), _lib.NST_IO_F32_NCHW, n, h, w, 0, y.data_ptr(),
+                                _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(), _lib.stream_ptr(self.device)),
+              "nst_forward")
+        return y
+
+    def stylize_u8(self, frames: torch.Tensor, preset: str) -> torch.Tensor:
+        """uint8 RGB frames [n,h,w,3] -> stylized uint8 frames [n,h,w,3] (preset, clamp, truncation fused).
+
+        Output is always the content size: when the net's output size differs
+        (Johnson/ReCoNet with h or w not divisible by 4) the raw output is decoded and
+        bilinearly fitted as pipeline.py:1512-1516 does.
+        """
+        _lib.require_gpu_tensor(frames, "frames")
+        if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
+            raise NstError(f"expected uint8 [N,H,W,3] frames, got {frames.dtype} {tuple(frames.shape)}")
+        if preset not in _lib.PRESETS or preset == "none":
+            raise NstError(f"unknown io_preset {preset!r}")
+        frames = frames.contiguous()
+        n, h, w, _ = frames.shape
+        oh, ow = self.output_hw(h, w)
+        ws = self.workspace(n, h, w)
+        out = torch.empty((n, h, w, 3), dtype=torch.uint8, device=self.device)
+        st = _lib.stream_ptr(self.device)
+        pid = _lib.PRESETS[preset]
+        if (oh, ow) == (h, w):
+            check(lib().nst_forward(self._h, frames.data_ptr(), _lib.NST_IO_U8_NHWC, n, h, w, pid, out.data_ptr(),
+                                    _lib.NST_IO_U8_NHWC, ws.data_ptr(), ws.numel(), st), "nst_forward")
+            return out
+        y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=self.device)
+        check(lib().nst_forward(self._h, frames.data_ptr(), _lib.NST_IO_U8_NHWC, n, h, w, pid, y.data_ptr(),
+                                _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(), st), "nst_forward")
+        check(lib().nst_decode_resize_u8(y.data_ptr(), n, oh, ow, pid, out.data_ptr(), h, w, st),
+              "nst_decode_resize_u8")
+        return out
+
+
+class StylizationNet(nn.Module):
+    """Base of the drop-in TransformerNet / ReCoNet modules (parameters = containers)."""
+
+    ARCH: int = -1
+
+    def __init__(self):
+        super().__init__()
+        # "fp32": parity mode (exact-f32 MFMA); "bf16": throughput mode (bf16 MFMA, fp32 accumulate)
+        self.compute_dtype = "fp32"
+        self._engines: Dict[Tuple[str, int, str], Tuple[tuple, Engine]] = {}
+
+    def _param_key(self) -> tuple:
+        return tuple((p.data_ptr(), p._version) for p in self.state_dict().values())
+
+    def engine(self, device: Optional[torch.device] = None, dtype: Optional[str] = None) -> Engine:
+        """Packed handle for the current parameters (re-packed after load_state_dict / in-place edits)."""
+        if device is None:
+            device = next(self.parameters()).device
+            if device.type != "cuda":
+                raise NstError("move the module (or pass a device) to an MI355X first: there is no CPU path")
+        device = torch.device(device)
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        dtype = dtype or self.compute_dtype
+        if dtype not in _DTYPES:
+            raise NstError(f"compute_dtype must be fp32 or bf16, got {dtype!r}")
+        key = (device.type, device.index, dtype)
+        pk = self._param_key()
+        hit = self._engines.get(key)
+        if hit is not None and hit[0] == pk:
+            return hit[1]
+        eng = Engine(self.ARCH, self.state_dict(), dtype, device)
+        self._engines[key] = (pk, eng)
+        return eng
+
+    def forward(self, X: torch.Tensor) -> torch.Tensor:
+        _lib.require_gpu_tensor(X, "X")
+        return self.engine(X.device).forward_tensor(X)
+
+    def stylize_frames(self, frames_u8: torch.Tensor, io_preset: str) -> torch.Tensor:
+        """Fused frame path: uint8 [N,H,W,3] on device -> stylized uint8 [N,H,W,3]."""
+        _lib.require_gpu_tensor(frames_u8, "frames")
+        return self.engine(frames_u8.device).stylize_u8(frames_u8, io_preset)
+
+    def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate packed handles
+        self._engines = {}
+        return super()._apply(fn, *args, **kwargs)

@@ -1,0 +1,129 @@
+"""GPU post chain of the per-frame loop (pipeline.py:1942-2092) over libnst_hip kernels.
+
+* `LabSmoother`: LAB lightness/chroma EMA (pipeline.py:1942-1978).  Pillow routes RGB<->LAB
+  through LittleCMS (8-bit LAB: L 0..255, a/b signed bytes stored as uint8); both transforms
+  are per-pixel, so each is exactly one 2^24-entry table.  The tables are made ONCE from
+  Pillow itself (the reference's own dependency) and gathered on the GPU per pixel; the EMA
+  state (prev_L, prev_a, prev_b) lives in HBM as fp32.
+* `blend_frames`: mask composite (pipeline.py:2040-2043) + uniform blend (:2087-2092) + the
+  final ToPILImage truncation.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+_LUT_LOCK = threading.Lock()
+_LUTS: Optional[tuple] = None
+
+
+def pillow_lab_luts() -> tuple:
+    """(rgb2lab, lab2rgb) as uint8 [2^24*3] numpy arrays, built from Pillow/LittleCMS."""
+    global _LUTS
+    with _LUT_LOCK:
+        if _LUTS is None:
+            from PIL import Image
+            idx = np.arange(1 << 24, dtype=np.uint32)
+            grid = np.stack([(idx >> 16) & 255, (idx >> 8) & 255, idx & 255], -1).astype(np.uint8)
+            grid = grid.reshape(4096, 4096, 3)
+            rgb2lab = np.ascontiguousarray(np.array(Image.fromarray(grid, "RGB").convert("LAB")).reshape(-1))
+            lab2rgb = np.ascontiguousarray(
+                np.array(Image.frombytes("LAB", (4096, 4096), grid.tobytes()).convert("RGB")).reshape(-1))
+            _LUTS = (rgb2lab, lab2rgb)
+        return _LUTS
+
+
+class LabTables:
+    """Device copy of the two LittleCMS tables (nst_lab handle)."""
+
+    def __init__(self, device: torch.device):
+        rgb2lab, lab2rgb = pillow_lab_luts()
+        h = ctypes.c_void_p()
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        check(lib().nst_lab_create(rgb2lab.ctypes.data, lab2rgb.ctypes.data, idx, ctypes.byref(h)), "nst_lab_create")
+        self._h = h
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().nst_lab_destroy(h)
+            except Exception:
+                pass
+
+
+_TABLES = {}
+
+
+def lab_tables(device: torch.device) -> LabTables:
+    key = (device.type, device.index)
+    if key not in _TABLES:
+        _TABLES[key] = LabTables(device)
+    return _TABLES[key]
+
+
+class LabSmoother:
+    """Stateful LAB EMA over a frame sequence (frames in order, possibly in batches)."""
+
+    def __init__(self, device, smooth_lightness=True, smooth_alpha=0.7, smooth_chroma=False, chroma_alpha=0.85):
+        self.device = torch.device(device)
+        self.sl, self.sc = bool(smooth_lightness), bool(smooth_chroma)
+        # numpy: python-float * float32 array computes in float32 with the scalar cast to float32
+        self.a, self.oma = np.float32(smooth_alpha), np.float32(1.0 - smooth_alpha)
+        self.ca, self.coma = np.float32(chroma_alpha), np.float32(1.0 - chroma_alpha)
+        self.state: Optional[torch.Tensor] = None
+        self.hw = None
+
+    def reset(self):
+        self.state = None
+        self.hw = None
+
+    def __call__(self, frames_u8: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        _lib.require_gpu_tensor(frames_u8, "frames")
+        if not (self.sl or self.sc):
+            return frames_u8
+        frames_u8 = frames_u8.contiguous()
+        n, h, w, _ = frames_u8.shape
+        first = 0
+        if self.state is None or self.hw != (h, w):  # pipeline.py:1104-1113 resets caches on size change
+            self.state = torch.zeros(3 * h * w, dtype=torch.float32, device=self.device)
+            self.hw = (h, w)
+            first = 1
+        if out is None:
+            out = torch.empty_like(frames_u8)
+        t = lab_tables(self.device)
+        check(lib().nst_lab_ema_u8(t._h, frames_u8.data_ptr(), out.data_ptr(), n, h, w, int(self.sl), float(self.a),
+                                   float(self.oma), int(self.sc), float(self.ca), float(self.coma),
+                                   self.state.data_ptr(), first, _lib.stream_ptr(self.device)), "nst_lab_ema_u8")
+        return out
+
+
+def blend_frames(styled_u8: torch.Tensor, orig_u8: torch.Tensor, blend: float = 1.0,
+                 mask: Optional[torch.Tensor] = None, composite_mode: str = "keep") -> torch.Tensor:
+    """[n,h,w,3] uint8 styled/original (+ optional [n,h,w] fp32 alpha) -> [n,h,w,3] uint8."""
+    _lib.require_gpu_tensor(styled_u8, "styled")
+    _lib.require_gpu_tensor(orig_u8, "orig")
+    if styled_u8.shape != orig_u8.shape:
+        raise _lib.NstError(f"styled {tuple(styled_u8.shape)} and original {tuple(orig_u8.shape)} differ")
+    styled_u8, orig_u8 = styled_u8.contiguous(), orig_u8.contiguous()
+    n, h, w, _ = styled_u8.shape
+    mptr = None
+    if mask is not None:
+        mask = mask.to(styled_u8.device, torch.float32).contiguous()
+        if mask.numel() != n * h * w:
+            raise _lib.NstError("mask must be [n,h,w] alpha")
+        mptr = mask.data_ptr()
+    out = torch.empty_like(styled_u8)
+    mode = 0 if composite_mode == "keep" else 1
+    check(lib().nst_blend_u8(styled_u8.data_ptr(), orig_u8.data_ptr(), mptr, mode, float(np.float32(blend)),
+                             float(np.float32(1.0 - blend)), out.data_ptr(), n, h, w,
+                             _lib.stream_ptr(styled_u8.device)), "nst_blend_u8")
+    return out

@@ -1,0 +1,93 @@
+"""Seeded synthetic checkpoints and frames (the reference's .pth weights are not shipped:
+.MISSING_LARGE_BLOBS lists candy/mosaic/rain_princess/udnie/mosaic_reconet).
+
+Weights come from numpy's PCG64 (portable across machines and torch versions) with the
+reference's exact state_dict names/shapes, and are output-calibrated so the stylized
+image spans the io_preset's range instead of collapsing to black:
+  * every conv before an InstanceNorm: N(0, 2/fan_in); bias U(-0.05, 0.05)
+  * InstanceNorm affine: gamma U(0.8, 1.2), beta U(-0.2, 0.2)
+  * the output conv: std chosen so the raw output has std ~TARGET_STD around TARGET_MEAN
+    (Johnson raw/imagenet_255: 127.5 +- 60; NST raw_01: 0.5 +- 0.25; ReCoNet pre-tanh: 0 +- 1).
+Frames: smooth gradients + shapes + low-amplitude noise so InstanceNorm statistics are
+natural-image-like.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import numpy as np
+import torch
+
+ARCHS = ("johnson", "nst", "reconet")
+_OUTPUT_CAL = {"johnson": (127.5, 60.0), "nst": (0.5, 0.25), "reconet": (0.0, 1.0)}
+
+
+def build_module(arch: str):
+    if arch == "johnson":
+        from .transformer_net import TransformerNet
+        return TransformerNet()
+    if arch == "nst":
+        from .transformer_net_nst import TransformerNet
+        return TransformerNet()
+    if arch == "reconet":
+        from .model import ReCoNet
+        return ReCoNet()
+    raise ValueError(f"unknown arch {arch!r}")
+
+
+def _final_conv_name(arch: str) -> str:
+    return {"johnson": "deconv3.conv2d", "nst": "final", "reconet": "decoder.layers.4.layers.0.layers.1"}[arch]
+
+
+def make_state_dict(arch: str, seed: int = 0) -> Dict[str, torch.Tensor]:
+    """Ordered {name: fp32 tensor} with the reference's keys for `arch`."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    template = build_module(arch).state_dict()
+    final = _final_conv_name(arch)
+    mean, std = _OUTPUT_CAL[arch]
+    out: Dict[str, torch.Tensor] = {}
+    for name, t in template.items():
+        shape = tuple(t.shape)
+        if name == final + ".weight":
+            fan_in = shape[1] * shape[2] * shape[3]
+            v = rng.standard_normal(shape) * (std / np.sqrt(fan_in * 0.5))
+        elif name == final + ".bias":
+            v = mean + rng.uniform(-0.02, 0.02, shape) * max(std, 1e-3)
+        elif len(shape) == 4:
+            # Conv2d [out,in,k,k]; ConvTranspose2d [in,out,k,k] (fan_in = out*k*k seen per output)
+            fan_in = shape[1] * shape[2] * shape[3]
+            v = rng.standard_normal(shape) * np.sqrt(2.0 / fan_in)
+        elif name.endswith(".weight"):  # InstanceNorm gamma
+            v = rng.uniform(0.8, 1.2, shape)
+        elif name.endswith(".bias"):
+            is_norm = name.rsplit(".", 1)[0] + ".weight" in template and template[name.rsplit(".", 1)[0] + ".weight"].dim() == 1
+            v = rng.uniform(-0.2, 0.2, shape) if is_norm else rng.uniform(-0.05, 0.05, shape)
+        else:
+            v = np.zeros(shape)
+        out[name] = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32))
+    return out
+
+
+def make_frames(n: int, h: int, w: int, seed: int = 0) -> np.ndarray:
+    """uint8 [n,h,w,3] seeded natural-ish RGB frames."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    yy = np.linspace(0.0, 1.0, h, dtype=np.float32)[:, None]
+    xx = np.linspace(0.0, 1.0, w, dtype=np.float32)[None, :]
+    frames = np.empty((n, h, w, 3), dtype=np.uint8)
+    for f in range(n):
+        img = np.empty((h, w, 3), dtype=np.float32)
+        for c in range(3):
+            a, b, ph = rng.uniform(0.2, 1.0), rng.uniform(0.2, 1.0), rng.uniform(0, 2 * np.pi)
+            img[..., c] = 0.5 + 0.35 * np.sin(2 * np.pi * (a * xx + b * yy) + ph)
+        for _ in range(6):  # discs and boxes
+            cy, cx = rng.uniform(0, 1, 2)
+            r = rng.uniform(0.05, 0.25)
+            col = rng.uniform(0, 1, 3).astype(np.float32)
+            if rng.uniform() < 0.5:
+                m = ((yy - cy) ** 2 + ((xx - cx) * (w / h)) ** 2) < r * r
+            else:
+                m = (np.abs(yy - cy) < r) & (np.abs(xx - cx) * (w / h) < r)
+            img[m] = 0.6 * img[m] + 0.4 * col
+        img += rng.normal(0.0, 0.02, (h, w, 3)).astype(np.float32)
+        frames[f] = np.clip(img * 255.0, 0, 255).astype(np.uint8)
+    return frames
