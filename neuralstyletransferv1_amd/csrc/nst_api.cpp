@@ -377,7 +377,12 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
   h->arch = arch; h->dtype = compute_dtype; h->device = device;
   std::vector<LayerDef> defs;
   build_program(arch, defs, h->prog);
-  const int align = compute_dtype == NST_DT_BF16 ? 32 : 16;
+  // activation channel padding: fp32 chunks hold 4 channels (K step 16); bf16 chunks 8 (K step 32),
+  // and bf16 tiles above 32 channels come in multiples of 64 (48->64, 96->128)
+  auto pad_ch = [&](int c) {
+    if (compute_dtype == NST_DT_F32) return round_up(c, 16);
+    return c <= 32 ? 32 : round_up(c, 64);
+  };
   int rc = NST_OK;
   for (size_t li = 0; li < defs.size() && rc == NST_OK; ++li) {
     Layer Ly;
@@ -385,8 +390,8 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     const LayerDef& d = Ly.d;
     const bool image_in = li == 0;
     const bool final_layer = d.norm.empty();
-    Ly.cinp = image_in ? 4 : round_up(d.cin, align);
-    Ly.coutp = final_layer ? 16 : round_up(d.cout, align);
+    Ly.cinp = image_in ? 4 : pad_ch(d.cin);
+    Ly.coutp = final_layer ? 16 : pad_ch(d.cout);
     const int ink = image_in ? IN_U8_NHWC : IN_ACT;
     const int outk = final_layer ? OUT_U8_NHWC : OUT_ACT;
     Ly.k_main = find_conv_kernel(compute_dtype, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk);
