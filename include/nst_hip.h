@@ -108,6 +108,16 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
 int nst_decode_resize_u8(const float* y, int n, int h, int w, int preset, uint8_t* out, int out_h,
                          int out_w, void* stream);
 
+/*
+ * Multi-model RGB blend (slots A..H, pipeline.py:1872-1879 with parse_blend_weights :502-511):
+ * out01 = sum_i w_i * clamp(decode_i(y_i)), each y_i a raw model output f32 NCHW [n,3,h,w] with its
+ * own io preset, fitted to out_h x out_w (bilinear, align_corners=False); clamp(0,1); truncate to
+ * u8 NHWC.  ys: host array of m (<= 8) device pointers.  Weights are the fp32 values of the slots'
+ * Python floats (the caller validates they sum to 1 +- 1e-6, as the reference does).
+ */
+int nst_blend_models_u8(const float* const* ys, const int* presets, const float* weights, int m, int n,
+                        int h, int w, uint8_t* out, int out_h, int out_w, void* stream);
+
 /* ---- LAB temporal smoothing (pipeline.py:1942-1978) ---- */
 
 /* Upload the two 2^24-entry LittleCMS (Pillow) LUTs: rgb2lab[(r<<16)|(g<<8)|b] = {L,a,b}

@@ -245,7 +245,8 @@ struct Plan {
   size_t partial_floats = 0;
   int out_h = 0, out_w = 0;
   size_t ws_bytes = 0;
-  size_t off_buf[NBUF], off_partial, off_stats;
+  size_t seg_bytes = 0;
+  size_t off_buf[NBUF], off_partial, off_seg, off_stats;
 };
 
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
@@ -284,6 +285,8 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         const int tiles = ((ch + Ly.k_main->th - 1) / Ly.k_main->th) * ((cw + Ly.k_main->tw - 1) / Ly.k_main->tw);
         const size_t pf = (size_t)n * tiles * Ly.coutp * 2;
         if (pf > P.partial_floats) P.partial_floats = pf;
+        const size_t sb = (size_t)n * IN_MAX_SEGMENTS * Ly.coutp * 16;
+        if (sb > P.seg_bytes) P.seg_bytes = sb;
       }
     } else {
       P.ih[i] = P.oh[i] = bh[op.src];
@@ -296,6 +299,8 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
   for (int b = 0; b < NBUF; ++b) { P.off_buf[b] = off; off += align256(P.buf_bytes[b]); }
   P.off_partial = off;
   off += align256(P.partial_floats * 4);
+  P.off_seg = off;
+  off += align256(P.seg_bytes);
   P.off_stats = off;
   for (const Layer& Ly : h->layers) off += align256((size_t)n * Ly.coutp * 8);
   P.ws_bytes = off;
@@ -572,7 +577,7 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     if (e != hipSuccess) { set_error("conv " + Ly.d.conv + " launch: " + hipGetErrorString(e)); return NST_E_HIP; }
     if (!final_out) {
       e = launch_in_finalize(partial, n, p.tiles_x * p.tiles_y, Ly.coutp, (double)p.hconv * (double)p.wconv,
-                             Ly.gamma, Ly.beta, 1e-5f, stats[op.layer], st);
+                             Ly.gamma, Ly.beta, 1e-5f, stats[op.layer], ws + P.off_seg, st);
       if (e != hipSuccess) { set_error(std::string("finalize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
     }
   }
@@ -626,6 +631,31 @@ int nst_decode_resize_u8(const float* y, int n, int h, int w, int preset, uint8_
   hipError_t e = launch_decode_resize_u8(y, n, h, w, pc.dp, pc.dq, pc.dr, pc.ds, pc.dperm, out, out_h, out_w,
                                          (hipStream_t)stream);
   if (e != hipSuccess) { set_error(std::string("decode_resize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+int nst_blend_models_u8(const float* const* ys, const int* presets, const float* weights, int m, int n, int h,
+                        int w, uint8_t* out, int out_h, int out_w, void* stream) {
+  if (!ys || !presets || !weights || !out || m <= 0 || m > NST_MAX_MODELS || n <= 0 || h <= 0 || w <= 0 ||
+      out_h <= 0 || out_w <= 0) {
+    set_error("nst_blend_models_u8: invalid arguments");
+    return NST_E_INVALID;
+  }
+  float dp[NST_MAX_MODELS][3], dq[NST_MAX_MODELS][3], dr[NST_MAX_MODELS][3], ds[NST_MAX_MODELS][3];
+  int perm[NST_MAX_MODELS][3];
+  for (int k = 0; k < m; ++k) {
+    PresetConsts pc;
+    if (!ys[k] || !preset_consts(presets[k], pc)) {
+      set_error("nst_blend_models_u8: bad model output or preset for slot " + std::to_string(k));
+      return NST_E_INVALID;
+    }
+    for (int c = 0; c < 3; ++c) {
+      dp[k][c] = pc.dp[c]; dq[k][c] = pc.dq[c]; dr[k][c] = pc.dr[c]; ds[k][c] = pc.ds[c]; perm[k][c] = pc.dperm[c];
+    }
+  }
+  hipError_t e = launch_blend_models_u8(ys, dp, dq, dr, ds, perm, weights, m, n, h, w, out, out_h, out_w,
+                                        (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("blend_models launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
   return NST_OK;
 }
 

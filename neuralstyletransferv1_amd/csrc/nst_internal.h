@@ -77,15 +77,22 @@ const ConvKernelInfo* find_conv_kernel(int dtype, int ks, int stride, int cinp, 
                                        int out_kind);
 
 // ---- elementwise / reduction launchers (nst_ops.hip) ----
+constexpr int IN_MAX_SEGMENTS = 128;
+int in_finalize_segments(int tiles);
+// seg_ws: n * IN_MAX_SEGMENTS * cstride * 16 bytes of scratch
 hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
                               const float* gamma, const float* beta, float eps, float2* out,
-                              hipStream_t st);
+                              void* seg_ws, hipStream_t st);
 hipError_t launch_residual(int dtype, const void* y, const float2* ys, const void* r,
                            const float2* rs, int r_relu, int relu_out, void* out, int n, int hw,
                            int c, hipStream_t st);
 hipError_t launch_decode_resize_u8(const float* y, int n, int h, int w, const float* p,
                                    const float* q, const float* r, const float* s, const int* perm,
                                    uint8_t* out, int oh, int ow, hipStream_t st);
+constexpr int NST_MAX_MODELS = 8;  // slots A..H (pipeline.py model_b..model_h)
+hipError_t launch_blend_models_u8(const float* const* ys, const float (*dp)[3], const float (*dq)[3],
+                                  const float (*dr)[3], const float (*ds)[3], const int (*perm)[3], const float* wts,
+                                  int m, int n, int h, int w, uint8_t* out, int oh, int ow, hipStream_t st);
 hipError_t launch_lab_ema(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* in,
                           uint8_t* out, int n, int hw, int sl, float a, float oma, int sc, float ca,
                           float coma, float* state, int first, hipStream_t st);

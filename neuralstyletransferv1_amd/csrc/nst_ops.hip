@@ -16,27 +16,29 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // semantics identical to train for IN).  Reduces the conv epilogue's per-tile partial sums
 // in fp64 and emits the affine {scale, shift} the consumer's prologue applies:
 //   y = x*scale + shift, scale = gamma/sqrt(var+eps), shift = beta - mean*scale.
-// grid (n, cstride/64), block 256 = 64 channels x 4 tile phases.
-__global__ __launch_bounds__(256) void in_finalize_kernel(const float* __restrict__ partial, int tiles,
-                                                          int cstride, double count,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float eps,
-                                                          float2* __restrict__ out) {
+// Two deterministic stages (fixed summation order, no atomics):
+//   stage 1  grid (n, cstride/64, nseg), block 256 = 64 channels x 4 tile phases: each block
+//            sums a contiguous segment of tiles in fp64 -> seg[n][s][c] (double2)
+//   stage 2  grid (n, cstride/64), 64 threads: sums the nseg segments, emits {scale, shift}.
+__global__ __launch_bounds__(256) void in_partial_reduce_kernel(const float* __restrict__ partial, int tiles,
+                                                                int cstride, int per_seg,
+                                                                double2* __restrict__ seg) {
   __shared__ double red[4][64][2];
-  const int n = blockIdx.x;
+  const int n = blockIdx.x, s = blockIdx.z;
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl;
+  const int t0 = s * per_seg, t1 = min(tiles, t0 + per_seg);
   double s1 = 0.0, s2 = 0.0;
   if (c < cstride) {
     const float2* p = (const float2*)partial + (size_t)n * tiles * cstride + c;
-    int t = q;
-    for (; t + 12 < tiles; t += 16) {
+    int t = t0 + q;
+    for (; t + 12 < t1; t += 16) {
       const float2 a = p[(size_t)t * cstride], b = p[(size_t)(t + 4) * cstride];
       const float2 d = p[(size_t)(t + 8) * cstride], e = p[(size_t)(t + 12) * cstride];
       s1 += (double)a.x + (double)b.x + (double)d.x + (double)e.x;
       s2 += (double)a.y + (double)b.y + (double)d.y + (double)e.y;
     }
-    for (; t < tiles; t += 4) {
+    for (; t < t1; t += 4) {
       const float2 a = p[(size_t)t * cstride];
       s1 += a.x;
       s2 += a.y;
@@ -48,21 +50,44 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(const float* __restric
   if (q == 0 && c < cstride) {
     s1 = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
     s2 = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
-    const double mean = s1 / count;
-    double var = s2 / count - mean * mean;
-    var = var < 0.0 ? 0.0 : var;
-    const double rstd = 1.0 / sqrt(var + (double)eps);
-    const double scale = (double)gamma[c] * rstd;
-    out[(size_t)n * cstride + c] = make_float2((float)scale, (float)((double)beta[c] - mean * scale));
+    seg[((size_t)n * gridDim.z + s) * cstride + c] = make_double2(s1, s2);
   }
 }
 
+__global__ __launch_bounds__(64) void in_finalize_kernel(const double2* __restrict__ seg, int nseg, int cstride,
+                                                         double count, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps,
+                                                         float2* __restrict__ out) {
+  const int n = blockIdx.x;
+  const int c = blockIdx.y * 64 + threadIdx.x;
+  if (c >= cstride) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < nseg; ++s) {
+    const double2 v = seg[((size_t)n * nseg + s) * cstride + c];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  const double mean = s1 / count;
+  double var = s2 / count - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  const double rstd = 1.0 / sqrt(var + (double)eps);
+  const double scale = (double)gamma[c] * rstd;
+  out[(size_t)n * cstride + c] = make_float2((float)scale, (float)((double)beta[c] - mean * scale));
+}
+
+int in_finalize_segments(int tiles) { return max(1, min(IN_MAX_SEGMENTS, tiles / 64)); }
+
 hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
                               const float* gamma, const float* beta, float eps, float2* out,
-                              hipStream_t st) {
-  dim3 grid(n, (cstride + 63) / 64);
-  hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(256), 0, st, partial, tiles, cstride, count, gamma,
-                     beta, eps, out);
+                              void* seg_ws, hipStream_t st) {
+  const int nseg = in_finalize_segments(tiles);
+  const int per_seg = (tiles + nseg - 1) / nseg;
+  hipLaunchKernelGGL(in_partial_reduce_kernel, dim3(n, (cstride + 63) / 64, nseg), dim3(256), 0, st, partial,
+                     tiles, cstride, per_seg, (double2*)seg_ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(in_finalize_kernel, dim3(n, (cstride + 63) / 64), dim3(64), 0, st, (const double2*)seg_ws,
+                     nseg, cstride, count, gamma, beta, eps, out);
   return hipGetLastError();
 }
 
@@ -216,6 +241,89 @@ hipError_t launch_decode_resize_u8(const float* y, int n, int h, int w, const fl
   const size_t total = (size_t)n * oh * ow;
   hipLaunchKernelGGL(decode_resize_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, y, n, h,
                      w, d, out, oh, ow);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-model RGB blend (pipeline.py:1872-1879): out01 = zeros; out01 += w_i * out_i (in slot order);
+// clamp(0,1); ToPILImage truncation.  out_i = decode_i(y_i) clamped (each slot's own io_preset),
+// fitted bilinearly to the content size like model A's (pipeline.py:1512-1516).
+struct ModelSet {
+  const float* y[NST_MAX_MODELS];
+  DecodeConsts d[NST_MAX_MODELS];
+  float w[NST_MAX_MODELS];
+  int m;
+};
+
+__device__ __forceinline__ void decode_fit(const float* yb, int h, int w, const DecodeConsts& d, int oy, int ox,
+                                           int oh, int ow, float* v) {
+  const size_t plane = (size_t)h * w;
+  if (oh == h && ow == w) {
+    const size_t i = (size_t)oy * w + ox;
+    const float yy[3] = {yb[i], yb[plane + i], yb[2 * plane + i]};
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) v[ch] = decode01(yy, ch, d);
+    return;
+  }
+  const float sh = (float)h / (float)oh, sw = (float)w / (float)ow;
+  float fy = sh * ((float)oy + 0.5f) - 0.5f;
+  fy = fy < 0.f ? 0.f : fy;
+  float fx = sw * ((float)ox + 0.5f) - 0.5f;
+  fx = fx < 0.f ? 0.f : fx;
+  const int y0 = (int)fy, x0 = (int)fx;
+  const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+  const size_t i00 = (size_t)y0 * w + x0, i01 = (size_t)y0 * w + x1, i10 = (size_t)y1 * w + x0, i11 = (size_t)y1 * w + x1;
+  float t00[3], t01[3], t10[3], t11[3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    t00[ch] = yb[ch * plane + i00]; t01[ch] = yb[ch * plane + i01];
+    t10[ch] = yb[ch * plane + i10]; t11[ch] = yb[ch * plane + i11];
+  }
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float c00 = decode01(t00, ch, d), c01 = decode01(t01, ch, d), c10 = decode01(t10, ch, d),
+                c11 = decode01(t11, ch, d);
+    v[ch] = ly0 * (lx0 * c00 + lx1 * c01) + ly1 * (lx0 * c10 + lx1 * c11);
+  }
+}
+
+__global__ __launch_bounds__(256) void blend_models_kernel(ModelSet ms, int n, int h, int w, uint8_t* __restrict__ out,
+                                                           int oh, int ow) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)n * oh * ow;
+  if (i >= total) return;
+  const int ox = (int)(i % ow), oy = (int)((i / ow) % oh), b = (int)(i / ((size_t)ow * oh));
+  float acc[3] = {0.f, 0.f, 0.f};
+  for (int k = 0; k < ms.m; ++k) {
+    float v[3];
+    decode_fit(ms.y[k] + (size_t)b * 3 * h * w, h, w, ms.d[k], oy, ox, oh, ow, v);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float t = ms.w[k] * v[ch];
+      acc[ch] = acc[ch] + t;
+    }
+  }
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) out[i * 3 + ch] = (uint8_t)(fminf(fmaxf(acc[ch], 0.f), 1.f) * 255.0f);
+}
+
+hipError_t launch_blend_models_u8(const float* const* ys, const float (*dp)[3], const float (*dq)[3],
+                                  const float (*dr)[3], const float (*ds)[3], const int (*perm)[3], const float* wts,
+                                  int m, int n, int h, int w, uint8_t* out, int oh, int ow, hipStream_t st) {
+  ModelSet ms;
+  ms.m = m;
+  for (int k = 0; k < m; ++k) {
+    ms.y[k] = ys[k];
+    ms.w[k] = wts[k];
+    for (int c = 0; c < 3; ++c) {
+      ms.d[k].p[c] = dp[k][c]; ms.d[k].q[c] = dq[k][c]; ms.d[k].r[c] = dr[k][c]; ms.d[k].s[c] = ds[k][c];
+      ms.d[k].perm[c] = perm[k][c];
+    }
+  }
+  const size_t total = (size_t)n * oh * ow;
+  hipLaunchKernelGGL(blend_models_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ms, n, h, w, out,
+                     oh, ow);
   return hipGetLastError();
 }
 

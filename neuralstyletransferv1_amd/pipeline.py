@@ -1,0 +1,720 @@
+#!/usr/bin/env python3
+"""pipeline.py — drop-in for the reference's CLI (pipeline.py:2156-2671) on the MI355X engine.
+
+Same flags, defaults and modes (single image / batch images / video) as the reference; the
+per-frame loop (`style_frames`, pipeline.py:527-2122, standard path :1409-1519 + post chain
+:1881-2119) runs batched on the GPU:
+
+    host: PIL decode (thread pool) -> uint8 frames --H2D--> [GPU] preset encode + net forward +
+    decode + clamp + ToPILImage truncation (one nst_forward per model slot) -> multi-model blend
+    -> LAB EMA (LUT, frame order) -> mask composite -> uniform blend --D2H--> host: PIL encode.
+
+Additions: --gpus N (frames round-robin over N GPUs, ordered gather to rank 0 over RCCL),
+--batch B (frames per GPU step), --dtype {fp32,bf16} (fp32 = parity with the reference's
+arithmetic, default; bf16 = throughput mode), --synthetic WxH / --synthetic_frames N (an
+in-memory synthetic frame stream instead of files; config 4 of BASELINE.json).
+
+Out of scope for this engine (rejected with a clear message if requested):
+region blending (--region_*), optical-flow EMA / motion blend (--flow_ema, --motion_blend),
+Magenta (TF-Hub) and Torch7 (OpenCV DNN) backends, LAB multi-model blend (--blend_models_lab),
+mask feathering (needs OpenCV's GaussianBlur; --mask_feather/--mask_feather_pct).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import os
+import re
+import shutil
+import subprocess
+import sys
+import time
+import uuid
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+from typing import Dict, List, Optional
+
+import numpy as np
+
+IO_PRESETS_AUTO = {  # pipeline.py:2518-2523
+    "transformer": "imagenet_255",
+    "torch7": "caffe_bgr",
+    "magenta": "imagenet_01",
+    "reconet": "imagenet_01",
+}
+SLOTS = ["b", "c", "d", "e", "f", "g", "h"]
+
+
+def _log(msg: str) -> None:
+    print(msg, flush=True)
+
+
+# ----------------------------------------------------------------------------- argparse
+def build_parser() -> argparse.ArgumentParser:
+    """Flag-for-flag mirror of pipeline.py:2157-2410 (+ engine flags at the end)."""
+    ap = argparse.ArgumentParser(description="Extract -> Style -> Assemble (with temporal smoothing) on MI355X")
+    ap.add_argument("--input_video", default=None)
+    ap.add_argument("--output_video", default=None)
+    ap.add_argument("--model", required=False)
+    ap.add_argument("--work_dir", default="./_work")
+    ap.add_argument("--fps", type=int, default=None)
+    ap.add_argument("--pre_fps", type=int, default=None)
+    ap.add_argument("--scale", type=int, default=None)
+    ap.add_argument("--canvas", type=str, default=None)
+    ap.add_argument("--image_ext", choices=["png", "jpg"], default="png")
+    ap.add_argument("--jpeg_quality", type=int, default=85)
+    ap.add_argument("--threads", type=int, default=4, help="host threads for frame decode/encode")
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--max_frames", type=int, default=None)
+    ap.add_argument("--device", choices=["cpu", "mps", "cuda"], default="cuda")
+    ap.add_argument("--gpu_memory_limit", type=int, default=32000)
+    ap.add_argument("--inference_res", type=int, default=0)
+    ap.add_argument("--io_preset", choices=["auto", "imagenet_255", "imagenet_01", "tanh", "caffe_bgr", "raw_255", "raw_01"],
+                    default="auto")
+    ap.add_argument("--input_image", type=str)
+    ap.add_argument("--output_image", type=str)
+    ap.add_argument("--input_dir", type=str)
+    ap.add_argument("--output_dir", type=str)
+    ap.add_argument("--pattern", type=str, default=None)
+    ap.add_argument("--keep_ext", action="store_true")
+    ap.add_argument("--output_suffix", type=str, default="")
+    ap.add_argument("--output_prefix", type=str, default="styled_frame")
+    ap.add_argument("--smooth_lightness", action="store_true", default=True)
+    ap.add_argument("--no-smooth_lightness", action="store_false", dest="smooth_lightness")
+    ap.add_argument("--smooth_alpha", type=float, default=0.7)
+    ap.add_argument("--smooth_chroma", action="store_true", default=False)
+    ap.add_argument("--chroma_alpha", type=float, default=0.85)
+    ap.add_argument("--blend", type=float, default=1.0)
+    ap.add_argument("--mask", type=str, default=None)
+    ap.add_argument("--mask_invert", action="store_true")
+    ap.add_argument("--mask_feather", type=int, default=0)
+    ap.add_argument("--mask_dir", type=str, default=None)
+    ap.add_argument("--mask_feather_pct", type=float, default=0.0)
+    ap.add_argument("--mask_autofix", action="store_true", default=True)
+    ap.add_argument("--mask_force_transpose", action="store_true")
+    ap.add_argument("--mask_debug_overlay", action="store_true")
+    ap.add_argument("--mask_debug_alpha", action="store_true")
+    ap.add_argument("--fit_mask_to", choices=["input", "output"], default="input")
+    ap.add_argument("--composite_mode", choices=["keep", "replace"], default="keep")
+    ap.add_argument("--flow_ema", action="store_true", default=False)
+    ap.add_argument("--flow_alpha", type=float, default=0.85)
+    ap.add_argument("--flow_method", choices=["farneback", "dis"], default="dis")
+    ap.add_argument("--flow_downscale", type=int, default=1)
+    ap.add_argument("--model_type", choices=["transformer", "reconet", "magenta", "torch7"], default="transformer")
+    for s in SLOTS:
+        ap.add_argument(f"--model_{s}", type=str, default=None)
+        ap.add_argument(f"--model_{s}_type", choices=["transformer", "reconet", "magenta", "torch7"], default=None)
+        ap.add_argument(f"--io_preset_{s}", choices=["imagenet_255", "imagenet_01", "tanh", "caffe_bgr", "raw_255", "raw_01"],
+                        default=None)
+        ap.add_argument(f"--magenta_style_{s}", type=str, default=None)
+    ap.add_argument("--blend_models_weights", type=str, default=None)
+    ap.add_argument("--blend_models_lab", action="store_true")
+    ap.add_argument("--blend_models_lab_weights", type=str, default=None)
+    for flag, kw in (("--region_mode", dict(type=str, default=None)), ("--region_count", dict(type=int, default=4)),
+                     ("--region_sizes", dict(type=str, default=None)), ("--region_seed", dict(type=int, default=None)),
+                     ("--region_feather", dict(type=int, default=20)), ("--region_assignment", dict(type=str, default="random")),
+                     ("--region_original", dict(type=float, default=0.0)), ("--region_rotate", dict(type=float, default=0.0)),
+                     ("--region_blend_spec", dict(type=str, default=None)), ("--region_scales", dict(type=str, default=None)),
+                     ("--region_optimize", dict(action="store_true")), ("--region_padding", dict(type=int, default=64)),
+                     ("--blend_animate", dict(type=str, default=None)), ("--blend_animate_regions", dict(type=str, default=None)),
+                     ("--scale_animate", dict(type=str, default=None)), ("--scale_animate_regions", dict(type=str, default=None)),
+                     ("--region_morph", dict(type=str, default=None))):
+        ap.add_argument(flag, **kw)
+    ap.add_argument("--magenta_style", type=str, default=None)
+    ap.add_argument("--magenta_model_root", type=str, default="/app/models/magenta")
+    ap.add_argument("--magenta_tile", type=int, default=256)
+    ap.add_argument("--magenta_overlap", type=int, default=32)
+    ap.add_argument("--magenta_target_res", type=int, default=None)
+    ap.add_argument("--motion_blend", action="store_true")
+    ap.add_argument("--clean_frames", action="store_true")
+    ap.add_argument("--clean_work_dir", action="store_true")
+    # ---- engine flags ----
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("GPUS", "1")),
+                    help="frames round-robin over N GPUs (one process per GPU), ordered gather to rank 0")
+    ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="fp32 = parity with the reference arithmetic; bf16 = throughput mode")
+    ap.add_argument("--synthetic", type=str, default=None, help="WxH: stylize an in-memory synthetic frame stream")
+    ap.add_argument("--synthetic_frames", type=int, default=16)
+    ap.add_argument("--no_save", action="store_true", help="do not encode/write outputs (throughput runs)")
+    return ap
+
+
+def reject_out_of_scope(args) -> None:
+    bad = []
+    if args.model_type in ("magenta", "torch7"):
+        bad.append(f"--model_type {args.model_type}")
+    for s in SLOTS:
+        if getattr(args, f"model_{s}") and (getattr(args, f"model_{s}_type") in ("magenta", "torch7")
+                                             or str(getattr(args, f"model_{s}")).lower() in ("magenta",)
+                                             or str(getattr(args, f"model_{s}")).endswith(".t7")):
+            bad.append(f"--model_{s} (magenta/torch7)")
+    if args.region_mode or args.region_optimize:
+        bad.append("--region_mode/--region_optimize")
+    if args.flow_ema or args.motion_blend:
+        bad.append("--flow_ema/--motion_blend")
+    if args.blend_models_lab:
+        bad.append("--blend_models_lab")
+    if args.mask_feather > 0 or args.mask_feather_pct > 0:
+        bad.append("--mask_feather/--mask_feather_pct (OpenCV GaussianBlur)")
+    if args.device != "cuda":
+        bad.append(f"--device {args.device} (this engine runs on MI355X only; there is no CPU path)")
+    if bad:
+        _log("[error] not supported by the MI355X engine: " + ", ".join(bad))
+        sys.exit(2)
+
+
+# ----------------------------------------------------------------------------- host I/O helpers
+def _get_image_with_exif_pil(image_path: str):
+    """pipeline.py:171-187."""
+    from PIL import ExifTags, Image
+    img = Image.open(image_path)
+    exif = getattr(img, "_getexif", lambda: None)()
+    orientation = None
+    if exif:
+        for tag, value in exif.items():
+            if ExifTags.TAGS.get(tag) == "Orientation":
+                orientation = value
+                break
+    if orientation == 3:
+        img = img.rotate(180, expand=True)
+    elif orientation == 6:
+        img = img.rotate(270, expand=True)
+    elif orientation == 8:
+        img = img.rotate(90, expand=True)
+    return img.convert("RGB")
+
+
+def sh(cmd: str, check=True):
+    _log(f"$ {cmd}")
+    r = subprocess.run(cmd, shell=True)
+    if check and r.returncode != 0:
+        _log(f"[sh][ERROR] exit {r.returncode}")
+        sys.exit(r.returncode)
+    return r.returncode
+
+
+def _require_ffmpeg():
+    if shutil.which("ffmpeg") is None:
+        _log("[error] video mode needs ffmpeg on PATH (frame extract/assemble, pipeline.py:384-419, 2128-2150)")
+        sys.exit(2)
+
+
+def extract_frames(input_video: Path, frames_dir: Path, fps, scale, img_ext: str, jpeg_quality: int, canvas_wh=None):
+    """pipeline.py:384-419 (ffmpeg subprocess)."""
+    _require_ffmpeg()
+    frames_dir.mkdir(parents=True, exist_ok=True)
+    vf = []
+    if canvas_wh:
+        cw, ch = canvas_wh
+        vf.append(f"scale={cw}:{ch}:flags=lanczos:force_original_aspect_ratio=decrease")
+        vf.append(f"pad={cw}:{ch}:(ow-iw)/2:(oh-ih)/2:color=black")
+    elif scale:
+        vf.append(f"scale='if(gte(iw,ih),{scale},-2)':'if(gte(ih,iw),{scale},-2)':flags=lanczos")
+    if fps:
+        vf.append(f"fps={fps}")
+    ext = "png" if img_ext.lower() == "png" else "jpg"
+    pattern = frames_dir / f"frame_%04d.{ext}"
+    vfs = f'-vf "{",".join(vf)}" ' if vf else ""
+    sh(f'ffmpeg -y -i "{input_video}" {vfs}-c:v mjpeg -q:v {jpeg_quality} -pix_fmt yuvj420p "{pattern}"')
+
+
+def assemble_video(frames_dir: Path, output_video: Path, in_fps, out_fps, prefix: str):
+    """pipeline.py:2128-2150."""
+    _require_ffmpeg()
+    fr_in = f"-framerate {in_fps}" if in_fps else ""
+    fr_out = f"-r {out_fps}" if out_fps else ""
+    if sorted(frames_dir.glob(f"{prefix}_*.jpg")):
+        pattern = frames_dir / f"{prefix}_%04d.jpg"
+    elif sorted(frames_dir.glob(f"{prefix}_*.png")):
+        pattern = frames_dir / f"{prefix}_%04d.png"
+    else:
+        _log("No styled frames found (jpg/png).")
+        sys.exit(1)
+    sh(f'ffmpeg -y {fr_in} -i "{pattern}" {fr_out} -c:v libx264 -pix_fmt yuv420p "{output_video}"')
+
+
+def parse_blend_weights(weights_str: Optional[str], num_models: int) -> List[float]:
+    """pipeline.py:502-511."""
+    if not weights_str:
+        return [1.0 / num_models] * num_models
+    weights = [float(w) for w in weights_str.split(",")]
+    if len(weights) != num_models:
+        raise ValueError(f"Expected {num_models} weights, got {len(weights)}")
+    if abs(sum(weights) - 1.0) > 1e-6:
+        raise ValueError(f"Weights must sum to 1.0, got {sum(weights):.6f}")
+    return weights
+
+
+def _pct_to_px(pct: float, H: int) -> int:
+    """pipeline.py:278-282."""
+    try:
+        return int(round(max(0.0, float(pct)) * 0.01 * H))
+    except Exception:
+        return 0
+
+
+def load_mask_fit(mask_path: str, target_hw, invert: bool, autofix: bool = True, force_transpose: bool = False) -> np.ndarray:
+    """pipeline.py:284-353 without feathering: float32 HxW alpha in [0,1] (host file decode + NEAREST fit)."""
+    from PIL import Image
+    W_tgt, H_tgt = target_hw[1], target_hw[0]
+    m_img = Image.open(mask_path).convert("L")
+    mw, mh = m_img.size
+    if force_transpose:
+        m_img = m_img.transpose(Image.TRANSPOSE)
+        mw, mh = m_img.size
+    if autofix and (W_tgt != H_tgt):
+        reason = None
+        if (mw, mh) == (H_tgt, W_tgt):
+            reason = "exact-dimension swap"
+        else:
+            def _dist(a, b):
+                return abs(np.log(max(a, 1e-6)) - np.log(max(b, 1e-6)))
+            ar_tgt, ar_mask, ar_sw = float(W_tgt) / float(H_tgt), float(mw) / float(mh), float(H_tgt) / float(W_tgt)
+            if _dist(ar_mask, ar_sw) + 1e-6 < _dist(ar_mask, ar_tgt):
+                reason = "aspect-ratio closer to swapped"
+        if reason:
+            _log(f"[mask][autofix] {Path(mask_path).name}: {reason}; applying Image.TRANSPOSE")
+            m_img = m_img.transpose(Image.TRANSPOSE)
+    m_img = m_img.resize((W_tgt, H_tgt), Image.Resampling.NEAREST)
+    m = np.array(m_img, dtype=np.uint8)
+    if invert:
+        m = 255 - m
+    return m.astype(np.float32) / 255.0
+
+
+def _detect_transformer_type(checkpoint_path: str) -> str:
+    """pipeline.py:72-79: NST_Train checkpoints have 'down1.' keys."""
+    import torch
+    state = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+    if isinstance(state, dict) and "state_dict" in state and isinstance(state["state_dict"], dict):
+        state = state["state_dict"]
+    return "nst" if any(k.startswith("down1.") for k in state.keys()) else "original"
+
+
+def _load_checkpoint_compat(model, ckpt_path: str) -> None:
+    """pipeline.py:554-569 (weights_only loads only: never unpickle arbitrary objects)."""
+    import torch
+    state = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+    if isinstance(state, dict) and "state_dict" in state and isinstance(state["state_dict"], dict):
+        state = state["state_dict"]
+    drop = ("running_mean", "running_var", "num_batches_tracked")
+    state = {k: v for k, v in state.items() if not any(t in k for t in drop)}
+    missing, unexpected = model.load_state_dict(state, strict=False)
+    _log(f">> load_state_dict: missing={len(missing)} unexpected={len(unexpected)}")
+
+
+def load_model(path: str, model_type: str, device, dtype: str, slot: str = "A", auto_nst: bool = True):
+    """Model construction + load (pipeline.py:597-619; slots B..H always use the Johnson class for
+    type transformer, :651-661 — kept)."""
+    if model_type == "reconet":
+        from .model import ReCoNet
+        model, arch = ReCoNet(), "reconet"
+    else:
+        arch = _detect_transformer_type(path) if auto_nst else "original"
+        if arch == "nst":
+            from .transformer_net_nst import TransformerNet
+            _log(f"[model] Detected NST_Train architecture for {path}")
+        else:
+            from .transformer_net import TransformerNet
+        model = TransformerNet()
+    _load_checkpoint_compat(model, path)
+    model = model.to(device).eval()
+    model.compute_dtype = dtype
+    _log(f"[backend] {slot}: type={model_type} path={path} device={device} arch={arch} dtype={dtype}")
+    return model, arch
+
+
+# ----------------------------------------------------------------------------- the frame loop
+class FrameSource:
+    """Frames by index: files (PIL decode, optional --inference_res LANCZOS) or a synthetic stream."""
+
+    def __init__(self, files: Optional[List[Path]] = None, synthetic=None, infer_res: int = 0):
+        self.files = files
+        self.synthetic = synthetic  # (n, h, w)
+        self.infer_res = infer_res
+
+    def __len__(self):
+        return len(self.files) if self.files is not None else self.synthetic[0]
+
+    def size(self, i: int):
+        if self.files is None:
+            return (self.synthetic[1], self.synthetic[2])
+        from PIL import Image
+        with Image.open(self.files[i]) as im:
+            w, h = im.size
+        return (h, w)
+
+    def load(self, i: int):
+        """-> (original uint8 HxWx3, model-input uint8 hxwx3)."""
+        if self.files is None:
+            from .synthetic import make_frames
+            f = make_frames(1, self.synthetic[1], self.synthetic[2], seed=10_000 + i)[0]
+            return f, f
+        from PIL import Image
+        pil_rgb = Image.open(self.files[i]).convert("RGB")
+        pil_src = pil_rgb
+        if self.infer_res > 0:  # pipeline.py:1089-1097
+            w0, h0 = pil_rgb.size
+            m0 = max(w0, h0)
+            if m0 > self.infer_res:
+                r = self.infer_res / float(m0)
+                pil_src = pil_rgb.resize((int(round(w0 * r)), int(round(h0 * r))), Image.Resampling.LANCZOS)
+        a = np.asarray(pil_rgb, dtype=np.uint8)
+        return a, (a if pil_src is pil_rgb else np.asarray(pil_src, dtype=np.uint8))
+
+
+def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: str, image_ext_out: str, device_str: str,
+                 threads: int, stride: int, max_frames: Optional[int], smooth_lightness: bool, smooth_alpha: float,
+                 jpeg_quality: int, io_preset: str, smooth_chroma: bool = False, chroma_alpha: float = 0.85,
+                 blend: float = 1.0, image_mode: bool = False, save_map: Optional[Dict[int, str]] = None,
+                 rank: int = 0, world: int = 1):
+    """Same signature/behaviour as pipeline.py:527-2122 (in-scope paths), GPU-batched."""
+    import torch
+    from PIL import Image
+
+    from .frames import plan_groups, run_sharded
+    from .postproc import LabSmoother, blend_frames
+
+    dev = torch.device("cuda", rank if world > 1 else torch.cuda.current_device())
+    torch.cuda.set_device(dev)
+    blend = float(max(0.0, min(1.0, blend)))
+    save_map = save_map or {}
+
+    # ---- models: A + optional B..H (RGB blend, pipeline.py:1872-1879) ----
+    slots = []
+    model_a, arch_a = load_model(str(model_path), args.model_type, dev, args.dtype, "A")
+    if arch_a == "nst" and io_preset in ("auto", "raw_255", "imagenet_255"):  # pipeline.py:610-614
+        _log(f"[model] Auto-switching io_preset from '{io_preset}' to 'raw_01' for NST_Train model")
+        io_preset = "raw_01"
+    slots.append((model_a, io_preset))
+    for s in SLOTS:
+        p = getattr(args, f"model_{s}", None)
+        if not p:
+            continue
+        t = getattr(args, f"model_{s}_type", None) or args.model_type
+        ip = getattr(args, f"io_preset_{s}", None) or io_preset
+        m, _ = load_model(p, t, dev, args.dtype, s.upper(), auto_nst=False)
+        slots.append((m, ip))
+    weights = parse_blend_weights(args.blend_models_weights, len(slots)) if len(slots) > 1 else [1.0]
+    _log(f"[cfg] io_preset={io_preset} models={len(slots)} weights={weights} dtype={args.dtype} gpus={world} batch={args.batch}")
+    _log(f">> smoothing: {smooth_lightness}  alpha={smooth_alpha}  |  blend={blend}")
+
+    # ---- frames ----
+    if args.synthetic:
+        m = re.match(r"^\s*(\d+)\s*[xX]\s*(\d+)\s*$", args.synthetic)
+        if not m:
+            _log(f"[error] --synthetic expects WxH, got {args.synthetic}")
+            sys.exit(2)
+        n_syn = int(args.synthetic_frames)
+        if max_frames:
+            n_syn = min(n_syn, int(max_frames))
+        src = FrameSource(synthetic=(n_syn, int(m.group(2)), int(m.group(1))))
+        names = [f"frame_{i + 1:04d}" for i in range(n_syn)]
+    else:
+        files = sorted(p for p in frames_dir.iterdir() if p.is_file() and p.name.startswith("frame_")
+                       and p.suffix.lower() in {".png", ".jpg", ".jpeg"})
+        if stride and stride > 1:
+            files = files[::stride]
+        if max_frames:
+            files = files[:max_frames]
+        if not files:
+            _log(f"[error] No frames found to style in: {frames_dir}")
+            sys.exit(1)
+        src = FrameSource(files=files, infer_res=int(getattr(args, "inference_res", 0) or 0))
+        names = [p.stem for p in files]
+    _log(f"[debug] found {len(src)} staged frame(s)")
+
+    if getattr(args, "mask_dir", None) and not getattr(args, "mask", None) and not args.synthetic:
+        md = Path(args.mask_dir)
+        missing = [nm for nm in names if not (md / f"mask_{nm.split('_')[-1]}.png").exists()]
+        if missing and len(missing) == len(names):
+            _log(f"[mask][ERROR] --mask_dir set to {md} but no masks like mask_0001.png were found.")
+            sys.exit(2)
+        if missing:
+            _log(f"[mask][WARN] {len(missing)}/{len(names)} mask(s) missing under {md}.")
+
+    pool = ThreadPoolExecutor(max_workers=max(1, threads))
+    sizes = [src.size(i) for i in range(len(src))]
+    groups = plan_groups(sizes, world, max(1, args.batch))
+    need_orig = blend < 1.0 or bool(args.mask or args.mask_dir)
+
+    # the reference fits model A's output to the content size; with --inference_res the model
+    # input is smaller than the content
+    def stylize(idx: List[int]):
+        if not idx:
+            h0, w0 = sizes[0]
+            return torch.empty((0, h0, w0, 6 if need_orig else 3), dtype=torch.uint8, device=dev)
+        loaded = list(pool.map(src.load, idx))
+        orig = torch.from_numpy(np.stack([a for a, _ in loaded])).to(dev, non_blocking=True)
+        xin = orig if loaded[0][1] is loaded[0][0] else torch.from_numpy(np.stack([b for _, b in loaded])).to(dev)
+        h0, w0 = orig.shape[1], orig.shape[2]
+        if len(slots) == 1 and xin.shape[1:3] == orig.shape[1:3]:
+            styled = slots[0][0].stylize_frames(xin, slots[0][1])
+        else:
+            styled = _blend_slots(slots, weights, xin, h0, w0)
+        return torch.cat([styled, orig], dim=3) if need_orig else styled
+
+    lab = LabSmoother(dev, smooth_lightness, smooth_alpha, smooth_chroma, chroma_alpha)
+    mask_cache = {}
+    pending = []
+    t_start = time.perf_counter()
+    done = [0]
+
+    def consume(g: List[int], full):
+        styled = full[..., :3].contiguous() if need_orig else full
+        h0, w0 = styled.shape[1], styled.shape[2]
+        if lab.hw is not None and lab.hw != (h0, w0):
+            _log(f"[size][reset] frame dims changed {lab.hw} -> {(h0, w0)}; resetting EMA caches")
+            lab.reset()
+        styled = lab(styled)  # frame order within and across groups
+        if need_orig:
+            orig = full[..., 3:].contiguous()
+            alpha = _masks_for(g, h0, w0)
+            styled = blend_frames(styled, orig, blend, alpha, args.composite_mode)
+        host = styled.cpu().numpy()
+        if not args.no_save:
+            for j, f in enumerate(g):
+                pending.append(pool.submit(_save, host[j], f))
+        done[0] += len(g)
+        el = time.perf_counter() - t_start
+        _log(f"[frame] {done[0]}/{len(src)} styled  ({done[0] / max(el, 1e-9):.2f} frames/s)")
+
+    def _masks_for(g, h0, w0):
+        mfile_global = getattr(args, "mask", None)
+        if not mfile_global and not getattr(args, "mask_dir", None):
+            return None
+        ms = []
+        any_mask = False
+        for f in g:
+            mfile = mfile_global
+            if not mfile and not args.synthetic:
+                cand = Path(args.mask_dir) / f"mask_{names[f].split('_')[-1]}.png"
+                mfile = str(cand) if cand.exists() else None
+            if mfile is None:
+                # no mask for this frame -> no composite (pipeline.py:1985-1993): the alpha that
+                # leaves S unchanged is 1 for 'keep' and 0 for 'replace'
+                ident = 1.0 if args.composite_mode == "keep" else 0.0
+                ms.append(np.full((h0, w0), ident, np.float32))
+                continue
+            any_mask = True
+            key = (mfile, h0, w0)
+            if key not in mask_cache:
+                mask_cache[key] = load_mask_fit(mfile, (h0, w0), bool(args.mask_invert), bool(args.mask_autofix),
+                                                bool(args.mask_force_transpose))
+            ms.append(mask_cache[key])
+        if not any_mask:
+            return None
+        return torch.from_numpy(np.stack(ms)).to(dev)
+
+    def _save(img: np.ndarray, f: int):
+        out_img = Image.fromarray(img)
+        save_as_jpg = image_ext_out.lower() == "jpg"
+        if image_mode and (f + 1) in save_map:
+            out_path = Path(save_map[f + 1])
+            out_path.parent.mkdir(parents=True, exist_ok=True)
+            save_as_jpg = out_path.suffix.lower() in (".jpg", ".jpeg")
+        else:
+            idx_str = names[f].split("_")[-1]
+            base = frames_dir if frames_dir is not None else Path(args.work_dir)
+            base.mkdir(parents=True, exist_ok=True)
+            out_path = (base / f"{output_prefix}_{idx_str}").with_suffix(".jpg" if save_as_jpg else ".png")
+        if save_as_jpg:
+            out_img.save(out_path, format="JPEG", quality=int(jpeg_quality))
+        else:
+            out_img.save(out_path)
+        return str(out_path)
+
+    run_sharded(groups, world, rank, stylize, consume)
+    for p in pending:
+        p.result()
+    pool.shutdown()
+    if rank == 0:
+        el = time.perf_counter() - t_start
+        _log(f"Styled {len(src)}/{len(src)} frames in {el:.2f}s ({len(src) / max(el, 1e-9):.2f} frames/s)")
+
+
+def _blend_slots(slots, weights, xin, h0, w0):
+    """Raw f32 outputs of every slot -> nst_blend_models_u8 (decode, fit, weighted sum, clamp, truncation)."""
+    import ctypes
+
+    import torch
+
+    from . import _lib
+    from ._lib import check, lib
+    dev = xin.device
+    ys, presets = [], []
+    for model, preset in slots:
+        eng = model.engine(dev)
+        n, h, w, _ = xin.shape
+        oh, ow = eng.output_hw(h, w)
+        y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=dev)
+        ws = eng.workspace(n, h, w)
+        check(lib().nst_forward(eng._h, xin.data_ptr(), _lib.NST_IO_U8_NHWC, n, h, w, _lib.PRESETS[preset],
+                                y.data_ptr(), _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(),
+                                _lib.stream_ptr(dev)), "nst_forward")
+        ys.append(y)
+        presets.append(_lib.PRESETS[preset])
+    shapes = {tuple(y.shape) for y in ys}
+    if len(shapes) != 1:
+        raise _lib.NstError(f"model outputs differ in size {shapes}: the reference cannot blend them either")
+    m = len(ys)
+    out = torch.empty((xin.shape[0], h0, w0, 3), dtype=torch.uint8, device=dev)
+    yp = (ctypes.c_void_p * m)(*[y.data_ptr() for y in ys])
+    pr = (ctypes.c_int * m)(*presets)
+    wt = (ctypes.c_float * m)(*[float(np.float32(w)) for w in weights])
+    n, _, oh, ow = ys[0].shape
+    check(lib().nst_blend_models_u8(yp, pr, wt, m, n, oh, ow, out.data_ptr(), h0, w0, _lib.stream_ptr(dev)),
+          "nst_blend_models_u8")
+    return out
+
+
+# ----------------------------------------------------------------------------- main
+def _parse_canvas(s):
+    if not s:
+        return None
+    m = re.match(r"^\s*(\d+)\s*[xX]\s*(\d+)\s*$", str(s))
+    if not m:
+        _log(f"[canvas][ERROR] Expected WxH (e.g., 1920x1080), got: {s}")
+        sys.exit(2)
+    return int(m.group(1)), int(m.group(2))
+
+
+def prepare(args):
+    """Mode decision + staging (pipeline.py:2430-2606). Returns (frames_dir, model_path, save_map, image_mode, video_mode)."""
+    canvas_wh = _parse_canvas(getattr(args, "canvas", None))
+    for k in ("input_video", "output_video", "input_image", "output_image", "input_dir", "output_dir"):
+        v = getattr(args, k, None)
+        if v is not None and str(v).strip() == "":
+            setattr(args, k, None)
+    if getattr(args, "pattern", None) in (None, ""):
+        args.pattern = f"*.{args.image_ext}"
+    image_single = bool(args.input_image) and bool(args.output_image)
+    image_batch = bool(args.input_dir) and bool(args.output_dir)
+    video = bool(args.input_video) and bool(args.output_video)
+    synthetic = bool(args.synthetic)
+    if (image_single or image_batch) and video:
+        _log("Provide exactly one of: (input_video & output_video) OR (input_image & output_image) OR (input_dir & output_dir).")
+        sys.exit(2)
+    if not (image_single or image_batch or video or synthetic):
+        _log("Specify (input_video & output_video) OR (input_image & output_image) OR (input_dir & output_dir).")
+        sys.exit(2)
+    if not args.model:
+        _log("[error] --model is required")
+        sys.exit(2)
+    model_path = Path(args.model).resolve()
+    if model_path.suffix.lower() == ".t7":
+        args.model_type = "torch7"
+    if args.io_preset == "auto":
+        args.io_preset = IO_PRESETS_AUTO.get(args.model_type, "imagenet_01")
+        _log(f"[auto] io_preset resolved to '{args.io_preset}' for backend '{args.model_type}'")
+    reject_out_of_scope(args)
+    save_map: Dict[int, str] = {}
+    base_work = Path(args.work_dir).resolve()
+    if synthetic:
+        return None, model_path, save_map, False, False
+    work_dir = base_work / f"job_{uuid.uuid4().hex[:8]}" if (image_single or image_batch) else base_work
+    frames_dir = work_dir / "frames"
+    if frames_dir.exists() and video:
+        shutil.rmtree(frames_dir, ignore_errors=True)
+    frames_dir.mkdir(parents=True, exist_ok=True)
+    if video:
+        in_v = Path(args.input_video).resolve()
+        if args.pre_fps:
+            tmp = work_dir / f"prefps_{args.pre_fps}.mp4"
+            _require_ffmpeg()
+            sh(f'ffmpeg -y -i "{in_v}" -vf fps={args.pre_fps} -c:v libx264 -pix_fmt yuv420p "{tmp}"')
+            in_v = tmp
+        extract_frames(in_v, frames_dir, args.fps if not args.pre_fps else None, args.scale, args.image_ext,
+                       args.jpeg_quality, canvas_wh)
+    elif image_single:
+        src = Path(args.input_image).resolve()
+        ext = src.suffix.lower() if src.suffix.lower() in (".png", ".jpg", ".jpeg") else ".png"
+        dst = frames_dir / f"frame_0001{ext}"
+        pil = _get_image_with_exif_pil(str(src))
+        if ext in (".jpg", ".jpeg"):
+            pil.save(dst, format="JPEG", quality=max(1, min(95, int(args.jpeg_quality))))
+        else:
+            pil.save(dst)
+        save_map[1] = str(Path(args.output_image).resolve())
+    else:
+        in_files = sorted(glob.glob(os.path.join(args.input_dir, args.pattern)))
+        if not in_files:
+            _log(f"No files matched: {args.input_dir}/{args.pattern}")
+            sys.exit(2)
+        Path(args.output_dir).mkdir(parents=True, exist_ok=True)
+        for i, f in enumerate(in_files, start=1):
+            src = Path(f).resolve()
+            ext = src.suffix.lower()
+            dst = frames_dir / f"frame_{i:04d}{ext}"
+            pil = _get_image_with_exif_pil(str(src))
+            if ext in (".jpg", ".jpeg"):
+                pil.save(dst, format="JPEG", quality=max(1, min(95, int(args.jpeg_quality))))
+            else:
+                pil.save(dst)
+            base = src.stem
+            out_ext = ext if args.keep_ext else (".jpg" if args.image_ext.lower() == "jpg" else ".png")
+            m = re.match(r"^frame_(\d+)$", base)
+            out_stem = f"{args.output_prefix}_{m.group(1)}" if m else f"{base}{args.output_suffix or ''}"
+            save_map[i] = str((Path(args.output_dir) / f"{out_stem}{out_ext}").resolve())
+    return frames_dir, model_path, save_map, (image_single or image_batch), video
+
+
+def _worker(rank: int, world: int, argv: List[str], port: int, prep):
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", rank))
+    try:
+        args = build_parser().parse_args(argv)
+        frames_dir, model_path, save_map, image_mode, _ = prep
+        _run_style(args, frames_dir, model_path, save_map, image_mode, rank, world)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_style(args, frames_dir, model_path, save_map, image_mode, rank=0, world=1):
+    return style_frames(args, frames_dir, model_path, output_prefix="styled_frame", image_ext_out=args.image_ext,
+                        device_str=args.device, threads=args.threads, stride=args.stride, max_frames=args.max_frames,
+                        smooth_lightness=args.smooth_lightness, smooth_alpha=args.smooth_alpha,
+                        jpeg_quality=args.jpeg_quality, io_preset=args.io_preset, smooth_chroma=args.smooth_chroma,
+                        chroma_alpha=args.chroma_alpha, blend=args.blend, image_mode=image_mode, save_map=save_map,
+                        rank=rank, world=world)
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = build_parser().parse_args(argv)
+    prep = prepare(args)
+    frames_dir, model_path, save_map, image_mode, video = prep
+    # re-parse inside workers with the resolved preset/model type
+    resolved = argv + ["--io_preset", args.io_preset, "--model_type", args.model_type]
+    if args.gpus > 1:
+        import socket
+
+        import torch.multiprocessing as mp
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        mp.start_processes(_worker, args=(args.gpus, resolved, port, prep), nprocs=args.gpus, start_method="spawn")
+    else:
+        _run_style(args, frames_dir, model_path, save_map, image_mode)
+    if video:
+        in_fps = int(args.pre_fps) if args.pre_fps else (int(args.fps) if args.fps else None)
+        out_fps = int(args.fps) if (args.pre_fps and args.fps) else None
+        assemble_video(frames_dir, Path(args.output_video).resolve(), in_fps, out_fps, prefix="styled_frame")
+        _log(f"\n Done. Styled video at: {Path(args.output_video).resolve()}")
+    elif image_mode:
+        written = sum(1 for v in save_map.values() if Path(v).exists())
+        _log(f"Wrote {written}/{len(save_map)} image(s)")
+    if args.clean_frames and frames_dir is not None:
+        for pat in ("frame_*.png", "frame_*.jpg", "styled_frame_*.png", "styled_frame_*.jpg"):
+            for p in frames_dir.glob(pat):
+                p.unlink(missing_ok=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

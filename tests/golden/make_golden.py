@@ -102,6 +102,20 @@ def main():
     np.savez_compressed(os.path.join(HERE, "gram_2x48x16x24.npz"), F=Fm.numpy(), G=G.numpy())
     print("gram ok", tuple(G.shape))
 
+    # the reference CLI's flag names (pipeline.py:2157-2410), for the CLI-parity test
+    import json
+    import re
+    src = open(os.path.join(REF, "pipeline.py")).read()
+    flags = sorted(set(re.findall(r'add_argument\(\s*"(--[A-Za-z0-9_-]+)"', src)))
+    with open(os.path.join(HERE, "reference_flags.json"), "w") as f:
+        json.dump({"source": "pipeline.py:2157-2410 add_argument names (extracted by tests/golden/make_golden.py)",
+                   "flags": flags}, f, indent=0)
+    # mask fixtures: copies of the reference's own input/masks data files
+    import shutil
+    os.makedirs(os.path.join(HERE, "masks"), exist_ok=True)
+    for m in ("center_circle.png", "gradient_horizontal.png"):
+        shutil.copyfile(os.path.join(REF, "input", "masks", m), os.path.join(HERE, "masks", m))
+
 
 if __name__ == "__main__":
     main()

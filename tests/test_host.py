@@ -1,0 +1,127 @@
+"""Host-side logic on CPU: CLI parity, sharding + ordered gather (gloo, world 2), env adapter."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from neuralstyletransferv1_amd import frames as F
+from neuralstyletransferv1_amd import pipeline as P
+from neuralstyletransferv1_amd import run_videos as RV
+
+
+def test_cli_has_every_reference_flag():
+    ref = json.load(open(os.path.join(GOLDEN, "reference_flags.json")))["flags"]
+    ours = {a for act in P.build_parser()._actions for a in act.option_strings}
+    missing = [f for f in ref if f not in ours]
+    assert not missing, missing
+
+
+def test_cli_defaults_match_reference():
+    a = P.build_parser().parse_args([])
+    assert (a.smooth_lightness, a.smooth_alpha, a.blend, a.io_preset, a.image_ext, a.jpeg_quality, a.threads,
+            a.composite_mode, a.fit_mask_to, a.model_type, a.chroma_alpha) == (
+        True, 0.7, 1.0, "auto", "png", 85, 4, "keep", "input", "transformer", 0.85)
+
+
+@pytest.mark.parametrize("extra", [["--region_mode", "grid"], ["--flow_ema"], ["--model_type", "magenta"],
+                                   ["--device", "cpu"], ["--mask_feather", "5"], ["--blend_models_lab"]])
+def test_out_of_scope_requests_fail_loudly(extra, tmp_path):
+    args = P.build_parser().parse_args(["--model", "x.pth", "--synthetic", "64x48"] + extra)
+    with pytest.raises(SystemExit) as e:
+        P.prepare(args)
+    assert e.value.code == 2
+
+
+def test_parse_blend_weights():
+    assert P.parse_blend_weights(None, 4) == [0.25] * 4
+    assert P.parse_blend_weights("0.5,0.5", 2) == [0.5, 0.5]
+    with pytest.raises(ValueError):
+        P.parse_blend_weights("0.5,0.6", 2)
+    with pytest.raises(ValueError):
+        P.parse_blend_weights("1.0", 2)
+
+
+def test_plan_groups_and_round_robin_shard():
+    sizes = [(4, 4)] * 5 + [(8, 8)] * 3
+    g = F.plan_groups(sizes, world=2, batch=2)
+    assert g == [[0, 1, 2, 3], [4], [5, 6, 7]]
+    assert F.shard(g[0], 2, 0) == [0, 2] and F.shard(g[0], 2, 1) == [1, 3]
+    assert F.shard([4], 2, 1) == []
+
+
+def _gather_worker(rank, world, port, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    seen = []
+    groups = F.plan_groups([(2, 3)] * 7 + [(5, 1)] * 2, world, batch=2)
+
+    def stylize(idx):
+        if not idx:
+            return torch.empty((0, 2, 3, 3), dtype=torch.uint8)
+        h, w = (2, 3) if idx[0] < 7 else (5, 1)
+        return torch.stack([torch.full((h, w, 3), f, dtype=torch.uint8) for f in idx])
+
+    def consume(g, full):
+        seen.append((g, [int(full[j].flatten()[0]) for j in range(full.shape[0])]))
+
+    F.run_sharded(groups, world, rank, stylize, consume)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, seen))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ordered_gather_gloo(world):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    seen0 = res[0]
+    assert all(not res[r] for r in range(1, world))
+    flat = [f for g, vals in seen0 for f in g]
+    assert flat == list(range(9))
+    for g, vals in seen0:
+        assert vals == g  # frame j of each group is the frame itself, in order
+
+
+def test_run_videos_env_mapping(monkeypatch):
+    for k in list(os.environ):
+        if k.startswith(("MODEL_", "IO_PRESET", "BLEND", "GPUS", "SMOOTH", "MAX_FRAMES")):
+            monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("MODEL_A", "/m/candy.pth")
+    monkeypatch.setenv("MODEL_B", "mosaic")
+    monkeypatch.setenv("MODEL_B_TYPE", "pytorch")
+    monkeypatch.setenv("IO_PRESET", "raw_255")
+    monkeypatch.setenv("BLEND_WEIGHTS", "0.7,0.3")
+    monkeypatch.setenv("GPUS", "4")
+    monkeypatch.setenv("MAX_FRAMES", "10")
+    cmd = RV.build_pipeline_cmd("/in/clip.mp4")
+    s = " ".join(cmd)
+    assert "--model /m/candy.pth --model_type transformer --io_preset raw_255" in s
+    assert "--model_b /app/models/pytorch/mosaic.pth --model_b_type transformer" in s
+    assert "--blend_models_weights 0.7,0.3" in s and "--gpus 4" in s and "--max_frames 10" in s
+    assert "--smooth_alpha 0.65" in s and "--blend 0.9" in s and "--scale 720" in s
+    args = P.build_parser().parse_args(cmd[3:])  # the pipeline accepts the adapter's command line
+    assert args.gpus == 4 and args.model_b.endswith("mosaic.pth")
+
+
+def test_mask_fit_matches_oracle():
+    from oracle import nst_oracle as O
+    for m in ("center_circle.png", "gradient_horizontal.png"):
+        path = os.path.join(GOLDEN, "masks", m)
+        for hw, inv in (((96, 128), False), ((128, 96), True), ((50, 50), False)):
+            ours = P.load_mask_fit(path, hw, inv)
+            ref = O.load_mask_fit(path, hw, inv)[..., 0]
+            assert np.array_equal(ours, ref)
