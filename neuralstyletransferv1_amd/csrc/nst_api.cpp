@@ -23,14 +23,14 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 const ConvKernelInfo* conv_table_bf16(int* count);
 const ConvKernelInfo* conv_table_f32(int* count);
 
-const ConvKernelInfo* find_conv_kernel(int dtype, int ks, int stride, int cinp, int bn, int in_kind,
+const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind) {
   int count = 0;
   const ConvKernelInfo* t = dtype == NST_DT_BF16 ? conv_table_bf16(&count) : conv_table_f32(&count);
   for (int i = 0; i < count; ++i) {
     const ConvKernelInfo& k = t[i];
-    if (k.ks == ks && k.stride == stride && k.cinp == cinp && k.bn == bn && k.in_kind == in_kind &&
-        k.out_kind == out_kind)
+    if (k.mode == mode && k.ks == ks && k.stride == stride && k.cinp == cinp && k.bn == bn &&
+        k.in_kind == in_kind && k.out_kind == out_kind)
       return &k;
   }
   return nullptr;
@@ -50,10 +50,13 @@ struct LayerDef {
 struct Layer {
   LayerDef d;
   int cinp, coutp;
+  int mode = MODE_STD;                     // conv_kernel mapping chosen for this layer
   const ConvKernelInfo* k_main = nullptr;  // in/out kind of the activation path
   const ConvKernelInfo* k_alt = nullptr;   // image layer: F32 NCHW input; final: F32 NCHW output
   void* wpk = nullptr;
   float* bias = nullptr;
+  void* wpk_rev = nullptr;   // MODE_XSHIFT: channel-reversed rows (caffe_bgr decode), see pack_weights
+  float* bias_rev = nullptr;
   float* gamma = nullptr;
   float* beta = nullptr;
 };
@@ -166,37 +169,97 @@ uint16_t f32_to_bf16_rne(float f) {
   return (uint16_t)(u >> 16);
 }
 
-// Pack conv weights into MFMA A-fragment order: [cblk][step (nstep+1, last zero)][n-subtile][lane][cpc]
+// Pack conv weights into MFMA A-fragment order: [cblk][step (nstep_pack; >= nstep zero)][n-subtile][lane][cpc]
 // lane l = (g = l>>4, q = l&15): output channel of row q in subtile t (wave wn, local t):
 //   cb*bn + wn*nsub*16 + 4*nsub*(q>>2) + 4*t + (q&3);  K chunk 4*step+g -> (tap, channel chunk).
-std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W, int coutp) {
+//
+// MODE_PHASE: n-subtile tg = phase*nsub + t (phase (a,b) = (tg/nsub)>>1, &1), tap = (ty,tx) of the
+//   phase's 2x2 window on the source grid; the weight is the sum of the 3x3 taps that land on that
+//   source pixel: nearest-x2 (a=0: ty0<-{k0}, ty1<-{k1,k2}; a=1: ty0<-{k0,k1}, ty1<-{k2}), or the one
+//   ConvTranspose2d(s2,p1) tap (a=0: ty0<-k1; a=1: ty0<-k2, ty1<-k0), per axis.
+// MODE_XSHIFT: row q = 3*s + c (q < 15) is output channel perm[c] at x-shift s; tap (dy, u) over
+//   13 columns carries W[.][.][dy][u - s] when 0 <= u - s < 9.
+std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W, int coutp,
+                                bool reverse_channels = false) {
   const int ncblk = coutp / k.bn;
   const size_t per_frag = 64 * (size_t)k.cpc;
-  std::vector<float> out((size_t)ncblk * (k.nstep + 1) * k.nsubt * per_frag, 0.f);
-  auto w_at = [&](int co, int ci, int dy, int dx) -> float {
-    if (d.convT)  // ConvTranspose2d weight [cin][cout][kh][kw], flipped
+  std::vector<float> out((size_t)ncblk * k.nstep_pack * k.nsubt * per_frag, 0.f);
+  auto w_at = [&](int co, int ci, int dy, int dx) -> double {
+    if (d.convT)  // ConvTranspose2d weight [cin][cout][kh][kw], flipped for the zero-inserted conv
       return W[(((size_t)ci * d.cout + co) * d.ks + (d.ks - 1 - dy)) * d.ks + (d.ks - 1 - dx)];
     return W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
+  };
+  // phase taps: kernel indices (along one axis) that fall on window position t of phase a
+  auto phase_taps = [&](int a, int t, int* ks_out) -> int {
+    if (d.convT) {  // unflipped ConvTranspose indices
+      if (a == 0) { if (t == 0) { ks_out[0] = 1; return 1; } return 0; }
+      ks_out[0] = t == 0 ? 2 : 0;
+      return 1;
+    }
+    if (a == 0) {
+      if (t == 0) { ks_out[0] = 0; return 1; }
+      ks_out[0] = 1; ks_out[1] = 2; return 2;
+    }
+    if (t == 0) { ks_out[0] = 0; ks_out[1] = 1; return 2; }
+    ks_out[0] = 2;
+    return 1;
   };
   for (int cb = 0; cb < ncblk; ++cb)
     for (int s = 0; s < k.nstep; ++s)
       for (int tg = 0; tg < k.nsubt; ++tg)
         for (int lane = 0; lane < 64; ++lane) {
-          const int wn = tg / k.nsub, t = tg % k.nsub, q = lane & 15, g = lane >> 4;
-          const int co = cb * k.bn + wn * k.nsub * 16 + 4 * k.nsub * (q >> 2) + 4 * t + (q & 3);
+          const int q = lane & 15, g = lane >> 4;
           const int i = 4 * s + g;
-          float* dst = &out[((((size_t)cb * (k.nstep + 1) + s) * k.nsubt + tg) * 64 + lane) * k.cpc];
-          if (i >= k.nchunk || co >= d.cout) continue;
+          float* dst = &out[((((size_t)cb * k.nstep_pack + s) * k.nsubt + tg) * 64 + lane) * k.cpc];
+          if (i >= k.nchunk) continue;
           const int tap = i / k.nch, c = i % k.nch;
-          const int dy = tap / k.kp, dxp = tap % k.kp;
-          for (int j = 0; j < k.cpc; ++j) {
-            int dx, ci;
-            if (k.pair) { dx = 2 * dxp + (j >= 4 ? 1 : 0); ci = j & 3; }
-            else { dx = dxp; ci = c * k.cpc + j; }
-            if (dx < d.ks && ci < d.cin) dst[j] = w_at(co, ci, dy, dx);
+          if (k.mode == MODE_PHASE) {
+            const int ph = tg / k.nsub, t = tg % k.nsub;
+            const int co = cb * k.bn + 4 * k.nsub * (q >> 2) + 4 * t + (q & 3);
+            if (co >= d.cout) continue;
+            int ky[2], kx[2];
+            const int ny = phase_taps(ph >> 1, tap >> 1, ky), nx = phase_taps(ph & 1, tap & 1, kx);
+            for (int j = 0; j < k.cpc; ++j) {
+              const int ci = c * k.cpc + j;
+              if (ci >= d.cin) continue;
+              double sum = 0.0;
+              for (int yy = 0; yy < ny; ++yy)
+                for (int xx = 0; xx < nx; ++xx)
+                  sum += d.convT ? (double)W[(((size_t)ci * d.cout + co) * d.ks + ky[yy]) * d.ks + kx[xx]]
+                                 : (double)W[(((size_t)co * d.cin + ci) * d.ks + ky[yy]) * d.ks + kx[xx]];
+              dst[j] = (float)sum;
+            }
+          } else if (k.mode == MODE_XSHIFT) {
+            if (q >= 15) continue;
+            const int sft = q / 3, ch = q % 3;
+            const int co = reverse_channels ? 2 - ch : ch;
+            const int dy = tap / k.kp, u = tap % k.kp, dx = u - sft;
+            if (dx < 0 || dx >= d.ks || co >= d.cout) continue;
+            for (int j = 0; j < k.cpc; ++j) {
+              const int ci = c * k.cpc + j;
+              if (ci < d.cin) dst[j] = (float)w_at(co, ci, dy, dx);
+            }
+          } else {
+            const int wn = tg / k.nsub, t = tg % k.nsub;
+            const int co = cb * k.bn + wn * k.nsub * 16 + 4 * k.nsub * (q >> 2) + 4 * t + (q & 3);
+            if (co >= d.cout) continue;
+            const int dy = tap / k.kp, dxp = tap % k.kp;
+            for (int j = 0; j < k.cpc; ++j) {
+              int dx, ci;
+              if (k.pair) { dx = 2 * dxp + (j >= 4 ? 1 : 0); ci = j & 3; }
+              else { dx = dxp; ci = c * k.cpc + j; }
+              if (dx < d.ks && ci < d.cin) dst[j] = (float)w_at(co, ci, dy, dx);
+            }
           }
         }
   return out;
+}
+
+// bias rows of an x-shift layer: row q = 3*s + c -> bias of output channel (perm) c
+std::vector<float> xshift_bias(const float* b, bool reverse_channels) {
+  std::vector<float> r(16, 0.f);
+  for (int q = 0; q < 15; ++q) r[q] = b[reverse_channels ? 2 - q % 3 : q % 3];
+  return r;
 }
 
 int upload(const void* host, size_t bytes, void** dev) {
@@ -251,6 +314,17 @@ struct Plan {
 
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 
+// workgroup tiles of a conv launch: phase mode tiles the SOURCE grid (each source pixel -> 4 outputs)
+void tile_grid(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx, int* ty) {
+  if (k.mode == MODE_PHASE) {
+    *tx = (sw + k.tw - 1) / k.tw;
+    *ty = (sh + k.th - 1) / k.th;
+  } else {
+    *tx = (ow + k.tw - 1) / k.tw;
+    *ty = (oh + k.th - 1) / k.th;
+  }
+}
+
 Plan make_plan(const nst_handle* h, int n, int H, int W) {
   Plan P;
   const size_t esz = h->dtype == NST_DT_BF16 ? 2 : 4;
@@ -282,7 +356,9 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         bh[op.dst] = ch; bw[op.dst] = cw;
         const size_t bytes = (size_t)n * ch * cw * Ly.coutp * esz;
         if (bytes > P.buf_bytes[op.dst]) P.buf_bytes[op.dst] = bytes;
-        const int tiles = ((ch + Ly.k_main->th - 1) / Ly.k_main->th) * ((cw + Ly.k_main->tw - 1) / Ly.k_main->tw);
+        int ttx, tty;
+        tile_grid(*Ly.k_main, sh, sw, ch, cw, &ttx, &tty);
+        const int tiles = ttx * tty;
         const size_t pf = (size_t)n * tiles * Ly.coutp * 2;
         if (pf > P.partial_floats) P.partial_floats = pf;
         const size_t sb = (size_t)n * IN_MAX_SEGMENTS * Ly.coutp * 16;
@@ -399,9 +475,21 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     Ly.coutp = final_layer ? 16 : pad_ch(d.cout);
     const int ink = image_in ? IN_U8_NHWC : IN_ACT;
     const int outk = final_layer ? OUT_U8_NHWC : OUT_ACT;
-    Ly.k_main = find_conv_kernel(compute_dtype, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk);
-    if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk);
-    if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW);
+    // preferred mapping: sub-pixel phases for x2 up-convs, x-shift rows for the 3-channel output
+    // conv; the plain mapping is the fallback for shapes without a compiled variant
+    const bool up = d.axis_mode == AX_REFLECT_UP2 || d.axis_mode == AX_ZINSERT;
+    std::vector<int> modes;
+    if (up) modes.push_back(MODE_PHASE);
+    if (final_layer && d.cout == 3) modes.push_back(MODE_XSHIFT);
+    modes.push_back(MODE_STD);
+    for (int mode : modes) {
+      Ly.k_main = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk);
+      Ly.k_alt = nullptr;
+      if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk);
+      if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW);
+      if (Ly.k_main && (!(image_in || final_layer) || Ly.k_alt)) { Ly.mode = mode; break; }
+      Ly.k_main = nullptr;
+    }
     if (!Ly.k_main || ((image_in || final_layer) && !Ly.k_alt)) {
       set_error("no compiled conv kernel for layer " + d.conv + " (ks " + std::to_string(d.ks) + " stride " +
                 std::to_string(d.stride) + " cin " + std::to_string(Ly.cinp) + " cout " + std::to_string(Ly.coutp) + ")");
@@ -416,19 +504,26 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
       if ((rc = get(d.norm + ".weight", d.cout, &gm)) != NST_OK) break;
       if ((rc = get(d.norm + ".bias", d.cout, &bt)) != NST_OK) break;
     }
-    std::vector<float> pk = pack_weights(*Ly.k_main, d, W, Ly.coutp);
-    if (compute_dtype == NST_DT_BF16) {
-      std::vector<uint16_t> pb(pk.size());
-      for (size_t i = 0; i < pk.size(); ++i) pb[i] = f32_to_bf16_rne(pk[i]);
-      rc = upload(pb.data(), pb.size() * 2, &Ly.wpk);
-    } else {
-      rc = upload(pk.data(), pk.size() * 4, &Ly.wpk);
-    }
-    if (rc != NST_OK) break;
+    auto upload_packed = [&](const std::vector<float>& pk, void** dst) -> int {
+      if (compute_dtype == NST_DT_BF16) {
+        std::vector<uint16_t> pb(pk.size());
+        for (size_t i = 0; i < pk.size(); ++i) pb[i] = f32_to_bf16_rne(pk[i]);
+        return upload(pb.data(), pb.size() * 2, dst);
+      }
+      return upload(pk.data(), pk.size() * 4, dst);
+    };
+    if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) break;
     std::vector<float> bp(Ly.coutp, 0.f), gp(Ly.coutp, 0.f), btp(Ly.coutp, 0.f);
     for (int c = 0; c < d.cout; ++c) {
       bp[c] = b[c];
       if (gm) { gp[c] = gm[c]; btp[c] = bt[c]; }
+    }
+    if (Ly.mode == MODE_XSHIFT) {
+      // rows carry (shift, channel); a second, channel-reversed packing serves caffe_bgr's BGR decode
+      bp = xshift_bias(b, false);
+      std::vector<float> br = xshift_bias(b, true);
+      if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp, true), &Ly.wpk_rev)) != NST_OK) break;
+      if ((rc = upload(br.data(), br.size() * 4, (void**)&Ly.bias_rev)) != NST_OK) break;
     }
     if ((rc = upload(bp.data(), bp.size() * 4, (void**)&Ly.bias)) != NST_OK) break;
     if (!final_layer) {
@@ -450,6 +545,8 @@ void nst_destroy(nst_handle* h) {
   DeviceGuard guard(h->device);
   for (Layer& Ly : h->layers) {
     if (Ly.wpk) (void)hipFree(Ly.wpk);
+    if (Ly.wpk_rev) (void)hipFree(Ly.wpk_rev);
+    if (Ly.bias_rev) (void)hipFree(Ly.bias_rev);
     if (Ly.bias) (void)hipFree(Ly.bias);
     if (Ly.gamma) (void)hipFree(Ly.gamma);
     if (Ly.beta) (void)hipFree(Ly.beta);
@@ -535,6 +632,14 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     p.cs = image_in ? 3 : Ly.cinp;
     p.axis_mode = Ly.d.axis_mode;
     p.pad = Ly.d.axis_mode == AX_ZINSERT ? 1 : Ly.d.pad;
+    if (Ly.mode == MODE_PHASE) {
+      // source-grid halo of one pixel; nearest-x2 reflect(1) == clamp on the source grid,
+      // ConvTranspose reads zeros past the edge
+      p.axis_mode = Ly.d.axis_mode == AX_ZINSERT ? AX_ZERO : AX_CLAMP;
+      p.pad = 1;
+      p.ph_off[0] = Ly.d.axis_mode == AX_ZINSERT ? 1 : 0;
+      p.ph_off[1] = 1;
+    }
     p.pre = Ly.d.pre;
     p.in_norm = op.in_norm >= 0 ? stats[op.in_norm] : nullptr;
     p.in_relu = op.in_norm >= 0 ? 1 : 0;
@@ -548,6 +653,10 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     p.dec_tanh = (h->arch == NST_ARCH_RECONET && final_out) ? 1 : 0;
     p.wpk = Ly.wpk;
     p.bias = Ly.bias;
+    if (Ly.mode == MODE_XSHIFT && final_out && y_fmt == NST_IO_U8_NHWC && pc.dperm[0] == 2) {
+      p.wpk = Ly.wpk_rev;  // decode channel c from model channel 2-c (caffe_bgr)
+      p.bias = Ly.bias_rev;
+    }
     p.hconv = P.ch[i];
     p.wconv = P.cw[i];
     p.oh = P.oh[i];
@@ -557,8 +666,7 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     p.out = final_out ? y : bufs[op.dst];
     p.cout_real = Ly.d.cout;
     p.cout_stride = Ly.coutp;
-    p.tiles_x = (p.ow + k->tw - 1) / k->tw;
-    p.tiles_y = (p.oh + k->th - 1) / k->th;
+    tile_grid(*k, p.hs, p.ws, p.oh, p.ow, &p.tiles_x, &p.tiles_y);
     p.n_cblk = Ly.coutp / k->bn;
     p.partial = final_out ? nullptr : partial;
     dim3 grid(p.tiles_x * p.tiles_y, n * p.n_cblk);

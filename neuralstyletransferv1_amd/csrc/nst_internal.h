@@ -32,7 +32,12 @@ enum OutKind { OUT_ACT = 0, OUT_U8_NHWC = 1, OUT_F32_NCHW = 2 };
 //   AX_ZERO_PREREFLECT  ReflectionPad2d(pre) then Conv2d(padding)  transformer_net_nst.py:74,99,76
 //   AX_ZINSERT          ConvTranspose2d(3, s2, p1, op1) as a conv over the zero-inserted grid
 //                                                                  transformer_net_nst.py:50-53
-enum AxisMode { AX_REFLECT = 0, AX_REFLECT_UP2 = 1, AX_ZERO = 2, AX_ZERO_PREREFLECT = 3, AX_ZINSERT = 4 };
+//   AX_CLAMP            clamp to the source grid (phase-mode nearest-x2 convs: reflect-pad(1) of the
+//                       upsampled grid == clamp on the source grid)
+enum AxisMode { AX_REFLECT = 0, AX_REFLECT_UP2 = 1, AX_ZERO = 2, AX_ZERO_PREREFLECT = 3, AX_ZINSERT = 4, AX_CLAMP = 5 };
+
+// conv_kernel mappings (see conv_impl.h)
+enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2 };
 
 struct ConvParams {
   // input
@@ -61,19 +66,21 @@ struct ConvParams {
   float dec_p[3], dec_q[3], dec_r[3], dec_s[3];
   int dec_perm[3];
   int dec_tanh;  // apply tanh to the raw output first (ReCoNet ConvTanhLayer, model.py:77-80)
+  int ph_off[2];  // MODE_PHASE: LDS row/col offset of sub-pixel phase 0/1 ({0,1} nearest-up, {1,1} ConvTranspose)
 };
 
 // Static description of one compiled conv kernel instantiation.
 struct ConvKernelInfo {
   int dtype;  // NST_DT_*
+  int mode;   // ConvMode
   int ks, stride, cinp, bn, th, tw, wm, wn, in_kind, out_kind;
   // derived
-  int pair, nch, cpc, kp, nchunk, nstep, nsubt, nsub, lds_bytes;
+  int pair, nch, cpc, kp, nchunk, nstep, nstep_pack, nsubt, nsub, lds_bytes;
   void (*launch)(const ConvParams&, dim3 grid, hipStream_t);
 };
 
 // Look up a compiled instantiation; nullptr if the combination was not built.
-const ConvKernelInfo* find_conv_kernel(int dtype, int ks, int stride, int cinp, int bn, int in_kind,
+const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind);
 
 // ---- elementwise / reduction launchers (nst_ops.hip) ----
