@@ -12,7 +12,7 @@ const ConvKernelInfo* conv_table_bf16(int* count) {
       E(B, SD, 9, 1, 4, 32, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),    // Johnson/NST conv1 (frames)
       E(B, SD, 9, 1, 4, 32, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),   // Johnson/NST conv1 (tensor API)
       E(B, SD, 3, 2, 32, 64, 8, 16, 4, 1, IN_ACT, OUT_ACT),       // conv2 / down2
-      E(B, SD, 3, 2, 64, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),      // conv3 / down3 / ReCoNet enc1
+      E(B, SD, 3, 2, 64, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),      // conv3 / down3 / ReCoNet enc1
       E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // residual trunk
       E(B, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT),      // deconv1 / up1 / ReCoNet dec2 (phases)
       E(B, PH, 3, 1, 64, 32, 8, 16, 1, 4, IN_ACT, OUT_ACT),       // deconv2 / up2 (phases)
@@ -21,11 +21,11 @@ const ConvKernelInfo* conv_table_bf16(int* count) {
       // ReCoNet (48/96/192 channels, bf16 padded to 64/128/192)
       E(B, SD, 9, 1, 4, 64, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
       E(B, SD, 9, 1, 4, 64, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),
-      E(B, SD, 3, 2, 128, 192, 8, 16, 2, 2, IN_ACT, OUT_ACT),
+      E(B, SD, 3, 2, 128, 192, 4, 16, 2, 2, IN_ACT, OUT_ACT),
       E(B, SD, 3, 1, 192, 192, 8, 16, 2, 2, IN_ACT, OUT_ACT),
       E(B, PH, 3, 1, 192, 128, 2, 16, 1, 4, IN_ACT, OUT_ACT),
-      E(B, XS, 9, 1, 64, 16, 4, 80, 4, 1, IN_ACT, OUT_U8_NHWC),
-      E(B, XS, 9, 1, 64, 16, 4, 80, 4, 1, IN_ACT, OUT_F32_NCHW),
+      E(B, SD, 9, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
+      E(B, SD, 9, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

@@ -5,7 +5,7 @@
 namespace nst {
 typedef float F;
 #define E(...) ConvInst<__VA_ARGS__>::info()
-constexpr int SD = MODE_STD, PH = MODE_PHASE, XS = MODE_XSHIFT;
+constexpr int SD = MODE_STD, PH = MODE_PHASE;
 const ConvKernelInfo* conv_table_f32(int* count) {
   static const ConvKernelInfo table[] = {
       //  T  MODE KS S CINP BN TH TW WM WN  IN           OUT
@@ -16,8 +16,8 @@ const ConvKernelInfo* conv_table_f32(int* count) {
       E(F, SD, 3, 1, 128, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),
       E(F, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT),
       E(F, PH, 3, 1, 64, 32, 4, 16, 1, 4, IN_ACT, OUT_ACT),
-      E(F, XS, 9, 1, 32, 16, 4, 80, 4, 1, IN_ACT, OUT_U8_NHWC),
-      E(F, XS, 9, 1, 32, 16, 4, 80, 4, 1, IN_ACT, OUT_F32_NCHW),
+      E(F, SD, 9, 1, 32, 16, 4, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
+      E(F, SD, 9, 1, 32, 16, 4, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
       // ReCoNet (48/96/192 channels: multiples of 16, no padding in fp32)
       E(F, SD, 9, 1, 4, 48, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
       E(F, SD, 9, 1, 4, 48, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),

@@ -90,7 +90,11 @@ struct ConvCfg {
   static constexpr int CPC = 16 / (int)sizeof(T);                                 // channels per 16-B chunk
   static constexpr bool PAIR = (MODE == MODE_STD) && (sizeof(T) == 2) && (CINP == 4);  // chunk = 2 px x 4 ch
   static constexpr int NCH = PAIR ? 1 : CINP / CPC;                               // chunks per LDS entry
-  static constexpr int EB = 16 * NCH;                                             // bytes per LDS entry
+  // LDS entry stride: channel-chunked entries (NCH % 4 == 0) are padded to NCH+2 chunks.  A stride
+  // of 2*odd chunks puts the 16 lanes of every ds_read_b128 lane group ({0-3,12-15,20-27}, ...:
+  // 8 pixels of lane group g and 8 of g^1) on 16 distinct bank slots with no XOR swizzle (pixel
+  // parity alternates with g's chunk parity), so operand addresses are lane base + immediates.
+  static constexpr int EB = ((NCH % 4) == 0 ? NCH + 2 : NCH) * 16;               // bytes per LDS entry
   static constexpr int NXS = 5;                                                   // x-shifts (XSHIFT)
   static constexpr int KP = PAIR ? (KS + 1) / 2 : (MODE == MODE_XSHIFT ? KS + NXS - 1 : KS);  // x-taps per row
   static constexpr int NTAP = MODE == MODE_PHASE ? 4 : KS * KP;
@@ -246,9 +250,16 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
   int* rowmap = (int*)(smem + C::MAP_OFF);
   int* colmap = rowmap + C::LH;
   if constexpr (INK == IN_ACT) {
+    // byte offsets within the frame (host guarantees a frame is < 2 GiB), -1 = zero padding
+    const int pix_bytes = p.cs * (int)sizeof(T);
     for (int t = tid; t < C::LH + LW; t += 256) {
-      if (t < C::LH) rowmap[t] = map_axis(vy0 + t, p.hs, p.axis_mode, p.pre);
-      else colmap[t - C::LH] = map_axis(vx0 + t - C::LH, p.ws, p.axis_mode, p.pre);
+      if (t < C::LH) {
+        const int sy = map_axis(vy0 + t, p.hs, p.axis_mode, p.pre);
+        rowmap[t] = sy < 0 ? -1 : sy * p.ws * pix_bytes;
+      } else {
+        const int sx = map_axis(vx0 + t - C::LH, p.ws, p.axis_mode, p.pre);
+        colmap[t - C::LH] = sx < 0 ? -1 : sx * pix_bytes;
+      }
     }
     __syncthreads();
   }
@@ -278,18 +289,24 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
       constexpr bool FIXED_CHUNK = (256 % NCH) == 0;
       const int c_fixed = tid % NCH;
       const char* img = (const char*)p.in + (size_t)n * p.hs * p.ws * p.cs * sizeof(T);
+      // a FIXED_CHUNK thread applies the same CPC channels' IN constants to every item
+      float2 nmc[C::CPC];
+      if (FIXED_CHUNK && p.in_norm != nullptr) {
+#pragma unroll
+        for (int j = 0; j < C::CPC; ++j) nmc[j] = p.in_norm[(size_t)n * p.cs + c_fixed * C::CPC + j];
+      }
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
         const int it = tid + k * 256;
         const int e = it / NCH, c = FIXED_CHUNK ? c_fixed : it - e * NCH;
         int ly, lx;
         bool ok = entry_xy(e, ly, lx) && it < NITEMS;
-        const int sy = ok ? rowmap[ly] : -1;
-        const int sx = ok ? colmap[lx] : -1;
-        ok = ok && sy >= 0 && sx >= 0;
+        const int ro = ok ? rowmap[ly] : -1;
+        const int co = ok ? colmap[lx] : -1;
+        ok = ok && ro >= 0 && co >= 0;
         live[k] = ok;
         raw[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (ok) raw[k] = *(const uint4*)(img + (((size_t)sy * p.ws + sx) * p.cs + c * C::CPC) * sizeof(T));
+        if (ok) raw[k] = *(const uint4*)(img + (unsigned)(ro + co + c * 16));
       }
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
@@ -297,8 +314,9 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
         if (it < NITEMS) {
           const int e = it / NCH, c = FIXED_CHUNK ? c_fixed : it - e * NCH;
           uint4 v = raw[k];
-          if (live[k] && p.in_norm != nullptr) v = norm_chunk<T>(v, p.in_norm + (size_t)n * p.cs + c * C::CPC, p.in_relu);
-          *(uint4*)(smem + e * EB + 16 * (c ^ swz<NCH>(e))) = v;
+          if (live[k] && p.in_norm != nullptr)
+            v = norm_chunk<T>(v, FIXED_CHUNK ? nmc : p.in_norm + (size_t)n * p.cs + c * C::CPC, p.in_relu);
+          *(uint4*)(smem + e * EB + 16 * c) = v;
         }
       }
     } else {
@@ -359,29 +377,28 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     // rows (runtime) x x-taps x chunk groups (unrolled): step s = row*RS + dx*NCH4 + cg reads
     // chunk 4*cg + g of tap (row, dx); PF divides RS, so the ring slot of each position is static
     constexpr int NCH4 = C::NCH4, KPR = C::KPR, RS = C::RS;
+    // per-lane LDS byte base of each m-subtile (lane group g's chunk folded in); per row one add,
+    // per tap / chunk group only immediate offsets
+    int lbase[MSUB];
+#pragma unroll
+    for (int m = 0; m < MSUB; ++m) lbase[m] = base[m] * EB + 16 * g;
     for (int row = 0; row < C::ROWS; ++row) {
-      const int rowoff = MODE == MODE_PHASE ? (phy + row) * LWP + phx : row * LWP;
+      const int rowoff = (MODE == MODE_PHASE ? (phy + row) * LWP + phx : row * LWP) * EB;
+      const char* rp[MSUB];
+#pragma unroll
+      for (int m = 0; m < MSUB; ++m) rp[m] = smem + lbase[m] + rowoff;
 #pragma unroll
       for (int dx = 0; dx < KPR; ++dx) {
-        int xo;  // constant column offset of x-tap dx in this mode's LDS column order
-        if constexpr (MODE == MODE_XSHIFT) xo = (dx % C::NXS) * W5 + dx / C::NXS;
-        else if constexpr (S == 2) xo = (dx & 1) * HALF + (dx >> 1);
-        else xo = dx;
-        int addr[MSUB], sw[MSUB];
-#pragma unroll
-        for (int m = 0; m < MSUB; ++m) {
-          const int e = base[m] + rowoff + xo;
-          sw[m] = swz<NCH>(e);
-          addr[m] = e * EB;
-        }
+        // constant column offset of x-tap dx in this mode's LDS column order
+        const int xo = MODE == MODE_XSHIFT ? (dx % C::NXS) * W5 + dx / C::NXS
+                                           : (S == 2 ? (dx & 1) * HALF + (dx >> 1) : dx);
 #pragma unroll
         for (int cg = 0; cg < NCH4; ++cg) {
           const int pos = dx * NCH4 + cg;  // position within the row (compile-time after unrolling)
           const int slot = pos % PF;
-          const int c = 4 * cg + g;
           uint4 b[MSUB];
 #pragma unroll
-          for (int m = 0; m < MSUB; ++m) b[m] = *(const uint4*)(smem + addr[m] + 16 * (c ^ sw[m]));
+          for (int m = 0; m < MSUB; ++m) b[m] = *(const uint4*)(rp[m] + xo * EB + 64 * cg);
           mfma_step(a_ring[slot], b);
           const int s = row * RS + pos;
 #pragma unroll
