@@ -16,8 +16,8 @@ const ConvKernelInfo* conv_table_bf16(int* count) {
       E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // residual trunk
       E(B, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT),      // deconv1 / up1 / ReCoNet dec2 (phases)
       E(B, PH, 3, 1, 64, 32, 8, 16, 1, 4, IN_ACT, OUT_ACT),       // deconv2 / up2 (phases)
-      E(B, XS, 9, 1, 32, 16, 8, 80, 4, 1, IN_ACT, OUT_U8_NHWC),   // deconv3 / final (frames, x-shift)
-      E(B, XS, 9, 1, 32, 16, 8, 80, 4, 1, IN_ACT, OUT_F32_NCHW),  // deconv3 / final (tensor API)
+      E(B, XS, 9, 1, 32, 16, 8, 80, 8, 1, IN_ACT, OUT_U8_NHWC),   // deconv3 / final (frames, x-shift, 8 waves)
+      E(B, XS, 9, 1, 32, 16, 8, 80, 8, 1, IN_ACT, OUT_F32_NCHW),  // deconv3 / final (tensor API)
       // ReCoNet (48/96/192 channels, bf16 padded to 64/128/192)
       E(B, SD, 9, 1, 4, 64, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
       E(B, SD, 9, 1, 4, 64, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),

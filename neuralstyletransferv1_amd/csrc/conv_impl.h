@@ -141,7 +141,9 @@ struct ConvCfg {
   static constexpr int LDS_ALLOC0 = MAP_OFF + MAP_BYTES;
   static constexpr int LDS_ALLOC = LDS_ALLOC0 > RED_BYTES ? LDS_ALLOC0 : RED_BYTES;
   static_assert(!ROWED || NSTEP == ROWS * RS, "rowed K loop covers every step");
-  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static constexpr int NW = WM * WN;                                              // waves per workgroup
+  static constexpr int NT = 64 * NW;                                              // threads per workgroup
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves per workgroup");
   static_assert(TW % COLS == 0 && MSUBT % WM == 0, "m-subtiles must split over WM waves");
   static_assert(BN % 16 == 0, "n-subtiles of 16 channels");
   static_assert(MODE == MODE_PHASE || (BN / 16) % WN == 0, "n-subtiles must split over WN waves");
@@ -215,8 +217,9 @@ __device__ __forceinline__ float decode_ch(float y, int ch, const ConvParams& p)
 }
 
 template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW, int WM, int WN, int INK, int OUTK>
-__global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
+__global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
   using C = ConvCfg<T, MODE, KS, S, CINP, BN, TH, TW, WM, WN>;
+  constexpr int NT = C::NT;
   constexpr int NCH = C::NCH, EB = C::EB, LWP = C::LWP, HALF = C::HALF, LW = C::LW, W5 = C::W5;
   constexpr int MSUB = C::MSUB, NSUB = C::NSUB, NSUBT = C::NSUBT, COLS = C::COLS;
   constexpr bool PAIR = C::PAIR;
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
   if constexpr (INK == IN_ACT) {
     // byte offsets within the frame (host guarantees a frame is < 2 GiB), -1 = zero padding
     const int pix_bytes = p.cs * (int)sizeof(T);
-    for (int t = tid; t < C::LH + LW; t += 256) {
+    for (int t = tid; t < C::LH + LW; t += NT) {
       if (t < C::LH) {
         const int sy = map_axis(vy0 + t, p.hs, p.axis_mode, p.pre);
         rowmap[t] = sy < 0 ? -1 : sy * p.ws * pix_bytes;
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
   }
   {
     constexpr int NITEMS = C::NENT * NCH;
-    constexpr int IPT = (NITEMS + 255) / 256;
+    constexpr int IPT = (NITEMS + NT - 1) / NT;
     // entry e -> logical (ly, lx) of the halo, false for the padding entries of a polyphase order
     auto entry_xy = [&](int e, int& ly, int& lx) -> bool {
       ly = e / LWP;
@@ -285,8 +288,8 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     if constexpr (INK == IN_ACT) {
       uint4 raw[IPT];
       bool live[IPT];
-      // when 256 % NCH == 0 a thread always stages the same channel chunk
-      constexpr bool FIXED_CHUNK = (256 % NCH) == 0;
+      // when NT % NCH == 0 a thread always stages the same channel chunk
+      constexpr bool FIXED_CHUNK = (NT % NCH) == 0;
       const int c_fixed = tid % NCH;
       const char* img = (const char*)p.in + (size_t)n * p.hs * p.ws * p.cs * sizeof(T);
       // a FIXED_CHUNK thread applies the same CPC channels' IN constants to every item
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
       }
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
-        const int it = tid + k * 256;
+        const int it = tid + k * NT;
         const int e = it / NCH, c = FIXED_CHUNK ? c_fixed : it - e * NCH;
         int ly, lx;
         bool ok = entry_xy(e, ly, lx) && it < NITEMS;
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
       }
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
-        const int it = tid + k * 256;
+        const int it = tid + k * NT;
         if (it < NITEMS) {
           const int e = it / NCH, c = FIXED_CHUNK ? c_fixed : it - e * NCH;
           uint4 v = raw[k];
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
       static_assert(MODE == MODE_STD, "image input only on plain convs");
 #pragma unroll
       for (int k = 0; k < IPT; ++k) {
-        const int it = tid + k * 256;
+        const int it = tid + k * NT;
         if (it < NITEMS) {
           const int e = it / NCH;
           const int ly = e / LWP, lx = e - ly * LWP;
@@ -509,7 +512,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
       }
       __syncthreads();
       const int ntiles = p.tiles_x * p.tiles_y;
-      for (int cl = tid; cl < BN; cl += 256) {
+      for (int cl = tid; cl < BN; cl += NT) {
         float a = 0.f, b2 = 0.f;
 #pragma unroll
         for (int w = 0; w < C::REDW; ++w) { a += red[(w * BN + cl) * 2]; b2 += red[(w * BN + cl) * 2 + 1]; }
@@ -572,7 +575,7 @@ template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW,
 struct ConvInst {
   using C = ConvCfg<T, MODE, KS, S, CINP, BN, TH, TW, WM, WN>;
   static void launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL((conv_kernel<T, MODE, KS, S, CINP, BN, TH, TW, WM, WN, INK, OUTK>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((conv_kernel<T, MODE, KS, S, CINP, BN, TH, TW, WM, WN, INK, OUTK>), grid, dim3(C::NT), 0, st, p);
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
