@@ -13,7 +13,7 @@ const ConvKernelInfo* conv_table_bf16(int* count) {
       E(B, SD, 9, 1, 4, 32, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),   // Johnson/NST conv1 (tensor API)
       E(B, SD, 3, 2, 32, 64, 8, 16, 4, 1, IN_ACT, OUT_ACT),       // conv2 / down2
       E(B, SD, 3, 2, 64, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),      // conv3 / down3 / ReCoNet enc1
-      E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // residual trunk
+      E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // residual trunk (register-streamed; see conv_bf16_wl.hip)
       E(B, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT),      // deconv1 / up1 / ReCoNet dec2 (phases)
       E(B, PH, 3, 1, 64, 32, 8, 16, 1, 4, IN_ACT, OUT_ACT),       // deconv2 / up2 (phases)
       E(B, XS, 9, 1, 32, 16, 8, 80, 8, 1, IN_ACT, OUT_U8_NHWC),   // deconv3 / final (frames, x-shift, 8 waves)

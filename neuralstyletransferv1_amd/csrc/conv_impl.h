@@ -156,26 +156,33 @@ struct ConvCfg {
 };
 
 // Producer InstanceNorm apply (+ReLU) on one 16-byte chunk: v = v*scale + shift.
+// bf16: per channel pair, unpack (2 ops), one packed fp32 FMA (v_pk_fma_f32), one RNE pack
+// (v_cvt_pk_bf16_f32) and the ReLU as a packed int16 max with 0 on the bf16 bit patterns
+// (sign bit = int16 sign; rounding is monotone, so ReLU-after-round == round-after-ReLU).
+// Every producer IN the prologue applies is followed by a ReLU (ConvLayer -> IN -> ReLU in all
+// three nets; the residual's second IN is applied by the residual add instead), so the ReLU is
+// unconditional here.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef short i16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 template <typename T>
-__device__ __forceinline__ uint4 norm_chunk(uint4 raw, const float2* nm, int relu) {
+__device__ __forceinline__ uint4 norm_chunk(uint4 raw, const float2* nm) {
   if constexpr (sizeof(T) == 2) {
     uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float2 s0 = nm[2 * j], s1 = nm[2 * j + 1];
-      float lo = bf16_lo(w[j]) * s0.x + s0.y;
-      float hi = bf16_hi(w[j]) * s1.x + s1.y;
-      if (relu) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
-      w[j] = pack_bf16(lo, hi);
+      const f32x2_t x = {bf16_lo(w[j]), bf16_hi(w[j])};
+      const f32x2_t sc = {nm[2 * j].x, nm[2 * j + 1].x};
+      const f32x2_t sh = {nm[2 * j].y, nm[2 * j + 1].y};
+      f32x2_t y; y.x = __builtin_fmaf(x.x, sc.x, sh.x); y.y = __builtin_fmaf(x.y, sc.y, sh.y);
+      const i16x2_t r = __builtin_bit_cast(i16x2_t, __builtin_convertvector(y, bf16x2_t));
+      w[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
   } else {
     float v[4] = {__uint_as_float(raw.x), __uint_as_float(raw.y), __uint_as_float(raw.z), __uint_as_float(raw.w)};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[j] = v[j] * nm[j].x + nm[j].y;
-      if (relu) v[j] = fmaxf(v[j], 0.f);
-    }
+    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j] * nm[j].x + nm[j].y, 0.f);
     return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
   }
 }
@@ -211,49 +218,193 @@ __device__ __forceinline__ uint4 load_image_entry(const ConvParams& p, int n, in
   }
 }
 
+// Sum over the 16 lanes of a DPP row (every lane gets the total): row_mirror pairs lane i with
+// 15-i, row_half_mirror folds each half, then quad xor 2 and xor 1.
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xf, 0xf, false));  // row_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, false));   // quad [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, false));   // quad [1,0,3,2]
+  return v;
+}
+
 __device__ __forceinline__ float decode_ch(float y, int ch, const ConvParams& p) {
   float v = (((y + p.dec_p[ch]) * p.dec_q[ch]) / p.dec_r[ch]) + p.dec_s[ch];
   return fminf(fmaxf(v, 0.f), 1.f);  // .clamp(0, 1)
 }
 
-template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW, int WM, int WN, int INK, int OUTK>
+// Kernel variants (VAR bits):
+//  VAR_PERS  persistent form (activation-input layers with one channel block): a grid of resident
+//            workgroups walks the tiles; each one issues the NEXT tile's halo loads into registers
+//            before running the current tile's K loop, so the global-load latency of the fill hides
+//            behind MFMAs and the weight-fragment ring rolls straight from one tile into the next.
+//  VAR_WL    weights through LDS: the K loop's weight fragments are loaded ONCE per workgroup (each
+//            wave loads 1/NW of every stage into registers, RR stages ahead) and shared by all waves
+//            through a 3-stage LDS ring, instead of every wave streaming its own fragments from L2.
+//            L2 weight traffic per output pixel drops by the number of waves sharing a channel range,
+//            which is what bounds the register-streamed form on the wide (128-192 channel) layers.
+enum { VAR_PERS = 1, VAR_WL = 2 };
+
+// Weight-ring stage: SC K-steps (all NSUBT fragments of each), split evenly over the NW waves.
+template <int NSTEP, int NSUBT, int NW>
+constexpr int wl_stage_steps() {
+  for (int sc = 2; sc <= 8; ++sc)
+    if (NSTEP % sc == 0 && (sc * NSUBT) % NW == 0) return sc;
+  return 0;
+}
+
+template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW, int WM, int WN, int INK, int OUTK,
+          int VAR>
 __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
   using C = ConvCfg<T, MODE, KS, S, CINP, BN, TH, TW, WM, WN>;
+  constexpr bool PERS = (VAR & VAR_PERS) != 0;
+  constexpr bool WL = (VAR & VAR_WL) != 0;
   constexpr int NT = C::NT;
   constexpr int NCH = C::NCH, EB = C::EB, LWP = C::LWP, HALF = C::HALF, LW = C::LW, W5 = C::W5;
   constexpr int MSUB = C::MSUB, NSUB = C::NSUB, NSUBT = C::NSUBT, COLS = C::COLS;
   constexpr bool PAIR = C::PAIR;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS_ALLOC];
+  static_assert(!PERS || (INK == IN_ACT && C::ROWED), "persistent form: activation-input rowed layers");
+  static_assert(!WL || C::ROWED, "LDS weight ring: rowed K loop");
+  static_assert(!PERS || WL, "the persistent form streams weights through the LDS ring");
+  // weight ring geometry (WL)
+  constexpr int SC = WL ? wl_stage_steps<C::NSTEP, NSUBT, C::NW>() : 1;  // K-steps per stage
+  static_assert(!WL || SC >= 2, "weight-ring stage: >= 2 steps, split evenly over the waves");
+  constexpr int NSTG = C::NSTEP / SC;                                      // stages per tile
+  constexpr int FR_STG = SC * NSUBT;                                       // 1-KiB fragments per stage
+  constexpr int FPW = FR_STG / C::NW;                                      // fragments each wave loads
+  constexpr int RR = 3;                                                    // stages in flight in registers
+  constexpr int STG_BYTES = FR_STG * 1024;
+  // LDS: [halo][row/col maps x (PERS ? 2 : 1)][weight ring x 3 (WL)][bias (WL)][IN constants (PERS)]
+  //      [reduction (PERS: own region; else aliases the halo)]
+  constexpr int MAPB = (C::MAP_BYTES + 15) / 16 * 16;
+  constexpr int RING_OFF = C::MAP_OFF + (PERS ? 2 : 1) * MAPB;
+  constexpr int BIAS_OFF = RING_OFF + (WL ? 3 * STG_BYTES : 0);
+  constexpr int NORM_OFF = BIAS_OFF + (WL ? BN * 4 : 0);       // PERS: next frame's IN {scale, shift}
+  constexpr int RING_END = NORM_OFF + (PERS ? CINP * 8 : 0);
+  constexpr int RED_OFF = PERS ? RING_END : 0;
+  constexpr int LDS_TOTAL0 = PERS ? RED_OFF + C::RED_BYTES : RING_END;
+  constexpr int LDS_TOTAL = LDS_TOTAL0 > C::LDS_ALLOC ? LDS_TOTAL0 : C::LDS_ALLOC;
+  static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_TOTAL];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, px = lane & 15;
-  const int tile = blockIdx.x;
-  const int tyi = tile / p.tiles_x, txi = tile - tyi * p.tiles_x;
-  const int n = blockIdx.y / p.n_cblk, cb = blockIdx.y - n * p.n_cblk;
-  const int ty0 = tyi * TH, tx0 = txi * TW;  // PHASE: tile origin on the source grid
+
+  // work item w = (frame n, channel block cb, tile)
+  struct Work {
+    int n, cb, tile, ty0, tx0;  // PHASE: tile origin on the source grid
+  };
+  const int ntile = p.tiles_x * p.tiles_y;
+  auto decode_work = [&](int wi) {
+    Work r;
+    r.tile = wi % ntile;
+    const int ny = wi / ntile;
+    r.n = ny / p.n_cblk;
+    r.cb = ny - r.n * p.n_cblk;
+    const int tyi = r.tile / p.tiles_x;
+    r.ty0 = tyi * TH;
+    r.tx0 = (r.tile - tyi * p.tiles_x) * TW;
+    return r;
+  };
+  int w;
+  if constexpr (PERS) {
+    // workgroups b, b+8, ... run on one XCD (round-robin dispatch): give each XCD a contiguous run
+    // of tiles per sweep so vertically/horizontally neighbouring halos meet in the same L2
+    const int G = gridDim.x, b = blockIdx.x;
+    w = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+    if (w >= p.n_work) return;
+  } else {
+    w = blockIdx.y * ntile + blockIdx.x;
+  }
+  Work cur = decode_work(w);
 
   // weights: fragment (step s, n-subtile t) of this wave lives at wp[(s*NSUBT + t)*64]; a ring of
-  // PF steps is kept in flight (steps >= NSTEP are zero padding)
+  // PF steps is kept in flight (steps >= NSTEP are zero padding; PERS wraps to the next tile's step 0)
   constexpr int PF = C::PF;
-  const uint4* wp = (const uint4*)p.wpk + ((size_t)cb * C::NSTEP_PACK * NSUBT + wn * NSUB) * 64 + lane;
-  uint4 a_ring[PF][NSUB];
+  const uint4* wp = (const uint4*)p.wpk + ((size_t)cur.cb * C::NSTEP_PACK * NSUBT + wn * NSUB) * 64 + lane;
+  uint4 a_ring[WL ? 1 : PF][NSUB];
+  if constexpr (!WL) {
 #pragma unroll
-  for (int d = 0; d < PF; ++d)
+    for (int d = 0; d < PF; ++d)
 #pragma unroll
-    for (int t = 0; t < NSUB; ++t) a_ring[d][t] = wp[(d * NSUBT + t) * 64];
+      for (int t = 0; t < NSUB; ++t) a_ring[d][t] = wp[(d * NSUBT + t) * 64];
+  }
+  // WL: stage j's fragments are contiguous in the packed weights; this wave loads fragments
+  // [wave*FPW, wave*FPW+FPW) of each stage and stores them to the same place in the LDS ring
+  // (buffer loads: the stage offset rides in an SGPR, so every stage shares one lane-offset VGPR)
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)p.wpk + (size_t)cur.cb * C::NSTEP_PACK * NSUBT * 1024), (short)0,
+      C::NSTEP_PACK * NSUBT * 1024, 0x00020000);
+  const uint32_t wvoff = (uint32_t)((wave * FPW * 64 + lane) * 16);
+  auto wld = [&](int j, int f) -> uint4 {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff, (j * FR_STG + f) * 1024, 0));
+  };
+  char* ring = smem + RING_OFF;
+  // in-flight stages form a shift register (oldest in wreg[0]) so every register index is static
+  constexpr int RRA = WL ? RR : 1;
+  uint4 wreg[RRA][FPW > 0 ? FPW : 1];
+  auto wl_issue = [&](int j) {  // load stage j into the youngest slot
+#pragma unroll
+    for (int f = 0; f < FPW; ++f) wreg[RRA - 1][f] = wld(j, f);
+  };
+  auto wl_store = [&](int slot_off) {  // store the oldest stage to a ring slot, shift the rest down
+#pragma unroll
+    for (int f = 0; f < FPW; ++f)
+      *(uint4*)(ring + slot_off + ((wave * FPW + f) * 64 + lane) * 16) = wreg[0][f];
+#pragma unroll
+    for (int r = 0; r + 1 < RRA; ++r)
+#pragma unroll
+      for (int f = 0; f < FPW; ++f) wreg[r][f] = wreg[r + 1][f];
+  };
+  if constexpr (WL) {
+    if constexpr (OUTK == OUT_ACT) {
+      float* bias_l = (float*)(smem + BIAS_OFF);
+      for (int t = tid; t < BN; t += NT) bias_l[t] = p.bias[cur.cb * BN + t];
+    }
+    // stages 0..RR-1 in flight while the halo is staged
+#pragma unroll
+    for (int j = 0; j < RR; ++j) {
+      if (PERS || j < NSTG) {
+#pragma unroll
+        for (int f = 0; f < FPW; ++f) wreg[j][f] = wld(j % NSTG, f);
+      }
+    }
+  }
 
   // ---- stage the input halo (prologue transform applied) ----
   // The padding / reflection / upsample / crop mapping of halo row ly and column lx to a source
-  // row/column (or -1 = zero) is evaluated once per block into two small LDS maps.  Then all of
+  // row/column (or -1 = zero) is evaluated once per tile into two small LDS maps.  Then all of
   // a thread's loads are issued before any is consumed (IPT independent 16-B loads in flight per
   // lane), transformed (producer IN + ReLU) and written to LDS: the fill costs ~one latency.
-  const int vy0 = (ty0 + p.crop_y) * S - p.pad;
-  const int vx0 = (tx0 + p.crop_x) * S - p.pad;
-  int* rowmap = (int*)(smem + C::MAP_OFF);
-  int* colmap = rowmap + C::LH;
-  if constexpr (INK == IN_ACT) {
+  constexpr int NITEMS = C::NENT * NCH;
+  constexpr int IPT = (NITEMS + NT - 1) / NT;
+  // entry e -> logical (ly, lx) of the halo, false for the padding entries of a polyphase order
+  auto entry_xy = [&](int e, int& ly, int& lx) -> bool {
+    ly = e / LWP;
+    const int pc = e - ly * LWP;
+    if constexpr (MODE == MODE_XSHIFT) {
+      const int ph = pc / W5;
+      lx = C::NXS * (pc - ph * W5) + ph;
+      return lx < LW;
+    } else if constexpr (S == 2) {
+      lx = pc < HALF ? 2 * pc : 2 * (pc - HALF) + 1;
+      return lx < LW;
+    } else {
+      lx = pc;
+      return true;
+    }
+  };
+  // when NT % NCH == 0 a thread always stages the same channel chunk, so it applies the same
+  // CPC channels' IN constants to every item
+  constexpr bool FIXED_CHUNK = (NT % NCH) == 0;
+  const int c_fixed = tid % NCH;
+  auto build_maps = [&](const Work& wk, int slot) {
     // byte offsets within the frame (host guarantees a frame is < 2 GiB), -1 = zero padding
+    int* rowmap = (int*)(smem + C::MAP_OFF + slot * MAPB);
+    int* colmap = rowmap + C::LH;
+    const int vy0 = (wk.ty0 + p.crop_y) * S - p.pad;
+    const int vx0 = (wk.tx0 + p.crop_x) * S - p.pad;
     const int pix_bytes = p.cs * (int)sizeof(T);
     for (int t = tid; t < C::LH + LW; t += NT) {
       if (t < C::LH) {
@@ -264,79 +415,123 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
         colmap[t - C::LH] = sx < 0 ? -1 : sx * pix_bytes;
       }
     }
-    __syncthreads();
-  }
-  {
-    constexpr int NITEMS = C::NENT * NCH;
-    constexpr int IPT = (NITEMS + NT - 1) / NT;
-    // entry e -> logical (ly, lx) of the halo, false for the padding entries of a polyphase order
-    auto entry_xy = [&](int e, int& ly, int& lx) -> bool {
-      ly = e / LWP;
-      const int pc = e - ly * LWP;
-      if constexpr (MODE == MODE_XSHIFT) {
-        const int ph = pc / W5;
-        lx = C::NXS * (pc - ph * W5) + ph;
-        return lx < LW;
-      } else if constexpr (S == 2) {
-        lx = pc < HALF ? 2 * pc : 2 * (pc - HALF) + 1;
-        return lx < LW;
-      } else {
-        lx = pc;
-        return true;
-      }
-    };
-    if constexpr (INK == IN_ACT) {
-      uint4 raw[IPT];
-      bool live[IPT];
-      // when NT % NCH == 0 a thread always stages the same channel chunk
-      constexpr bool FIXED_CHUNK = (NT % NCH) == 0;
-      const int c_fixed = tid % NCH;
-      const char* img = (const char*)p.in + (size_t)n * p.hs * p.ws * p.cs * sizeof(T);
-      // a FIXED_CHUNK thread applies the same CPC channels' IN constants to every item
-      float2 nmc[C::CPC];
-      if (FIXED_CHUNK && p.in_norm != nullptr) {
+  };
+  // item k of this thread -> LDS entry e, chunk c; returns the source byte offset in the frame,
+  // -1 for zero padding (evaluated from the maps in slot, at load time and again at store time)
+  auto item_src = [&](int slot, int k, int& e, int& c) -> int {
+    const int* rowmap = (const int*)(smem + C::MAP_OFF + slot * MAPB);
+    const int* colmap = rowmap + C::LH;
+    const int it = tid + k * NT;
+    e = it / NCH;
+    c = FIXED_CHUNK ? c_fixed : it - e * NCH;
+    int ly, lx;
+    const bool ok = entry_xy(e, ly, lx) && it < NITEMS;
+    const int ro = ok ? rowmap[ly] : -1;
+    const int co = ok ? colmap[lx] : -1;
+    return (ro >= 0 && co >= 0) ? ro + co + c * 16 : -1;
+  };
+  // srcs[k] keeps each item's source offset (-1 = zero padding) for the store pass
+  auto issue_loads = [&](const Work& wk, int slot, uint4 (&raw)[IPT], int (&srcs)[IPT]) {
+    const char* img = (const char*)p.in + (size_t)wk.n * p.hs * p.ws * p.cs * sizeof(T);
 #pragma unroll
-        for (int j = 0; j < C::CPC; ++j) nmc[j] = p.in_norm[(size_t)n * p.cs + c_fixed * C::CPC + j];
-      }
+    for (int k = 0; k < IPT; ++k) {
+      int e, c;
+      const int src = item_src(slot, k, e, c);
+      srcs[k] = src;
+      raw[k] = make_uint4(0u, 0u, 0u, 0u);
+      if (src >= 0) raw[k] = *(const uint4*)(img + (unsigned)src);
+    }
+  };
+  auto load_norm = [&](int n, float2 (&nmc)[C::CPC]) {
+    if (FIXED_CHUNK && p.in_norm != nullptr) {
 #pragma unroll
-      for (int k = 0; k < IPT; ++k) {
-        const int it = tid + k * NT;
+      for (int j = 0; j < C::CPC; ++j) nmc[j] = p.in_norm[(size_t)n * p.cs + c_fixed * C::CPC + j];
+    }
+  };
+  auto stage = [&](const Work& wk, const uint4 (&raw)[IPT], const int (&srcs)[IPT], const float2 (&nmc)[C::CPC]) {
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int it = tid + k * NT;
+      if (it < NITEMS) {
         const int e = it / NCH, c = FIXED_CHUNK ? c_fixed : it - e * NCH;
-        int ly, lx;
-        bool ok = entry_xy(e, ly, lx) && it < NITEMS;
-        const int ro = ok ? rowmap[ly] : -1;
-        const int co = ok ? colmap[lx] : -1;
-        ok = ok && ro >= 0 && co >= 0;
-        live[k] = ok;
-        raw[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (ok) raw[k] = *(const uint4*)(img + (unsigned)(ro + co + c * 16));
-      }
+        uint4 v = raw[k];
+        if (srcs[k] >= 0 && p.in_norm != nullptr) {
+          if constexpr (FIXED_CHUNK) {
+            v = norm_chunk<T>(v, nmc);
+          } else {
+            float2 nmv[C::CPC];
 #pragma unroll
-      for (int k = 0; k < IPT; ++k) {
-        const int it = tid + k * NT;
-        if (it < NITEMS) {
-          const int e = it / NCH, c = FIXED_CHUNK ? c_fixed : it - e * NCH;
-          uint4 v = raw[k];
-          if (live[k] && p.in_norm != nullptr)
-            v = norm_chunk<T>(v, FIXED_CHUNK ? nmc : p.in_norm + (size_t)n * p.cs + c * C::CPC, p.in_relu);
-          *(uint4*)(smem + e * EB + 16 * c) = v;
+            for (int j = 0; j < C::CPC; ++j) nmv[j] = p.in_norm[(size_t)wk.n * p.cs + c * C::CPC + j];
+            v = norm_chunk<T>(v, nmv);
+          }
         }
-      }
-    } else {
-      static_assert(MODE == MODE_STD, "image input only on plain convs");
-#pragma unroll
-      for (int k = 0; k < IPT; ++k) {
-        const int it = tid + k * NT;
-        if (it < NITEMS) {
-          const int e = it / NCH;
-          const int ly = e / LWP, lx = e - ly * LWP;
-          const uint4 v = load_image_entry<T, INK, PAIR>(p, n, vy0 + ly, vx0 + lx);
-          *(uint4*)(smem + e * EB) = v;
-        }
+        *(uint4*)(smem + e * EB + 16 * c) = v;
       }
     }
-  }
-  __syncthreads();
+  };
+  // PERS streams the next tile's halo in NCH4 parts, part q = channel chunks 4q..4q+3 of every
+  // entry (the K loop runs chunk group q's taps before q+1's, so part q's LDS is free once they
+  // are done); item i of a part -> entry i/4, chunk 4q + i%4 (a thread keeps its chunk i%4)
+  constexpr int NPART = C::NCH4;
+  constexpr int PITEMS = C::NENT * 4;
+  constexpr int IPP = (PITEMS + NT - 1) / NT;
+  int tid_p = tid;  // laundered per use: part item addresses are recomputed, not held across the K loop
+  auto part_src = [&](int slot, int q, int k, int& e, int& c) -> int {
+    const int* rowmap = (const int*)(smem + C::MAP_OFF + slot * MAPB);
+    const int* colmap = rowmap + C::LH;
+    asm volatile("" : "+v"(tid_p));
+    const int it = tid_p + k * NT;
+    e = it >> 2;
+    c = 4 * q + (it & 3);
+    int ly, lx;
+    const bool ok = entry_xy(e, ly, lx) && it < PITEMS;
+    const int ro = ok ? rowmap[ly] : -1;
+    const int co = ok ? colmap[lx] : -1;
+    return (ro >= 0 && co >= 0) ? ro + co + c * 16 : -1;
+  };
+  auto issue_part = [&](const Work& wk, int slot, int q, uint4 (&praw)[IPP]) {
+    const char* img = (const char*)p.in + (size_t)wk.n * p.hs * p.ws * p.cs * sizeof(T);
+#pragma unroll
+    for (int k = 0; k < IPP; ++k) {
+      int e, c;
+      const int src = part_src(slot, q, k, e, c);
+      praw[k] = make_uint4(0u, 0u, 0u, 0u);
+      if (src >= 0) praw[k] = *(const uint4*)(img + (unsigned)src);
+    }
+  };
+  // the IN constants of the part's frame come from the LDS table (norm_l)
+  auto write_part = [&](int slot, int q, const uint4 (&praw)[IPP], const float2* norm_l) {
+    float2 nm[C::CPC];
+    if (p.in_norm != nullptr) {
+#pragma unroll
+      for (int j = 0; j < C::CPC; ++j) nm[j] = norm_l[(4 * q + (tid & 3)) * C::CPC + j];
+    }
+#pragma unroll
+    for (int k = 0; k < IPP; ++k) {
+      if (tid + k * NT < PITEMS) {
+        int e, c;
+        const int src = part_src(slot, q, k, e, c);
+        uint4 v = praw[k];
+        if (src >= 0 && p.in_norm != nullptr) v = norm_chunk<T>(v, nm);
+        *(uint4*)(smem + e * EB + 16 * c) = v;
+      }
+    }
+  };
+  auto stage_image = [&](const Work& wk) {
+    static_assert(INK == IN_ACT || MODE == MODE_STD, "image input only on plain convs");
+    const int vy0 = (wk.ty0 + p.crop_y) * S - p.pad;
+    const int vx0 = (wk.tx0 + p.crop_x) * S - p.pad;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int it = tid + k * NT;
+      if (it < NITEMS) {
+        const int e = it / NCH;
+        const int ly = e / LWP, lx = e - ly * LWP;
+        const uint4 v = load_image_entry<T, INK, PAIR>(p, wk.n, vy0 + ly, vx0 + lx);
+        *(uint4*)(smem + e * EB) = v;
+      }
+    }
+  };
 
   // ---- K loop: taps x channel chunks ----
   int base[MSUB];
@@ -352,13 +547,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
     phy = p.ph_off[wn >> 1];
     phx = p.ph_off[wn & 1];
   }
-  f32x4_t acc[MSUB][NSUB];
-#pragma unroll
-  for (int m = 0; m < MSUB; ++m)
-#pragma unroll
-    for (int t = 0; t < NSUB; ++t) acc[m][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  typedef f32x4_t AccT[MSUB][NSUB];
 
-  auto mfma_step = [&](const uint4 (&a)[NSUB], const uint4 (&b)[MSUB]) {
+  auto mfma_step = [&](AccT& acc, const uint4 (&a)[NSUB], const uint4 (&b)[MSUB]) {
 #pragma unroll
     for (int m = 0; m < MSUB; ++m) {
 #pragma unroll
@@ -376,206 +567,418 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
     }
   };
 
-  if constexpr (C::ROWED) {
-    // rows (runtime) x x-taps x chunk groups (unrolled): step s = row*RS + dx*NCH4 + cg reads
-    // chunk 4*cg + g of tap (row, dx); PF divides RS, so the ring slot of each position is static
-    constexpr int NCH4 = C::NCH4, KPR = C::KPR, RS = C::RS;
-    // per-lane LDS byte base of each m-subtile (lane group g's chunk folded in); per row one add,
-    // per tap / chunk group only immediate offsets
-    int lbase[MSUB];
+  // kloop(acc, rot, hook): rot = ring slot of this tile's stage 0 (PERS: the ring runs on across
+  // tiles); hook(k) runs after stage k's barrier (PERS: the next tile's maps / halo loads)
+  auto kloop = [&](AccT& acc, int rot, auto&& hook) {
 #pragma unroll
-    for (int m = 0; m < MSUB; ++m) lbase[m] = base[m] * EB + 16 * g;
-    for (int row = 0; row < C::ROWS; ++row) {
-      const int rowoff = (MODE == MODE_PHASE ? (phy + row) * LWP + phx : row * LWP) * EB;
-      const char* rp[MSUB];
+    for (int m = 0; m < MSUB; ++m)
 #pragma unroll
-      for (int m = 0; m < MSUB; ++m) rp[m] = smem + lbase[m] + rowoff;
+      for (int t = 0; t < NSUB; ++t) acc[m][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    if constexpr (WL) {
+      // fully unrolled steps; stage k = steps [k*SC, k*SC+SC) reads ring slot k%3.  After the first
+      // step of stage k a barrier retires every wave's reads of slot (k+2)%3 (stage k-1), so stage
+      // k+2 (loaded RR stages ago) is stored there and stage k+2+RR is issued into the freed registers;
+      // the next stage's barrier publishes the store before stage k+2's first read (SC >= 2).
+      constexpr int NCH4 = C::NCH4, RS = C::RS;
+      int lbase[MSUB];
 #pragma unroll
-      for (int dx = 0; dx < KPR; ++dx) {
-        // constant column offset of x-tap dx in this mode's LDS column order
+      for (int m = 0; m < MSUB; ++m) lbase[m] = base[m] * EB + 16 * g;
+      const char* abase = ring + ((wn * NSUB) * 64 + lane) * 16;
+      // byte offset of the ring slot holding stage k (+3 for the wrap): so[k % 3]
+      int so[3];
+      if constexpr (NSTG % 3 == 0) rot = 0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) so[i] = ((rot + i) % 3) * STG_BYTES;
+      // operands of step s (double-buffered by parity: step s+1's reads are issued before step s's
+      // barrier, so no LDS latency is exposed after it)
+      uint4 a[2][NSUB], b[2][MSUB];
+      auto load_step = [&](int s, uint4 (&av)[NSUB], uint4 (&bv)[MSUB]) {
+        // K order: tap-major (s = tap*NCH4 + cg) or, PERS, chunk-group-major (s = cg*taps + tap)
+        int row, dx, cg;
+        if constexpr (PERS) {
+          cg = s / (C::ROWS * C::KPR);
+          const int tap = s - cg * (C::ROWS * C::KPR);
+          row = tap / C::KPR;
+          dx = tap - row * C::KPR;
+        } else {
+          row = s / RS;
+          const int pos = s - row * RS;
+          dx = pos / NCH4;
+          cg = pos - dx * NCH4;
+        }
+        const int rowoff = (MODE == MODE_PHASE ? (phy + row) * LWP + phx : row * LWP) * EB;
         const int xo = MODE == MODE_XSHIFT ? (dx % C::NXS) * W5 + dx / C::NXS
                                            : (S == 2 ? (dx & 1) * HALF + (dx >> 1) : dx);
+        const int k = s / SC, ss = s - k * SC;
 #pragma unroll
-        for (int cg = 0; cg < NCH4; ++cg) {
-          const int pos = dx * NCH4 + cg;  // position within the row (compile-time after unrolling)
-          const int slot = pos % PF;
+        for (int t = 0; t < NSUB; ++t) av[t] = *(const uint4*)(abase + so[k % 3] + (ss * NSUBT + t) * 1024);
+#pragma unroll
+        for (int m = 0; m < MSUB; ++m) bv[m] = *(const uint4*)(smem + lbase[m] + rowoff + xo * EB + 64 * cg);
+      };
+      load_step(0, a[0], b[0]);
+#pragma unroll
+      for (int s = 0; s < C::NSTEP; ++s) {
+        // one scheduling region per step: step s+1's operand reads interleaved with step s's MFMAs
+        if (s + 1 < C::NSTEP) load_step(s + 1, a[(s + 1) & 1], b[(s + 1) & 1]);
+        // the work hooked to stage k's barrier (step k*SC) runs in the next step's region, so the
+        // scheduler interleaves it with MFMAs instead of every wave stalling on it together
+        if (s >= 1 && (s - 1) % SC == 0) hook((s - 1) / SC);
+        mfma_step(acc, a[s & 1], b[s & 1]);
+#pragma unroll
+        for (int i = 0; i < NSUB + MSUB; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, MSUB * NSUB - (NSUB + MSUB), 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const int k = s / SC;
+        if (s - k * SC == 0) {
+          // every wave is past its stage k-1 reads: refill slot (k+2)%3
+          __syncthreads();
+          if constexpr (PERS) {
+            // the ring runs on into the next tile (same channel block, so the same weights)
+            wl_store(so[(k + 2) % 3]);
+            wl_issue((k + 2 + RR) % NSTG);
+          } else if (k + 2 < NSTG) {
+            wl_store(so[(k + 2) % 3]);
+            if (k + 2 + RR < NSTG) wl_issue(k + 2 + RR);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else if constexpr (C::ROWED) {
+      // rows (runtime) x x-taps x chunk groups (unrolled): step s = row*RS + dx*NCH4 + cg reads
+      // chunk 4*cg + g of tap (row, dx); PF divides RS, so the ring slot of each position is static
+      constexpr int NCH4 = C::NCH4, KPR = C::KPR, RS = C::RS;
+      // per-lane LDS byte base of each m-subtile (lane group g's chunk folded in); per row one add,
+      // per tap / chunk group only immediate offsets
+      int lbase[MSUB];
+#pragma unroll
+      for (int m = 0; m < MSUB; ++m) lbase[m] = base[m] * EB + 16 * g;
+      for (int row = 0; row < C::ROWS; ++row) {
+        const int rowoff = (MODE == MODE_PHASE ? (phy + row) * LWP + phx : row * LWP) * EB;
+        const char* rp[MSUB];
+#pragma unroll
+        for (int m = 0; m < MSUB; ++m) rp[m] = smem + lbase[m] + rowoff;
+#pragma unroll
+        for (int dx = 0; dx < KPR; ++dx) {
+          // constant column offset of x-tap dx in this mode's LDS column order
+          const int xo = MODE == MODE_XSHIFT ? (dx % C::NXS) * W5 + dx / C::NXS
+                                             : (S == 2 ? (dx & 1) * HALF + (dx >> 1) : dx);
+#pragma unroll
+          for (int cg = 0; cg < NCH4; ++cg) {
+            const int pos = dx * NCH4 + cg;  // position within the row (compile-time after unrolling)
+            const int slot = pos % PF;
+            uint4 b[MSUB];
+#pragma unroll
+            for (int m = 0; m < MSUB; ++m) b[m] = *(const uint4*)(rp[m] + xo * EB + 64 * cg);
+            mfma_step(acc, a_ring[slot], b);
+            const int sn = row * RS + pos + PF;
+#pragma unroll
+            for (int t = 0; t < NSUB; ++t) a_ring[slot][t] = wp[(sn * NSUBT + t) * 64];
+          }
+        }
+      }
+    } else {
+      for (int s0 = 0; s0 < C::NSTEP_P; s0 += PF) {
+#pragma unroll
+        for (int d = 0; d < PF; ++d) {
+          const int s = s0 + d;
+          const int i = 4 * s + g;
+          int tap = 0, c = 0;
+          if (i < C::NCHUNK) {
+            tap = i / NCH;
+            c = i - tap * NCH;
+          }
+          const int dy = tap / C::KP, dxp = tap - dy * C::KP;
+          const int dx = PAIR ? 2 * dxp : dxp;
+          const int toff = dy * LWP + dx;
           uint4 b[MSUB];
 #pragma unroll
-          for (int m = 0; m < MSUB; ++m) b[m] = *(const uint4*)(rp[m] + xo * EB + 64 * cg);
-          mfma_step(a_ring[slot], b);
-          const int s = row * RS + pos;
+          for (int m = 0; m < MSUB; ++m) {
+            const int e = base[m] + toff;
+            b[m] = *(const uint4*)(smem + e * EB + 16 * (c ^ swz<NCH>(e)));
+          }
+          mfma_step(acc, a_ring[d], b);
 #pragma unroll
-          for (int t = 0; t < NSUB; ++t) a_ring[slot][t] = wp[((s + PF) * NSUBT + t) * 64];
+          for (int t = 0; t < NSUB; ++t) a_ring[d][t] = wp[((s + PF) * NSUBT + t) * 64];
         }
       }
-    }
-  } else {
-    for (int s0 = 0; s0 < C::NSTEP_P; s0 += PF) {
-#pragma unroll
-      for (int d = 0; d < PF; ++d) {
-        const int s = s0 + d;
-        const int i = 4 * s + g;
-        int tap = 0, c = 0;
-        if (i < C::NCHUNK) {
-          tap = i / NCH;
-          c = i - tap * NCH;
-        }
-        const int dy = tap / C::KP, dxp = tap - dy * C::KP;
-        const int dx = PAIR ? 2 * dxp : dxp;
-        const int toff = dy * LWP + dx;
-        uint4 b[MSUB];
-#pragma unroll
-        for (int m = 0; m < MSUB; ++m) {
-          const int e = base[m] + toff;
-          b[m] = *(const uint4*)(smem + e * EB + 16 * (c ^ swz<NCH>(e)));
-        }
-        mfma_step(a_ring[d], b);
-#pragma unroll
-        for (int t = 0; t < NSUB; ++t) a_ring[d][t] = wp[((s + PF) * NSUBT + t) * 64];
-      }
-    }
-  }
-
-  // ---- epilogue ----
-  // output pixel of m-subtile m for this lane (STD / PHASE)
-  auto out_px = [&](int m, int& oy, int& ox) {
-    const int ms = wm * MSUB + m;
-    const int r = ms / (TW / COLS), cbk = ms - r * (TW / COLS);
-    if constexpr (MODE == MODE_PHASE) {
-      oy = 2 * (ty0 + r) + (wn >> 1);
-      ox = 2 * (tx0 + cbk * 16 + px) + (wn & 1);
-    } else {
-      oy = ty0 + r;
-      ox = tx0 + cbk * 16 + px;
     }
   };
-  if constexpr (OUTK == OUT_ACT) {
-    const int cwave = cb * BN + (MODE == MODE_PHASE ? 0 : wn * NSUB * 16);  // first channel of this wave
-    const int cbase = cwave + 4 * NSUB * g;                                 // this lane's 4*NSUB channels
-    float bias_v[4 * NSUB];
-#pragma unroll
-    for (int j = 0; j < 4 * NSUB; ++j) bias_v[j] = p.bias[cbase + j];
-    float s1[4 * NSUB], s2[4 * NSUB];
-#pragma unroll
-    for (int j = 0; j < 4 * NSUB; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-#pragma unroll
-    for (int m = 0; m < MSUB; ++m) {
-      int oy, ox;
-      out_px(m, oy, ox);
-      const bool valid = (oy < p.oh) && (ox < p.ow);
-      float v[4 * NSUB];
-#pragma unroll
-      for (int t = 0; t < NSUB; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[4 * t + q] = acc[m][t][q] + bias_v[4 * t + q];
-      if (valid) {
-        char* dst = (char*)p.out + ((((size_t)n * p.oh + oy) * p.ow + ox) * p.cout_stride + cbase) * sizeof(T);
-        if constexpr (sizeof(T) == 2) {
-#pragma unroll
-          for (int h = 0; h < NSUB; h += 2) {
-            if (h + 1 < NSUB) {
-              *(uint4*)(dst + h * 8) = make_uint4(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]),
-                                                  pack_bf16(v[4 * h + 4], v[4 * h + 5]), pack_bf16(v[4 * h + 6], v[4 * h + 7]));
-            } else {
-              *(uint2*)(dst + h * 8) = make_uint2(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]));
-            }
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < NSUB; ++t)
-            *(float4*)(dst + t * 16) = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4 * NSUB; ++j) { s1[j] += v[j]; s2[j] += v[j] * v[j]; }
+
+  // ---- epilogue ----
+  auto epilogue = [&](const Work& wk, const AccT& acc) {
+    const int n = wk.n, cb = wk.cb, ty0 = wk.ty0, tx0 = wk.tx0;
+    // output pixel of m-subtile m for this lane (STD / PHASE)
+    auto out_px = [&](int m, int& oy, int& ox) {
+      const int ms = wm * MSUB + m;
+      const int r = ms / (TW / COLS), cbk = ms - r * (TW / COLS);
+      if constexpr (MODE == MODE_PHASE) {
+        oy = 2 * (ty0 + r) + (wn >> 1);
+        ox = 2 * (tx0 + cbk * 16 + px) + (wn & 1);
+      } else {
+        oy = ty0 + r;
+        ox = tx0 + cbk * 16 + px;
       }
-    }
-    if (p.partial != nullptr) {
-      // reduce over the 16 pixel lanes of each lane group
+    };
+    if constexpr (OUTK == OUT_ACT) {
+      const int cwave = cb * BN + (MODE == MODE_PHASE ? 0 : wn * NSUB * 16);  // first channel of this wave
+      const int cbase = cwave + 4 * NSUB * g;                                 // this lane's 4*NSUB channels
+      float bias_v[4 * NSUB];
+      if constexpr (WL) {
+        const float* bias_l = (const float*)(smem + BIAS_OFF) + (cbase - cb * BN);
 #pragma unroll
-      for (int j = 0; j < 4 * NSUB; ++j) {
+        for (int j = 0; j < 4 * NSUB; ++j) bias_v[j] = bias_l[j];
+      } else {
 #pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) {
-          s1[j] += __shfl_xor(s1[j], off);
-          s2[j] += __shfl_xor(s2[j], off);
-        }
+        for (int j = 0; j < 4 * NSUB; ++j) bias_v[j] = p.bias[cbase + j];
       }
-      __syncthreads();  // LDS tile no longer read
-      float* red = (float*)smem;  // [REDW][BN][2]
-      const int rw = MODE == MODE_PHASE ? wave : wm;
-      if (px == 0) {
+      float s1[4 * NSUB], s2[4 * NSUB];
 #pragma unroll
-        for (int j = 0; j < 4 * NSUB; ++j) {
-          const int cl = cwave - cb * BN + 4 * NSUB * g + j;
-          red[(rw * BN + cl) * 2 + 0] = s1[j];
-          red[(rw * BN + cl) * 2 + 1] = s2[j];
-        }
-      }
-      __syncthreads();
-      const int ntiles = p.tiles_x * p.tiles_y;
-      for (int cl = tid; cl < BN; cl += NT) {
-        float a = 0.f, b2 = 0.f;
-#pragma unroll
-        for (int w = 0; w < C::REDW; ++w) { a += red[(w * BN + cl) * 2]; b2 += red[(w * BN + cl) * 2 + 1]; }
-        float* dst = p.partial + (((size_t)n * ntiles + tile) * p.cout_stride + cb * BN + cl) * 2;
-        dst[0] = a;
-        dst[1] = b2;
-      }
-    }
-  } else if constexpr (MODE == MODE_XSHIFT) {
-    // lane (base px, group g) holds rows q = 4g+j = 3*shift + channel (channel order baked
-    // into the packed weights and bias); base px's 15 outputs are bytes 15*px .. 15*px+14
-#pragma unroll
-    for (int m = 0; m < MSUB; ++m) {
-      const int oy = ty0 + wm * MSUB + m;
-      if (oy >= p.oh) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = 4 * g + j;
-        if (q >= 15) continue;
-        const int sft = q / 3, ch = q - 3 * sft;
-        const int ox = tx0 + C::NXS * px + sft;
-        if (ox >= p.ow) continue;
-        float y = acc[m][0][j] + p.bias[q];
-        if (p.dec_tanh) y = tanhf(y);
-        if constexpr (OUTK == OUT_F32_NCHW) {
-          ((float*)p.out)[(((size_t)n * 3 + ch) * p.oh + oy) * p.ow + ox] = y;
-        } else {
-          ((uint8_t*)p.out)[(((size_t)n * p.oh + oy) * p.ow + ox) * 3 + ch] =
-              (uint8_t)(decode_ch(y, ch, p) * 255.0f);  // ToPILImage: pic.mul(255).byte()
-        }
-      }
-    }
-  } else {
-    // STD final layer: 3 output channels live in lane group 0 (channels 0..3 of n-subtile 0)
-    if (g == 0) {
-      const float b0 = p.bias[0], b1 = p.bias[1], b2v = p.bias[2];
+      for (int j = 0; j < 4 * NSUB; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
 #pragma unroll
       for (int m = 0; m < MSUB; ++m) {
         int oy, ox;
         out_px(m, oy, ox);
-        if (oy >= p.oh || ox >= p.ow) continue;
-        float y[3] = {acc[m][0][0] + b0, acc[m][0][1] + b1, acc[m][0][2] + b2v};
-        if (p.dec_tanh) { y[0] = tanhf(y[0]); y[1] = tanhf(y[1]); y[2] = tanhf(y[2]); }
-        if constexpr (OUTK == OUT_F32_NCHW) {
-          float* o = (float*)p.out;
+        const bool valid = (oy < p.oh) && (ox < p.ow);
+        float v[4 * NSUB];
 #pragma unroll
-          for (int ch = 0; ch < 3; ++ch) o[(((size_t)n * 3 + ch) * p.oh + oy) * p.ow + ox] = y[ch];
-        } else {
-          uint8_t* o = (uint8_t*)p.out + (((size_t)n * p.oh + oy) * p.ow + ox) * 3;
+        for (int t = 0; t < NSUB; ++t)
 #pragma unroll
-          for (int ch = 0; ch < 3; ++ch) o[ch] = (uint8_t)(decode_ch(y[p.dec_perm[ch]], ch, p) * 255.0f);
+          for (int q = 0; q < 4; ++q) v[4 * t + q] = acc[m][t][q] + bias_v[4 * t + q];
+        if (valid) {
+          char* dst = (char*)p.out + ((((size_t)n * p.oh + oy) * p.ow + ox) * p.cout_stride + cbase) * sizeof(T);
+          if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int h = 0; h < NSUB; h += 2) {
+              if (h + 1 < NSUB) {
+                *(uint4*)(dst + h * 8) = make_uint4(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]),
+                                                    pack_bf16(v[4 * h + 4], v[4 * h + 5]), pack_bf16(v[4 * h + 6], v[4 * h + 7]));
+              } else {
+                *(uint2*)(dst + h * 8) = make_uint2(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]));
+              }
+            }
+          } else {
+#pragma unroll
+            for (int t = 0; t < NSUB; ++t)
+              *(float4*)(dst + t * 16) = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4 * NSUB; ++j) { s1[j] += v[j]; s2[j] += v[j] * v[j]; }
+        }
+      }
+      if (p.partial != nullptr) {
+        // reduce over the 16 pixel lanes of each lane group (one DPP row)
+#pragma unroll
+        for (int j = 0; j < 4 * NSUB; ++j) {
+          s1[j] = row_sum16(s1[j]);
+          s2[j] = row_sum16(s2[j]);
+        }
+        const int rw = MODE == MODE_PHASE ? wave : wm;
+        if constexpr (PERS) {
+          // one partial row per channel-sharing wave (tile*REDW + rw): no barrier, no LDS
+          if (px == 0) {
+            float* dst = p.partial + ((((size_t)n * ntile + wk.tile) * C::REDW + rw) * p.cout_stride +
+                                      cwave + 4 * NSUB * g) * 2;
+#pragma unroll
+            for (int j = 0; j < 4 * NSUB; j += 2)
+              *(float4*)(dst + 2 * j) = make_float4(s1[j], s2[j], s1[j + 1], s2[j + 1]);
+          }
+          return;
+        }
+        __syncthreads();  // LDS tile no longer read (the reduction aliases it)
+        float* red = (float*)(smem + RED_OFF);  // [REDW][BN][2]
+        if (px == 0) {
+#pragma unroll
+          for (int j = 0; j < 4 * NSUB; ++j) {
+            const int cl = cwave - cb * BN + 4 * NSUB * g + j;
+            red[(rw * BN + cl) * 2 + 0] = s1[j];
+            red[(rw * BN + cl) * 2 + 1] = s2[j];
+          }
+        }
+        __syncthreads();
+        for (int cl = tid; cl < BN; cl += NT) {
+          float a = 0.f, b2 = 0.f;
+#pragma unroll
+          for (int rr = 0; rr < C::REDW; ++rr) { a += red[(rr * BN + cl) * 2]; b2 += red[(rr * BN + cl) * 2 + 1]; }
+          float* dst = p.partial + (((size_t)n * ntile + wk.tile) * p.cout_stride + cb * BN + cl) * 2;
+          dst[0] = a;
+          dst[1] = b2;
+        }
+      }
+    } else if constexpr (MODE == MODE_XSHIFT) {
+      // lane (base px, group g) holds rows q = 4g+j = 3*shift + channel (channel order baked
+      // into the packed weights and bias); base px's 15 outputs are bytes 15*px .. 15*px+14
+#pragma unroll
+      for (int m = 0; m < MSUB; ++m) {
+        const int oy = ty0 + wm * MSUB + m;
+        if (oy >= p.oh) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = 4 * g + j;
+          if (q >= 15) continue;
+          const int sft = q / 3, ch = q - 3 * sft;
+          const int ox = tx0 + C::NXS * px + sft;
+          if (ox >= p.ow) continue;
+          float y = acc[m][0][j] + p.bias[q];
+          if (p.dec_tanh) y = tanhf(y);
+          if constexpr (OUTK == OUT_F32_NCHW) {
+            ((float*)p.out)[(((size_t)n * 3 + ch) * p.oh + oy) * p.ow + ox] = y;
+          } else {
+            ((uint8_t*)p.out)[(((size_t)n * p.oh + oy) * p.ow + ox) * 3 + ch] =
+                (uint8_t)(decode_ch(y, ch, p) * 255.0f);  // ToPILImage: pic.mul(255).byte()
+          }
+        }
+      }
+    } else {
+      // STD final layer: 3 output channels live in lane group 0 (channels 0..3 of n-subtile 0)
+      if (g == 0) {
+        const float b0 = p.bias[0], b1 = p.bias[1], b2v = p.bias[2];
+#pragma unroll
+        for (int m = 0; m < MSUB; ++m) {
+          int oy, ox;
+          out_px(m, oy, ox);
+          if (oy >= p.oh || ox >= p.ow) continue;
+          float y[3] = {acc[m][0][0] + b0, acc[m][0][1] + b1, acc[m][0][2] + b2v};
+          if (p.dec_tanh) { y[0] = tanhf(y[0]); y[1] = tanhf(y[1]); y[2] = tanhf(y[2]); }
+          if constexpr (OUTK == OUT_F32_NCHW) {
+            float* o = (float*)p.out;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) o[(((size_t)n * 3 + ch) * p.oh + oy) * p.ow + ox] = y[ch];
+          } else {
+            uint8_t* o = (uint8_t*)p.out + (((size_t)n * p.oh + oy) * p.ow + ox) * 3;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) o[ch] = (uint8_t)(decode_ch(y[p.dec_perm[ch]], ch, p) * 255.0f);
+          }
         }
       }
     }
+  };
+
+  AccT acc;
+  auto no_hook = [](int) {};
+  if constexpr (PERS) {
+    // part q of the next tile is stored at the first stage barrier after which no read of chunk
+    // group q remains (the barrier after step s follows the reads of steps <= s+1)
+    constexpr int TAPS = C::ROWS * C::KPR;
+    auto part_stage = [](int q) { return ((q + 1) * TAPS - 2 + SC - 1) / SC; };  // ceil((.)/SC)
+    static_assert(part_stage(0) >= 2, "part 0 is issued after stage 1's barrier");
+    float2* norm_l = (float2*)(smem + NORM_OFF);
+    auto load_norm_table = [&](int n) {
+      if (p.in_norm != nullptr)
+        for (int t = tid; t < CINP; t += NT) norm_l[t] = p.in_norm[(size_t)n * p.cs + t];
+    };
+    uint4 praw[IPP];
+    // prologue: tile w staged part by part, weight stages 0/1 in ring slots 0/1, RR stages in flight
+    build_maps(cur, 0);
+    load_norm_table(cur.n);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NPART; ++q) {
+      issue_part(cur, 0, q, praw);
+      write_part(0, q, praw, norm_l);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      wl_store(j * STG_BYTES);
+      wl_issue((j + RR) % NSTG);
+    }
+    __syncthreads();
+    int wnext = w + (int)gridDim.x;
+    int rot = 0;  // ring slot of the current tile's stage 0
+    for (int it = 0;; ++it) {
+      const bool more = wnext < p.n_work;
+      const Work nxt = more ? decode_work(wnext) : cur;
+      const int ns = (it + 1) & 1;  // map slot of the next tile
+      kloop(acc, rot, [&](int k) {
+        if (!more) return;
+        if (k == 0) {  // the current tile's halo is complete: reuse the table and the other map slot
+          build_maps(nxt, ns);
+          load_norm_table(nxt.n);
+        }
+        if (k == 1) issue_part(nxt, ns, 0, praw);
+#pragma unroll
+        for (int q = 0; q < NPART; ++q) {
+          if (k == part_stage(q) && k < NSTG) {
+            write_part(ns, q, praw, norm_l);
+            if (q + 1 < NPART) issue_part(nxt, ns, q + 1, praw);
+          }
+        }
+      });
+      if constexpr (part_stage(NPART - 1) >= NSTG) {
+        // the last part(s) have no stage barrier after their reads: store after the K loop
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NPART; ++q) {
+          if (more && part_stage(q) >= NSTG) {
+            write_part(ns, q, praw, norm_l);
+            if (q + 1 < NPART) issue_part(nxt, ns, q + 1, praw);
+          }
+        }
+      }
+      epilogue(cur, acc);
+      if (!more) break;
+      __syncthreads();  // publishes the next tile's halo parts
+      cur = nxt;
+      wnext += (int)gridDim.x;
+      rot = (rot + NSTG) % 3;
+    }
+  } else {
+    if constexpr (INK == IN_ACT) {
+      uint4 raw[IPT];
+      int srcs[IPT];
+      float2 nmc[C::CPC];
+      build_maps(cur, 0);
+      __syncthreads();
+      issue_loads(cur, 0, raw, srcs);
+      load_norm(cur.n, nmc);
+      stage(cur, raw, srcs, nmc);
+    } else {
+      stage_image(cur);
+    }
+    if constexpr (WL) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (j < NSTG) {
+          wl_store(j * STG_BYTES);
+          if (j + RR < NSTG) wl_issue(j + RR);
+        }
+      }
+    }
+    __syncthreads();
+    kloop(acc, 0, no_hook);
+    epilogue(cur, acc);
   }
 }
 
 // Instantiation helper: a launcher + a registry entry.
-template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW, int WM, int WN, int INK, int OUTK>
+template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW, int WM, int WN, int INK, int OUTK,
+          int VAR = 0>
 struct ConvInst {
   using C = ConvCfg<T, MODE, KS, S, CINP, BN, TH, TW, WM, WN>;
-  static void launch(const ConvParams& p, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL((conv_kernel<T, MODE, KS, S, CINP, BN, TH, TW, WM, WN, INK, OUTK>), grid, dim3(C::NT), 0, st, p);
+  static constexpr bool PERS = (VAR & VAR_PERS) != 0;
+  static constexpr auto kernel = conv_kernel<T, MODE, KS, S, CINP, BN, TH, TW, WM, WN, INK, OUTK, VAR>;
+  // resident workgroups of the persistent form on this device (CUs x occupancy)
+  static int resident_blocks() {
+    static const int slots = [] {
+      int dev = 0, cus = 0, occ = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, C::NT, 0) != hipSuccess || occ < 1) occ = 1;
+      return cus * occ;
+    }();
+    return slots;
+  }
+  static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
+    if constexpr (PERS) {
+      ConvParams p = p0;
+      p.n_work = (int)(grid.x * grid.y);
+      const int nb = p.n_work < resident_blocks() ? p.n_work : resident_blocks();
+      hipLaunchKernelGGL(kernel, dim3(nb), dim3(C::NT), 0, st, p);
+    } else {
+      hipLaunchKernelGGL(kernel, grid, dim3(C::NT), 0, st, p0);
+    }
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
@@ -585,6 +988,9 @@ struct ConvInst {
     k.in_kind = INK; k.out_kind = OUTK;
     k.pair = C::PAIR ? 1 : 0; k.nch = C::NCH; k.cpc = C::CPC; k.kp = C::KP; k.nchunk = C::NCHUNK;
     k.nstep = C::NSTEP; k.nstep_pack = C::NSTEP_PACK; k.nsubt = C::NSUBT; k.nsub = C::NSUB; k.lds_bytes = C::LDS_ALLOC;
+    k.persistent = PERS ? 1 : 0;
+    k.korder = PERS ? 1 : 0;
+    k.part_rows = PERS ? C::REDW : 1;
     k.launch = &launch;
     return k;
   }

@@ -7,7 +7,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdio>
+#include <algorithm>
 #include <cstring>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <vector>
@@ -21,17 +24,27 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 const ConvKernelInfo* conv_table_bf16(int* count);
+const ConvKernelInfo* conv_table_bf16_wl(int* count);
 const ConvKernelInfo* conv_table_f32(int* count);
 
+// first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind) {
-  int count = 0;
-  const ConvKernelInfo* t = dtype == NST_DT_BF16 ? conv_table_bf16(&count) : conv_table_f32(&count);
-  for (int i = 0; i < count; ++i) {
-    const ConvKernelInfo& k = t[i];
-    if (k.mode == mode && k.ks == ks && k.stride == stride && k.cinp == cinp && k.bn == bn &&
-        k.in_kind == in_kind && k.out_kind == out_kind)
-      return &k;
+  typedef const ConvKernelInfo* (*TableFn)(int*);
+  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_bf16};
+  const TableFn tables_f32[] = {conv_table_f32};
+  const TableFn* tables = dtype == NST_DT_BF16 ? tables_bf16 : tables_f32;
+  const int ntables = dtype == NST_DT_BF16 ? 2 : 1;
+  static const bool no_wl = std::getenv("NST_NO_PERSISTENT") != nullptr;  // experiment switch
+  for (int ti = (dtype == NST_DT_BF16 && no_wl) ? 1 : 0; ti < ntables; ++ti) {
+    int count = 0;
+    const ConvKernelInfo* t = tables[ti](&count);
+    for (int i = 0; i < count; ++i) {
+      const ConvKernelInfo& k = t[i];
+      if (k.mode == mode && k.ks == ks && k.stride == stride && k.cinp == cinp && k.bn == bn &&
+          k.in_kind == in_kind && k.out_kind == out_kind)
+        return &k;
+    }
   }
   return nullptr;
 }
@@ -209,7 +222,10 @@ std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, cons
       for (int tg = 0; tg < k.nsubt; ++tg)
         for (int lane = 0; lane < 64; ++lane) {
           const int q = lane & 15, g = lane >> 4;
-          const int i = 4 * s + g;
+          // korder 1 (persistent kernels): packed step s runs chunk group s / taps of tap s % taps
+          const int taps = k.nchunk / k.nch;
+          const int sl = k.korder ? (s % taps) * (k.nch / 4) + s / taps : s;
+          const int i = 4 * sl + g;
           float* dst = &out[((((size_t)cb * k.nstep_pack + s) * k.nsubt + tg) * 64 + lane) * k.cpc];
           if (i >= k.nchunk) continue;
           const int tap = i / k.nch, c = i % k.nch;
@@ -359,7 +375,7 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         int ttx, tty;
         tile_grid(*Ly.k_main, sh, sw, ch, cw, &ttx, &tty);
         const int tiles = ttx * tty;
-        const size_t pf = (size_t)n * tiles * Ly.coutp * 2;
+        const size_t pf = (size_t)n * tiles * Ly.k_main->part_rows * Ly.coutp * 2;
         if (pf > P.partial_floats) P.partial_floats = pf;
         const size_t sb = (size_t)n * IN_MAX_SEGMENTS * Ly.coutp * 16;
         if (sb > P.seg_bytes) P.seg_bytes = sb;
@@ -668,6 +684,7 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     p.cout_stride = Ly.coutp;
     tile_grid(*k, p.hs, p.ws, p.oh, p.ow, &p.tiles_x, &p.tiles_y);
     p.n_cblk = Ly.coutp / k->bn;
+    if (k->persistent && p.n_cblk != 1) { set_error("conv " + Ly.d.conv + ": persistent kernel needs one channel block"); return NST_E_SHAPE; }
     p.partial = final_out ? nullptr : partial;
     dim3 grid(p.tiles_x * p.tiles_y, n * p.n_cblk);
     nst_handle::Rec rec{op.layer, nullptr, nullptr};
@@ -684,7 +701,7 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     }
     if (e != hipSuccess) { set_error("conv " + Ly.d.conv + " launch: " + hipGetErrorString(e)); return NST_E_HIP; }
     if (!final_out) {
-      e = launch_in_finalize(partial, n, p.tiles_x * p.tiles_y, Ly.coutp, (double)p.hconv * (double)p.wconv,
+      e = launch_in_finalize(partial, n, p.tiles_x * p.tiles_y * k->part_rows, Ly.coutp, (double)p.hconv * (double)p.wconv,
                              Ly.gamma, Ly.beta, 1e-5f, stats[op.layer], ws + P.off_seg, st);
       if (e != hipSuccess) { set_error(std::string("finalize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
     }

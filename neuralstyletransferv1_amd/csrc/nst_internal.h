@@ -46,7 +46,7 @@ struct ConvParams {
   int cs;       // source channel stride (elements) for IN_ACT
   int axis_mode, pad, pre;
   const float2* in_norm;  // [n][cs] {scale, shift} of the producer's InstanceNorm, or nullptr
-  int in_relu;            // apply ReLU after in_norm
+  int in_relu;            // 1 whenever in_norm is set (the prologue always applies ReLU after the IN)
   // image-input preset encode: x_in[c] = ((x01[perm[c]] * a[c]) - b[c]) / d[c]
   float enc_a[3], enc_b[3], enc_d[3];
   int enc_perm[3];
@@ -62,6 +62,7 @@ struct ConvParams {
   int cout_stride;     // channel stride of OUT_ACT buffers (= padded cout)
   float* partial;      // [n][tiles][cout_stride][2] InstanceNorm partial sums (OUT_ACT), or nullptr
   int tiles_x, tiles_y, n_cblk;
+  int n_work;          // persistent form: work items (frames x channel blocks x tiles)
   // output decode: v[c] = (((y[perm[c]] + p[c]) * q[c]) / r[c]) + s[c]; clamp(0,1)
   float dec_p[3], dec_q[3], dec_r[3], dec_s[3];
   int dec_perm[3];
@@ -76,6 +77,9 @@ struct ConvKernelInfo {
   int ks, stride, cinp, bn, th, tw, wm, wn, in_kind, out_kind;
   // derived
   int pair, nch, cpc, kp, nchunk, nstep, nstep_pack, nsubt, nsub, lds_bytes;
+  int persistent;  // resident workgroups walk the tiles (requires one channel block)
+  int korder;      // packed K order: 0 tap-major, 1 chunk-group-major (persistent kernels)
+  int part_rows;   // InstanceNorm partial rows per tile (persistent: one per channel-sharing wave)
   void (*launch)(const ConvParams&, dim3 grid, hipStream_t);
 };
 
