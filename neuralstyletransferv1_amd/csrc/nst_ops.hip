@@ -96,72 +96,101 @@ hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstrid
 // transformer_net_nst.py:138-142), r either materialised or itself IN+ReLU of a raw conv
 // output (the first block's input, never materialised); ReCoNet ResLayer applies ReLU after
 // the add (model.py:55-60).  16 bytes per thread, NHWC.
+// Thread layout: a block covers tpp pixels x CV channel vectors (CV = c / CPC) per sweep, so each
+// thread keeps ONE channel vector (its IN constants loaded once) and walks RES_UNROLL pixels with
+// all loads issued before use.
+constexpr int RES_UNROLL = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void residual_kernel(const T* __restrict__ y, const float2* __restrict__ ys,
                                                        const T* r, const float2* __restrict__ rs,
-                                                       int r_relu, int relu_out, T* out, int hw, int c,
-                                                       size_t nvec) {
+                                                       int r_relu, int relu_out, T* out, int hw, int c) {
   constexpr int CPC = 16 / (int)sizeof(T);
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nvec) return;
-  const size_t e0 = i * CPC;
-  const int ch0 = (int)(e0 % (size_t)c);
-  const int n = (int)(e0 / ((size_t)c * hw));
-  const float2* ysn = ys + (size_t)n * c + ch0;
-  const float2* rsn = rs ? rs + (size_t)n * c + ch0 : nullptr;
-  float vy[CPC], vr[CPC];
-  if constexpr (sizeof(T) == 2) {
-    const uint4 a = *(const uint4*)(y + e0), b = *(const uint4*)(r + e0);
-    const uint32_t wa[4] = {a.x, a.y, a.z, a.w}, wb[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      vy[2 * j] = __uint_as_float(wa[j] << 16);
-      vy[2 * j + 1] = __uint_as_float(wa[j] & 0xffff0000u);
-      vr[2 * j] = __uint_as_float(wb[j] << 16);
-      vr[2 * j + 1] = __uint_as_float(wb[j] & 0xffff0000u);
-    }
-  } else {
-    const float4 a = *(const float4*)(y + e0), b = *(const float4*)(r + e0);
-    vy[0] = a.x; vy[1] = a.y; vy[2] = a.z; vy[3] = a.w;
-    vr[0] = b.x; vr[1] = b.y; vr[2] = b.z; vr[3] = b.w;
-  }
-  float o[CPC];
+  const int cv_n = c / CPC;
+  const int tpp = blockDim.x / cv_n;  // pixels per sweep
+  const int cv = threadIdx.x % cv_n, pl = threadIdx.x / cv_n;
+  const int n = blockIdx.y;
+  const int ch0 = cv * CPC;
+  float ysc[CPC], ysh[CPC], rsc[CPC], rsh[CPC];
 #pragma unroll
   for (int j = 0; j < CPC; ++j) {
-    float rr = vr[j];
-    if (rsn) {
-      rr = rr * rsn[j].x + rsn[j].y;
-      if (r_relu) rr = fmaxf(rr, 0.f);
-    }
-    float v = vy[j] * ysn[j].x + ysn[j].y;
-    v = rr + v;
-    if (relu_out) v = fmaxf(v, 0.f);
-    o[j] = v;
+    const float2 a = ys[(size_t)n * c + ch0 + j];
+    ysc[j] = a.x; ysh[j] = a.y;
+    rsc[j] = 1.f; rsh[j] = 0.f;
+    if (rs) { const float2 b = rs[(size_t)n * c + ch0 + j]; rsc[j] = b.x; rsh[j] = b.y; }
   }
-  if constexpr (sizeof(T) == 2) {
-    uint32_t w[4];
+  const size_t base = (size_t)n * hw * c + ch0;
+  const int px0 = blockIdx.x * tpp * RES_UNROLL + pl;
+  uint4 va[RES_UNROLL], vb[RES_UNROLL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      __bf16 lo = (__bf16)o[2 * j], hi = (__bf16)o[2 * j + 1];
-      w[j] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+  for (int u = 0; u < RES_UNROLL; ++u) {
+    const int px = px0 + u * tpp;
+    if (px < hw) {
+      va[u] = *(const uint4*)(y + base + (size_t)px * c);
+      vb[u] = *(const uint4*)(r + base + (size_t)px * c);
     }
-    *(uint4*)(out + e0) = make_uint4(w[0], w[1], w[2], w[3]);
-  } else {
-    *(float4*)(out + e0) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+#pragma unroll
+  for (int u = 0; u < RES_UNROLL; ++u) {
+    const int px = px0 + u * tpp;
+    if (px >= hw) continue;
+    float vy[CPC], vr[CPC];
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t wa[4] = {va[u].x, va[u].y, va[u].z, va[u].w}, wb[4] = {vb[u].x, vb[u].y, vb[u].z, vb[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vy[2 * j] = __uint_as_float(wa[j] << 16);
+        vy[2 * j + 1] = __uint_as_float(wa[j] & 0xffff0000u);
+        vr[2 * j] = __uint_as_float(wb[j] << 16);
+        vr[2 * j + 1] = __uint_as_float(wb[j] & 0xffff0000u);
+      }
+    } else {
+      vy[0] = __uint_as_float(va[u].x); vy[1] = __uint_as_float(va[u].y);
+      vy[2] = __uint_as_float(va[u].z); vy[3] = __uint_as_float(va[u].w);
+      vr[0] = __uint_as_float(vb[u].x); vr[1] = __uint_as_float(vb[u].y);
+      vr[2] = __uint_as_float(vb[u].z); vr[3] = __uint_as_float(vb[u].w);
+    }
+    float o[CPC];
+#pragma unroll
+    for (int j = 0; j < CPC; ++j) {
+      float rr = vr[j];
+      if (rs) {
+        rr = rr * rsc[j] + rsh[j];
+        if (r_relu) rr = fmaxf(rr, 0.f);
+      }
+      float v = vy[j] * ysc[j] + ysh[j];
+      v = rr + v;
+      if (relu_out) v = fmaxf(v, 0.f);
+      o[j] = v;
+    }
+    T* dst = out + base + (size_t)px * c;
+    if constexpr (sizeof(T) == 2) {
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        __bf16 lo = (__bf16)o[2 * j], hi = (__bf16)o[2 * j + 1];
+        w[j] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+      }
+      *(uint4*)dst = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      *(float4*)dst = make_float4(o[0], o[1], o[2], o[3]);
+    }
   }
 }
 
 hipError_t launch_residual(int dtype, const void* y, const float2* ys, const void* r, const float2* rs,
                            int r_relu, int relu_out, void* out, int n, int hw, int c, hipStream_t st) {
   const int cpc = dtype == NST_DT_BF16 ? 8 : 4;
-  const size_t nvec = (size_t)n * hw * c / cpc;
-  const unsigned blocks = (unsigned)((nvec + 255) / 256);
+  const int cv_n = c / cpc;
+  if (c % cpc != 0 || cv_n > 256) return hipErrorInvalidValue;
+  const int tpp = 256 / cv_n;
+  const dim3 grid((unsigned)((hw + tpp * RES_UNROLL - 1) / (tpp * RES_UNROLL)), (unsigned)n);
+  const dim3 block((unsigned)(tpp * cv_n));
   if (dtype == NST_DT_BF16)
-    hipLaunchKernelGGL(residual_kernel<__bf16>, dim3(blocks), dim3(256), 0, st, (const __bf16*)y, ys,
-                       (const __bf16*)r, rs, r_relu, relu_out, (__bf16*)out, hw, c, nvec);
+    hipLaunchKernelGGL(residual_kernel<__bf16>, grid, block, 0, st, (const __bf16*)y, ys, (const __bf16*)r, rs,
+                       r_relu, relu_out, (__bf16*)out, hw, c);
   else
-    hipLaunchKernelGGL(residual_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)y, ys,
-                       (const float*)r, rs, r_relu, relu_out, (float*)out, hw, c, nvec);
+    hipLaunchKernelGGL(residual_kernel<float>, grid, block, 0, st, (const float*)y, ys, (const float*)r, rs, r_relu,
+                       relu_out, (float*)out, hw, c);
   return hipGetLastError();
 }
 
