@@ -1,0 +1,68 @@
+"""Per-kernel summary of tools/prof_pass.sh output (rocprofv3 CSV), averaged over dispatches.
+
+  python tools/pmc_summary.py gpurun_out/<tag> [--json out.json]
+
+Prints per kernel: average duration (kernel-trace pass), every PMC counter averaged over its
+dispatches, and derived figures: HBM bytes (gfx950 correction: 2*FETCH_SIZE + WRITE_SIZE, KiB;
+MI355X_MICROARCH.md HBM section), MFMA busy fraction, effective clock from GRBM_GUI_ACTIVE/8.
+Scratch analysis tool, not part of the product."""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+
+def short(k):
+    m = re.search(r"conv_kernelI(DF16b|f)Li(\d)ELi(\d)ELi(\d)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)E", k)
+    if m:
+        t, mode, ks, s, ci, bn, th, tw, wm, wn, ink, outk, var = m.groups()
+        return f"conv{'b' if t == 'DF16b' else 'f'} md{mode} k{ks}s{s} ci{ci} bn{bn} {th}x{tw} w{wm}x{wn} in{ink} out{outk} v{var}"
+    m = re.search(r"conv_kernel<[^>]*>", k)
+    if m:
+        return m.group(0)[:90]
+    return re.sub(r"\(.*", "", k)[:70]
+
+
+def load(d):
+    dur = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "stats", "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    ctr = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
+    for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            ctr[r["Kernel_Name"]][r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+    return dur, ctr
+
+
+def main():
+    d = sys.argv[1]
+    dur, ctr = load(d)
+    out = {}
+    names = sorted(set(dur) | set(ctr), key=lambda k: -sum(dur.get(k, [0])))
+    for k in names:
+        if "copyBuffer" in k or "fillBuffer" in k:
+            continue
+        ds = dur.get(k, [])
+        rec = {"launches_traced": len(ds), "avg_us": (sum(ds) / len(ds) / 1e3) if ds else None,
+               "total_us": sum(ds) / 1e3}
+        for c, per in ctr.get(k, {}).items():
+            rec[c] = sum(per.values()) / len(per)
+        if "FETCH_SIZE" in rec and "WRITE_SIZE" in rec:
+            rec["hbm_bytes"] = (2 * rec["FETCH_SIZE"] + rec["WRITE_SIZE"]) * 1024
+        if "GRBM_GUI_ACTIVE" in rec and rec.get("avg_us"):
+            rec["eff_clock_ghz"] = rec["GRBM_GUI_ACTIVE"] / 8 / (rec["avg_us"] * 1e3)
+        out[k] = rec
+        print(f"== {short(k)}   avg {rec['avg_us'] or 0:.1f} us x{len(ds)}")
+        print("   " + "  ".join(f"{c.replace('SQ_', '')}={v:.4g}" for c, v in sorted(rec.items())
+                              if c not in ("launches_traced", "avg_us", "total_us") and v is not None))
+    if "--json" in sys.argv:
+        with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
