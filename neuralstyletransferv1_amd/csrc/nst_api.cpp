@@ -26,15 +26,16 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 const ConvKernelInfo* conv_table_bf16(int* count);
 const ConvKernelInfo* conv_table_bf16_wl(int* count);
 const ConvKernelInfo* conv_table_f32(int* count);
+const ConvKernelInfo* conv_table_out9(int* count);
 
 // first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
-  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_bf16};
+  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_out9, conv_table_bf16};
   const TableFn tables_f32[] = {conv_table_f32};
   const TableFn* tables = dtype == NST_DT_BF16 ? tables_bf16 : tables_f32;
-  const int ntables = dtype == NST_DT_BF16 ? 2 : 1;
+  const int ntables = dtype == NST_DT_BF16 ? 3 : 1;
   static const bool no_wl = std::getenv("NST_NO_PERSISTENT") != nullptr;  // experiment switch
   for (int ti = (dtype == NST_DT_BF16 && no_wl) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
@@ -271,6 +272,24 @@ std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, cons
   return out;
 }
 
+// MODE_KYROT weight table (conv_out9.hip): [ky][kx][kc][c][16 input channels], kc = 16-channel
+// block of the (padded) input channels, c = model output channel 0..2.
+std::vector<float> pack_kyrot_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
+  const int kc_n = k.cinp / 16;
+  std::vector<float> out((size_t)k.wbytes / 2, 0.f);
+  for (int ky = 0; ky < 9; ++ky)
+    for (int kx = 0; kx < 9; ++kx)
+      for (int kc = 0; kc < kc_n; ++kc)
+        for (int c = 0; c < 3; ++c)
+          for (int j = 0; j < 16; ++j) {
+            const int ci = kc * 16 + j;
+            if (ci >= d.cin) continue;
+            out[((((size_t)ky * 9 + kx) * kc_n + kc) * 3 + c) * 16 + j] =
+                W[(((size_t)c * d.cin + ci) * d.ks + ky) * d.ks + kx];
+          }
+  return out;
+}
+
 // bias rows of an x-shift layer: row q = 3*s + c -> bias of output channel (perm) c
 std::vector<float> xshift_bias(const float* b, bool reverse_channels) {
   std::vector<float> r(16, 0.f);
@@ -496,7 +515,10 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     const bool up = d.axis_mode == AX_REFLECT_UP2 || d.axis_mode == AX_ZINSERT;
     std::vector<int> modes;
     if (up) modes.push_back(MODE_PHASE);
-    if (final_layer && d.cout == 3) modes.push_back(MODE_XSHIFT);
+    if (final_layer && d.cout == 3) {
+      if (!std::getenv("NST_NO_KYROT")) modes.push_back(MODE_KYROT);  // experiment switch
+      modes.push_back(MODE_XSHIFT);
+    }
     modes.push_back(MODE_STD);
     for (int mode : modes) {
       Ly.k_main = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk);
@@ -528,7 +550,11 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
       }
       return upload(pk.data(), pk.size() * 4, dst);
     };
-    if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) break;
+    if (Ly.mode == MODE_KYROT) {
+      if ((rc = upload_packed(pack_kyrot_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
+    } else if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) {
+      break;
+    }
     std::vector<float> bp(Ly.coutp, 0.f), gp(Ly.coutp, 0.f), btp(Ly.coutp, 0.f);
     for (int c = 0; c < d.cout; ++c) {
       bp[c] = b[c];

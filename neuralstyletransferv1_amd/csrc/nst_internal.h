@@ -37,7 +37,7 @@ enum OutKind { OUT_ACT = 0, OUT_U8_NHWC = 1, OUT_F32_NCHW = 2 };
 enum AxisMode { AX_REFLECT = 0, AX_REFLECT_UP2 = 1, AX_ZERO = 2, AX_ZERO_PREREFLECT = 3, AX_ZINSERT = 4, AX_CLAMP = 5 };
 
 // conv_kernel mappings (see conv_impl.h)
-enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2 };
+enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2, MODE_KYROT = 3 };  // KYROT: conv_out9.hip
 
 struct ConvParams {
   // input
@@ -67,6 +67,7 @@ struct ConvParams {
   float dec_p[3], dec_q[3], dec_r[3], dec_s[3];
   int dec_perm[3];
   int dec_tanh;  // apply tanh to the raw output first (ReCoNet ConvTanhLayer, model.py:77-80)
+  int seg_len;    // MODE_KYROT: output rows per work item (set by the launcher)
   int ph_off[2];  // MODE_PHASE: LDS row/col offset of sub-pixel phase 0/1 ({0,1} nearest-up, {1,1} ConvTranspose)
 };
 
@@ -80,6 +81,7 @@ struct ConvKernelInfo {
   int persistent;  // resident workgroups walk the tiles (requires one channel block)
   int korder;      // packed K order: 0 tap-major, 1 chunk-group-major (persistent kernels)
   int part_rows;   // InstanceNorm partial rows per tile (persistent: one per channel-sharing wave)
+  int wbytes;      // MODE_KYROT: bytes of the packed weight table
   void (*launch)(const ConvParams&, dim3 grid, hipStream_t);
 };
 

@@ -149,3 +149,28 @@ def test_gram_vs_reference_golden():
     assert np.abs(G - z["G"]).max() / np.abs(z["G"]).max() < 1e-5
     Gb = gram_matrix(F.to(torch.bfloat16)).cpu().numpy()
     assert np.abs(Gb - z["G"]).max() / np.abs(z["G"]).max() < 2e-2
+
+
+@pytest.mark.parametrize("arch,h,w,preset", [
+    ("johnson", 96, 200, "imagenet_255"),   # partial strip (200 = 2x96 + 8)
+    ("johnson", 37, 61, "caffe_bgr"),       # ragged + BGR decode permutation
+    ("nst", 72, 100, "raw_01"),             # zero padding + centre crop
+    ("reconet", 48, 84, "tanh"),            # 48 -> 64 padded channels, tanh output
+])
+def test_bf16_output_conv_mappings_agree(arch, h, w, preset, monkeypatch):
+    """The row-streaming ky-rotation output conv (conv_out9.hip) against the x-shift / plain
+    implicit-GEMM mapping of the same layer: same bf16 operands, fp32 accumulation in another
+    order, so u8 frames agree to 1 LSB and raw outputs to fp32 rounding."""
+    sd_seed = 4
+    frames = torch.from_numpy(synthetic.make_frames(2, h, w, seed=7)).cuda()
+    fast = _net(arch, sd_seed, "bf16")
+    a = fast.stylize_frames(frames, preset).cpu().numpy()
+    x = torch.randn(2, 3, h, w, generator=torch.Generator().manual_seed(0)).cuda()
+    ya = fast(x).cpu().numpy()
+    monkeypatch.setenv("NST_NO_KYROT", "1")
+    slow = _net(arch, sd_seed, "bf16")
+    b = slow.stylize_frames(frames, preset).cpu().numpy()
+    yb = slow(x).cpu().numpy()
+    d = np.abs(a.astype(int) - b.astype(int))
+    assert d.max() <= 1 and (d > 0).mean() < 0.01, (d.max(), (d > 0).mean())
+    assert np.abs(ya - yb).max() <= 1e-4 * np.abs(yb).max() + 1e-6
