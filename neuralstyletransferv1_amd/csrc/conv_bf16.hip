@@ -24,6 +24,11 @@ const ConvKernelInfo* conv_table_bf16(int* count) {
       E(B, SD, 3, 2, 128, 192, 4, 16, 2, 2, IN_ACT, OUT_ACT),
       E(B, SD, 3, 1, 192, 192, 8, 16, 2, 2, IN_ACT, OUT_ACT),
       E(B, PH, 3, 1, 192, 128, 2, 16, 1, 4, IN_ACT, OUT_ACT),
+      // consumers of the residual stream (residual join fused into the fill)
+      E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
+      E(B, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
+      E(B, SD, 3, 1, 192, 192, 8, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
+      E(B, PH, 3, 1, 192, 128, 2, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
       E(B, SD, 9, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
       E(B, SD, 9, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
   };

@@ -11,7 +11,8 @@ constexpr int WLP = VAR_WL | VAR_PERS;
 const ConvKernelInfo* conv_table_bf16_wl(int* count) {
   static const ConvKernelInfo table[] = {
       //  T  MODE KS S CINP BN TH TW WM WN  IN      OUT      VAR
-      E(B, SD, 3, 1, 128, 128, 16, 16, 4, 2, IN_ACT, OUT_ACT, WLP),  // residual trunk
+      E(B, SD, 3, 1, 128, 128, 16, 16, 4, 2, IN_ACT, OUT_ACT, WLP),            // residual trunk
+      E(B, SD, 3, 1, 128, 128, 16, 16, 4, 2, IN_ACT, OUT_ACT, WLP | VAR_RES),  // + residual join
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

@@ -26,6 +26,11 @@ const ConvKernelInfo* conv_table_f32(int* count) {
       E(F, SD, 3, 1, 192, 192, 4, 16, 2, 2, IN_ACT, OUT_ACT),
       E(F, PH, 3, 1, 192, 96, 2, 16, 1, 4, IN_ACT, OUT_ACT),
       E(F, PH, 3, 1, 96, 48, 4, 16, 1, 4, IN_ACT, OUT_ACT),
+      // consumers of the residual stream (residual join fused into the fill)
+      E(F, SD, 3, 1, 128, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
+      E(F, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
+      E(F, SD, 3, 1, 192, 192, 4, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
+      E(F, PH, 3, 1, 192, 96, 2, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
       E(F, SD, 9, 1, 48, 16, 2, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
       E(F, SD, 9, 1, 48, 16, 2, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
   };

@@ -187,6 +187,41 @@ __device__ __forceinline__ uint4 norm_chunk(uint4 raw, const float2* nm) {
   }
 }
 
+// Residual join, fused into the consumer conv's fill (ResidualBlock.forward transformer_net.py:71-76,
+// transformer_net_nst.py:138-142; ReCoNet ResLayer model.py:55-60 adds the ReLU after the sum):
+//   v = IN_y(y) + (rn ? ReLU(IN_r(r)) : r)  [then ReLU if relu_out]
+// in the residual kernel's fp32 arithmetic (product, then sum: no contraction) with one rounding.
+template <typename T>
+__device__ __forceinline__ uint4 res_chunk(uint4 y, uint4 r, const float2* yn, const float2* rn, bool has_rn,
+                                           bool relu_out) {
+  constexpr int CPC = 16 / (int)sizeof(T);
+  float fy[CPC], fr[CPC], o[CPC];
+  const uint32_t wy[4] = {y.x, y.y, y.z, y.w}, wr[4] = {r.x, r.y, r.z, r.w};
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fy[2 * j] = bf16_lo(wy[j]); fy[2 * j + 1] = bf16_hi(wy[j]);
+      fr[2 * j] = bf16_lo(wr[j]); fr[2 * j + 1] = bf16_hi(wr[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { fy[j] = __uint_as_float(wy[j]); fr[j] = __uint_as_float(wr[j]); }
+  }
+#pragma unroll
+  for (int j = 0; j < CPC; ++j) {
+    float rr = fr[j];
+    if (has_rn) rr = fmaxf(rr * rn[j].x + rn[j].y, 0.f);
+    float v = fy[j] * yn[j].x + yn[j].y;
+    v = rr + v;
+    o[j] = relu_out ? fmaxf(v, 0.f) : v;
+  }
+  if constexpr (sizeof(T) == 2) {
+    return make_uint4(pack_bf16(o[0], o[1]), pack_bf16(o[2], o[3]), pack_bf16(o[4], o[5]), pack_bf16(o[6], o[7]));
+  } else {
+    return make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
+  }
+}
+
 // One 16-byte LDS entry of an image-input layer (3 channels, preset encode fused):
 // PAIR -> pixels vx, vx+1 (4 bf16 each); else one pixel (4 f32).
 template <typename T, int INK, bool PAIR>
@@ -243,7 +278,8 @@ __device__ __forceinline__ float decode_ch(float y, int ch, const ConvParams& p)
 //            through a 3-stage LDS ring, instead of every wave streaming its own fragments from L2.
 //            L2 weight traffic per output pixel drops by the number of waves sharing a channel range,
 //            which is what bounds the register-streamed form on the wide (128-192 channel) layers.
-enum { VAR_PERS = 1, VAR_WL = 2 };
+//  VAR_RES   residual join fused into the fill (ConvParams::res_r): a second source per halo item.
+enum { VAR_PERS = 1, VAR_WL = 2, VAR_RES = 4 };
 
 // Weight-ring stage: SC K-steps (all NSUBT fragments of each), split evenly over the NW waves.
 template <int NSTEP, int NSUBT, int NW>
@@ -280,7 +316,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
   constexpr int RING_OFF = C::MAP_OFF + (PERS ? 2 : 1) * MAPB;
   constexpr int BIAS_OFF = RING_OFF + (WL ? 3 * STG_BYTES : 0);
   constexpr int NORM_OFF = BIAS_OFF + (WL ? BN * 4 : 0);       // PERS: next frame's IN {scale, shift}
-  constexpr int RING_END = NORM_OFF + (PERS ? CINP * 8 : 0);
+  constexpr int RING_END = NORM_OFF + (PERS ? 2 * CINP * 8 : 0);
   constexpr int RED_OFF = PERS ? RING_END : 0;
   constexpr int LDS_TOTAL0 = PERS ? RED_OFF + C::RED_BYTES : RING_END;
   constexpr int LDS_TOTAL = LDS_TOTAL0 > C::LDS_ALLOC ? LDS_TOTAL0 : C::LDS_ALLOC;
@@ -430,38 +466,73 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
     const int co = ok ? colmap[lx] : -1;
     return (ro >= 0 && co >= 0) ? ro + co + c * 16 : -1;
   };
+  // residual join fused into the fill (p.res_r): second source, optional residual-stream write of
+  // the tile's own pixels (plain stride-1 convs: those halo entries are the pixels themselves)
+  constexpr bool CAN_RESOUT = MODE == MODE_STD && S == 1 && INK == IN_ACT;
+  constexpr bool resf = INK == IN_ACT && (VAR & VAR_RES) != 0;
+  const bool has_rn = p.res_rnorm != nullptr;
+  const size_t frame_bytes = (size_t)p.hs * p.ws * p.cs * sizeof(T);
+  // halo entry (ly, lx) of tile wk is one of the tile's own output pixels
+  auto interior = [&](const Work& wk, int ly, int lx) -> bool {
+    return ly >= p.pad && ly < p.pad + TH && lx >= p.pad && lx < p.pad + TW && wk.ty0 + ly - p.pad < p.oh &&
+           wk.tx0 + lx - p.pad < p.ow;
+  };
   // srcs[k] keeps each item's source offset (-1 = zero padding) for the store pass
-  auto issue_loads = [&](const Work& wk, int slot, uint4 (&raw)[IPT], int (&srcs)[IPT]) {
-    const char* img = (const char*)p.in + (size_t)wk.n * p.hs * p.ws * p.cs * sizeof(T);
+  auto issue_loads = [&](const Work& wk, int slot, uint4 (&raw)[IPT], uint4 (&raw2)[IPT], int (&srcs)[IPT]) {
+    const char* img = (const char*)p.in + (size_t)wk.n * frame_bytes;
+    const char* img2 = (const char*)p.res_r + (size_t)wk.n * frame_bytes;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       int e, c;
       const int src = item_src(slot, k, e, c);
       srcs[k] = src;
       raw[k] = make_uint4(0u, 0u, 0u, 0u);
-      if (src >= 0) raw[k] = *(const uint4*)(img + (unsigned)src);
+      raw2[k] = make_uint4(0u, 0u, 0u, 0u);
+      if (src >= 0) {
+        raw[k] = *(const uint4*)(img + (unsigned)src);
+        if (resf) raw2[k] = *(const uint4*)(img2 + (unsigned)src);
+      }
     }
   };
-  auto load_norm = [&](int n, float2 (&nmc)[C::CPC]) {
+  auto load_norm = [&](int n, float2 (&nmc)[C::CPC], float2 (&rnmc)[C::CPC]) {
     if (FIXED_CHUNK && p.in_norm != nullptr) {
 #pragma unroll
       for (int j = 0; j < C::CPC; ++j) nmc[j] = p.in_norm[(size_t)n * p.cs + c_fixed * C::CPC + j];
     }
+    if (FIXED_CHUNK && resf && has_rn) {
+#pragma unroll
+      for (int j = 0; j < C::CPC; ++j) rnmc[j] = p.res_rnorm[(size_t)n * p.cs + c_fixed * C::CPC + j];
+    }
   };
-  auto stage = [&](const Work& wk, const uint4 (&raw)[IPT], const int (&srcs)[IPT], const float2 (&nmc)[C::CPC]) {
+  auto stage = [&](const Work& wk, const uint4 (&raw)[IPT], const uint4 (&raw2)[IPT], const int (&srcs)[IPT],
+                   const float2 (&nmc)[C::CPC], const float2 (&rnmc)[C::CPC]) {
+    char* rout = (char*)p.res_out + (size_t)wk.n * frame_bytes;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const int it = tid + k * NT;
       if (it < NITEMS) {
         const int e = it / NCH, c = FIXED_CHUNK ? c_fixed : it - e * NCH;
         uint4 v = raw[k];
-        if (srcs[k] >= 0 && p.in_norm != nullptr) {
+        if (srcs[k] >= 0 && (resf || p.in_norm != nullptr)) {
+          float2 nmv[C::CPC], rnv[C::CPC];
           if constexpr (FIXED_CHUNK) {
-            v = norm_chunk<T>(v, nmc);
-          } else {
-            float2 nmv[C::CPC];
 #pragma unroll
-            for (int j = 0; j < C::CPC; ++j) nmv[j] = p.in_norm[(size_t)wk.n * p.cs + c * C::CPC + j];
+            for (int j = 0; j < C::CPC; ++j) { nmv[j] = nmc[j]; rnv[j] = rnmc[j]; }
+          } else {
+#pragma unroll
+            for (int j = 0; j < C::CPC; ++j) {
+              nmv[j] = p.in_norm[(size_t)wk.n * p.cs + c * C::CPC + j];
+              rnv[j] = has_rn && resf ? p.res_rnorm[(size_t)wk.n * p.cs + c * C::CPC + j] : make_float2(1.f, 0.f);
+            }
+          }
+          if (resf) {
+            v = res_chunk<T>(v, raw2[k], nmv, rnv, has_rn, p.res_relu != 0);
+            if constexpr (CAN_RESOUT) {
+              int ly, lx;
+              if (p.res_out != nullptr && entry_xy(e, ly, lx) && interior(wk, ly, lx))
+                *(uint4*)(rout + (unsigned)srcs[k]) = v;
+            }
+          } else {
             v = norm_chunk<T>(v, nmv);
           }
         }
@@ -475,45 +546,77 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
   constexpr int NPART = C::NCH4;
   constexpr int PITEMS = C::NENT * 4;
   constexpr int IPP = (PITEMS + NT - 1) / NT;
-  int tid_p = tid;  // laundered per use: part item addresses are recomputed, not held across the K loop
-  auto part_src = [&](int slot, int q, int k, int& e, int& c) -> int {
+  // The next tile's item sources are resolved ONCE per tile (psrc: part-0 byte offset in the frame,
+  // -1 = zero padding / no item; part q adds 64*q), with the interior flags of the residual-stream
+  // write in pint.  Loads are raw buffer loads (frame base in SGPRs, one VGPR offset, no branch),
+  // so the wait counter stays countable across the K loop; an invalid item loads offset 0 and is
+  // replaced by zero at write time.
+  int psrc[IPP];
+  unsigned pint = 0;
+  int tid_p = tid;  // laundered per use: LDS item addresses are recomputed, not held across the K loop
+  auto part_items = [&](const Work& wk, int slot) {
     const int* rowmap = (const int*)(smem + C::MAP_OFF + slot * MAPB);
     const int* colmap = rowmap + C::LH;
+    pint = 0;
+#pragma unroll
+    for (int k = 0; k < IPP; ++k) {
+      const int it = tid + k * NT;
+      int ly, lx;
+      const bool ok = entry_xy(it >> 2, ly, lx) && it < PITEMS;
+      const int ro = ok ? rowmap[ly] : -1;
+      const int co = ok ? colmap[lx] : -1;
+      psrc[k] = (ro >= 0 && co >= 0) ? ro + co + (it & 3) * 16 : -1;
+      if (CAN_RESOUT && ok && interior(wk, ly, lx)) pint |= 1u << k;
+    }
+  };
+  auto frame_rsrc = [&](const void* base, int n) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (size_t)n * frame_bytes), (short)0,
+                                             (int)frame_bytes, 0x00020000);
+  };
+  auto issue_part = [&](const Work& wk, int q, uint4 (&praw)[IPP], uint4 (&praw2)[IPP]) {
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(p.in, wk.n);
+#pragma unroll
+    for (int k = 0; k < IPP; ++k) {
+      const uint32_t off = psrc[k] >= 0 ? (uint32_t)(psrc[k] + 64 * q) : 0u;
+      praw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+    if (resf) {
+      const __amdgpu_buffer_rsrc_t rs2 = frame_rsrc(p.res_r, wk.n);
+#pragma unroll
+      for (int k = 0; k < IPP; ++k) {
+        const uint32_t off = psrc[k] >= 0 ? (uint32_t)(psrc[k] + 64 * q) : 0u;
+        praw2[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs2, off, 0, 0));
+      }
+    }
+  };
+  // the IN constants of the part's frame come from the LDS tables (norm_l: producer / residual y,
+  // rnorm_l: residual r)
+  auto write_part = [&](const Work& wk, int q, const uint4 (&praw)[IPP], const uint4 (&praw2)[IPP],
+                        const float2* norm_l, const float2* rnorm_l) {
+    float2 nm[C::CPC], rnm[C::CPC];
+    const int cq = (4 * q + (tid & 3)) * C::CPC;
+#pragma unroll
+    for (int j = 0; j < C::CPC; ++j) {
+      nm[j] = p.in_norm != nullptr ? norm_l[cq + j] : make_float2(1.f, 0.f);
+      rnm[j] = resf && has_rn ? rnorm_l[cq + j] : make_float2(1.f, 0.f);
+    }
+    char* rout = (char*)p.res_out + (size_t)wk.n * frame_bytes;
     asm volatile("" : "+v"(tid_p));
-    const int it = tid_p + k * NT;
-    e = it >> 2;
-    c = 4 * q + (it & 3);
-    int ly, lx;
-    const bool ok = entry_xy(e, ly, lx) && it < PITEMS;
-    const int ro = ok ? rowmap[ly] : -1;
-    const int co = ok ? colmap[lx] : -1;
-    return (ro >= 0 && co >= 0) ? ro + co + c * 16 : -1;
-  };
-  auto issue_part = [&](const Work& wk, int slot, int q, uint4 (&praw)[IPP]) {
-    const char* img = (const char*)p.in + (size_t)wk.n * p.hs * p.ws * p.cs * sizeof(T);
 #pragma unroll
     for (int k = 0; k < IPP; ++k) {
-      int e, c;
-      const int src = part_src(slot, q, k, e, c);
-      praw[k] = make_uint4(0u, 0u, 0u, 0u);
-      if (src >= 0) praw[k] = *(const uint4*)(img + (unsigned)src);
-    }
-  };
-  // the IN constants of the part's frame come from the LDS table (norm_l)
-  auto write_part = [&](int slot, int q, const uint4 (&praw)[IPP], const float2* norm_l) {
-    float2 nm[C::CPC];
-    if (p.in_norm != nullptr) {
-#pragma unroll
-      for (int j = 0; j < C::CPC; ++j) nm[j] = norm_l[(4 * q + (tid & 3)) * C::CPC + j];
-    }
-#pragma unroll
-    for (int k = 0; k < IPP; ++k) {
-      if (tid + k * NT < PITEMS) {
-        int e, c;
-        const int src = part_src(slot, q, k, e, c);
-        uint4 v = praw[k];
-        if (src >= 0 && p.in_norm != nullptr) v = norm_chunk<T>(v, nm);
-        *(uint4*)(smem + e * EB + 16 * c) = v;
+      const int it = tid_p + k * NT;
+      if (it < PITEMS) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);  // zero padding stays zero (pad after IN + ReLU)
+        if (psrc[k] >= 0) {
+          if (resf) {
+            v = res_chunk<T>(praw[k], praw2[k], nm, rnm, has_rn, p.res_relu != 0);
+            if (CAN_RESOUT && ((pint >> k) & 1u) && p.res_out != nullptr)
+              *(uint4*)(rout + (unsigned)(psrc[k] + 64 * q)) = v;
+          } else {
+            v = p.in_norm != nullptr ? norm_chunk<T>(praw[k], nm) : praw[k];
+          }
+        }
+        *(uint4*)(smem + (it >> 2) * EB + (it & 3) * 16 + 64 * q) = v;
       }
     }
   };
@@ -865,19 +968,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
     auto part_stage = [](int q) { return ((q + 1) * TAPS - 2 + SC - 1) / SC; };  // ceil((.)/SC)
     static_assert(part_stage(0) >= 2, "part 0 is issued after stage 1's barrier");
     float2* norm_l = (float2*)(smem + NORM_OFF);
+    float2* rnorm_l = norm_l + CINP;
     auto load_norm_table = [&](int n) {
       if (p.in_norm != nullptr)
         for (int t = tid; t < CINP; t += NT) norm_l[t] = p.in_norm[(size_t)n * p.cs + t];
+      if (resf && has_rn)
+        for (int t = tid; t < CINP; t += NT) rnorm_l[t] = p.res_rnorm[(size_t)n * p.cs + t];
     };
-    uint4 praw[IPP];
+    uint4 praw[IPP], praw2[IPP];
     // prologue: tile w staged part by part, weight stages 0/1 in ring slots 0/1, RR stages in flight
     build_maps(cur, 0);
     load_norm_table(cur.n);
     __syncthreads();
+    part_items(cur, 0);
 #pragma unroll
     for (int q = 0; q < NPART; ++q) {
-      issue_part(cur, 0, q, praw);
-      write_part(0, q, praw, norm_l);
+      issue_part(cur, q, praw, praw2);
+      write_part(cur, q, praw, praw2, norm_l, rnorm_l);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -893,16 +1000,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
       const int ns = (it + 1) & 1;  // map slot of the next tile
       kloop(acc, rot, [&](int k) {
         if (!more) return;
-        if (k == 0) {  // the current tile's halo is complete: reuse the table and the other map slot
+        if (k == 0) {  // the current tile's halo is complete: reuse the tables and the other map slot
           build_maps(nxt, ns);
           load_norm_table(nxt.n);
         }
-        if (k == 1) issue_part(nxt, ns, 0, praw);
+        if (k == 1) {
+          part_items(nxt, ns);
+          issue_part(nxt, 0, praw, praw2);
+        }
 #pragma unroll
         for (int q = 0; q < NPART; ++q) {
           if (k == part_stage(q) && k < NSTG) {
-            write_part(ns, q, praw, norm_l);
-            if (q + 1 < NPART) issue_part(nxt, ns, q + 1, praw);
+            write_part(nxt, q, praw, praw2, norm_l, rnorm_l);
+            if (q + 1 < NPART) issue_part(nxt, q + 1, praw, praw2);
           }
         }
       });
@@ -912,8 +1022,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
 #pragma unroll
         for (int q = 0; q < NPART; ++q) {
           if (more && part_stage(q) >= NSTG) {
-            write_part(ns, q, praw, norm_l);
-            if (q + 1 < NPART) issue_part(nxt, ns, q + 1, praw);
+            write_part(nxt, q, praw, praw2, norm_l, rnorm_l);
+            if (q + 1 < NPART) issue_part(nxt, q + 1, praw, praw2);
           }
         }
       }
@@ -926,14 +1036,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
     }
   } else {
     if constexpr (INK == IN_ACT) {
-      uint4 raw[IPT];
+      uint4 raw[IPT], raw2[IPT];
       int srcs[IPT];
-      float2 nmc[C::CPC];
+      float2 nmc[C::CPC], rnmc[C::CPC];
       build_maps(cur, 0);
       __syncthreads();
-      issue_loads(cur, 0, raw, srcs);
-      load_norm(cur.n, nmc);
-      stage(cur, raw, srcs, nmc);
+      issue_loads(cur, 0, raw, raw2, srcs);
+      load_norm(cur.n, nmc, rnmc);
+      stage(cur, raw, raw2, srcs, nmc, rnmc);
     } else {
       stage_image(cur);
     }
@@ -991,6 +1101,7 @@ struct ConvInst {
     k.persistent = PERS ? 1 : 0;
     k.korder = PERS ? 1 : 0;
     k.part_rows = PERS ? C::REDW : 1;
+    k.res = (VAR & VAR_RES) != 0 ? 1 : 0;
     k.launch = &launch;
     return k;
   }

@@ -30,7 +30,7 @@ const ConvKernelInfo* conv_table_out9(int* count);
 
 // first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
-                                       int out_kind) {
+                                       int out_kind, int res) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
   const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_out9, conv_table_bf16};
   const TableFn tables_f32[] = {conv_table_f32};
@@ -43,7 +43,7 @@ const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, 
     for (int i = 0; i < count; ++i) {
       const ConvKernelInfo& k = t[i];
       if (k.mode == mode && k.ks == ks && k.stride == stride && k.cinp == cinp && k.bn == bn &&
-          k.in_kind == in_kind && k.out_kind == out_kind)
+          k.in_kind == in_kind && k.out_kind == out_kind && k.res == res)
         return &k;
     }
   }
@@ -77,20 +77,28 @@ struct Layer {
 
 // Program steps
 enum OpKind { OP_CONV = 0, OP_RESADD = 1 };
-enum Buf { B_IMG = -1, B_OUT = -2, B_A = 0, B_B = 1, B_C = 2, B_D = 3, B_E = 4, NBUF = 5 };
+enum Buf { B_IMG = -1, B_OUT = -2, B_A = 0, B_B = 1, B_C = 2, B_D = 3, B_E = 4, B_F = 5, B_G = 6, NBUF = 7 };
 struct Op {
   int kind;
   int layer;     // OP_CONV: layer to run; OP_RESADD: layer whose IN applies to y
   int src, dst;  // buffers
-  int in_norm;   // OP_CONV: layer whose IN+ReLU the prologue applies (-1: identity)
-  int r_buf, r_norm, r_relu, relu_out;  // OP_RESADD
+  int in_norm;   // OP_CONV: layer whose IN+ReLU the prologue applies (-1: identity); with res_buf: IN of src, no ReLU
+  int r_buf, r_norm, r_relu, relu_out;  // OP_RESADD; OP_CONV with res_buf >= 0: the residual join in the fill
+  int res_buf = -1, res_out = -1;       // OP_CONV: residual stream r (joined into the fill) / where it is written
 };
 
 static int round_up(int v, int a) { return (v + a - 1) / a * a; }
 
-static void build_program(int arch, std::vector<LayerDef>& L, std::vector<Op>& P) {
+static void build_program(int arch, bool fuse_res, std::vector<LayerDef>& L, std::vector<Op>& P) {
   auto conv = [&](int layer, int src, int dst, int in_norm) {
     P.push_back(Op{OP_CONV, layer, src, dst, in_norm, 0, 0, 0, 0});
+  };
+  // conv whose fill joins the residual stream: IN(y = src) + r (r itself IN+ReLU of r_norm, lazily)
+  auto convres = [&](int layer, int y, int y_norm, int r_buf, int r_norm, int res_out, int relu_out, int dst) {
+    Op o{OP_CONV, layer, y, dst, y_norm, r_buf, r_norm, r_norm >= 0 ? 1 : 0, relu_out};
+    o.res_buf = r_buf;
+    o.res_out = res_out;
+    P.push_back(o);
   };
   auto resadd = [&](int layer, int y, int dst, int r_buf, int r_norm, int relu_out) {
     P.push_back(Op{OP_RESADD, layer, y, dst, -1, r_buf, r_norm, r_norm >= 0 ? 1 : 0, relu_out});
@@ -137,18 +145,37 @@ static void build_program(int arch, std::vector<LayerDef>& L, std::vector<Op>& P
   }
   const int nres = arch == NST_ARCH_RECONET ? 4 : 5;
   const int relu_out = arch == NST_ARCH_RECONET ? 1 : 0;  // ReCoNet ResLayer: ReLU after the add
+  const int u1 = 3 + 2 * nres, u2 = u1 + 1, fin = u1 + 2;
   conv(0, B_IMG, B_A, -1);
   conv(1, B_A, B_B, 0);
   conv(2, B_B, B_C, 1);
-  // residual stream lives in B_C; block k's input is C (block 1: IN+ReLU of layer 2, lazily)
-  for (int r = 0; r < nres; ++r) {
-    const int l1 = 3 + 2 * r, l2 = 4 + 2 * r;
-    conv(l1, B_C, B_D, r == 0 ? 2 : -1);
-    conv(l2, B_D, B_E, l1);
-    resadd(l2, B_E, B_C, B_C, r == 0 ? 2 : -1, relu_out);
+  if (!fuse_res) {
+    // residual stream lives in B_C; block k's input is C (block 1: IN+ReLU of layer 2, lazily)
+    for (int r = 0; r < nres; ++r) {
+      const int l1 = 3 + 2 * r, l2 = 4 + 2 * r;
+      conv(l1, B_C, B_D, r == 0 ? 2 : -1);
+      conv(l2, B_D, B_E, l1);
+      resadd(l2, B_E, B_C, B_C, r == 0 ? 2 : -1, relu_out);
+    }
+    conv(u1, B_C, B_A, -1);
+  } else {
+    // the residual add x_{k+1} = IN(y_k) + x_k runs inside the NEXT conv's fill, which also writes
+    // x_{k+1} (ping-pong F/G) for its own pixels; x_0 = ReLU(IN_2(C)) is never materialised
+    int xbuf = B_C, xnorm = 2;
+    for (int r = 0; r < nres; ++r) {
+      const int l1 = 3 + 2 * r, l2 = 4 + 2 * r;
+      if (r == 0) {
+        conv(l1, B_C, B_D, 2);
+      } else {
+        const int xout = (r & 1) ? B_F : B_G;
+        convres(l1, B_E, l2 - 2, xbuf, xnorm, xout, relu_out, B_D);
+        xbuf = xout;
+        xnorm = -1;
+      }
+      conv(l2, B_D, B_E, l1);
+    }
+    convres(u1, B_E, u1 - 1, xbuf, xnorm, -1, relu_out, B_A);
   }
-  const int u1 = 3 + 2 * nres, u2 = u1 + 1, fin = u1 + 2;
-  conv(u1, B_C, B_A, -1);
   conv(u2, B_A, B_B, u1);
   conv(fin, B_B, B_OUT, u2);
 }
@@ -339,7 +366,7 @@ struct Plan {
   std::string err;
   // per op: input and output dims
   std::vector<int> ih, iw, oh, ow, ch, cw;  // ch/cw: conv extent (before crop)
-  size_t buf_bytes[NBUF] = {0, 0, 0, 0, 0};
+  size_t buf_bytes[NBUF] = {0, 0, 0, 0, 0, 0, 0};
   size_t partial_floats = 0;
   int out_h = 0, out_w = 0;
   size_t ws_bytes = 0;
@@ -378,6 +405,11 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         return P;
       }
       const int ch = conv_out_dim(Ly.d, sh), cw = conv_out_dim(Ly.d, sw);
+      if (op.res_out >= 0) {  // the joined residual stream: same geometry as the conv input
+        bh[op.res_out] = sh; bw[op.res_out] = sw;
+        const size_t rb = (size_t)n * sh * sw * Ly.cinp * esz;
+        if (rb > P.buf_bytes[op.res_out]) P.buf_bytes[op.res_out] = rb;
+      }
       P.ih[i] = sh; P.iw[i] = sw; P.ch[i] = ch; P.cw[i] = cw;
       if (op.dst == B_OUT) {
         if (h->arch == NST_ARCH_NST) {  // centre crop back to the input size (transformer_net_nst.py:121-125)
@@ -492,7 +524,11 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
   auto* h = new nst_handle();
   h->arch = arch; h->dtype = compute_dtype; h->device = device;
   std::vector<LayerDef> defs;
-  build_program(arch, defs, h->prog);
+  build_program(arch, std::getenv("NST_NO_RESFUSE") == nullptr, defs, h->prog);  // env: experiment switch
+  // layers whose fill joins the residual stream run the VAR_RES instantiation
+  std::vector<int> res_layer(defs.size(), 0);
+  for (const Op& op : h->prog)
+    if (op.kind == OP_CONV && op.res_buf >= 0) res_layer[op.layer] = 1;
   // activation channel padding: fp32 chunks hold 4 channels (K step 16); bf16 chunks 8 (K step 32),
   // and bf16 tiles above 32 channels come in multiples of 64 (48->64, 96->128)
   auto pad_ch = [&](int c) {
@@ -521,7 +557,7 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     }
     modes.push_back(MODE_STD);
     for (int mode : modes) {
-      Ly.k_main = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk);
+      Ly.k_main = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk, res_layer[li]);
       Ly.k_alt = nullptr;
       if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk);
       if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW);
@@ -684,7 +720,13 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     }
     p.pre = Ly.d.pre;
     p.in_norm = op.in_norm >= 0 ? stats[op.in_norm] : nullptr;
-    p.in_relu = op.in_norm >= 0 ? 1 : 0;
+    p.in_relu = op.in_norm >= 0 && op.res_buf < 0 ? 1 : 0;
+    if (op.res_buf >= 0) {
+      p.res_r = bufs[op.res_buf];
+      p.res_rnorm = op.r_norm >= 0 ? stats[op.r_norm] : nullptr;
+      p.res_out = op.res_out >= 0 ? bufs[op.res_out] : nullptr;
+      p.res_relu = op.relu_out;
+    }
     for (int c = 0; c < 3; ++c) {
       p.enc_a[c] = pc.ea[c]; p.enc_b[c] = pc.eb[c]; p.enc_d[c] = pc.ed[c]; p.enc_perm[c] = pc.eperm[c];
       p.dec_p[c] = pc.dp[c]; p.dec_q[c] = pc.dq[c]; p.dec_r[c] = pc.dr[c]; p.dec_s[c] = pc.ds[c]; p.dec_perm[c] = pc.dperm[c];

@@ -47,6 +47,14 @@ struct ConvParams {
   int axis_mode, pad, pre;
   const float2* in_norm;  // [n][cs] {scale, shift} of the producer's InstanceNorm, or nullptr
   int in_relu;            // 1 whenever in_norm is set (the prologue always applies ReLU after the IN)
+  // residual join fused into the fill (res_r != nullptr): the staged input is
+  //   IN_in(in) + (res_rnorm ? ReLU(IN_r(res_r)) : res_r)  [+ ReLU if res_relu]
+  // with in_norm = IN of `in` WITHOUT ReLU; res_out (optional, same layout as `in`) receives the
+  // joined residual stream for the tile's own pixels (ResidualBlock / ResLayer output)
+  const void* res_r;
+  const float2* res_rnorm;
+  void* res_out;
+  int res_relu;
   // image-input preset encode: x_in[c] = ((x01[perm[c]] * a[c]) - b[c]) / d[c]
   float enc_a[3], enc_b[3], enc_d[3];
   int enc_perm[3];
@@ -82,12 +90,13 @@ struct ConvKernelInfo {
   int korder;      // packed K order: 0 tap-major, 1 chunk-group-major (persistent kernels)
   int part_rows;   // InstanceNorm partial rows per tile (persistent: one per channel-sharing wave)
   int wbytes;      // MODE_KYROT: bytes of the packed weight table
+  int res;         // fill joins the residual stream (VAR_RES)
   void (*launch)(const ConvParams&, dim3 grid, hipStream_t);
 };
 
 // Look up a compiled instantiation; nullptr if the combination was not built.
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
-                                       int out_kind);
+                                       int out_kind, int res = 0);
 
 // ---- elementwise / reduction launchers (nst_ops.hip) ----
 constexpr int IN_MAX_SEGMENTS = 128;

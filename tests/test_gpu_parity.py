@@ -174,3 +174,21 @@ def test_bf16_output_conv_mappings_agree(arch, h, w, preset, monkeypatch):
     d = np.abs(a.astype(int) - b.astype(int))
     assert d.max() <= 1 and (d > 0).mean() < 0.01, (d.max(), (d > 0).mean())
     assert np.abs(ya - yb).max() <= 1e-4 * np.abs(yb).max() + 1e-6
+
+
+@pytest.mark.parametrize("arch", ["johnson", "nst", "reconet"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_fused_residual_join_bit_exact(arch, dtype, monkeypatch):
+    """The residual add fused into the next conv's fill (VAR_RES, x_{k+1} written by that conv for
+    its own pixels) against the separate residual kernel: identical fp32 arithmetic, so the
+    outputs are bit-identical (u8 frames and the raw tensor output)."""
+    h, w = (72, 100) if arch == "nst" else (70, 90)
+    frames = torch.from_numpy(synthetic.make_frames(2, h, w, seed=3)).cuda()
+    x = torch.randn(2, 3, h, w, generator=torch.Generator().manual_seed(1)).cuda()
+    fused = _net(arch, 2, dtype)
+    a, ya = fused.stylize_frames(frames, "imagenet_255"), fused(x)
+    monkeypatch.setenv("NST_NO_RESFUSE", "1")
+    plain = _net(arch, 2, dtype)
+    b, yb = plain.stylize_frames(frames, "imagenet_255"), plain(x)
+    assert torch.equal(a, b)
+    assert torch.equal(ya, yb)
