@@ -36,6 +36,7 @@
 //               are 5 pixels apart (LDS columns in a polyphase-5 order): 3.46x fewer MFMAs than
 //               padding N=3 to 16, and each base's 15 uint8 outputs are 15 consecutive bytes.
 #pragma once
+#include <type_traits>
 #include "nst_internal.h"
 #include "nst_hip.h"
 
@@ -80,9 +81,12 @@ __device__ __forceinline__ int swz(int e) {
 
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair (round to nearest even): one v_cvt_pk_bf16_f32
 __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
-  __bf16 a = (__bf16)lo, b = (__bf16)hi;
-  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  const f32x2v_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_t));
 }
 
 template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW, int WM, int WN>
@@ -261,6 +265,33 @@ __device__ __forceinline__ float row_sum16(float v) {
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, false));   // quad [2,3,0,1]
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, false));   // quad [1,0,3,2]
   return v;
+}
+
+// Reduce-scatter of 32 values over the 16 lanes of a DPP row (30 exchanges instead of 32 full
+// row sums): partners 15-px (row_mirror), px^7 within 8 (row_half_mirror), px^3 and px^1 within
+// a quad; at each step the lower partner keeps the lower half.  Afterwards lane px holds the row
+// totals of values 2*px and 2*px+1.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int N, int CTRL>
+__device__ __forceinline__ void rs_step(const float* in, float* out, bool upper) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float keep = upper ? in[i + N] : in[i];
+    const float send = upper ? in[i] : in[i + N];
+    out[i] = keep + dpp_f<CTRL>(send);
+  }
+}
+__device__ __forceinline__ void row_reduce_scatter32(const float (&v)[32], int px, float& o0, float& o1) {
+  float a[16], b[8], c[4], d[2];
+  rs_step<16, 0x140>(v, a, px >= 8);
+  rs_step<8, 0x141>(a, b, (px & 4) != 0);
+  rs_step<4, 0x1b>(b, c, (px & 2) != 0);
+  rs_step<2, 0xb1>(c, d, (px & 1) != 0);
+  o0 = d[0];
+  o1 = d[1];
 }
 
 __device__ __forceinline__ float decode_ch(float y, int ch, const ConvParams& p) {
@@ -840,36 +871,67 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
       float s1[4 * NSUB], s2[4 * NSUB];
 #pragma unroll
       for (int j = 0; j < 4 * NSUB; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+      // 32-bit offsets inside the frame (host guarantees a frame is < 2 GiB); a wave whose pixels
+      // are all inside the image (every wave but the edge tiles') takes the branch-free copy
+      char* fout = (char*)p.out + (size_t)n * p.oh * p.ow * p.cout_stride * sizeof(T);
+      bool lane_ok = true;
 #pragma unroll
       for (int m = 0; m < MSUB; ++m) {
         int oy, ox;
         out_px(m, oy, ox);
-        const bool valid = (oy < p.oh) && (ox < p.ow);
-        float v[4 * NSUB];
+        lane_ok = lane_ok && (oy < p.oh) && (ox < p.ow);
+      }
+      auto store_tile = [&](auto all_valid) {
 #pragma unroll
-        for (int t = 0; t < NSUB; ++t)
+        for (int m = 0; m < MSUB; ++m) {
+          int oy, ox;
+          out_px(m, oy, ox);
+          const bool valid = decltype(all_valid)::value || ((oy < p.oh) && (ox < p.ow));
+          float v[4 * NSUB];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[4 * t + q] = acc[m][t][q] + bias_v[4 * t + q];
-        if (valid) {
-          char* dst = (char*)p.out + ((((size_t)n * p.oh + oy) * p.ow + ox) * p.cout_stride + cbase) * sizeof(T);
-          if constexpr (sizeof(T) == 2) {
+          for (int t = 0; t < NSUB; ++t)
 #pragma unroll
-            for (int h = 0; h < NSUB; h += 2) {
-              if (h + 1 < NSUB) {
-                *(uint4*)(dst + h * 8) = make_uint4(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]),
-                                                    pack_bf16(v[4 * h + 4], v[4 * h + 5]), pack_bf16(v[4 * h + 6], v[4 * h + 7]));
-              } else {
-                *(uint2*)(dst + h * 8) = make_uint2(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]));
+            for (int q = 0; q < 4; ++q) v[4 * t + q] = acc[m][t][q] + bias_v[4 * t + q];
+          if (valid) {
+            char* dst = fout + (unsigned)(((oy * p.ow + ox) * p.cout_stride + cbase) * (int)sizeof(T));
+            if constexpr (sizeof(T) == 2) {
+#pragma unroll
+              for (int h = 0; h < NSUB; h += 2) {
+                if (h + 1 < NSUB) {
+                  *(uint4*)(dst + h * 8) = make_uint4(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]),
+                                                      pack_bf16(v[4 * h + 4], v[4 * h + 5]), pack_bf16(v[4 * h + 6], v[4 * h + 7]));
+                } else {
+                  *(uint2*)(dst + h * 8) = make_uint2(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]));
+                }
               }
+            } else {
+#pragma unroll
+              for (int t = 0; t < NSUB; ++t)
+                *(float4*)(dst + t * 16) = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
             }
-          } else {
 #pragma unroll
-            for (int t = 0; t < NSUB; ++t)
-              *(float4*)(dst + t * 16) = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
+            for (int j = 0; j < 4 * NSUB; ++j) { s1[j] += v[j]; s2[j] = __builtin_fmaf(v[j], v[j], s2[j]); }
           }
-#pragma unroll
-          for (int j = 0; j < 4 * NSUB; ++j) { s1[j] += v[j]; s2[j] += v[j] * v[j]; }
         }
+      };
+      if (__builtin_amdgcn_ballot_w64(!lane_ok) == 0) {
+        store_tile(std::true_type{});
+      } else {
+        store_tile(std::false_type{});
+      }
+      if constexpr (PERS && 4 * NSUB == 16) {
+        // one partial row per channel-sharing wave (tile*REDW + rw): no barrier, no LDS; the 16
+        // pixel lanes of a lane group reduce-scatter so lane px ends with channel cbase + px
+        if (p.partial != nullptr) {
+          float v[32];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) { v[2 * j] = s1[j]; v[2 * j + 1] = s2[j]; }
+          float t1, t2;
+          row_reduce_scatter32(v, px, t1, t2);
+          float* dst = p.partial + ((((size_t)n * ntile + wk.tile) * C::REDW + wm) * p.cout_stride + cbase + px) * 2;
+          *(float2*)dst = make_float2(t1, t2);
+        }
+        return;
       }
       if (p.partial != nullptr) {
         // reduce over the 16 pixel lanes of each lane group (one DPP row)

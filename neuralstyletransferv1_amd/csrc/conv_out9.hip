@@ -39,32 +39,35 @@ struct Out9Cfg {
   static constexpr int LWS = SW + 8;              // input columns per strip row
   static constexpr int ROWB = LWS * EB;
   static constexpr int WAVE_LDS = 2 * ROWB;
-  static constexpr int KSTRIDE = 9 * KC * 96;     // bytes per kernel row ky in the weight table
-  static constexpr int W_BYTES = 9 * KSTRIDE;
-  static constexpr int Z_BYTES = KSTRIDE;         // zero block read by the unused rows 27..31
+  // weight table: [part p][block (kx, kc)][K half h][row i = 3*ky + c] x 8 bytes (4 bf16); a lane's
+  // 16-B A fragment is two ds_read_b64 (parts 0 and 1, PART_BYTES apart).  The 32 lanes of one
+  // half read 27 different rows (the rotation permutes them), i.e. 27 consecutive 8-B slots: no
+  // bank conflict for any rotation; the 5 unused rows re-read row 0's address (broadcast).
+  static constexpr int NBLK = 9 * KC;
+  static constexpr int BLK_BYTES = 2 * 27 * 8;
+  static constexpr int PART_BYTES = NBLK * BLK_BYTES;
+  static constexpr int W_BYTES = 2 * PART_BYTES;
   static constexpr int W_OFF = NW * WAVE_LDS;
-  static constexpr int Z_OFF = W_OFF + W_BYTES;
-  static constexpr int LDS = Z_OFF + Z_BYTES;
+  static constexpr int LDS = W_OFF + W_BYTES;
   static constexpr int ITEMS = LWS * NCH;         // 16-B loads per strip row
   static constexpr int IPL = (ITEMS + 63) / 64;   // per lane
   static_assert(64 % NCH == 0, "a lane keeps one channel chunk");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int CINP, int G, int NW, int OUTK>
+template <int CINP, int G, int NW, int OUTK, bool TANH>
 __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   using C = Out9Cfg<CINP, G, NW>;
   constexpr int KC = C::KC, NCH = C::NCH, EB = C::EB;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: work-item math in SGPRs
 
-  // ---- weights -> LDS (packed host-side in table order), zero block ----
+  // ---- weights -> LDS (packed host-side in table order) ----
   {
     const uint4* src = (const uint4*)p.wpk;
     uint4* dst = (uint4*)(smem + C::W_OFF);
     for (int i = tid; i < C::W_BYTES / 16; i += 64 * NW) dst[i] = src[i];
-    uint4* z = (uint4*)(smem + C::Z_OFF);
-    for (int i = tid; i < C::Z_BYTES / 16; i += 64 * NW) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
 
@@ -86,14 +89,13 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   // A operand (weights): lane row rho = lane & 31 -> (slot k, channel c); K half h = lane >> 5
   const int rho = lane & 31, h = lane >> 5;
   int a_off[9];
+  {
+    const int k = rho < 27 ? rho / 3 : 0;  // unused rows 27..31 re-read row 0's address (broadcast)
+    const int c = rho < 27 ? rho - 3 * (rho / 3) : 0;
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    if (rho < 27) {
-      const int k = rho / 3, c = rho - 3 * (rho / 3);
-      const int ky = (t - k + 9) % 9;
-      a_off[t] = C::W_OFF + ky * C::KSTRIDE + c * 32 + 16 * h;
-    } else {
-      a_off[t] = C::Z_OFF + 16 * h;
+    for (int t = 0; t < 9; ++t) {
+      a_off[t] = C::W_OFF + (h * 27 + 3 * ((t - k + 9) % 9) + c) * 8;
+      asm volatile("" : "+v"(a_off[t]));  // keep the 9 bases opaque: no per-tap address re-derivation
     }
   }
   // B operand (pixels): column rho of the 32-column group, K half h
@@ -122,46 +124,60 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
     return sy < 0 ? -1 : sy * row_bytes;
   };
   uint4 raw[C::IPL];
-  auto issue = [&](int v) {
-    const int ro = row_src(v);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)img, (short)0, p.hs * row_bytes, 0x00020000);
+  // an out-of-range buffer offset reads 0 (zero padding); the IN+ReLU is skipped for those items
+  constexpr uint32_t OOB = 0x80000000u;
+  auto issue = [&](int ro) {
 #pragma unroll
     for (int j = 0; j < C::IPL; ++j) {
       const bool ok = ro >= 0 && coloff[j] >= 0;
-      raw[j] = *(const uint4*)(img + (ok ? (unsigned)(ro + coloff[j]) : 0u));
-      if (!ok) raw[j] = make_uint4(0u, 0u, 0u, 0u);
+      raw[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (uint32_t)(ro + coloff[j]) : OOB, 0, 0));
     }
   };
   // zero padding stays zero (the pad applies after the producer's IN + ReLU)
-  auto store_row = [&](int v) {
-    const int ro = row_src(v);
+  auto store_row = [&](int v, int ro) {
     char* dst = ring + (v & 1) * C::ROWB + (lane / NCH) * EB + chunk * 16;
 #pragma unroll
     for (int j = 0; j < C::IPL; ++j) {
       if (lane + 64 * j < C::ITEMS) {
         const bool ok = ro >= 0 && coloff[j] >= 0;
-        const uint4 v4 = ok ? norm_chunk<__bf16>(raw[j], nm) : make_uint4(0u, 0u, 0u, 0u);
-        *(uint4*)(dst + j * (64 / NCH) * EB) = v4;
+        const uint4 v4 = norm_chunk<__bf16>(raw[j], nm);
+        *(uint4*)(dst + j * (64 / NCH) * EB) = ok ? v4 : make_uint4(0u, 0u, 0u, 0u);
       }
     }
   };
 
   // ---- output ----
-  const float bias0 = p.bias[0], bias1 = p.bias[1], bias2 = p.bias[2];
-  auto emit = [&](const f32x16_t (&acc)[G], int reg, int c, int oy) {
-    const float b = c == 0 ? bias0 : (c == 1 ? bias1 : bias2);
+  // decode v = ((y + p) * q) / r + s as a multiply by 1/r (bf16 throughput mode: within one ulp of
+  // the division, bar a truncation boundary)
+  const float bias[3] = {p.bias[0], p.bias[1], p.bias[2]};
+  float dp[3], dq[3], dri[3], ds[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int ch = p.dec_perm[c];  // the presets' channel permutations are involutions
+    dp[c] = p.dec_p[ch]; dq[c] = p.dec_q[ch]; dri[c] = 1.0f / p.dec_r[ch]; ds[c] = p.dec_s[ch];
+  }
+  // stores through a buffer resource: masked-out lanes get an out-of-range offset and are dropped,
+  // so the emission is branch-free
+  const int out_bytes = OUTK == OUT_F32_NCHW ? 3 * p.oh * p.ow * 4 : p.oh * p.ow * 3;
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((char*)p.out + (size_t)n * out_bytes), (short)0, out_bytes, 0x00020000);
+  int perm[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) perm[c] = p.dec_perm[c];
+  auto emit = [&](const f32x16_t (&acc)[G], int reg, int c, int oy, bool on) {
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
       const int ox = x0 + gi * 32 + rho;
-      if (ox < p.ow) {
-        float y = acc[gi][reg] + b;
-        if (p.dec_tanh) y = tanhf(y);
-        if constexpr (OUTK == OUT_F32_NCHW) {
-          ((float*)p.out)[(((size_t)n * 3 + c) * p.oh + oy) * p.ow + ox] = y;
-        } else {
-          const int ch = p.dec_perm[c];  // the presets' channel permutations are involutions
-          ((uint8_t*)p.out)[(((size_t)n * p.oh + oy) * p.ow + ox) * 3 + ch] =
-              (uint8_t)(decode_ch(y, ch, p) * 255.0f);  // ToPILImage: pic.mul(255).byte()
-        }
+      const bool ok = on && ox < p.ow;
+      float y = acc[gi][reg] + bias[c];
+      if constexpr (TANH) y = tanhf(y);  // ReCoNet ConvTanhLayer (model.py:77-80)
+      if constexpr (OUTK == OUT_F32_NCHW) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(y), ors, ok ? (uint32_t)(((c * p.oh + oy) * p.ow + ox) * 4) : OOB, 0, 0);
+      } else {
+        const float v = fminf(fmaxf((y + dp[c]) * dq[c] * dri[c] + ds[c], 0.f), 1.f);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v * 255.0f), ors,  // pic.mul(255).byte()
+                                             ok ? (uint32_t)((oy * p.ow + ox) * 3 + perm[c]) : OOB, 0, 0);
       }
     }
   };
@@ -172,29 +188,46 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[gi][r] = 0.f;
 
-  issue(0);
-  store_row(0);
+  {
+    const int ro0 = row_src(0);
+    issue(ro0);
+    store_row(0, ro0);
+  }
   for (int vb = 0; vb < NV; vb += 9) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int v = vb + t;
       if (v >= NV) break;
       const bool next = v + 1 < NV;
-      if (next) issue(v + 1);
+      const int ro_next = next ? row_src(v + 1) : -1;
+      if (next) issue(ro_next);
       const char* rb = ring + (v & 1) * C::ROWB + b_lane;
       const char* ab = smem + a_off[t];
-#pragma unroll
-      for (int kx = 0; kx < 9; ++kx) {
+      // operands of tap column kx, double-buffered: tap kx+1's reads are issued before tap kx's
+      // MFMAs, one scheduling region per tap (keeps the live operand set at two taps)
+      uint4 av[2][KC], bv[2][KC][G];
+      auto ld = [&](int kx, uint4 (&a)[KC], uint4 (&b)[KC][G]) {
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
-          const uint4 a = *(const uint4*)(ab + (kx * KC + kc) * 96);
+          const uint2 a0 = *(const uint2*)(ab + (kx * KC + kc) * C::BLK_BYTES);
+          const uint2 a1 = *(const uint2*)(ab + (kx * KC + kc) * C::BLK_BYTES + C::PART_BYTES);
+          a[kc] = make_uint4(a0.x, a0.y, a1.x, a1.y);
 #pragma unroll
-          for (int gi = 0; gi < G; ++gi) {
-            const uint4 b = *(const uint4*)(rb + (gi * 32 + kx) * EB + kc * 32);
-            acc[gi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                              __builtin_bit_cast(bf16x8_t, b), acc[gi], 0, 0, 0);
-          }
+          for (int gi = 0; gi < G; ++gi) b[kc][gi] = *(const uint4*)(rb + (gi * 32 + kx) * EB + kc * 32);
         }
+      };
+      ld(0, av[0], bv[0]);
+#pragma unroll
+      for (int kx = 0; kx < 9; ++kx) {
+        if (kx + 1 < 9) ld(kx + 1, av[(kx + 1) & 1], bv[(kx + 1) & 1]);
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+          for (int gi = 0; gi < G; ++gi)
+            acc[gi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, av[kx & 1][kc]),
+                                                              __builtin_bit_cast(bf16x8_t, bv[kx & 1][kc][gi]),
+                                                              acc[gi], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
       // slot (t+1) % 9 now holds output row v - 8: store it, then clear it for output row v + 1
       const int kk = (t + 1) % 9;
@@ -202,19 +235,19 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
       for (int c = 0; c < 3; ++c) {
         const int r3 = 3 * kk + c;
         const int reg = (r3 & 3) + 4 * (r3 >> 3), hh = (r3 >> 2) & 1;
-        if (v >= 8 && h == hh) emit(acc, reg, c, o0 + v - 8);
+        emit(acc, reg, c, o0 + v - 8, v >= 8 && h == hh);
 #pragma unroll
         for (int gi = 0; gi < G; ++gi) acc[gi][reg] = (h == hh) ? 0.f : acc[gi][reg];
       }
-      if (next) store_row(v + 1);
+      if (next) store_row(v + 1, ro_next);
     }
   }
 }
 
-template <int CINP, int G, int NW, int OUTK>
+template <int CINP, int G, int NW, int OUTK, bool TANH>
 struct Out9Inst {
   using C = Out9Cfg<CINP, G, NW>;
-  static constexpr auto kernel = out9_kernel<CINP, G, NW, OUTK>;
+  static constexpr auto kernel = out9_kernel<CINP, G, NW, OUTK, TANH>;
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;
@@ -250,6 +283,7 @@ struct Out9Inst {
     k.cpc = 8; k.nch = C::NCH; k.lds_bytes = C::LDS;
     k.wbytes = C::W_BYTES;
     k.part_rows = 1;
+    k.tanh_out = TANH ? 1 : 0;
     k.launch = &launch;
     return k;
   }
@@ -258,11 +292,11 @@ struct Out9Inst {
 #define E(...) Out9Inst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_out9(int* count) {
   static const ConvKernelInfo table[] = {
-      //  CINP G NW OUT
-      E(32, 3, 8, OUT_U8_NHWC),   // Johnson deconv3 / NST final (frames)
-      E(32, 3, 8, OUT_F32_NCHW),  // tensor API
-      E(64, 3, 4, OUT_U8_NHWC),   // ReCoNet (48 channels, bf16 padded to 64)
-      E(64, 3, 4, OUT_F32_NCHW),
+      //  CINP G NW OUT          TANH
+      E(32, 3, 8, OUT_U8_NHWC, false),   // Johnson deconv3 / NST final (frames)
+      E(32, 3, 8, OUT_F32_NCHW, false),  // tensor API
+      E(64, 3, 4, OUT_U8_NHWC, true),    // ReCoNet (48 channels, bf16 padded to 64; tanh output)
+      E(64, 3, 4, OUT_F32_NCHW, true),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

@@ -299,21 +299,24 @@ std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, cons
   return out;
 }
 
-// MODE_KYROT weight table (conv_out9.hip): [ky][kx][kc][c][16 input channels], kc = 16-channel
-// block of the (padded) input channels, c = model output channel 0..2.
+// MODE_KYROT weight table (conv_out9.hip): [part p][block (kx, kc)][K half h][row 3*ky + c][4],
+// element j of a row = input channel kc*16 + 8h + 4p + j (kc = 16-channel block of the padded
+// input channels), c = model output channel 0..2.
 std::vector<float> pack_kyrot_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
-  const int kc_n = k.cinp / 16;
+  const int kc_n = k.cinp / 16, nblk = 9 * kc_n;
   std::vector<float> out((size_t)k.wbytes / 2, 0.f);
-  for (int ky = 0; ky < 9; ++ky)
-    for (int kx = 0; kx < 9; ++kx)
-      for (int kc = 0; kc < kc_n; ++kc)
-        for (int c = 0; c < 3; ++c)
-          for (int j = 0; j < 16; ++j) {
-            const int ci = kc * 16 + j;
-            if (ci >= d.cin) continue;
-            out[((((size_t)ky * 9 + kx) * kc_n + kc) * 3 + c) * 16 + j] =
-                W[(((size_t)c * d.cin + ci) * d.ks + ky) * d.ks + kx];
-          }
+  for (int pp = 0; pp < 2; ++pp)
+    for (int ky = 0; ky < 9; ++ky)
+      for (int kx = 0; kx < 9; ++kx)
+        for (int kc = 0; kc < kc_n; ++kc)
+          for (int hh = 0; hh < 2; ++hh)
+            for (int c = 0; c < 3; ++c)
+              for (int j = 0; j < 4; ++j) {
+                const int ci = kc * 16 + 8 * hh + 4 * pp + j;
+                if (ci >= d.cin) continue;
+                const size_t row = (((size_t)pp * nblk + kx * kc_n + kc) * 2 + hh) * 27 + 3 * ky + c;
+                out[row * 4 + j] = W[(((size_t)c * d.cin + ci) * d.ks + ky) * d.ks + kx];
+              }
   return out;
 }
 
@@ -561,7 +564,10 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
       Ly.k_alt = nullptr;
       if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk);
       if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW);
-      if (Ly.k_main && (!(image_in || final_layer) || Ly.k_alt)) { Ly.mode = mode; break; }
+      const bool tanh_ok = mode != MODE_KYROT || !Ly.k_main ||
+                           (Ly.k_main->tanh_out == (arch == NST_ARCH_RECONET ? 1 : 0) && Ly.k_alt &&
+                            Ly.k_alt->tanh_out == Ly.k_main->tanh_out);
+      if (Ly.k_main && tanh_ok && (!(image_in || final_layer) || Ly.k_alt)) { Ly.mode = mode; break; }
       Ly.k_main = nullptr;
     }
     if (!Ly.k_main || ((image_in || final_layer) && !Ly.k_alt)) {

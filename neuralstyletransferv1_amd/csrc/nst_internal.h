@@ -91,6 +91,7 @@ struct ConvKernelInfo {
   int part_rows;   // InstanceNorm partial rows per tile (persistent: one per channel-sharing wave)
   int wbytes;      // MODE_KYROT: bytes of the packed weight table
   int res;         // fill joins the residual stream (VAR_RES)
+  int tanh_out;    // MODE_KYROT: tanh compiled into the output (ReCoNet); other kernels: p.dec_tanh
   void (*launch)(const ConvParams&, dim3 grid, hipStream_t);
 };
 
