@@ -139,6 +139,26 @@ int nst_lab_ema_u8(const nst_lab* lab, const uint8_t* rgb_in, uint8_t* rgb_out, 
                    void* stream);
 
 /*
+ * Multi-model LAB blend (pipeline.py:1841-1870, --blend_models_lab): L from model A; per pixel
+ *   a = trunc(clip(wL * a_A + wab * (sum_i w_i * a_i), 0, 255))  (float32, models B.. in order; same for b)
+ * on Pillow's raw LAB bytes (signed a/b stored as uint8), then LAB -> RGB through the LittleCMS
+ * tables.  frames: host array of m device pointers to [n,h,w,3] uint8 outputs (A first, each the
+ * decoded + clamped + truncated model output, pipeline.py's to_pil(out.clamp(0,1))); the first
+ * min(m-1, n_rest) of weights_rest pair with frames[1..] (zip semantics).
+ */
+int nst_blend_models_lab_u8(const nst_lab* lab, const uint8_t* const* frames, int m, const float* weights_rest,
+                            int n_rest, float w_l, float w_ab, int n, int h, int w, uint8_t* out, void* stream);
+
+/*
+ * Mask feathering (pipeline.py:349-351 cv2.GaussianBlur(m, (0,0), sigmaX=sigmaY=sigma) then /255,
+ * :353): masks [n,h,w] uint8 (after the NEAREST fit and optional invert) -> alpha [n,h,w] f32 in
+ * [0,1].  ksize = round(6*sigma+1)|1, separable Gaussian, BORDER_REFLECT_101, uint8 rounding.
+ * scratch: n*h*w floats.  sigma = feather_px * 0.5 (> 0; radius <= 1023).
+ */
+int nst_mask_feather(const uint8_t* mask, int n, int h, int w, float sigma, float* scratch, float* alpha,
+                     void* stream);
+
+/*
  * Uniform / masked blend with the original frame (pipeline.py:1984-2092):
  *   mask (optional, [n,h,w] f32 alpha in [0,1]): keep: C = a*S + (1-a)*O; replace: (1-a)*S + a*O; clip
  *   then if 0 <= blend < 1: out = clamp(blend*C + (1-blend)*O, 0, 1); truncate to u8.

@@ -33,7 +33,8 @@ EXPORTED_SYMBOLS = (
     "nst_last_error", "nst_version", "nst_create", "nst_destroy", "nst_output_hw",
     "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8", "nst_lab_create",
     "nst_lab_destroy", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
-    "nst_profile_end", "nst_num_layers", "nst_layer_name", "nst_blend_models_u8",
+    "nst_profile_end", "nst_num_layers", "nst_layer_name", "nst_blend_models_u8", "nst_blend_models_lab_u8",
+    "nst_mask_feather",
 )
 
 
@@ -80,6 +81,8 @@ def lib() -> ctypes.CDLL:
         L.nst_blend_models_u8.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(i), ctypes.POINTER(f), i, i, i, i, vp,
                                           i, i, vp]
         L.nst_blend_models_u8.restype = i
+        L.nst_blend_models_lab_u8.argtypes = [vp, ctypes.POINTER(vp), i, ctypes.POINTER(f), i, f, f, i, i, i, vp, vp]
+        L.nst_mask_feather.argtypes = [vp, i, i, i, f, vp, vp, vp]
         L.nst_profile_begin.argtypes = [vp]
         L.nst_profile_end.argtypes = [vp, i, ctypes.POINTER(f), ctypes.POINTER(i)]
         L.nst_num_layers.argtypes = [vp]

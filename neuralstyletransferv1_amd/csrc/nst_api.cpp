@@ -893,6 +893,33 @@ int nst_lab_ema_u8(const nst_lab* lab, const uint8_t* rgb_in, uint8_t* rgb_out, 
   return NST_OK;
 }
 
+int nst_blend_models_lab_u8(const nst_lab* lab, const uint8_t* const* frames, int m, const float* weights_rest,
+                            int n_rest, float w_l, float w_ab, int n, int h, int w, uint8_t* out, void* stream) {
+  if (!lab || !frames || !out || m < 1 || m > NST_MAX_MODELS || n_rest < 0 || (n_rest > 0 && !weights_rest) ||
+      n <= 0 || h <= 0 || w <= 0) {
+    set_error("nst_blend_models_lab_u8: invalid arguments");
+    return NST_E_INVALID;
+  }
+  for (int i = 0; i < m; ++i)
+    if (!frames[i]) { set_error("nst_blend_models_lab_u8: null frame pointer"); return NST_E_INVALID; }
+  const int nrest = std::min(m - 1, n_rest);  // zip(outputs[1:], weights_rest)
+  hipError_t e = launch_lab_blend(lab->rgb2lab, lab->lab2rgb, frames, weights_rest, nrest, w_l, w_ab,
+                                  (size_t)n * h * w, out, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("lab_blend launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+int nst_mask_feather(const uint8_t* mask, int n, int h, int w, float sigma, float* scratch, float* alpha,
+                     void* stream) {
+  if (!mask || !scratch || !alpha || n <= 0 || h <= 0 || w <= 0 || !(sigma > 0.f)) {
+    set_error("nst_mask_feather: invalid arguments");
+    return NST_E_INVALID;
+  }
+  hipError_t e = launch_mask_feather(mask, n, h, w, sigma, scratch, alpha, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("mask_feather launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
 int nst_blend_u8(const uint8_t* styled, const uint8_t* orig, const float* mask, int composite_mode, float blend,
                  float one_minus_blend, uint8_t* out, int n, int h, int w, void* stream) {
   if (!styled || !orig || !out || n <= 0 || h <= 0 || w <= 0 || composite_mode < 0 || composite_mode > 1) {

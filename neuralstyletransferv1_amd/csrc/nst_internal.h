@@ -119,6 +119,11 @@ hipError_t launch_blend_models_u8(const float* const* ys, const float (*dp)[3], 
 hipError_t launch_lab_ema(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* in,
                           uint8_t* out, int n, int hw, int sl, float a, float oma, int sc, float ca,
                           float coma, float* state, int first, hipStream_t st);
+hipError_t launch_lab_blend(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* const* frames,
+                            const float* wrest, int nrest, float wL, float wab, size_t npix, uint8_t* out,
+                            hipStream_t st);
+hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigma, float* tmp, float* alpha,
+                               hipStream_t st);
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,
                         float omb, uint8_t* out, int n, int hw, hipStream_t st);
 hipError_t launch_gram(const void* F, int dtype, int n, int c, int hw, float* G, hipStream_t st);

@@ -361,6 +361,16 @@ hipError_t launch_blend_models_u8(const float* const* ys, const float (*dp)[3], 
 // optionally a/b bytes), np.clip(0,255), astype(uint8) truncation, LAB->RGB.  The two
 // LittleCMS transforms are exact 2^24-entry LUT gathers (tables made from Pillow itself).
 // One thread per pixel walks the batch in frame order (the EMA state is per pixel).
+// Byte triples are read through volatile pointers: with ordinary loads hipcc (ROCm 7.2) merges
+// adjacent bytes into one 16-bit load and then shifts the pair left by 16 without masking the
+// upper byte ((uint32_t)b[0] << 16 came out as (b[0] | b[1] << 8) << 16), corrupting the
+// 24-bit table index (an out-of-range gather).
+__device__ __forceinline__ void load3(const uint8_t* q, uint32_t& x, uint32_t& y, uint32_t& z) {
+  const volatile uint8_t* v = q;
+  x = v[0];
+  y = v[1];
+  z = v[2];
+}
 __global__ __launch_bounds__(256) void lab_ema_kernel(const uint8_t* __restrict__ rgb2lab,
                                                       const uint8_t* __restrict__ lab2rgb,
                                                       const uint8_t* in, uint8_t* out, int n, int hw,
@@ -371,9 +381,10 @@ __global__ __launch_bounds__(256) void lab_ema_kernel(const uint8_t* __restrict_
   float pL = state[p], pa = state[hw + p], pb = state[2 * hw + p];
   for (int f = 0; f < n; ++f) {
     const size_t idx = ((size_t)f * hw + p) * 3;
-    const uint32_t rgb = ((uint32_t)in[idx] << 16) | ((uint32_t)in[idx + 1] << 8) | in[idx + 2];
-    const uint8_t* lab = rgb2lab + (size_t)rgb * 3;
-    float L = (float)lab[0], A = (float)lab[1], Bc = (float)lab[2];
+    uint32_t r, g, b, l0, l1, l2;
+    load3(in + idx, r, g, b);
+    load3(rgb2lab + (size_t)((r << 16) | (g << 8) | b) * 3, l0, l1, l2);
+    float L = (float)l0, A = (float)l1, Bc = (float)l2;
     if (sl) {
       if (first && f == 0) pL = L;
       const float t0 = a * L;
@@ -407,6 +418,131 @@ hipError_t launch_lab_ema(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const 
                           float* state, int first, hipStream_t st) {
   hipLaunchKernelGGL(lab_ema_kernel, dim3((unsigned)((hw + 255) / 256)), dim3(256), 0, st, rgb2lab, lab2rgb,
                      in, out, n, hw, sl, a, oma, sc, ca, coma, state, first);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-model LAB blend (pipeline.py:1841-1870): L from model A; a/b = clip(wL*a_A + wab*mix, 0, 255)
+// with mix = sum_i w_i * a_i over models B.. in order (float32 accumulation starting from 0), all on
+// the raw LAB bytes (Pillow keeps the signed a/b as uint8, so the reference mixes the wrapped
+// bytes); astype(uint8) truncation; LAB -> RGB.  Two LittleCMS table gathers per model and pixel.
+struct LabBlendArgs {
+  const uint8_t* f[NST_MAX_MODELS];  // f[0] = model A's uint8 frame, f[1..] = the others
+  float w[NST_MAX_MODELS];           // w[i] multiplies f[i + 1]
+};
+__global__ __launch_bounds__(256) void lab_blend_kernel(const uint8_t* __restrict__ rgb2lab,
+                                                        const uint8_t* __restrict__ lab2rgb, LabBlendArgs a,
+                                                        int nrest, float wL, float wab, size_t npix, uint8_t* out) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  auto lab_of = [&](const uint8_t* f, uint32_t& L, uint32_t& A, uint32_t& B) {
+    uint32_t r, g, b;
+    load3(f + p * 3, r, g, b);
+    load3(rgb2lab + (size_t)((r << 16) | (g << 8) | b) * 3, L, A, B);
+  };
+  uint32_t La, Aa, Ba;
+  lab_of(a.f[0], La, Aa, Ba);
+  float am = 0.f, bm = 0.f;
+  for (int i = 0; i < nrest; ++i) {
+    uint32_t Li, Ai, Bi;
+    lab_of(a.f[i + 1], Li, Ai, Bi);
+    am = am + a.w[i] * (float)Ai;
+    bm = bm + a.w[i] * (float)Bi;
+  }
+  const float A = fminf(fmaxf(wL * (float)Aa + wab * am, 0.f), 255.f);
+  const float B = fminf(fmaxf(wL * (float)Ba + wab * bm, 0.f), 255.f);
+  const uint32_t li = (La << 16) | ((uint32_t)(uint8_t)A << 8) | (uint32_t)(uint8_t)B;
+  uint32_t r, g, b;
+  load3(lab2rgb + (size_t)li * 3, r, g, b);
+  out[p * 3] = (uint8_t)r;
+  out[p * 3 + 1] = (uint8_t)g;
+  out[p * 3 + 2] = (uint8_t)b;
+}
+
+hipError_t launch_lab_blend(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* const* frames,
+                            const float* wrest, int nrest, float wL, float wab, size_t npix, uint8_t* out,
+                            hipStream_t st) {
+  if (nrest < 0 || nrest + 1 > NST_MAX_MODELS) return hipErrorInvalidValue;
+  LabBlendArgs a;
+  for (int i = 0; i < NST_MAX_MODELS; ++i) { a.f[i] = nullptr; a.w[i] = 0.f; }
+  for (int i = 0; i <= nrest; ++i) a.f[i] = frames[i];
+  for (int i = 0; i < nrest; ++i) a.w[i] = wrest[i];
+  hipLaunchKernelGGL(lab_blend_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, rgb2lab, lab2rgb, a,
+                     nrest, wL, wab, npix, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Mask feather (pipeline.py:349-351: cv2.GaussianBlur(m, (0, 0), sigmaX = sigmaY = feather_px * 0.5)
+// on the uint8 mask), restated from OpenCV's documented semantics: ksize = round(6*sigma + 1) | 1
+// for 8-bit data, taps exp(-x^2 / (2 sigma^2)) normalised to 1 (computed in double, as
+// getGaussianKernel), separable rows-then-columns, BORDER_REFLECT_101, round to uint8; then
+// alpha = m / 255 (pipeline.py:353).  cv2 is not importable here: parity unpinned (OpenCV's 8-bit
+// path quantises the taps to fixed point, which can move a rounding boundary by 1 LSB).
+constexpr int FEATHER_MAX_R = 1023;
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+__device__ void feather_taps(float* k, int r, double sigma) {
+  __shared__ double part[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i <= 2 * r; i += blockDim.x) {
+    const double x = (double)(i - r);
+    s += exp(-(x * x) / (2.0 * sigma * sigma));
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  const double inv = 1.0 / part[0];
+  for (int i = threadIdx.x; i <= 2 * r; i += blockDim.x) {
+    const double x = (double)(i - r);
+    k[i] = (float)(exp(-(x * x) / (2.0 * sigma * sigma)) * inv);
+  }
+  __syncthreads();
+}
+__global__ __launch_bounds__(256) void feather_rows_kernel(const uint8_t* __restrict__ m, int h, int w, int r,
+                                                           double sigma, float* __restrict__ tmp) {
+  __shared__ float k[2 * FEATHER_MAX_R + 1];
+  feather_taps(k, r, sigma);
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  const size_t f = (size_t)blockIdx.z * h * w;
+  if (x >= w) return;
+  float s = 0.f;
+  for (int i = -r; i <= r; ++i) s += k[i + r] * (float)m[f + (size_t)y * w + reflect101(x + i, w)];
+  tmp[f + (size_t)y * w + x] = s;
+}
+__global__ __launch_bounds__(256) void feather_cols_kernel(const float* __restrict__ tmp, int h, int w, int r,
+                                                           double sigma, float* __restrict__ alpha) {
+  __shared__ float k[2 * FEATHER_MAX_R + 1];
+  feather_taps(k, r, sigma);
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  const size_t f = (size_t)blockIdx.z * h * w;
+  if (x >= w) return;
+  float s = 0.f;
+  for (int i = -r; i <= r; ++i) s += k[i + r] * tmp[f + (size_t)reflect101(y + i, h) * w + x];
+  const float u8 = fminf(fmaxf(rintf(s), 0.f), 255.f);  // saturate_cast<uchar>
+  alpha[f + (size_t)y * w + x] = u8 / 255.0f;
+}
+
+int feather_radius(float sigma) {
+  const int ksize = ((int)lrint((double)sigma * 6.0 + 1.0)) | 1;
+  return ksize / 2;
+}
+
+hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigma, float* tmp, float* alpha,
+                               hipStream_t st) {
+  const int r = feather_radius(sigma);
+  if (r > FEATHER_MAX_R || !(sigma > 0.f)) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((w + 255) / 256), (unsigned)h, (unsigned)n);
+  hipLaunchKernelGGL(feather_rows_kernel, grid, dim3(256), 0, st, m, h, w, r, (double)sigma, tmp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(feather_cols_kernel, grid, dim3(256), 0, st, tmp, h, w, r, (double)sigma, alpha);
   return hipGetLastError();
 }
 

@@ -153,10 +153,6 @@ def reject_out_of_scope(args) -> None:
         bad.append("--region_mode/--region_optimize")
     if args.flow_ema or args.motion_blend:
         bad.append("--flow_ema/--motion_blend")
-    if args.blend_models_lab:
-        bad.append("--blend_models_lab")
-    if args.mask_feather > 0 or args.mask_feather_pct > 0:
-        bad.append("--mask_feather/--mask_feather_pct (OpenCV GaussianBlur)")
     if args.device != "cuda":
         bad.append(f"--device {args.device} (this engine runs on MI355X only; there is no CPU path)")
     if bad:
@@ -246,6 +242,26 @@ def parse_blend_weights(weights_str: Optional[str], num_models: int) -> List[flo
     return weights
 
 
+def parse_lab_weights(weights_str: Optional[str]):
+    """pipeline.py:514-521."""
+    if not weights_str:
+        return 0.5, 0.5
+    wL, wab = [float(w) for w in weights_str.split(",")]
+    if abs(wL + wab - 1.0) > 1e-6:
+        raise ValueError(f"LAB weights must sum to 1.0, got {wL + wab:.6f}")
+    return wL, wab
+
+
+def lab_weights_rest(weights_str: Optional[str], num_models: int) -> List[float]:
+    """pipeline.py:1843-1852: weights of models B.. for the LAB blend (the reference's length rule)."""
+    w = parse_blend_weights(weights_str, max(num_models - 1, 1))
+    if len(w) == 1:
+        return [1.0]
+    if len(w) in (2, 3):
+        return w
+    return [1.0 / max(num_models - 1, 1)] * max(num_models - 1, 1)
+
+
 def _pct_to_px(pct: float, H: int) -> int:
     """pipeline.py:278-282."""
     try:
@@ -256,6 +272,11 @@ def _pct_to_px(pct: float, H: int) -> int:
 
 def load_mask_fit(mask_path: str, target_hw, invert: bool, autofix: bool = True, force_transpose: bool = False) -> np.ndarray:
     """pipeline.py:284-353 without feathering: float32 HxW alpha in [0,1] (host file decode + NEAREST fit)."""
+    return load_mask_u8(mask_path, target_hw, invert, autofix, force_transpose).astype(np.float32) / 255.0
+
+
+def load_mask_u8(mask_path: str, target_hw, invert: bool, autofix: bool = True, force_transpose: bool = False) -> np.ndarray:
+    """pipeline.py:292-347: the fitted (and optionally inverted) uint8 mask, before the feather."""
     from PIL import Image
     W_tgt, H_tgt = target_hw[1], target_hw[0]
     m_img = Image.open(mask_path).convert("L")
@@ -280,7 +301,7 @@ def load_mask_fit(mask_path: str, target_hw, invert: bool, autofix: bool = True,
     m = np.array(m_img, dtype=np.uint8)
     if invert:
         m = 255 - m
-    return m.astype(np.float32) / 255.0
+    return m
 
 
 def _detect_transformer_type(checkpoint_path: str) -> str:
@@ -396,7 +417,14 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         ip = getattr(args, f"io_preset_{s}", None) or io_preset
         m, _ = load_model(p, t, dev, args.dtype, s.upper(), auto_nst=False)
         slots.append((m, ip))
-    weights = parse_blend_weights(args.blend_models_weights, len(slots)) if len(slots) > 1 else [1.0]
+    if len(slots) > 1 and getattr(args, "blend_models_lab", False):
+        # LAB blend (pipeline.py:1841-1870): L from A, a/b from the weighted mix of the others
+        lab_wl, lab_wab = parse_lab_weights(getattr(args, "blend_models_lab_weights", None))
+        lab_rest = lab_weights_rest(args.blend_models_weights, len(slots))
+        weights = [lab_wl, lab_wab] + lab_rest
+        _log(f"[blend] LAB blend: L={lab_wl},ab={lab_wab},rest={lab_rest}")
+    else:
+        weights = parse_blend_weights(args.blend_models_weights, len(slots)) if len(slots) > 1 else [1.0]
     _log(f"[cfg] io_preset={io_preset} models={len(slots)} weights={weights} dtype={args.dtype} gpus={world} batch={args.batch}")
     _log(f">> smoothing: {smooth_lightness}  alpha={smooth_alpha}  |  blend={blend}")
 
@@ -451,6 +479,10 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         h0, w0 = orig.shape[1], orig.shape[2]
         if len(slots) == 1 and xin.shape[1:3] == orig.shape[1:3]:
             styled = slots[0][0].stylize_frames(xin, slots[0][1])
+        elif len(slots) > 1 and getattr(args, "blend_models_lab", False):
+            from .postproc import blend_models_lab
+            outs = [_slot_u8(m, pr, xin, h0, w0) for m, pr in slots]
+            styled = blend_models_lab(outs, lab_rest, lab_wl, lab_wab)
         else:
             styled = _blend_slots(slots, weights, xin, h0, w0)
         return torch.cat([styled, orig], dim=3) if need_orig else styled
@@ -495,17 +527,27 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
                 # no mask for this frame -> no composite (pipeline.py:1985-1993): the alpha that
                 # leaves S unchanged is 1 for 'keep' and 0 for 'replace'
                 ident = 1.0 if args.composite_mode == "keep" else 0.0
-                ms.append(np.full((h0, w0), ident, np.float32))
+                ms.append(torch.full((h0, w0), ident, dtype=torch.float32, device=dev))
                 continue
             any_mask = True
             key = (mfile, h0, w0)
             if key not in mask_cache:
-                mask_cache[key] = load_mask_fit(mfile, (h0, w0), bool(args.mask_invert), bool(args.mask_autofix),
-                                                bool(args.mask_force_transpose))
+                # pipeline.py:2001-2003: feather radius from --mask_feather_pct of the target height,
+                # at least --mask_feather; the Gaussian feather runs on the GPU (nst_mask_feather)
+                fpx = _pct_to_px(getattr(args, "mask_feather_pct", 0.0) or 0.0, h0)
+                if getattr(args, "mask_feather", 0) and args.mask_feather > 0:
+                    fpx = max(fpx, int(args.mask_feather))
+                m8 = load_mask_u8(mfile, (h0, w0), bool(args.mask_invert), bool(args.mask_autofix),
+                                  bool(args.mask_force_transpose))
+                if fpx > 0:
+                    from .postproc import feather_masks
+                    mask_cache[key] = feather_masks(torch.from_numpy(m8)[None].to(dev), fpx)[0]
+                else:
+                    mask_cache[key] = torch.from_numpy(m8.astype(np.float32) / 255.0).to(dev)
             ms.append(mask_cache[key])
         if not any_mask:
             return None
-        return torch.from_numpy(np.stack(ms)).to(dev)
+        return torch.stack(ms)
 
     def _save(img: np.ndarray, f: int):
         out_img = Image.fromarray(img)
@@ -532,6 +574,30 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     if rank == 0:
         el = time.perf_counter() - t_start
         _log(f"Styled {len(src)}/{len(src)} frames in {el:.2f}s ({len(src) / max(el, 1e-9):.2f} frames/s)")
+
+
+def _slot_u8(model, preset, xin, h0, w0):
+    """One slot's frames as the reference's to_pil(out.clamp(0,1)): decoded, fitted to the content
+    size (bilinear, pipeline.py:1512-1516), clamped, truncated to uint8."""
+    import torch
+
+    from . import _lib
+    from ._lib import check, lib
+    dev = xin.device
+    eng = model.engine(dev)
+    n, h, w, _ = xin.shape
+    oh, ow = eng.output_hw(h, w)
+    if (oh, ow) == (h, w) == (h0, w0):
+        return model.stylize_frames(xin, preset)
+    y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=dev)
+    ws = eng.workspace(n, h, w)
+    check(lib().nst_forward(eng._h, xin.data_ptr(), _lib.NST_IO_U8_NHWC, n, h, w, _lib.PRESETS[preset],
+                            y.data_ptr(), _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(),
+                            _lib.stream_ptr(dev)), "nst_forward")
+    out = torch.empty((n, h0, w0, 3), dtype=torch.uint8, device=dev)
+    check(lib().nst_decode_resize_u8(y.data_ptr(), n, oh, ow, _lib.PRESETS[preset], out.data_ptr(), h0, w0,
+                                     _lib.stream_ptr(dev)), "nst_decode_resize_u8")
+    return out
 
 
 def _blend_slots(slots, weights, xin, h0, w0):

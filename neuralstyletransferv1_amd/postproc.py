@@ -127,3 +127,41 @@ def blend_frames(styled_u8: torch.Tensor, orig_u8: torch.Tensor, blend: float = 
                              float(np.float32(1.0 - blend)), out.data_ptr(), n, h, w,
                              _lib.stream_ptr(styled_u8.device)), "nst_blend_u8")
     return out
+
+
+def blend_models_lab(frames_u8, weights_rest, w_l: float = 0.5, w_ab: float = 0.5) -> torch.Tensor:
+    """LAB multi-model blend (pipeline.py:1841-1870) of [n,h,w,3] uint8 model outputs (A first).
+
+    L comes from A; a/b = clip(wL*a_A + wab*sum_i w_i*a_i, 0, 255) on the raw LAB bytes, truncated.
+    `weights_rest` pairs with frames_u8[1:] in zip order (the reference's zip(outputs[1:], ...))."""
+    frames = [f.contiguous() for f in frames_u8]
+    for f in frames:
+        _lib.require_gpu_tensor(f, "frames")
+        if f.shape != frames[0].shape or f.dtype != torch.uint8:
+            raise _lib.NstError(f"LAB blend needs equal uint8 frames, got {tuple(f.shape)} vs {tuple(frames[0].shape)}")
+    n, h, w, _ = frames[0].shape
+    out = torch.empty_like(frames[0])
+    m = len(frames)
+    fp = (ctypes.c_void_p * m)(*[f.data_ptr() for f in frames])
+    wr = [float(np.float32(x)) for x in weights_rest]
+    wp = (ctypes.c_float * max(1, len(wr)))(*wr)
+    t = lab_tables(frames[0].device)
+    check(lib().nst_blend_models_lab_u8(t._h, fp, m, wp, len(wr), float(np.float32(w_l)), float(np.float32(w_ab)),
+                                        n, h, w, out.data_ptr(), _lib.stream_ptr(frames[0].device)),
+          "nst_blend_models_lab_u8")
+    return out
+
+
+def feather_masks(masks_u8: torch.Tensor, feather_px: int) -> torch.Tensor:
+    """[n,h,w] uint8 fitted masks -> [n,h,w] fp32 alpha with the reference's Gaussian feather
+    (pipeline.py:349-353: sigma = feather_px * 0.5; feather_px <= 0 -> plain m / 255)."""
+    _lib.require_gpu_tensor(masks_u8, "masks")
+    masks_u8 = masks_u8.contiguous()
+    n, h, w = masks_u8.shape
+    alpha = torch.empty((n, h, w), dtype=torch.float32, device=masks_u8.device)
+    if not feather_px or feather_px <= 0:
+        raise _lib.NstError("feather_masks needs feather_px > 0 (unfeathered masks are m / 255 on the host)")
+    scratch = torch.empty_like(alpha)
+    check(lib().nst_mask_feather(masks_u8.data_ptr(), n, h, w, float(feather_px) * 0.5, scratch.data_ptr(),
+                                 alpha.data_ptr(), _lib.stream_ptr(masks_u8.device)), "nst_mask_feather")
+    return alpha

@@ -93,3 +93,64 @@ def test_synthetic_stream_bf16_nst_and_reconet(tmp_path):
         outs = sorted((tmp_path / f"w_{arch}").glob("styled_frame_*.png"))
         assert len(outs) == 5
         assert np.array(Image.open(outs[0])).shape == (96, 160, 3)
+
+
+def test_lab_blend_bit_exact_vs_oracle():
+    """nst_blend_models_lab_u8 == pipeline.py:1854-1869 on Pillow/LittleCMS (2..4 models, zip rule)."""
+    from neuralstyletransferv1_amd.postproc import blend_models_lab
+    rng = np.random.default_rng(5)
+    fr = [rng.integers(0, 256, (2, 33, 47, 3), dtype=np.uint8) for _ in range(4)]
+    for m, rest, wl, wab in ((2, [1.0], 0.5, 0.5), (3, [0.25, 0.75], 0.3, 0.7), (4, [0.2, 0.3, 0.5], 0.5, 0.5),
+                             (4, [0.6, 0.4], 0.9, 0.1)):
+        dev = [torch.from_numpy(f).cuda() for f in fr[:m]]
+        out = blend_models_lab(dev, rest, wl, wab).cpu().numpy()
+        for i in range(2):
+            ref = O.lab_blend_u8([f[i] for f in fr[:m]], rest, wl, wab)
+            assert np.array_equal(out[i], ref), (m, rest, wl, wab, i)
+
+
+def test_mask_feather_vs_restatement():
+    """nst_mask_feather against the numpy restatement of cv2.GaussianBlur (parity unpinned: cv2 is
+    absent; tolerance 1 LSB of the uint8 blur for float32 vs float64 taps)."""
+    from neuralstyletransferv1_amd.postproc import feather_masks
+    m = np.zeros((2, 61, 90), np.uint8)
+    m[0, 10:40, 20:70] = 255
+    m[1] = np.random.default_rng(2).integers(0, 256, (61, 90), dtype=np.uint8)
+    for fpx in (1, 4, 13, 40):
+        a = feather_masks(torch.from_numpy(m).cuda(), fpx).cpu().numpy()
+        for i in range(2):
+            ref = O.feather_mask_u8(m[i], fpx).astype(np.float32) / 255.0
+            assert np.abs(a[i] - ref).max() <= 1.0 / 255.0 + 1e-7, (fpx, i)
+            assert (np.abs(a[i] - ref) > 1e-7).mean() < 0.01
+
+
+def test_cli_lab_blend_and_feathered_mask(tmp_path):
+    """--blend_models_lab with three models and a feathered mask composite through the CLI."""
+    cka, sda = _ckpt(tmp_path, "johnson", 0)
+    ckb, sdb = _ckpt(tmp_path, "johnson", 1)
+    ckc, sdc = _ckpt(tmp_path, "johnson", 2)
+    frames = synthetic.make_frames(2, 48, 64, seed=8)
+    d = tmp_path / "frames"
+    d.mkdir()
+    for i, f in enumerate(frames):
+        Image.fromarray(f).save(d / f"frame_{i + 1:04d}.png")
+    mask = np.zeros((48, 64), np.uint8)
+    mask[8:40, 16:48] = 255
+    Image.fromarray(mask).save(tmp_path / "mask.png")
+    out_d = tmp_path / "out"
+    rc = P.main(["--input_dir", str(d), "--output_dir", str(out_d), "--model", cka, "--model_b", ckb, "--model_c", ckc,
+                 "--io_preset", "raw_255", "--blend_models_lab", "--blend_models_lab_weights", "0.4,0.6",
+                 "--blend_models_weights", "0.5,0.5", "--mask", str(tmp_path / "mask.png"), "--mask_feather", "6",
+                 "--no-smooth_lightness", "--work_dir", str(tmp_path / "w")])
+    assert rc == 0
+    alpha = O.feather_mask_u8(mask, 6).astype(np.float32) / 255.0
+    outs = sorted(out_d.iterdir())
+    assert len(outs) == 2
+    for i, fr in enumerate(frames):
+        per = []
+        for sd in (sda, sdb, sdc):
+            per.append(O.stylize_u8("johnson", sd, fr[None], "raw_255")[0])
+        lab = O.lab_blend_u8(per, [0.5, 0.5], 0.4, 0.6)
+        ref = O.blend_u8(lab, fr, alpha[..., None], "keep", 1.0)
+        got = np.array(Image.open(outs[i]))
+        _close(got, ref, frac=0.01)

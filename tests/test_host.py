@@ -28,7 +28,7 @@ def test_cli_defaults_match_reference():
 
 
 @pytest.mark.parametrize("extra", [["--region_mode", "grid"], ["--flow_ema"], ["--model_type", "magenta"],
-                                   ["--device", "cpu"], ["--mask_feather", "5"], ["--blend_models_lab"]])
+                                   ["--device", "cpu"], ["--motion_blend"]])
 def test_out_of_scope_requests_fail_loudly(extra, tmp_path):
     args = P.build_parser().parse_args(["--model", "x.pth", "--synthetic", "64x48"] + extra)
     with pytest.raises(SystemExit) as e:
@@ -125,3 +125,26 @@ def test_mask_fit_matches_oracle():
             ours = P.load_mask_fit(path, hw, inv)
             ref = O.load_mask_fit(path, hw, inv)[..., 0]
             assert np.array_equal(ours, ref)
+
+
+def test_lab_weight_rules_match_reference():
+    """pipeline.py:1843-1852 weight rules for the LAB blend, host mirror vs oracle restatement."""
+    from oracle import nst_oracle as O
+    for s, n in ((None, 2), (None, 3), (None, 5), ("0.3,0.7", 3), ("0.2,0.3,0.5", 4), ("0.1,0.2,0.3,0.4", 5)):
+        assert P.lab_weights_rest(s, n) == O.lab_weights_rest(s, n)
+    assert P.lab_weights_rest("0.1,0.2,0.3,0.4", 5) == [0.25] * 4  # the reference's length rule
+    assert P.parse_lab_weights(None) == (0.5, 0.5) and P.parse_lab_weights("0.3,0.7") == (0.3, 0.7)
+    with pytest.raises(ValueError):
+        P.parse_lab_weights("0.3,0.8")
+
+
+def test_feather_restatement_properties():
+    """Oracle feather (parity unpinned): symmetric kernel, constant image fixed, radius rule."""
+    import numpy as np
+    from oracle import nst_oracle as O
+    m = np.full((20, 30), 77, np.uint8)
+    assert np.array_equal(O.feather_mask_u8(m, 8), m)
+    m = np.zeros((31, 31), np.uint8)
+    m[15, 15] = 255
+    f = O.feather_mask_u8(m, 4).astype(int)
+    assert np.array_equal(f, f[::-1, ::-1]) and np.array_equal(f, f.T)
