@@ -6,7 +6,7 @@ CSRC := $(PKG)/csrc
 BUILD := build/obj
 CXXFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
-SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
+SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
 OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
 LIB := $(PKG)/libnst_hip.so
 

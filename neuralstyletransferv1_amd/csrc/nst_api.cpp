@@ -73,6 +73,7 @@ struct Layer {
   float* bias_rev = nullptr;
   float* gamma = nullptr;
   float* beta = nullptr;
+  bool prepad = false;  // image layer reading the pre-padded encoded input (conv_prep.hip)
 };
 
 // Program steps
@@ -374,7 +375,8 @@ struct Plan {
   int out_h = 0, out_w = 0;
   size_t ws_bytes = 0;
   size_t seg_bytes = 0;
-  size_t off_buf[NBUF], off_partial, off_seg, off_stats;
+  size_t off_buf[NBUF], off_partial, off_seg, off_stats, off_pre = 0;
+  size_t pre_bytes = 0;
 };
 
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
@@ -408,6 +410,10 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         return P;
       }
       const int ch = conv_out_dim(Ly.d, sh), cw = conv_out_dim(Ly.d, sw);
+      if (op.src == B_IMG && Ly.prepad) {  // bf16 x4 per pixel over the conv's padded input extent
+        const size_t pb = (size_t)n * (ch + Ly.d.ks - 1) * (cw + Ly.d.ks - 1) * 8;
+        if (pb > P.pre_bytes) P.pre_bytes = pb;
+      }
       if (op.res_out >= 0) {  // the joined residual stream: same geometry as the conv input
         bh[op.res_out] = sh; bw[op.res_out] = sw;
         const size_t rb = (size_t)n * sh * sw * Ly.cinp * esz;
@@ -447,6 +453,8 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
   off += align256(P.partial_floats * 4);
   P.off_seg = off;
   off += align256(P.seg_bytes);
+  P.off_pre = off;
+  off += align256(P.pre_bytes);
   P.off_stats = off;
   for (const Layer& Ly : h->layers) off += align256((size_t)n * Ly.coutp * 8);
   P.ws_bytes = off;
@@ -559,6 +567,13 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
       modes.push_back(MODE_XSHIFT);
     }
     modes.push_back(MODE_STD);
+    // image layer: prefer the conv over the pre-padded encoded input (one streaming pre-pass, plain
+    // 16-byte fill loads) when it is compiled for this shape; it serves u8 and f32 inputs alike
+    if (image_in && !std::getenv("NST_NO_PREPAD")) {  // env: experiment switch
+      Ly.k_main = find_conv_kernel(compute_dtype, MODE_STD, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0);
+      if (Ly.k_main && d.stride == 1) { Ly.prepad = true; Ly.k_alt = Ly.k_main; modes.clear(); }
+      else Ly.k_main = nullptr;
+    }
     for (int mode : modes) {
       Ly.k_main = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk, res_layer[li]);
       Ly.k_alt = nullptr;
@@ -739,6 +754,21 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     }
     if (image_in && x_fmt == NST_IO_F32_NCHW && preset == NST_PRESET_NONE) {
       for (int c = 0; c < 3; ++c) { p.enc_a[c] = 1.f; p.enc_b[c] = 0.f; p.enc_d[c] = 1.f; p.enc_perm[c] = c; }
+    }
+    if (image_in && Ly.prepad) {
+      // resolve padding + encode once into the workspace, then run the conv over it with an
+      // identity coordinate map (pad 0, no reflection)
+      const int hp = P.ch[i] + Ly.d.ks - 1, wp = P.cw[i] + Ly.d.ks - 1;
+      void* pre = ws + P.off_pre;
+      hipError_t e = launch_prepad_encode(p, x_fmt == NST_IO_U8_NHWC ? IN_U8_NHWC : IN_F32_NCHW, n, hp, wp, pre, st);
+      if (e != hipSuccess) { set_error(std::string("prepad launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+      p.in = pre;
+      p.hs = hp;
+      p.ws = wp;
+      p.cs = 4;
+      p.axis_mode = AX_ZERO;
+      p.pad = 0;
+      p.pre = 0;
     }
     p.dec_tanh = (h->arch == NST_ARCH_RECONET && final_out) ? 1 : 0;
     p.wpk = Ly.wpk;

@@ -124,6 +124,7 @@ hipError_t launch_lab_blend(const uint8_t* rgb2lab, const uint8_t* lab2rgb, cons
                             hipStream_t st);
 hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigma, float* tmp, float* alpha,
                                hipStream_t st);
+hipError_t launch_prepad_encode(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st);
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,
                         float omb, uint8_t* out, int n, int hw, hipStream_t st);
 hipError_t launch_gram(const void* F, int dtype, int n, int c, int hw, float* G, hipStream_t st);

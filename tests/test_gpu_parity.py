@@ -192,3 +192,22 @@ def test_fused_residual_join_bit_exact(arch, dtype, monkeypatch):
     b, yb = plain.stylize_frames(frames, "imagenet_255"), plain(x)
     assert torch.equal(a, b)
     assert torch.equal(ya, yb)
+
+
+@pytest.mark.parametrize("arch", ["johnson", "nst", "reconet"])
+def test_prepadded_image_layer_bit_exact(arch, monkeypatch):
+    """bf16 first layer over the pre-padded encoded input (conv_prep.hip) against the encode fused
+    into the conv's fill: same per-element arithmetic and the same LDS image, so bit-identical."""
+    h, w = (72, 100) if arch == "nst" else (61, 90)
+    frames = torch.from_numpy(synthetic.make_frames(2, h, w, seed=12)).cuda()
+    x = torch.randn(2, 3, h, w, generator=torch.Generator().manual_seed(2)).cuda()
+    fast = _net(arch, 5, "bf16")
+    outs_a = [fast.stylize_frames(frames, p) for p in ("imagenet_255", "caffe_bgr", "tanh")]
+    ya = fast(x)
+    monkeypatch.setenv("NST_NO_PREPAD", "1")
+    ref = _net(arch, 5, "bf16")
+    outs_b = [ref.stylize_frames(frames, p) for p in ("imagenet_255", "caffe_bgr", "tanh")]
+    yb = ref(x)
+    for a, b in zip(outs_a, outs_b):
+        assert torch.equal(a, b)
+    assert torch.equal(ya, yb)
