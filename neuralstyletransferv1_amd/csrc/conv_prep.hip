@@ -7,13 +7,14 @@
 // (reflection / NST's pre-reflect + zero padding resolved), as bf16 [n][hp][wp][4] (channel 3 = 0):
 // 8 bytes per pixel, so the conv fill is plain 16-byte loads (two pixels per LDS entry) with an
 // identity coordinate map.  Arithmetic per element is the reference's: x01 = byte / 255 (ToTensor),
-// ((x01 * a) - b) / d, one RNE rounding to bf16 — bit-identical to the fused encode it replaces.
+// ((x01 * a) - b) / d, one RNE rounding to bf16 — bit-identical to the fused encode it replaces
+// (for uint8 frames through a per-block table of the 3 x 256 possible values).
 #include "conv_impl.h"
 
 namespace nst {
 
-template <int INK>
-__global__ __launch_bounds__(256) void prepad_encode_kernel(ConvParams p, int hp, int wp, uint2* __restrict__ out) {
+// f32 NCHW input (tensor API): one thread per pixel, the encode formula per element
+__global__ __launch_bounds__(256) void prepad_encode_f32_kernel(ConvParams p, int hp, int wp, uint2* __restrict__ out) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x;
   const int y = blockIdx.y, n = blockIdx.z;
   if (x >= wp) return;
@@ -23,26 +24,64 @@ __global__ __launch_bounds__(256) void prepad_encode_kernel(ConvParams p, int hp
   if (sy >= 0 && sx >= 0) {
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-      const int src_c = p.enc_perm[ch];
-      float x01;
-      if constexpr (INK == IN_U8_NHWC) {
-        const uint8_t b = ((const uint8_t*)p.in)[(((size_t)n * p.hs + sy) * p.ws + sx) * 3 + src_c];
-        x01 = (float)b / 255.0f;  // ToTensor: .float().div(255)
-      } else {
-        x01 = ((const float*)p.in)[(((size_t)n * 3 + src_c) * p.hs + sy) * p.ws + sx];
-      }
+      const float x01 = ((const float*)p.in)[(((size_t)n * 3 + p.enc_perm[ch]) * p.hs + sy) * p.ws + sx];
       v[ch] = ((x01 * p.enc_a[ch]) - p.enc_b[ch]) / p.enc_d[ch];
     }
   }
   out[((size_t)n * hp + y) * wp + x] = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], 0.f));
 }
 
+// uint8 frames: the encoded bf16 value of a channel depends only on its byte, so each block first
+// tabulates the 3 x 256 values with the exact per-element formula (768 evaluations, amortised
+// over the block's 1024 pixels), then every pixel is 3 byte loads + 3 LDS lookups; 4 consecutive
+// output pixels per thread (32-byte contiguous stores).
+constexpr int PREP_PX = 4;
+__global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int hp, int wp, uint4* __restrict__ out) {
+  __shared__ uint16_t lut[3][256];
+  for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
+    const int ch = i >> 8, b = i & 255;
+    const float x01 = (float)b / 255.0f;  // ToTensor: .float().div(255)
+    const float v = ((x01 * p.enc_a[ch]) - p.enc_b[ch]) / p.enc_d[ch];
+    lut[ch][b] = (uint16_t)(pack_bf16(v, 0.f) & 0xffffu);
+  }
+  __syncthreads();
+  const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * PREP_PX;
+  const int y = blockIdx.y, n = blockIdx.z;
+  if (x0 >= wp) return;
+  const int sy = map_axis(y - p.pad, p.hs, p.axis_mode, p.pre);
+  const uint8_t* row = (const uint8_t*)p.in + ((size_t)n * p.hs + (sy < 0 ? 0 : sy)) * p.ws * 3;
+  uint32_t w[2 * PREP_PX];
+#pragma unroll
+  for (int j = 0; j < PREP_PX; ++j) {
+    const int sx = map_axis(x0 + j - p.pad, p.ws, p.axis_mode, p.pre);
+    uint32_t lo = 0u, hi = 0u;
+    if (sy >= 0 && sx >= 0 && x0 + j < wp) {
+      const uint8_t* px = row + (size_t)sx * 3;
+      lo = (uint32_t)lut[0][px[p.enc_perm[0]]] | ((uint32_t)lut[1][px[p.enc_perm[1]]] << 16);
+      hi = (uint32_t)lut[2][px[p.enc_perm[2]]] | ((uint32_t)pack_bf16(0.f, 0.f) & 0xffff0000u);
+    }
+    w[2 * j] = lo;
+    w[2 * j + 1] = hi;
+  }
+  uint2* o = (uint2*)out + ((size_t)n * hp + y) * wp + x0;
+  if (x0 + PREP_PX <= wp && ((((size_t)n * hp + y) * wp + x0) & 1) == 0) {
+    ((uint4*)o)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    ((uint4*)o)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < PREP_PX; ++j)
+      if (x0 + j < wp) o[j] = make_uint2(w[2 * j], w[2 * j + 1]);
+  }
+}
+
 hipError_t launch_prepad_encode(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st) {
-  const dim3 grid((unsigned)((wp + 255) / 256), (unsigned)hp, (unsigned)n);
-  if (in_kind == IN_U8_NHWC)
-    hipLaunchKernelGGL(prepad_encode_kernel<IN_U8_NHWC>, grid, dim3(256), 0, st, p, hp, wp, (uint2*)out);
-  else
-    hipLaunchKernelGGL(prepad_encode_kernel<IN_F32_NCHW>, grid, dim3(256), 0, st, p, hp, wp, (uint2*)out);
+  if (in_kind == IN_U8_NHWC) {
+    const dim3 grid((unsigned)((wp + 256 * PREP_PX - 1) / (256 * PREP_PX)), (unsigned)hp, (unsigned)n);
+    hipLaunchKernelGGL(prepad_encode_u8_kernel, grid, dim3(256), 0, st, p, hp, wp, (uint4*)out);
+  } else {
+    const dim3 grid((unsigned)((wp + 255) / 256), (unsigned)hp, (unsigned)n);
+    hipLaunchKernelGGL(prepad_encode_f32_kernel, grid, dim3(256), 0, st, p, hp, wp, (uint2*)out);
+  }
   return hipGetLastError();
 }
 

@@ -54,19 +54,30 @@ __global__ __launch_bounds__(256) void in_partial_reduce_kernel(const float* __r
   }
 }
 
-__global__ __launch_bounds__(64) void in_finalize_kernel(const double2* __restrict__ seg, int nseg, int cstride,
-                                                         double count, const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float eps,
-                                                         float2* __restrict__ out) {
+__global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restrict__ seg, int nseg, int cstride,
+                                                          double count, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          float2* __restrict__ out) {
+  // 64 channels x 4 segment phases per block (the segments' loads in flight together), then a
+  // fixed-order LDS combine: deterministic
+  __shared__ double red[4][64][2];
   const int n = blockIdx.x;
-  const int c = blockIdx.y * 64 + threadIdx.x;
-  if (c >= cstride) return;
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
-  for (int s = 0; s < nseg; ++s) {
-    const double2 v = seg[((size_t)n * nseg + s) * cstride + c];
-    s1 += v.x;
-    s2 += v.y;
+  if (c < cstride) {
+    for (int s = q; s < nseg; s += 4) {
+      const double2 v = seg[((size_t)n * nseg + s) * cstride + c];
+      s1 += v.x;
+      s2 += v.y;
+    }
   }
+  red[q][cl][0] = s1;
+  red[q][cl][1] = s2;
+  __syncthreads();
+  if (q != 0 || c >= cstride) return;
+  s1 = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+  s2 = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
   const double mean = s1 / count;
   double var = s2 / count - mean * mean;
   var = var < 0.0 ? 0.0 : var;
@@ -86,7 +97,7 @@ hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstrid
                      tiles, cstride, per_seg, (double2*)seg_ws);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(in_finalize_kernel, dim3(n, (cstride + 63) / 64), dim3(64), 0, st, (const double2*)seg_ws,
+  hipLaunchKernelGGL(in_finalize_kernel, dim3(n, (cstride + 63) / 64), dim3(256), 0, st, (const double2*)seg_ws,
                      nseg, cstride, count, gamma, beta, eps, out);
   return hipGetLastError();
 }
