@@ -27,15 +27,16 @@ const ConvKernelInfo* conv_table_bf16(int* count);
 const ConvKernelInfo* conv_table_bf16_wl(int* count);
 const ConvKernelInfo* conv_table_f32(int* count);
 const ConvKernelInfo* conv_table_out9(int* count);
+const ConvKernelInfo* conv_table_wstat(int* count);
 
 // first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind, int res) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
-  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_out9, conv_table_bf16};
+  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_out9, conv_table_bf16};
   const TableFn tables_f32[] = {conv_table_f32};
   const TableFn* tables = dtype == NST_DT_BF16 ? tables_bf16 : tables_f32;
-  const int ntables = dtype == NST_DT_BF16 ? 3 : 1;
+  const int ntables = dtype == NST_DT_BF16 ? 4 : 1;
   static const bool no_wl = std::getenv("NST_NO_PERSISTENT") != nullptr;  // experiment switch
   for (int ti = (dtype == NST_DT_BF16 && no_wl) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
@@ -321,6 +322,28 @@ std::vector<float> pack_kyrot_weights(const ConvKernelInfo& k, const LayerDef& d
   return out;
 }
 
+// MODE_WSTAT weight registers (conv_wstat.hip): [wave w][step s][lane][8 bf16].  Step s = part q
+// (input channels 32q..), tap t = 3 dy + dx, half jj: s = 18 q + 2 t + jj; lane l holds MFMA row
+// l & 31 = output channel 32 w + perm(l & 31) (perm puts channels 16h..16h+15 of the wave on the
+// lanes of half h of the 32x32 accumulator), K elements = input channels 32 q + 16 jj + 8 (l >> 5) + i.
+std::vector<float> pack_wstat_weights(const LayerDef& d, const float* W) {
+  std::vector<float> out((size_t)4 * 72 * 64 * 8, 0.f);
+  for (int w = 0; w < 4; ++w)
+    for (int s = 0; s < 72; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int q = s / 18, t = (s % 18) / 2, jj = s % 2;
+        const int dy = t / 3, dx = t % 3;
+        const int rho = l & 31;
+        const int co = 32 * w + 16 * ((rho >> 2) & 1) + 4 * (rho >> 3) + (rho & 3);
+        for (int i = 0; i < 8; ++i) {
+          const int ci = 32 * q + 16 * jj + 8 * (l >> 5) + i;
+          if (co < d.cout && ci < d.cin)
+            out[(((size_t)w * 72 + s) * 64 + l) * 8 + i] = W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
+        }
+      }
+  return out;
+}
+
 // bias rows of an x-shift layer: row q = 3*s + c -> bias of output channel (perm) c
 std::vector<float> xshift_bias(const float* b, bool reverse_channels) {
   std::vector<float> r(16, 0.f);
@@ -566,6 +589,11 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
       if (!std::getenv("NST_NO_KYROT")) modes.push_back(MODE_KYROT);  // experiment switch
       modes.push_back(MODE_XSHIFT);
     }
+    // residual-trunk convs (128 -> 128, 3x3): weight-stationary kernel (conv_wstat.hip); ReCoNet's
+    // trunk is 192 channels and its join has a ReLU after the sum, so it never matches
+    if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 1 && arch != NST_ARCH_RECONET &&
+        !std::getenv("NST_NO_WSTAT"))  // env: experiment switch
+      modes.push_back(MODE_WSTAT);
     modes.push_back(MODE_STD);
     // image layer: prefer the conv over the pre-padded encoded input (one streaming pre-pass, plain
     // 16-byte fill loads) when it is compiled for this shape; it serves u8 and f32 inputs alike
@@ -609,6 +637,8 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     };
     if (Ly.mode == MODE_KYROT) {
       if ((rc = upload_packed(pack_kyrot_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
+    } else if (Ly.mode == MODE_WSTAT) {
+      if ((rc = upload_packed(pack_wstat_weights(d, W), &Ly.wpk)) != NST_OK) break;
     } else if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) {
       break;
     }
@@ -788,6 +818,10 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     p.cout_stride = Ly.coutp;
     tile_grid(*k, p.hs, p.ws, p.oh, p.ow, &p.tiles_x, &p.tiles_y);
     p.n_cblk = Ly.coutp / k->bn;
+    if (Ly.mode == MODE_WSTAT && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out == nullptr || p.res_relu)) {
+      set_error("conv " + Ly.d.conv + ": weight-stationary kernel joins IN(y) + r into a residual-stream buffer");
+      return NST_E_SHAPE;
+    }
     if (k->persistent && p.n_cblk != 1) { set_error("conv " + Ly.d.conv + ": persistent kernel needs one channel block"); return NST_E_SHAPE; }
     p.partial = final_out ? nullptr : partial;
     dim3 grid(p.tiles_x * p.tiles_y, n * p.n_cblk);
