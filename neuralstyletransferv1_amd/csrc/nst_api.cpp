@@ -322,23 +322,20 @@ std::vector<float> pack_kyrot_weights(const ConvKernelInfo& k, const LayerDef& d
   return out;
 }
 
-// MODE_WSTAT weight registers (conv_wstat.hip): [wave w][step s][lane][8 bf16].  Step s = part q
-// (input channels 32q..), tap t = 3 dy + dx, half jj: s = 18 q + 2 t + jj; lane l holds MFMA row
-// l & 31 = output channel 32 w + perm(l & 31) (perm puts channels 16h..16h+15 of the wave on the
-// lanes of half h of the 32x32 accumulator), K elements = input channels 32 q + 16 jj + 8 (l >> 5) + i.
+// MODE_WSTAT weight registers (conv_wstat.hip): [wave w][step s][lane][8 bf16].  Step s = 9 q + tap,
+// part q = input channels 32q..32q+31, tap = 3 dy + dx; lane l holds MFMA row l & 15 = output
+// channel 16 w + (l & 15), K elements = input channels 32 q + 8 (l >> 4) + i.
 std::vector<float> pack_wstat_weights(const LayerDef& d, const float* W) {
-  std::vector<float> out((size_t)4 * 72 * 64 * 8, 0.f);
-  for (int w = 0; w < 4; ++w)
-    for (int s = 0; s < 72; ++s)
+  std::vector<float> out((size_t)8 * 36 * 64 * 8, 0.f);
+  for (int w = 0; w < 8; ++w)
+    for (int s = 0; s < 36; ++s)
       for (int l = 0; l < 64; ++l) {
-        const int q = s / 18, t = (s % 18) / 2, jj = s % 2;
-        const int dy = t / 3, dx = t % 3;
-        const int rho = l & 31;
-        const int co = 32 * w + 16 * ((rho >> 2) & 1) + 4 * (rho >> 3) + (rho & 3);
+        const int q = s / 9, t = s % 9, dy = t / 3, dx = t % 3;
+        const int co = 16 * w + (l & 15);
         for (int i = 0; i < 8; ++i) {
-          const int ci = 32 * q + 16 * jj + 8 * (l >> 5) + i;
+          const int ci = 32 * q + 8 * (l >> 4) + i;
           if (co < d.cout && ci < d.cin)
-            out[(((size_t)w * 72 + s) * 64 + l) * 8 + i] = W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
+            out[(((size_t)w * 36 + s) * 64 + l) * 8 + i] = W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
         }
       }
   return out;
