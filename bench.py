@@ -126,8 +126,11 @@ def main():
     # dominant kernel: the residual-trunk conv without a fused join (conv_wstat.hip, WF_NORM):
     # res1.conv1 and every res*.conv2, 6 launches per step; res2..5.conv1 also join the residual
     # stream in their fill (reported separately in whole_path)
-    plain = [(n, ms, c) for (n, ms, c) in prof if n.startswith("res") and (n.startswith("res1.") or ".conv2" in n)]
-    joined = [(n, ms, c) for (n, ms, c) in prof if n.startswith("res") and not (n.startswith("res1.") or ".conv2" in n)]
+    def _plain(n):  # "res1.conv1.conv2d", "res3.conv2.conv2d", ...
+        parts = n.split(".")
+        return parts[0] == "res1" or parts[1] == "conv2"
+    plain = [(n, ms, c) for (n, ms, c) in prof if n.startswith("res") and _plain(n)]
+    joined = [(n, ms, c) for (n, ms, c) in prof if n.startswith("res") and not _plain(n)]
     res_ms = sum(ms for _, ms, _ in plain)
     res_launches = sum(c for _, _, c in plain)
     res_avg_ms = res_ms / max(res_launches, 1)

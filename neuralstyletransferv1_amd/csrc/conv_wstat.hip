@@ -50,23 +50,35 @@ struct WsCfg {
   static constexpr int NSTEP = 36;                 // 4 parts x 9 taps (K = 32 per step)
   static constexpr int NUNIT = 8;                  // half parts: unit u = chunks 2u (team 0), 2u+1 (team 1)
   static constexpr int QENT = NENT / 4;            // entries per wave and unit (four waves per chunk)
-  static constexpr int IPL = (QENT + 63) / 64;     // items per lane and unit
+  static constexpr int NFMAX = 16;                 // frames per launch (IN tables resident in LDS)
+  static constexpr int NSLOT = 4;                  // staging slots: units in flight
+  static constexpr int SLOTB = 2 * NW * 1024;      // a slot: [y | r] x wave x lane x 16 B
   static constexpr int MAPB = ((LH + LW) * 4 + 15) / 16 * 16;
   static constexpr int MAP_OFF = NENT * EB;
-  static constexpr int NORM_OFF = MAP_OFF + 2 * MAPB;  // 2 slots x {y, r} x 16 chunks x {scale[8], shift[8]}
-  static constexpr int NORM_SLOT = 2 * CINP * 8;
-  static constexpr int BIAS_OFF = NORM_OFF + 2 * NORM_SLOT;  // 128 fp32
+  static constexpr int NORM_OFF = MAP_OFF + 2 * MAPB;        // [y | r][frame][channel] float2
+  static constexpr int NORM_TAB = NFMAX * CINP * 8;
+  static constexpr int BIAS_OFF = NORM_OFF + 2 * NORM_TAB;   // 128 fp32
   static constexpr int DUMMY_OFF = BIAS_OFF + CINP * 4;      // sink of the lanes without an item
-  static constexpr int LDS = DUMMY_OFF + 64 * 16;
+  static constexpr int STG_OFF = DUMMY_OFF + 64 * 16;
+  static constexpr int LDS = STG_OFF + NSLOT * SLOTB;
   static constexpr int WBYTES = NW * NSTEP * 64 * 16;  // packed weights
-  static_assert(NENT % 4 == 0, "four waves per unit chunk");
+  static_assert(NENT % 4 == 0 && QENT <= 64, "four waves per unit chunk, one item per lane");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
 // what the fill applies to a staged input chunk
 enum WsFill { WF_NORM = 0, WF_RAW = 1, WF_RES = 2, WF_RESRN = 3 };  // IN+ReLU / identity / join / join of ReLU(IN(r))
 
-template <int TH, int FILL>
+// s_waitcnt vmcnt(N) / the part barrier, as statements hipcc cannot move memory operations across
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int TH, int FILL, bool ZPAD>
 __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   using C = WsCfg<TH>;
   constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
@@ -102,6 +114,27 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
 #pragma unroll
     for (int s = 0; s < C::NSTEP; ++s) wr[s] = wsrc[s * 64];
   }
+  // ---- the launch's IN constants (<= NFMAX frames) and bias, resident in LDS ----
+  // per frame and 8-channel chunk: scale[8], shift[8] (planar, so a packed FMA takes its scale and
+  // shift pairs straight from one ds_read_b128 each)
+  float* norm_y = (float*)(smem + C::NORM_OFF);
+  float* norm_r = norm_y + C::NFMAX * C::CINP * 2;
+  if (FILL != WF_RAW) {
+    const int nfr = p.n_work / ntile;
+    for (int t = tid; t < nfr * C::CINP; t += C::NT) {
+      const int f = t / C::CINP, c = t - f * C::CINP;
+      const int o = (f * 16 + (c >> 3)) * 16 + (c & 7);
+      const float2 v = p.in_norm[(size_t)f * p.cs + c];
+      norm_y[o] = v.x;
+      norm_y[o + 8] = v.y;
+      if (RN) {
+        const float2 r = p.res_rnorm[(size_t)f * p.cs + c];
+        norm_r[o] = r.x;
+        norm_r[o + 8] = r.y;
+      }
+    }
+  }
+  if (tid < C::CINP) ((float*)(smem + C::BIAS_OFF))[tid] = p.bias[tid];
 
   // ---- halo staging ----
   const size_t frame_bytes = (size_t)p.hs * p.ws * p.cs * 2;
@@ -114,18 +147,6 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     int* colmap = rowmap + C::LH;
     const int vy0 = wk.ty0 - p.pad, vx0 = wk.tx0 - p.pad;
     const int pix = p.cs * 2;
-    // the tile's frame's IN constants (producer, or residual y), per chunk as scale[8], shift[8]
-    float* norm_l = (float*)(smem + C::NORM_OFF + slot * C::NORM_SLOT);
-    if (FILL != WF_RAW && tid < C::CINP) {
-      const float2 v = p.in_norm[(size_t)wk.n * p.cs + tid];
-      norm_l[(tid >> 3) * 16 + (tid & 7)] = v.x;
-      norm_l[(tid >> 3) * 16 + 8 + (tid & 7)] = v.y;
-      if (RN) {  // the residual's own IN (+ReLU): block 1's x_0 = ReLU(IN(conv3)) is not materialised
-        const float2 r = p.res_rnorm[(size_t)wk.n * p.cs + tid];
-        norm_l[2 * C::CINP + (tid >> 3) * 16 + (tid & 7)] = r.x;
-        norm_l[2 * C::CINP + (tid >> 3) * 16 + 8 + (tid & 7)] = r.y;
-      }
-    }
     for (int t = tid; t < C::LH + C::LW; t += C::NT) {
       if (t < C::LH) {
         const int sy = map_axis(vy0 + t, p.hs, p.axis_mode, p.pre);
@@ -136,107 +157,104 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
       }
     }
   };
-  // item k of this lane in every unit: entry ebase + 64k of chunk 2u + team; psrc = its byte offset
-  // in the frame (chunk 0), -1 = zero padding; pvalid / pint bit k: the item exists / is one of the
-  // tile's own pixels (RES: residual-stream write).  Branch-free, so it can sit between MFMAs.
+  // this lane's item in every unit of a tile: entry ebase of chunk 2u + team.  src = its byte offset
+  // in the frame (chunk 0), -1 = zero padding; valid: the entry exists; own: one of the tile's own
+  // pixels (RES: residual-stream write)
   const int ebase = (wv & 3) * C::QENT + lane;
-  int psrc[C::IPL];
-  unsigned pvalid = 0, pint = 0;
+  struct Item {
+    int src;
+    bool valid, own;
+  };
   auto items = [&](const Work& wk, int slot) {
     const int* rowmap = (const int*)(smem + C::MAP_OFF + slot * C::MAPB);
     const int* colmap = rowmap + C::LH;
-    pvalid = 0;
-    pint = 0;
-#pragma unroll
-    for (int k = 0; k < C::IPL; ++k) {
-      const bool ok = lane + 64 * k < C::QENT;
-      const int e = ok ? ebase + 64 * k : 0;
-      const int ly = e / C::LW, lx = e - ly * C::LW;
-      const int ro = rowmap[ly], co = colmap[lx];
-      psrc[k] = (ro >= 0 && co >= 0) ? ro + co : -1;
-      pvalid |= (ok ? 1u : 0u) << k;
-      const bool in = ok && ly >= p.pad && ly < p.pad + TH && lx >= p.pad && lx < p.pad + C::TW &&
-                      wk.ty0 + ly - p.pad < p.oh && wk.tx0 + lx - p.pad < p.ow;
-      pint |= (in ? 1u : 0u) << k;
-    }
+    Item it;
+    it.valid = lane < C::QENT;
+    const int e = it.valid ? ebase : 0;
+    const int ly = e / C::LW, lx = e - ly * C::LW;
+    const int ro = rowmap[ly], co = colmap[lx];
+    it.src = (ro >= 0 && co >= 0) ? ro + co : -1;
+    it.own = it.valid && ly >= p.pad && ly < p.pad + TH && lx >= p.pad && lx < p.pad + C::TW &&
+             wk.ty0 + ly - p.pad < p.oh && wk.tx0 + lx - p.pad < p.ow;
+    return it;
   };
-  uint4 praw[C::IPL], praw2[C::IPL];
-  auto issue_unit = [&](int n, int u) {
-#ifdef WS_NOLOAD  // experiment: no fill loads (measures the rest of the pipeline)
-    for (int k = 0; k < C::IPL; ++k) { praw[k] = make_uint4(0u, 0u, 0u, 0u); praw2[k] = praw[k]; }
-    return;
-#endif
-    const int soff = (2 * u + team) * 16;  // the unit's chunk for this wave
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(p.in, n);
-#pragma unroll
-    for (int k = 0; k < C::IPL; ++k)
-      praw[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, psrc[k] > 0 ? psrc[k] : 0, soff, 0));
-    if constexpr (RES) {
-      const __amdgpu_buffer_rsrc_t rs2 = frame_rsrc(p.res_r, n);
-#pragma unroll
-      for (int k = 0; k < C::IPL; ++k)
-        praw2[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs2, psrc[k] > 0 ? psrc[k] : 0, soff, 0));
-    }
+  // Units travel by LDS-DMA (buffer_load ... lds: no VGPR destination) into a 4-slot staging ring:
+  // unit g + 4 is requested right after unit g is consumed, so every unit has two parts of MFMAs to
+  // land.  Each lane reads back only its own 16 bytes, so only this wave's vmcnt orders them.  The
+  // loads are asm, invisible to hipcc's wait counting, and every vector-memory instruction issues in
+  // order: before unit g is consumed, vmcnt(K) with K = the instructions this wave issued after
+  // unit g's requests — 3 units' requests, 3 residual-stream stores (RES), and the epilogue's
+  // TH + 1 stores when one lies in between (units 0, 1, 6, 7).  Any extra instruction hipcc adds
+  // only makes such a wait stricter.
+  const uint32_t stg = (uint32_t)(uintptr_t)(smem + C::STG_OFF) + wv * 1024;
+  auto dma16 = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, uint32_t lds, int soff) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(lds), "s"(rs), "s"(soff)
+        : "memory");
   };
+  auto request = [&](int n, int u, const Item& it) {
+    const uint32_t voff = (it.valid && it.src >= 0) ? (uint32_t)it.src : 0x80000000u;  // pad: reads 0
+    const int soff = (2 * u + team) * 16;                                                // the unit's chunk
+    const uint32_t lds = stg + (u % C::NSLOT) * C::SLOTB;
+    dma16(frame_rsrc(p.in, n), voff, lds, soff);
+    if constexpr (RES) dma16(frame_rsrc(p.res_r, n), voff, lds + C::NW * 1024, soff);
+  };
+  // consume unit u of tile wk: IN + ReLU / residual join of the staged chunk into the halo.
   // live = false: a restaging pass past the last work item (LDS only, no residual-stream stores)
-  auto write_unit = [&](const Work& wk, int slot, int u, bool live) {
+  auto consume = [&](const Work& wk, int u, const Item& it, bool live) {
     const int ch = 2 * u + team;
-    // the chunk's 8 scales and 8 shifts: one wave-uniform (broadcast) LDS row
-    const float* nl = (const float*)(smem + C::NORM_OFF + slot * C::NORM_SLOT) + ch * 16;
-    float sc[8], sh[8], rsc[8], rsh[8];
+    const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
+    const uint4 y = *(const uint4*)sp;
+    const uint4 rr = RES ? *(const uint4*)(sp + C::NW * 1024) : make_uint4(0u, 0u, 0u, 0u);
+    const float* ny = norm_y + (wk.n * 16 + ch) * 16;  // scale[8], shift[8]
+    const float* nr = norm_r + (wk.n * 16 + ch) * 16;
+    const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+    uint32_t o[4];
+    if constexpr (RES) {
+      // ResidualBlock join (transformer_net.py:71-76): IN_y(y) + r in fp32, product then sum (the
+      // file is built with -ffp-contract=off), one rounding — as res_chunk / residual_kernel
+      const uint32_t w2[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = nl[j];
-      sh[j] = nl[8 + j];
-      rsc[j] = RN ? nl[2 * C::CINP + j] : 1.f;
-      rsh[j] = RN ? nl[2 * C::CINP + 8 + j] : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        float r0 = bf16_lo(w2[j]), r1 = bf16_hi(w2[j]);
+        if (RN) {
+          r0 = fmaxf(r0 * nr[2 * j] + nr[8 + 2 * j], 0.f);
+          r1 = fmaxf(r1 * nr[2 * j + 1] + nr[8 + 2 * j + 1], 0.f);
+        }
+        const float a = bf16_lo(w[j]) * ny[2 * j] + ny[8 + 2 * j];
+        const float bb = bf16_hi(w[j]) * ny[2 * j + 1] + ny[8 + 2 * j + 1];
+        o[j] = pack_bf16(r0 + a, r1 + bb);
+      }
+    } else if constexpr (FILL == WF_RAW) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = w[j];
+    } else {
+      // producer IN apply + ReLU, as norm_chunk
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = __builtin_fmaf(bf16_lo(w[j]), ny[2 * j], ny[8 + 2 * j]);
+        const float bb = __builtin_fmaf(bf16_hi(w[j]), ny[2 * j + 1], ny[8 + 2 * j + 1]);
+        const i16x2_t r = __builtin_bit_cast(i16x2_t, pack_bf16(a, bb));
+        o[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
+      }
     }
-    const __amdgpu_buffer_rsrc_t ro = frame_rsrc(p.res_out, wk.n);
+    const bool pad = ZPAD && it.src < 0;  // zero padding stays zero (pad after IN + ReLU); reflection never pads
+    const u32x4_t v = {pad ? 0u : o[0], pad ? 0u : o[1], pad ? 0u : o[2], pad ? 0u : o[3]};
+    if constexpr (RES) {
+      const bool own = live && it.own;
+      __builtin_amdgcn_raw_buffer_store_b128(v, frame_rsrc(p.res_out, wk.n), own ? (uint32_t)(it.src + ch * 16) : 0x80000000u,
+                                             0, 0);
+    }
     int eb = ebase * C::EB + ch * 16;  // recomputed per unit, not held across the loop
     asm volatile("" : "+v"(eb));
-#pragma unroll
-    for (int k = 0; k < C::IPL; ++k) {
-      const uint32_t w[4] = {praw[k].x, praw[k].y, praw[k].z, praw[k].w};
-      uint32_t o[4];
-      if constexpr (RES) {
-        // ResidualBlock join (transformer_net.py:71-76): IN_y(y) + r in fp32, product then sum
-        // (the file is built with -ffp-contract=off), one rounding — as res_chunk / residual_kernel
-        const uint32_t wr2[4] = {praw2[k].x, praw2[k].y, praw2[k].z, praw2[k].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float r0 = bf16_lo(wr2[j]), r1 = bf16_hi(wr2[j]);
-          if (RN) {
-            r0 = fmaxf(r0 * rsc[2 * j] + rsh[2 * j], 0.f);
-            r1 = fmaxf(r1 * rsc[2 * j + 1] + rsh[2 * j + 1], 0.f);
-          }
-          const float a = bf16_lo(w[j]) * sc[2 * j] + sh[2 * j];
-          const float bb = bf16_hi(w[j]) * sc[2 * j + 1] + sh[2 * j + 1];
-          o[j] = pack_bf16(r0 + a, r1 + bb);
-        }
-      } else if constexpr (FILL == WF_RAW) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = w[j];
-      } else {
-        // producer IN apply + ReLU, as norm_chunk
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float a = __builtin_fmaf(bf16_lo(w[j]), sc[2 * j], sh[2 * j]);
-          const float bb = __builtin_fmaf(bf16_hi(w[j]), sc[2 * j + 1], sh[2 * j + 1]);
-          const i16x2_t r = __builtin_bit_cast(i16x2_t, pack_bf16(a, bb));
-          o[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
-        }
-      }
-      const bool pad = psrc[k] < 0;  // zero padding stays zero (pad after IN + ReLU)
-      const u32x4_t v = {pad ? 0u : o[0], pad ? 0u : o[1], pad ? 0u : o[2], pad ? 0u : o[3]};
-      if constexpr (RES) {
-        const bool own = live && ((pint >> k) & 1u);
-        __builtin_amdgcn_raw_buffer_store_b128(v, ro, own ? (uint32_t)(psrc[k] + ch * 16) : 0x80000000u, 0, 0);
-      }
-      const bool valid = (pvalid >> k) & 1u;
-      const int dst = valid ? eb + 64 * k * C::EB : C::DUMMY_OFF + lane * 16;
-      *(u32x4_t*)(smem + dst) = v;
-    }
+    *(u32x4_t*)(smem + (it.valid ? eb : C::DUMMY_OFF + lane * 16)) = v;
   };
+  constexpr int DPU = RES ? 2 : 1;                // requests per unit
+  constexpr int KIN = 3 * DPU + (RES ? 3 : 0);    // vmcnt before a unit whose wait spans no epilogue
+  constexpr int KEP = KIN + TH + 1;               // ... one that spans the epilogue's stores
 
   // ---- K loop ----
   typedef f32x4_t Acc[TH];
@@ -250,12 +268,19 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const int dx = rem / NRD, y = rem % NRD;
     return *(const uint4*)(smem + lbase + (y * C::LW + dx) * C::EB + 64 * q);
   };
+  // The MFMAs are asm with the accumulator tied in place: hipcc's VGPR-form selection otherwise
+  // moves every accumulator into fresh registers and pads the reuse of the old ones with s_nops.
+  // The hazards hipcc cannot see are covered by construction: each tile's first MFMA of a row
+  // takes C = 0 (no VALU write feeds an MFMA), operands come from loads it waits for, an
+  // accumulation chain needs no wait states, and mfma_drain() pads before the epilogue reads.
+  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
+    const u32x4_t av = __builtin_bit_cast(u32x4_t, a), bv = __builtin_bit_cast(u32x4_t, bop);
+    if (first)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(av), "v"(bv));
+    else
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
+  };
   auto kloop = [&](Acc& acc, auto&& hook, auto&& bound) {
-    {  // accumulators start at the bias of this lane's 4 channels
-      const f32x4_t bv = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 * wv + 4 * g) * 4);
-#pragma unroll
-      for (int r = 0; r < TH; ++r) acc[r] = bv;
-    }
     constexpr int NI = 4 * PRD, D = WS_RING;
     uint4 ring[D];
 #pragma unroll
@@ -271,132 +296,147 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         const int r = y - dy;
         if (r < 0 || r >= TH) continue;
         const int s = q * 9 + 3 * dy + dx;  // packed weight step
-        acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wr[s]),
-                                                         __builtin_bit_cast(bf16x8_t, bcur), acc[r], 0, 0, 0);
+        mfma(acc[r], wr[s], bcur, q == 0 && dx == 0 && dy == 0);  // row r's first: y = r, dx = dy = 0
       }
-#ifndef WS_NOHOOK  // experiment: K loop + epilogue only
-#ifndef WS_NOUNIT  // experiment: barriers but no unit work
       hook(q, rem);
-#endif
       if (rem == PRD - 1) {
-#ifndef WS_NOBAR  // experiment: unit work without barriers (racy: timing only)
-        __syncthreads();  // every wave is past its reads of part q
-#endif
+        lds_barrier();  // every wave is past its reads of part q (in-flight unit requests stay in flight)
         bound(q);
       }
-#endif
       // pin the order: read i + D with read i's MFMAs (the scheduler otherwise pulls every read
       // down next to its consumers, exposing the LDS latency on each one)
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  // ---- epilogue: bf16 NHWC store (bias is the accumulators' initial value), InstanceNorm partial
-  // sums: lane (px, g) holds channels 16 wv + 4g .. +3 of pixel px of every tile row ----
+  // ---- epilogue: bias, bf16 NHWC store, InstanceNorm partial
+  // sums: lane (px, g) holds channels 16 wv + 4g .. +3 of pixel px of every tile row.  Exactly
+  // TH + 1 vector-memory instructions (the unit waits above count on it) ----
   auto epilogue = [&](const Work& wk, Acc& acc) {
+    // the last MFMAs' results: 8-pass XDL write -> VALU read needs >= 12 wait states (20 here)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     const int c0 = 16 * wv + 4 * g;
+    const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
     const size_t obytes = (size_t)p.oh * p.ow * p.cout_stride * 2;
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((char*)p.out + (size_t)wk.n * obytes), (short)0, (int)obytes, 0x00020000);
     const int ox = wk.tx0 + px;
-    float vv[8];
+    const uint32_t row_bytes = (uint32_t)p.ow * p.cout_stride * 2;
+    const uint32_t off0 = (uint32_t)(((wk.ty0 * p.ow + ox) * p.cout_stride + c0) * 2);
+    f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};  // packed-math statistics
+    auto rows = [&](auto all_valid) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) vv[e] = 0.f;
-#pragma unroll
-    for (int r = 0; r < TH; ++r) {
-      const int oy = wk.ty0 + r;
-      const bool valid = oy < p.oh && ox < p.ow;
-      const f32x4_t v = acc[r];
-      const uint32_t off = valid ? (uint32_t)(((oy * p.ow + ox) * p.cout_stride + c0) * 2) : 0x80000000u;
-      const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
-      __builtin_amdgcn_raw_buffer_store_b64(pk, ors, off, 0, 0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x = valid ? v[e] : 0.f;
-        vv[2 * e] += x;
-        vv[2 * e + 1] = __builtin_fmaf(x, x, vv[2 * e + 1]);
+      for (int r = 0; r < TH; ++r) {
+        const bool valid = decltype(all_valid)::value || (wk.ty0 + r < p.oh && ox < p.ow);
+        const f32x4_t v = acc[r] + bias;
+        const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+        __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : 0x80000000u, 0, 0);
+        const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        s1 += x;
+        s2 = __builtin_elementwise_fma(x, x, s2);
       }
-    }
-    if (p.partial != nullptr) {
-      // reduce-scatter of the 8 statistics over the 16 pixel lanes of the DPP row, then the xor-1
-      // partner: lane px (even) ends with statistic idx & 1 of channel c0 + (idx >> 1),
-      // idx = 4 (px >= 8) + 2 (px & 4) + (px & 2) / 2
-      float a4[4], a2[2], a1[1];
-      rs_step<4, 0x140>(vv, a4, px >= 8);
-      rs_step<2, 0x141>(a4, a2, (px & 4) != 0);
-      rs_step<1, 0x1b>(a2, a1, (px & 2) != 0);
-      const float t = a1[0] + dpp_f<0xb1>(a1[0]);
-      const int idx = (px >= 8 ? 4 : 0) + ((px & 4) ? 2 : 0) + ((px & 2) ? 1 : 0);
-      if ((px & 1) == 0)
-        p.partial[(((size_t)wk.n * ntile + wk.tile) * p.cout_stride + c0 + (idx >> 1)) * 2 + (idx & 1)] = t;
-    }
+    };
+    // every tile but those on the bottom / right edge: no per-row validity
+    if (wk.ty0 + TH <= p.oh && wk.tx0 + C::TW <= p.ow)
+      rows(std::true_type{});
+    else
+      rows(std::false_type{});
+    const float vv[8] = {s1[0], s2[0], s1[1], s2[1], s1[2], s2[2], s1[3], s2[3]};
+    // reduce-scatter of the 8 statistics over the 16 pixel lanes of the DPP row, then the xor-1
+    // partner: lane px (even) ends with statistic idx & 1 of channel c0 + (idx >> 1),
+    // idx = 4 (px >= 8) + 2 (px & 4) + (px & 2) / 2
+    float a4[4], a2[2], a1[1];
+    rs_step<4, 0x140>(vv, a4, px >= 8);
+    rs_step<2, 0x141>(a4, a2, (px & 4) != 0);
+    rs_step<1, 0x1b>(a2, a1, (px & 2) != 0);
+    const float t = a1[0] + dpp_f<0xb1>(a1[0]);
+    const int idx = (px >= 8 ? 4 : 0) + ((px & 4) ? 2 : 0) + ((px & 2) ? 1 : 0);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.partial + ((size_t)wk.n * ntile + wk.tile) * p.cout_stride * 2), (short)0, p.cout_stride * 8,
+        0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs,
+                                          (px & 1) ? 0x80000000u : (uint32_t)(((c0 + (idx >> 1)) * 2 + (idx & 1)) * 4), 0, 0);
   };
 
   // ---- persistent walk ----
-  if (tid < C::CINP) ((float*)(smem + C::BIAS_OFF))[tid] = p.bias[tid];
   Work cur = decode(w0);
   int wn = w0 + G;
   const int last = p.n_work - 1;
   build_maps(cur, 0);
   build_maps(decode(min(wn, last)), 1);
   __syncthreads();
-  items(cur, 0);
-  // units 0..5 now; unit 6 stays in flight and is written in part 0 like every later tile's
+  // prologue: the first tile's units (units 6, 7 and the next tile's 0, 1 stay in flight, as in
+  // the steady state); then drain once, so every later wait counts only steady-state instructions
+  Item xx = items(cur, 0);  // sources of the tile being consumed
+  Item xd = xx;             // ... and of the tile being requested
 #pragma unroll
-  for (int u = 0; u < C::NUNIT - 1; ++u) {
-    issue_unit(cur.n, u);
-    if (u + 2 < C::NUNIT) write_unit(cur, 0, u, true);
-    __builtin_amdgcn_sched_barrier(0);  // one unit's loads in flight at a time
+  for (int u = 0; u < C::NSLOT; ++u) request(cur.n, u, xd);
+  {
+    const Work n1 = decode(min(wn, last));
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      vm_wait<0>();
+      consume(cur, u, xx, true);
+      if (u + 4 < C::NUNIT) {
+        request(cur.n, u + 4, xd);
+      } else {
+        if (u + 4 == C::NUNIT) xd = items(n1, 1);
+        request(n1.n, u + 4 - C::NUNIT, xd);
+      }
+    }
   }
+  vm_wait<0>();
   __syncthreads();
   // Unit schedule (u = 2q + half; region q is free once the barrier ending part q has passed):
-  //   part 0: A: write 6 of cur, load 7 | B: write 7 of cur, next tile's item sources, load 0
-  //   part q = 1..3: A: write 2q-2, load 2q-1 | B: write 2q-1, load 2q      (of the next tile)
-  // so every unit's loads have half a part of MFMAs to land.  A is right after the part's first
-  // reads, B half a part later; team 1 runs a quarter part behind team 0.
+  //   part 0: A: unit 6 of cur, request 2 of nxt    | B: unit 7 of cur, request 3 of nxt
+  //   part 1: A: unit 0 of nxt, request 4 of nxt    | B: unit 1, request 5
+  //   part 2: A: unit 2, request 6                  | B: unit 3, request 7
+  //   part 3: A: unit 4, request 0 of the tile after nxt | B: unit 5, request 1 of it
+  // A is right after the part's first reads, B half a part later; team 1 runs a quarter part
+  // behind team 0 so the two waves of a SIMD never stage at the same time.
   constexpr int POS_A = 0, POS_B = PRD / 2, DT = PRD / 4;
   Acc acc;
   for (int it = 0;; ++it) {
-    // past the last work item the hooks restage LDS with whatever the next-tile slots hold (never
-    // read again) and store nothing, so they need no branch
+    // past the last work item the hooks restage LDS with whatever they are given (never read
+    // again) and store nothing, so they need no branch
     const bool more = wn < p.n_work;
     const Work nxt = more ? decode(wn) : cur;
-    const int cs = it & 1, ns = cs ^ 1;  // map / IN-table slots of cur and nxt
+    const Work nxt2 = decode(min(wn + G, last));
+    const int cs = it & 1, ns = cs ^ 1;  // map slots of cur and nxt
     kloop(
         acc,
         [&](int q, int rem) {  // after read rem of part q
           const int pa = POS_A + (team ? DT : 0), pb = POS_B + (team ? DT : 0);
+          if (rem != pa && rem != pb) return;
+          const int half = rem == pa ? 0 : 1;
           if (q == 0) {
-            if (rem == pa) {
-              write_unit(cur, cs, 6, true);
-              issue_unit(cur.n, 7);
-            }
-            if (rem == pb) {
-              write_unit(cur, cs, 7, true);
-              items(nxt, ns);
-              issue_unit(nxt.n, 0);
-            }
+            if (half == 0) vm_wait<KEP>(); else vm_wait<KEP>();
+            consume(cur, 6 + half, xx, true);
+            request(nxt.n, 2 + half, xd);
           } else {
-            if (rem == pa) {
-              write_unit(nxt, ns, 2 * q - 2, more);
-              issue_unit(nxt.n, 2 * q - 1);
-            }
-            if (rem == pb) {
-              write_unit(nxt, ns, 2 * q - 1, more);
-              issue_unit(nxt.n, 2 * q);
+            const int u = 2 * (q - 1) + half;
+            if (u == 0) xx = items(nxt, ns);
+            if (u <= 1) vm_wait<KEP>(); else vm_wait<KIN>();
+            consume(nxt, u, xx, more);
+            if (u + 4 < C::NUNIT) {
+              request(nxt.n, u + 4, xd);
+            } else {
+              if (u == 4) xd = items(nxt2, cs);
+              request(nxt2.n, u - 4, xd);
             }
           }
         },
         [&](int q) {  // after the barrier that ends part q
-          // the tile after nxt into cur's slot: its last reader (cur's units 6/7) ran in part 0, and
-          // the barriers ending parts 2 and 3 publish it before nxt's part 0 reads it (items)
-          if (q == 1) build_maps(decode(min(wn + G, last)), cs);
+          // the tile after nxt into cur's slot: cur's sources were last resolved in the previous
+          // iteration, and the barriers ending parts 1 and 2 publish it before part 3 resolves it
+          if (q == 0) build_maps(nxt2, cs);
         });
     epilogue(cur, acc);
     if (!more) break;
     cur = nxt;
     wn += G;
   }
+  vm_wait<0>();  // no LDS-DMA may land after the workgroup has released its LDS
 }
 
 template <int TH, bool RES>
@@ -411,20 +451,39 @@ struct WstatInst {
     }();
     return v;
   }
+  template <int FILL, bool ZPAD>
+  static void go(const ConvParams& p, int nb, hipStream_t st) {
+    hipLaunchKernelGGL((wstat_kernel<TH, FILL, ZPAD>), dim3(nb), dim3(C::NT), 0, st, p);
+  }
+  // grid.x = tiles per frame, grid.y = frames; launched in chunks of <= NFMAX frames (the IN tables
+  // of a launch's frames live in LDS)
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
-    ConvParams p = p0;
-    p.n_work = (int)(grid.x * grid.y);
-    const int nb = std::min(p.n_work, cus());  // one workgroup per CU (registers)
-    if constexpr (RES) {
-      if (p.res_rnorm != nullptr)  // block 1's join: the residual is ReLU(IN(conv3)), applied here
-        hipLaunchKernelGGL((wstat_kernel<TH, WF_RESRN>), dim3(nb), dim3(C::NT), 0, st, p);
-      else
-        hipLaunchKernelGGL((wstat_kernel<TH, WF_RES>), dim3(nb), dim3(C::NT), 0, st, p);
-    } else {
-      if (p.in_norm != nullptr)
-        hipLaunchKernelGGL((wstat_kernel<TH, WF_NORM>), dim3(nb), dim3(C::NT), 0, st, p);
-      else  // the residual stream itself (unfused joins)
-        hipLaunchKernelGGL((wstat_kernel<TH, WF_RAW>), dim3(nb), dim3(C::NT), 0, st, p);
+    const int ntile = (int)grid.x, n = (int)grid.y;
+    const size_t fin = (size_t)p0.hs * p0.ws * p0.cs * 2, fout = (size_t)p0.oh * p0.ow * p0.cout_stride * 2;
+    for (int f0 = 0; f0 < n; f0 += C::NFMAX) {
+      const int nf = std::min(C::NFMAX, n - f0);
+      ConvParams p = p0;
+      p.in = (const char*)p0.in + f0 * fin;
+      p.out = (char*)p0.out + f0 * fout;
+      if (p0.res_r) p.res_r = (const char*)p0.res_r + f0 * fin;
+      if (p0.res_out) p.res_out = (char*)p0.res_out + f0 * fin;
+      if (p0.in_norm) p.in_norm = p0.in_norm + (size_t)f0 * p0.cs;
+      if (p0.res_rnorm) p.res_rnorm = p0.res_rnorm + (size_t)f0 * p0.cs;
+      p.partial = p0.partial + (size_t)f0 * ntile * p0.cout_stride * 2;
+      p.n_work = nf * ntile;
+      const int nb = std::min(p.n_work, cus());  // one workgroup per CU (registers, LDS)
+      const bool zp = p.axis_mode != AX_REFLECT;  // zero-padded trunk (transformer_net_nst.py ConvBlock)
+      if constexpr (RES) {
+        if (p.res_rnorm != nullptr)  // block 1's join: the residual is ReLU(IN(conv3)), applied here
+          zp ? go<WF_RESRN, true>(p, nb, st) : go<WF_RESRN, false>(p, nb, st);
+        else
+          zp ? go<WF_RES, true>(p, nb, st) : go<WF_RES, false>(p, nb, st);
+      } else {
+        if (p.in_norm != nullptr)
+          zp ? go<WF_NORM, true>(p, nb, st) : go<WF_NORM, false>(p, nb, st);
+        else  // the residual stream itself (unfused joins)
+          zp ? go<WF_RAW, true>(p, nb, st) : go<WF_RAW, false>(p, nb, st);
+      }
     }
   }
   static ConvKernelInfo info() {
