@@ -72,10 +72,14 @@ enum WsFill { WF_NORM = 0, WF_RAW = 1, WF_RES = 2, WF_RESRN = 3 };  // IN+ReLU /
 // s_waitcnt vmcnt(N) / the part barrier, as statements hipcc cannot move memory operations across
 template <int N>
 __device__ __forceinline__ void vm_wait() {
+#ifndef WS_NOWAIT  // experiment (racy): no waits for the unit requests
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#endif
 }
 __device__ __forceinline__ void lds_barrier() {
+#ifndef WS_NOBAR  // experiment (racy): no part barriers
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
 }
 
 template <int TH, int FILL, bool ZPAD>
@@ -205,6 +209,9 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   // consume unit u of tile wk: IN + ReLU / residual join of the staged chunk into the halo.
   // live = false: a restaging pass past the last work item (LDS only, no residual-stream stores)
   auto consume = [&](const Work& wk, int u, const Item& it, bool live) {
+#ifdef WS_NOCONSUME  // experiment: no unit transform / halo write
+    return;
+#endif
     const int ch = 2 * u + team;
     const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
     const uint4 y = *(const uint4*)sp;
@@ -298,7 +305,9 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         const int s = q * 9 + 3 * dy + dx;  // packed weight step
         mfma(acc[r], wr[s], bcur, q == 0 && dx == 0 && dy == 0);  // row r's first: y = r, dx = dy = 0
       }
+#ifndef WS_NOHOOK  // experiment: no unit work at all
       hook(q, rem);
+#endif
       if (rem == PRD - 1) {
         lds_barrier();  // every wave is past its reads of part q (in-flight unit requests stay in flight)
         bound(q);
