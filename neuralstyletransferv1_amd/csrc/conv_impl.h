@@ -933,7 +933,49 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
         }
         return;
       }
-      if (p.partial != nullptr) {
+      constexpr bool RS_STATS = !PERS && (NSUB == 1 || NSUB == 2 || NSUB == 4);
+      if (RS_STATS && p.partial != nullptr) {
+        // reduce-scatter the 2 x 4*NSUB statistics over the 16 pixel lanes of each lane group (one
+        // DPP row; log2(16) exchange steps instead of a full row sum per value), then combine the
+        // channel-sharing waves in LDS
+        const int rw = MODE == MODE_PHASE ? wave : wm;
+        const int cl0 = cwave - cb * BN + 4 * NSUB * g;
+        __syncthreads();  // LDS tile no longer read (the reduction aliases it)
+        float* red = (float*)(smem + RED_OFF);  // [REDW][BN][2]
+        constexpr int NV = 8 * NSUB;
+        float v[NV];
+#pragma unroll
+        for (int j = 0; j < 4 * NSUB; ++j) { v[2 * j] = s1[j]; v[2 * j + 1] = s2[j]; }
+        if constexpr (NV == 32) {
+          float t1, t2;
+          row_reduce_scatter32(v, px, t1, t2);  // lane px: channel cl0 + px
+          *(float2*)(red + (rw * BN + cl0 + px) * 2) = make_float2(t1, t2);
+        } else if constexpr (NV == 16) {
+          float a8[8], a4[4], a2[2], a1[1];
+          rs_step<8, 0x140>(v, a8, px >= 8);
+          rs_step<4, 0x141>(a8, a4, (px & 4) != 0);
+          rs_step<2, 0x1b>(a4, a2, (px & 2) != 0);
+          rs_step<1, 0xb1>(a2, a1, (px & 1) != 0);  // lane px: statistic px & 1 of channel cl0 + px / 2
+          red[(rw * BN + cl0 + (px >> 1)) * 2 + (px & 1)] = a1[0];
+        } else if constexpr (NV == 8) {
+          float a4[4], a2[2], a1[1];
+          rs_step<4, 0x140>(v, a4, px >= 8);
+          rs_step<2, 0x141>(a4, a2, (px & 4) != 0);
+          rs_step<1, 0x1b>(a2, a1, (px & 2) != 0);
+          const float t = a1[0] + dpp_f<0xb1>(a1[0]);
+          const int idx = (px >= 8 ? 4 : 0) + ((px & 4) ? 2 : 0) + ((px & 2) ? 1 : 0);
+          if ((px & 1) == 0) red[(rw * BN + cl0 + (idx >> 1)) * 2 + (idx & 1)] = t;
+        }
+        __syncthreads();
+        for (int cl = tid; cl < BN; cl += NT) {
+          float a = 0.f, b2 = 0.f;
+#pragma unroll
+          for (int rr = 0; rr < C::REDW; ++rr) { a += red[(rr * BN + cl) * 2]; b2 += red[(rr * BN + cl) * 2 + 1]; }
+          float* dst = p.partial + (((size_t)n * ntile + wk.tile) * p.cout_stride + cb * BN + cl) * 2;
+          dst[0] = a;
+          dst[1] = b2;
+        }
+      } else if (p.partial != nullptr) {
         // reduce over the 16 pixel lanes of each lane group (one DPP row)
 #pragma unroll
         for (int j = 0; j < 4 * NSUB; ++j) {
