@@ -162,12 +162,11 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     }
   };
   // this lane's item in every unit of a tile: entry ebase of chunk 2u + team.  src = its byte offset
-  // in the frame (chunk 0), -1 = zero padding; valid: the entry exists; own: one of the tile's own
-  // pixels (RES: residual-stream write)
+  // in the frame (chunk 0), -1 = zero padding; valid: the entry exists
   const int ebase = (wv & 3) * C::QENT + lane;
   struct Item {
     int src;
-    bool valid, own;
+    bool valid;
   };
   auto items = [&](const Work& wk, int slot) {
     const int* rowmap = (const int*)(smem + C::MAP_OFF + slot * C::MAPB);
@@ -178,8 +177,6 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const int ly = e / C::LW, lx = e - ly * C::LW;
     const int ro = rowmap[ly], co = colmap[lx];
     it.src = (ro >= 0 && co >= 0) ? ro + co : -1;
-    it.own = it.valid && ly >= p.pad && ly < p.pad + TH && lx >= p.pad && lx < p.pad + C::TW &&
-             wk.ty0 + ly - p.pad < p.oh && wk.tx0 + lx - p.pad < p.ow;
     return it;
   };
   // Units travel by LDS-DMA (buffer_load ... lds: no VGPR destination) into a 4-slot staging ring:
@@ -187,9 +184,9 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   // land.  Each lane reads back only its own 16 bytes, so only this wave's vmcnt orders them.  The
   // loads are asm, invisible to hipcc's wait counting, and every vector-memory instruction issues in
   // order: before unit g is consumed, vmcnt(K) with K = the instructions this wave issued after
-  // unit g's requests — 3 units' requests, 3 residual-stream stores (RES), and the epilogue's
-  // TH + 1 stores when one lies in between (units 0, 1, 6, 7).  Any extra instruction hipcc adds
-  // only makes such a wait stricter.
+  // unit g's requests — 3 units' requests, 2 residual-stream region stores (RES), and the
+  // epilogue's TH + 1 stores when one lies in between (units 0, 1, 6, 7).  Any extra instruction
+  // hipcc adds only makes such a wait stricter.
   const uint32_t stg = (uint32_t)(uintptr_t)(smem + C::STG_OFF) + wv * 1024;
   auto dma16 = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, uint32_t lds, int soff) {
     uint32_t keep;
@@ -250,17 +247,25 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     }
     const bool pad = ZPAD && it.src < 0;  // zero padding stays zero (pad after IN + ReLU); reflection never pads
     const u32x4_t v = {pad ? 0u : o[0], pad ? 0u : o[1], pad ? 0u : o[2], pad ? 0u : o[3]};
-    if constexpr (RES) {
-      const bool own = live && it.own;
-      __builtin_amdgcn_raw_buffer_store_b128(v, frame_rsrc(p.res_out, wk.n), own ? (uint32_t)(it.src + ch * 16) : 0x80000000u,
-                                             0, 0);
-    }
     int eb = ebase * C::EB + ch * 16;  // recomputed per unit, not held across the loop
     asm volatile("" : "+v"(eb));
     *(u32x4_t*)(smem + (it.valid ? eb : C::DUMMY_OFF + lane * 16)) = v;
   };
+  // RES: the joined residual stream x_{k+1} of the tile's own pixels goes to res_out from the halo,
+  // region by region (region q during part q: complete since unit 2q+1 was consumed, overwritten
+  // only in part q+1), as 64-byte pixel quarters — one store per lane and part, instead of 16-byte
+  // pieces per unit (which cost as much as the rest of the join)
+  auto store_region = [&](const Work& wk, int q) {
+    const int pix = tid >> 2, c = 4 * q + (tid & 3);  // 128 pixels x 4 chunks
+    const int r = pix >> 4, x = pix & 15;
+    const int oy = wk.ty0 + r, ox = wk.tx0 + x;
+    const u32x4_t v = *(const u32x4_t*)(smem + ((r + 1) * C::LW + x + 1) * C::EB + c * 16);
+    const bool ok = oy < p.oh && ox < p.ow;
+    __builtin_amdgcn_raw_buffer_store_b128(v, frame_rsrc(p.res_out, wk.n),
+                                           ok ? (uint32_t)(((oy * p.ws + ox) * p.cs + c * 8) * 2) : 0x80000000u, 0, 0);
+  };
   constexpr int DPU = RES ? 2 : 1;                // requests per unit
-  constexpr int KIN = 3 * DPU + (RES ? 3 : 0);    // vmcnt before a unit whose wait spans no epilogue
+  constexpr int KIN = 3 * DPU + (RES ? 2 : 0);    // vmcnt before a unit whose wait spans no epilogue
   constexpr int KEP = KIN + TH + 1;               // ... one that spans the epilogue's stores
 
   // ---- K loop ----
@@ -419,9 +424,10 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
           if (rem != pa && rem != pb) return;
           const int half = rem == pa ? 0 : 1;
           if (q == 0) {
-            if (half == 0) vm_wait<KEP>(); else vm_wait<KEP>();
+            vm_wait<KEP>();
             consume(cur, 6 + half, xx, true);
             request(nxt.n, 2 + half, xd);
+            if (RES && half == 0) store_region(cur, 0);
           } else {
             const int u = 2 * (q - 1) + half;
             if (u == 0) xx = items(nxt, ns);
@@ -433,6 +439,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
               if (u == 4) xd = items(nxt2, cs);
               request(nxt2.n, u - 4, xd);
             }
+            if (RES && half == 0) store_region(cur, q);
           }
         },
         [&](int q) {  // after the barrier that ends part q
