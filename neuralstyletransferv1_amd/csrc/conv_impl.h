@@ -868,9 +868,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
 #pragma unroll
         for (int j = 0; j < 4 * NSUB; ++j) bias_v[j] = p.bias[cbase + j];
       }
-      float s1[4 * NSUB], s2[4 * NSUB];
+      // bias add and statistics as 4-wide vectors: the per-element arithmetic (add, fma) is the same,
+      // issued as packed v_pk_add_f32 / v_pk_fma_f32 pairs
+      f32x4_t bias4[NSUB], s1v[NSUB], s2v[NSUB];
 #pragma unroll
-      for (int j = 0; j < 4 * NSUB; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+      for (int t = 0; t < NSUB; ++t) {
+        bias4[t] = (f32x4_t){bias_v[4 * t], bias_v[4 * t + 1], bias_v[4 * t + 2], bias_v[4 * t + 3]};
+        s1v[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        s2v[t] = s1v[t];
+      }
       // 32-bit offsets inside the frame (host guarantees a frame is < 2 GiB); a wave whose pixels
       // are all inside the image (every wave but the edge tiles') takes the branch-free copy
       char* fout = (char*)p.out + (size_t)n * p.oh * p.ow * p.cout_stride * sizeof(T);
@@ -887,11 +893,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
           int oy, ox;
           out_px(m, oy, ox);
           const bool valid = decltype(all_valid)::value || ((oy < p.oh) && (ox < p.ow));
+          f32x4_t v4[NSUB];
           float v[4 * NSUB];
 #pragma unroll
-          for (int t = 0; t < NSUB; ++t)
+          for (int t = 0; t < NSUB; ++t) {
+            v4[t] = acc[m][t] + bias4[t];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[4 * t + q] = acc[m][t][q] + bias_v[4 * t + q];
+            for (int q = 0; q < 4; ++q) v[4 * t + q] = v4[t][q];
+          }
           if (valid) {
             char* dst = fout + (unsigned)(((oy * p.ow + ox) * p.cout_stride + cbase) * (int)sizeof(T));
             if constexpr (sizeof(T) == 2) {
@@ -910,7 +919,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
                 *(float4*)(dst + t * 16) = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
             }
 #pragma unroll
-            for (int j = 0; j < 4 * NSUB; ++j) { s1[j] += v[j]; s2[j] = __builtin_fmaf(v[j], v[j], s2[j]); }
+            for (int t = 0; t < NSUB; ++t) {
+              s1v[t] += v4[t];
+              s2v[t] = __builtin_elementwise_fma(v4[t], v4[t], s2v[t]);
+            }
           }
         }
       };
@@ -919,6 +931,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
       } else {
         store_tile(std::false_type{});
       }
+      float s1[4 * NSUB], s2[4 * NSUB];
+#pragma unroll
+      for (int t = 0; t < NSUB; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { s1[4 * t + q] = s1v[t][q]; s2[4 * t + q] = s2v[t][q]; }
       if constexpr (PERS && 4 * NSUB == 16) {
         // one partial row per channel-sharing wave (tile*REDW + rw): no barrier, no LDS; the 16
         // pixel lanes of a lane group reduce-scatter so lane px ends with channel cbase + px
