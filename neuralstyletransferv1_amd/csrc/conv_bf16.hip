@@ -7,7 +7,7 @@
 #define NST_C1_TILE 8, 32, 4, 1
 #endif
 #ifndef NST_C2_TILE
-#define NST_C2_TILE 8, 16, 4, 1
+#define NST_C2_TILE 4, 16, 2, 2
 #endif
 #ifndef NST_C3_TILE
 #define NST_C3_TILE 4, 16, 2, 2
@@ -16,7 +16,7 @@
 #define NST_D1_TILE 4, 16, 1, 4
 #endif
 #ifndef NST_D2_TILE
-#define NST_D2_TILE 8, 16, 1, 4
+#define NST_D2_TILE 4, 16, 1, 4
 #endif
 
 namespace nst {
