@@ -201,7 +201,9 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const int soff = (2 * u + team) * 16;                                                // the unit's chunk
     const uint32_t lds = stg + (u % C::NSLOT) * C::SLOTB;
     dma16(frame_rsrc(p.in, n), voff, lds, soff);
+#ifndef WS_NORLOAD  // experiment: no residual loads (wrong result; vmcnt count stays conservative)
     if constexpr (RES) dma16(frame_rsrc(p.res_r, n), voff, lds + C::NW * 1024, soff);
+#endif
   };
   // consume unit u of tile wk: IN + ReLU / residual join of the staged chunk into the halo.
   // live = false: a restaging pass past the last work item (LDS only, no residual-stream stores)
@@ -259,6 +261,9 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const int pix = tid >> 2, c = 4 * q + (tid & 3);  // 128 pixels x 4 chunks
     const int r = pix >> 4, x = pix & 15;
     const int oy = wk.ty0 + r, ox = wk.tx0 + x;
+#ifdef WS_NOREGION  // experiment: no residual-stream stores
+    return;
+#endif
     const u32x4_t v = *(const u32x4_t*)(smem + ((r + 1) * C::LW + x + 1) * C::EB + c * 16);
     const bool ok = oy < p.oh && ox < p.ow;
     __builtin_amdgcn_raw_buffer_store_b128(v, frame_rsrc(p.res_out, wk.n),
