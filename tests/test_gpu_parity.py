@@ -235,3 +235,14 @@ def test_weight_stationary_trunk_vs_generic(arch, h, w, monkeypatch):
     d = np.abs(a.astype(int) - b.astype(int))
     assert d.mean() < 0.5 and (d > 2).mean() < 0.01, (d.mean(), (d > 2).mean(), d.max())
     assert np.abs(ya - yb).max() <= 3e-2 * np.abs(yb).max(), np.abs(ya - yb).max() / np.abs(yb).max()
+
+
+def test_weight_stationary_trunk_batch_chunks():
+    """More frames than one weight-stationary launch holds IN tables for (16): the launcher splits
+    the batch into chunks with offset frame pointers; every frame must equal its own single-frame
+    run bit for bit (per-frame InstanceNorm, deterministic kernels)."""
+    net = _net("johnson", 7, "bf16")
+    frames = torch.from_numpy(synthetic.make_frames(20, 40, 56, seed=31)).cuda()
+    a = net.stylize_frames(frames, "imagenet_255")
+    for i in (0, 15, 16, 19):
+        assert torch.equal(net.stylize_frames(frames[i:i + 1].contiguous(), "imagenet_255")[0], a[i]), i
