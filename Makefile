@@ -6,13 +6,13 @@ CSRC := $(PKG)/csrc
 BUILD := build/obj
 CXXFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
-SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
+SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
 OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
 LIB := $(PKG)/libnst_hip.so
 
 all: $(LIB)
 
-$(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/nst_internal.h include/nst_hip.h
+$(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h $(CSRC)/nst_internal.h include/nst_hip.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
@@ -20,6 +20,7 @@ $(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/nst_internal.h inclu
 # pragma-unroll size cap for that translation unit only
 $(BUILD)/conv_bf16_wl.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=200000
 $(BUILD)/conv_wstat.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
+$(BUILD)/conv_wphase.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 
 $(BUILD)/%.cpp.o: $(CSRC)/%.cpp $(CSRC)/nst_internal.h include/nst_hip.h
 	@mkdir -p $(BUILD)

@@ -1,0 +1,463 @@
+// conv_wphase.hip — weight-stationary persistent x2 up-convs as four sub-pixel phases.
+//
+// Replaces UpsampleConvLayer (transformer_net.py:79-99: nearest x2 + ReflectionPad(1) + 3x3) and
+// ConvTranspose2d(3, s2, p1, op1) (transformer_net_nst.py:46-59) for the 128->64 and 64->32
+// layers, with the producer's InstanceNorm + ReLU (or the last residual join) in the fill and this
+// layer's InstanceNorm partial sums in the epilogue — the conv_wstat.hip machinery applied to the
+// phase decomposition of conv_impl.h's MODE_PHASE: output pixel (2y + a, 2x + b) is a 2x2 conv
+// over the SOURCE grid with phase-summed weights.
+//
+//   * workgroup = 8 waves: wave w computes phase (a, b) = ((w & 3) >> 1, w & 1) for output channels
+//     half w >> 2 (COUT / 2 channels); its 4 taps x CINP weights stay in registers for the launch.
+//   * persistent over (frame, TH x 16 source tiles); the halo (TH+2) x 18 x CINP in LDS (entry stride
+//     2 x odd chunks, conflict-free ds_read_b128); halo row y of x-tap tx is the B operand of rows
+//     y - ty for both y-taps, so each read feeds two MFMAs per 16-channel subtile.
+//   * K order part-major (part q = input channels 32q..32q+31 = one K step per tap); the next tile's
+//     halo streams in by LDS-DMA into a 4-slot staging ring (conv_wstat.hip's schedule, generalised
+//     to 2 or 4 parts) and is consumed (IN + ReLU / residual join) into each region once freed.
+//   * one InstanceNorm partial row per phase and tile (part_rows = 4).
+#include <algorithm>
+#include <cstring>
+
+#include "conv_ws_common.h"
+
+#ifndef WP_RING
+#define WP_RING 3  // operand reads in flight ahead of the MFMAs
+#endif
+
+namespace nst {
+
+template <int CINP, int COUT, int TH>
+struct WpCfg {
+  static constexpr int NW = 8, NT = 512;          // wave w: phase w & 3, channel half w >> 2
+  static constexpr int TW = 16;                   // source columns per tile = MFMA column block
+  static constexpr int NCH = CINP / 8;            // 16-B chunks per pixel
+  static constexpr int NPART = CINP / 32;         // parts: one 32-channel K step per tap
+  static constexpr int NUNIT = 2 * NPART;         // half parts: unit u = chunks 2u (team 0), 2u+1 (team 1)
+  static constexpr int NSUBW = COUT / 32;         // 16-channel subtiles per wave
+  static constexpr int NSTEP = 4 * NPART;         // weight steps per wave: part x tap (2x2)
+  static constexpr int LH = TH + 2, LW = TW + 2;  // source halo
+  static constexpr int NENT = LH * LW;
+  static constexpr int EB = (NCH + 2) * 16;       // 2 x odd chunks
+  static constexpr int QENT = NENT / 4;           // entries per wave and unit (four waves per chunk)
+  static constexpr int NFMAX = 16;                // frames per launch (IN tables resident in LDS)
+  static constexpr int NSLOT = 4;
+  static constexpr int SLOTB = 2 * NW * 1024;     // [y | r] x wave x lane x 16 B
+  static constexpr int MAPB = ((LH + LW) * 4 + 15) / 16 * 16;
+  static constexpr int MAP_OFF = NENT * EB;
+  static constexpr int NORM_OFF = MAP_OFF + 2 * MAPB;        // [y | r][frame][chunk]{scale[8], shift[8]}
+  static constexpr int NORM_TAB = NFMAX * CINP * 8;
+  static constexpr int BIAS_OFF = NORM_OFF + 2 * NORM_TAB;
+  static constexpr int DUMMY_OFF = BIAS_OFF + COUT * 4;
+  static constexpr int STG_OFF = DUMMY_OFF + 64 * 16;
+  static constexpr int LDS = STG_OFF + NSLOT * SLOTB;
+  static constexpr int WBYTES = NW * NSTEP * NSUBW * 64 * 16;
+  static_assert(CINP % 32 == 0 && COUT % 32 == 0 && (NPART == 2 || NPART == 4), "channel shapes");
+  static_assert(NENT % 4 == 0 && QENT <= 64, "four waves per unit chunk, one item per lane");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <int CINP, int COUT, int TH, int FILL, bool ZPAD>
+__global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
+  using C = WpCfg<CINP, COUT, TH>;
+  constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
+  constexpr int U = C::NUNIT, NS = C::NSUBW;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int team = wv >> 2, ph = wv & 3;
+  const int g = lane >> 4, px = lane & 15;
+
+  struct Work {
+    int n, tile, ty0, tx0;
+  };
+  const int ntile = p.tiles_x * p.tiles_y;
+  auto decode = [&](int wi) {
+    Work r;
+    r.n = wi / ntile;
+    r.tile = wi - r.n * ntile;
+    const int ty = r.tile / p.tiles_x;
+    r.ty0 = ty * TH;
+    r.tx0 = (r.tile - ty * p.tiles_x) * C::TW;
+    return r;
+  };
+  const int G = (int)gridDim.x, b = (int)blockIdx.x;
+  const int w0 = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+  if (w0 >= p.n_work) return;
+
+  // ---- this wave's phase weights (4 taps x CINP x COUT/2), resident for the launch ----
+  uint4 wr[C::NSTEP][NS];
+  {
+    const uint4* wsrc = (const uint4*)p.wpk + (size_t)wv * C::NSTEP * NS * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < C::NSTEP; ++s)
+#pragma unroll
+      for (int t = 0; t < NS; ++t) wr[s][t] = wsrc[(s * NS + t) * 64];
+  }
+  float* norm_y = (float*)(smem + C::NORM_OFF);
+  float* norm_r = norm_y + C::NFMAX * CINP * 2;
+  if (FILL != WF_RAW) {
+    const int nfr = p.n_work / ntile;
+    for (int t = tid; t < nfr * CINP; t += C::NT) {
+      const int f = t / CINP, c = t - f * CINP;
+      const int o = (f * C::NCH + (c >> 3)) * 16 + (c & 7);
+      const float2 v = p.in_norm[(size_t)f * p.cs + c];
+      norm_y[o] = v.x;
+      norm_y[o + 8] = v.y;
+      if (RN) {
+        const float2 r = p.res_rnorm[(size_t)f * p.cs + c];
+        norm_r[o] = r.x;
+        norm_r[o + 8] = r.y;
+      }
+    }
+  }
+  if (tid < COUT) ((float*)(smem + C::BIAS_OFF))[tid] = p.bias[tid];
+
+  // ---- halo staging (conv_wstat.hip) ----
+  const size_t frame_bytes = (size_t)p.hs * p.ws * p.cs * 2;
+  auto frame_rsrc = [&](const void* base, int n) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (size_t)n * frame_bytes), (short)0,
+                                             (int)frame_bytes, 0x00020000);
+  };
+  auto build_maps = [&](const Work& wk, int slot) {
+    int* rowmap = (int*)(smem + C::MAP_OFF + slot * C::MAPB);
+    int* colmap = rowmap + C::LH;
+    const int vy0 = wk.ty0 - p.pad, vx0 = wk.tx0 - p.pad;
+    const int pix = p.cs * 2;
+    for (int t = tid; t < C::LH + C::LW; t += C::NT) {
+      if (t < C::LH) {
+        const int sy = map_axis(vy0 + t, p.hs, p.axis_mode, p.pre);
+        rowmap[t] = sy < 0 ? -1 : sy * p.ws * pix;
+      } else {
+        const int sx = map_axis(vx0 + t - C::LH, p.ws, p.axis_mode, p.pre);
+        colmap[t - C::LH] = sx < 0 ? -1 : sx * pix;
+      }
+    }
+  };
+  const int ebase = (wv & 3) * C::QENT + lane;
+  struct Item {
+    int src;
+    bool valid;
+  };
+  auto items = [&](int slot) {
+    const int* rowmap = (const int*)(smem + C::MAP_OFF + slot * C::MAPB);
+    const int* colmap = rowmap + C::LH;
+    Item it;
+    it.valid = lane < C::QENT;
+    const int e = it.valid ? ebase : 0;
+    const int ly = e / C::LW, lx = e - ly * C::LW;
+    const int ro = rowmap[ly], co = colmap[lx];
+    it.src = (ro >= 0 && co >= 0) ? ro + co : -1;
+    return it;
+  };
+  const uint32_t stg = (uint32_t)(uintptr_t)(smem + C::STG_OFF) + wv * 1024;
+  auto request = [&](int n, int u, const Item& it) {
+    const uint32_t voff = (it.valid && it.src >= 0) ? (uint32_t)it.src : 0x80000000u;
+    const int soff = (2 * u + team) * 16;
+    const uint32_t lds = stg + (u % C::NSLOT) * C::SLOTB;
+    dma16(frame_rsrc(p.in, n), voff, lds, soff);
+    if constexpr (RES) dma16(frame_rsrc(p.res_r, n), voff, lds + C::NW * 1024, soff);
+  };
+  auto consume = [&](const Work& wk, int u, const Item& it) {
+    const int ch = 2 * u + team;
+    const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
+    const uint4 y = *(const uint4*)sp;
+    const uint4 rr = RES ? *(const uint4*)(sp + C::NW * 1024) : make_uint4(0u, 0u, 0u, 0u);
+    const float* ny = norm_y + (wk.n * C::NCH + ch) * 16;
+    const float* nr = norm_r + (wk.n * C::NCH + ch) * 16;
+    const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+    uint32_t o[4];
+    if constexpr (RES) {
+      // the last residual join IN_y(y) + r (ResidualBlock.forward): product then sum, one rounding
+      const uint32_t w2[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float r0 = bf16_lo(w2[j]), r1 = bf16_hi(w2[j]);
+        if (RN) {
+          r0 = fmaxf(r0 * nr[2 * j] + nr[8 + 2 * j], 0.f);
+          r1 = fmaxf(r1 * nr[2 * j + 1] + nr[8 + 2 * j + 1], 0.f);
+        }
+        const float a = bf16_lo(w[j]) * ny[2 * j] + ny[8 + 2 * j];
+        const float bb = bf16_hi(w[j]) * ny[2 * j + 1] + ny[8 + 2 * j + 1];
+        o[j] = pack_bf16(r0 + a, r1 + bb);
+      }
+    } else if constexpr (FILL == WF_RAW) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = w[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = __builtin_fmaf(bf16_lo(w[j]), ny[2 * j], ny[8 + 2 * j]);
+        const float bb = __builtin_fmaf(bf16_hi(w[j]), ny[2 * j + 1], ny[8 + 2 * j + 1]);
+        const i16x2_t r = __builtin_bit_cast(i16x2_t, pack_bf16(a, bb));
+        o[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
+      }
+    }
+    const bool pad = ZPAD && it.src < 0;
+    const u32x4_t v = {pad ? 0u : o[0], pad ? 0u : o[1], pad ? 0u : o[2], pad ? 0u : o[3]};
+    int eb = ebase * C::EB + ch * 16;
+    asm volatile("" : "+v"(eb));
+    *(u32x4_t*)(smem + (it.valid ? eb : C::DUMMY_OFF + lane * 16)) = v;
+  };
+  // vmcnt accounting as in conv_wstat.hip: 3 units' requests after unit g's, plus the epilogue's
+  // TH * NS output stores and NS partial stores when one lies in between
+  constexpr int DPU = RES ? 2 : 1;
+  constexpr int KIN = 3 * DPU;
+  constexpr int KEP = KIN + TH * NS + NS;
+
+  // ---- K loop ----
+  typedef f32x4_t Acc[TH][NS];
+  const int phy = p.ph_off[ph >> 1], phx = p.ph_off[ph & 1];
+  const int lbase = (phy * C::LW + phx + px) * C::EB + g * 16;
+  constexpr int NRD = TH + 1;   // reads per x-tap
+  constexpr int PRD = 2 * NRD;  // reads per part
+  auto bread = [&](int i) -> uint4 {  // read i of the tile: (q, tx, y)
+    const int q = i / PRD, rem = i - q * PRD;
+    const int tx = rem / NRD, y = rem % NRD;
+    return *(const uint4*)(smem + lbase + (y * C::LW + tx) * C::EB + 64 * q);
+  };
+  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
+    const u32x4_t av = __builtin_bit_cast(u32x4_t, a), bv = __builtin_bit_cast(u32x4_t, bop);
+    if (first)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(av), "v"(bv));
+    else
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
+  };
+  auto kloop = [&](Acc& acc, auto&& hook, auto&& bound) {
+    constexpr int NI = C::NPART * PRD, D = WP_RING;
+    uint4 ring[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) ring[i] = bread(i);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = i / PRD, rem = i - q * PRD;
+      const int tx = rem / NRD, y = rem % NRD;
+      const uint4 bcur = ring[i % D];
+      // two parts: part 1's region is consumed during part 0, so its reads wait for the part barrier
+      const bool defer = C::NPART == 2 && q == 0 && i + D >= PRD;
+      if (i + D < NI && !defer) ring[i % D] = bread(i + D);
+#pragma unroll
+      for (int ty = 0; ty < 2; ++ty) {
+        const int r = y - ty;
+        if (r < 0 || r >= TH) continue;
+#pragma unroll
+        for (int t = 0; t < NS; ++t) mfma(acc[r][t], wr[q * 4 + 2 * ty + tx][t], bcur, q == 0 && tx == 0 && ty == 0);
+      }
+      hook(q, rem);
+      if (rem == PRD - 1) {
+        lds_barrier();
+        bound(q);
+        if (C::NPART == 2 && q == 0) {
+#pragma unroll
+          for (int j = 0; j < D; ++j) ring[(i + 1 + j) % D] = bread(i + 1 + j);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- epilogue: bias, bf16 NHWC stores of this phase's pixels, one partial row per phase ----
+  auto epilogue = [&](const Work& wk, Acc& acc) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA results -> VALU reads
+    const size_t obytes = (size_t)p.oh * p.ow * p.cout_stride * 2;
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)p.out + (size_t)wk.n * obytes), (short)0, (int)obytes, 0x00020000);
+    const int ox = 2 * (wk.tx0 + px) + (ph & 1);
+    const int oy0 = 2 * wk.ty0 + (ph >> 1);
+    const uint32_t row2 = (uint32_t)p.ow * p.cout_stride * 2 * 2;  // two output rows
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.partial + (((size_t)wk.n * ntile + wk.tile) * 4 + ph) * p.cout_stride * 2), (short)0,
+        p.cout_stride * 8, 0x00020000);
+    const bool full = 2 * (wk.ty0 + TH) <= p.oh && 2 * (wk.tx0 + C::TW) <= p.ow;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const int c0 = team * (COUT / 2) + t * 16 + 4 * g;
+      const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
+      const uint32_t off0 = (uint32_t)(((oy0 * p.ow + ox) * p.cout_stride + c0) * 2);
+      f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
+      auto rows = [&](auto all_valid) {
+#pragma unroll
+        for (int r = 0; r < TH; ++r) {
+          const bool valid = decltype(all_valid)::value || (oy0 + 2 * r < p.oh && ox < p.ow);
+          const f32x4_t v = acc[r][t] + bias;
+          const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+          __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, 0);
+          const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+          s1 += x;
+          s2 = __builtin_elementwise_fma(x, x, s2);
+        }
+      };
+      if (full)
+        rows(std::true_type{});
+      else
+        rows(std::false_type{});
+      const float vv[8] = {s1[0], s2[0], s1[1], s2[1], s1[2], s2[2], s1[3], s2[3]};
+      float a4[4], a2[2], a1[1];
+      rs_step<4, 0x140>(vv, a4, px >= 8);
+      rs_step<2, 0x141>(a4, a2, (px & 4) != 0);
+      rs_step<1, 0x1b>(a2, a1, (px & 2) != 0);
+      const float sv = a1[0] + dpp_f<0xb1>(a1[0]);
+      const int idx = (px >= 8 ? 4 : 0) + ((px & 4) ? 2 : 0) + ((px & 2) ? 1 : 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv), prs,
+                                            (px & 1) ? 0x80000000u : (uint32_t)(((c0 + (idx >> 1)) * 2 + (idx & 1)) * 4), 0, 0);
+    }
+  };
+
+  // ---- persistent walk (conv_wstat.hip's, with NPART parts) ----
+  Work cur = decode(w0);
+  int wn = w0 + G;
+  const int last = p.n_work - 1;
+  build_maps(cur, 0);
+  build_maps(decode(min(wn, last)), 1);
+  __syncthreads();
+  Item xx = items(0);
+  Item xd = xx;
+#pragma unroll
+  for (int u = 0; u < C::NSLOT; ++u) request(cur.n, u, xd);
+  {
+    const Work n1 = decode(min(wn, last));
+#pragma unroll
+    for (int u = 0; u < U - 2; ++u) {
+      vm_wait<0>();
+      consume(cur, u, xx);
+      if (u + 4 < U) {
+        request(cur.n, u + 4, xd);
+      } else {
+        if (u + 4 == U) xd = items(1);
+        request(n1.n, u + 4 - U, xd);
+      }
+    }
+  }
+  if constexpr (C::NPART == 2) {
+    // two parts: the tile after next resolves its sources in part 1 of the first iteration
+    __syncthreads();  // every wave is past items(cur) (slot 0)
+    build_maps(decode(min(wn + G, last)), 0);
+  }
+  vm_wait<0>();
+  __syncthreads();
+  constexpr int POS_A = 0, POS_B = PRD / 2, DT = PRD / 4;
+  Acc acc;
+  for (int it = 0;; ++it) {
+    const bool more = wn < p.n_work;
+    const Work nxt = more ? decode(wn) : cur;
+    const Work nxt2 = decode(min(wn + G, last));
+    const int cs = it & 1, ns = cs ^ 1;
+    kloop(
+        acc,
+        [&](int q, int rem) {
+          const int pa = POS_A + (team ? DT : 0), pb = POS_B + (team ? DT : 0);
+          if (rem != pa && rem != pb) return;
+          const int half = rem == pa ? 0 : 1;
+          if (q == 0) {  // the current tile's last region: units U-2, U-1; request 2, 3 of nxt
+            vm_wait<KEP>();
+            consume(cur, U - 2 + half, xx);
+            request(nxt.n, 2 + half, xd);
+          } else {
+            const int u = 2 * (q - 1) + half;
+            if (u == 0) xx = items(ns);
+            if (2 * q + half < 4) vm_wait<KEP>(); else vm_wait<KIN>();
+            consume(nxt, u, xx);
+            if (u + 4 < U) {
+              request(nxt.n, u + 4, xd);
+            } else {
+              if (u == U - 4) xd = items(cs);
+              request(nxt2.n, u + 4 - U, xd);
+            }
+          }
+        },
+        [&](int q) {
+          if constexpr (C::NPART == 4) {
+            if (q == 0) build_maps(nxt2, cs);  // published by the barriers ending parts 1 and 2
+          } else {
+            // two parts: the tile after nxt2 into nxt's slot (nxt's sources were resolved in
+            // part 1); published by the next iteration's first barrier
+            if (q == 1) build_maps(decode(min(wn + 2 * G, last)), ns);
+          }
+        });
+    epilogue(cur, acc);
+    if (!more) break;
+    cur = nxt;
+    wn += G;
+  }
+  vm_wait<0>();  // no LDS-DMA may land after the workgroup has released its LDS
+}
+
+template <int CINP, int COUT, int TH, bool RES>
+struct WphaseInst {
+  using C = WpCfg<CINP, COUT, TH>;
+  static int cus() {
+    static const int v = [] {
+      int dev = 0, c = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        c = 256;
+      return c;
+    }();
+    return v;
+  }
+  template <int FILL, bool ZPAD>
+  static void go(const ConvParams& p, int nb, hipStream_t st) {
+    hipLaunchKernelGGL((wphase_kernel<CINP, COUT, TH, FILL, ZPAD>), dim3(nb), dim3(C::NT), 0, st, p);
+  }
+  // grid.x = source tiles per frame, grid.y = frames; chunks of <= NFMAX frames per launch
+  static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
+    const int ntile = (int)grid.x, n = (int)grid.y;
+    const size_t fin = (size_t)p0.hs * p0.ws * p0.cs * 2, fout = (size_t)p0.oh * p0.ow * p0.cout_stride * 2;
+    for (int f0 = 0; f0 < n; f0 += C::NFMAX) {
+      const int nf = std::min(C::NFMAX, n - f0);
+      ConvParams p = p0;
+      p.in = (const char*)p0.in + f0 * fin;
+      p.out = (char*)p0.out + f0 * fout;
+      if (p0.res_r) p.res_r = (const char*)p0.res_r + f0 * fin;
+      if (p0.in_norm) p.in_norm = p0.in_norm + (size_t)f0 * p0.cs;
+      if (p0.res_rnorm) p.res_rnorm = p0.res_rnorm + (size_t)f0 * p0.cs;
+      p.partial = p0.partial + (size_t)f0 * ntile * 4 * p0.cout_stride * 2;
+      p.n_work = nf * ntile;
+      const int nb = std::min(p.n_work, cus());
+      const bool zp = p.axis_mode == AX_ZERO;  // ConvTranspose: zeros past the edge
+      if constexpr (RES) {
+        if (p.res_rnorm != nullptr)
+          zp ? go<WF_RESRN, true>(p, nb, st) : go<WF_RESRN, false>(p, nb, st);
+        else
+          zp ? go<WF_RES, true>(p, nb, st) : go<WF_RES, false>(p, nb, st);
+      } else {
+        if (p.in_norm != nullptr)
+          zp ? go<WF_NORM, true>(p, nb, st) : go<WF_NORM, false>(p, nb, st);
+        else
+          zp ? go<WF_RAW, true>(p, nb, st) : go<WF_RAW, false>(p, nb, st);
+      }
+    }
+  }
+  static ConvKernelInfo info() {
+    ConvKernelInfo k;
+    std::memset(&k, 0, sizeof(k));
+    k.dtype = NST_DT_BF16;
+    k.mode = MODE_WPHASE;
+    k.ks = 3; k.stride = 1; k.cinp = CINP; k.bn = COUT; k.th = TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
+    k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
+    k.cpc = 8; k.nch = C::NCH; k.lds_bytes = C::LDS;
+    k.wbytes = C::WBYTES;
+    k.persistent = 1;
+    k.part_rows = 4;
+    k.res = RES ? 1 : 0;
+    k.launch = &launch;
+    return k;
+  }
+};
+
+#ifndef NST_WP1_TH
+#define NST_WP1_TH 6  // 128 -> 64: 8 rows spill (128 weight + 64 accumulator VGPRs)
+#endif
+#define E(...) WphaseInst<__VA_ARGS__>::info()
+const ConvKernelInfo* conv_table_wphase(int* count) {
+  static const ConvKernelInfo table[] = {
+      //  CINP COUT TH RES
+      E(128, 64, NST_WP1_TH, false),  // deconv1 / up1
+      E(128, 64, NST_WP1_TH, true),   // deconv1 joining the last residual block (fused join)
+      E(64, 32, 8, false),   // deconv2 / up2
+  };
+  *count = (int)(sizeof(table) / sizeof(table[0]));
+  return table;
+}
+#undef E
+
+}  // namespace nst

@@ -1,0 +1,39 @@
+// conv_ws_common.h — pieces shared by the weight-stationary persistent convs (conv_wstat.hip,
+// conv_wphase.hip): unit-fill kinds and the wait / barrier statements their LDS-DMA staging needs.
+#pragma once
+#include "conv_impl.h"
+
+namespace nst {
+
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// what the fill applies to a staged input chunk
+enum WsFill { WF_NORM = 0, WF_RAW = 1, WF_RES = 2, WF_RESRN = 3 };  // IN+ReLU / identity / join / join of ReLU(IN(r))
+
+// s_waitcnt vmcnt(N) / the part barrier, as statements hipcc cannot move memory operations across
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+#ifndef WS_NOWAIT  // experiment (racy): no waits for the unit requests
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#endif
+}
+__device__ __forceinline__ void lds_barrier() {
+#ifndef WS_NOBAR  // experiment (racy): no part barriers
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+}
+
+// One 16-byte LDS-DMA request: 64 lanes x 16 B from per-lane buffer offsets into LDS at
+// lds + lane * 16 (buffer_load ... lds: no VGPR destination).  M0 is saved and restored inside the
+// statement (hipcc owns it); the s_nop covers the M0 write -> LDS-DMA hazard.
+__device__ __forceinline__ void dma16(const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, uint32_t lds, int soff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(lds), "s"(rs), "s"(soff)
+      : "memory");
+}
+
+}  // namespace nst

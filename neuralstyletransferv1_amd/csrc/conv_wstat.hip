@@ -28,16 +28,13 @@
 #include <algorithm>
 #include <cstring>
 
-#include "conv_impl.h"
+#include "conv_ws_common.h"
 
 #ifndef WS_RING
 #define WS_RING 3  // operand reads in flight ahead of the MFMAs
 #endif
 
 namespace nst {
-
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 template <int TH>
 struct WsCfg {
@@ -65,22 +62,6 @@ struct WsCfg {
   static_assert(NENT % 4 == 0 && QENT <= 64, "four waves per unit chunk, one item per lane");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
-
-// what the fill applies to a staged input chunk
-enum WsFill { WF_NORM = 0, WF_RAW = 1, WF_RES = 2, WF_RESRN = 3 };  // IN+ReLU / identity / join / join of ReLU(IN(r))
-
-// s_waitcnt vmcnt(N) / the part barrier, as statements hipcc cannot move memory operations across
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-#ifndef WS_NOWAIT  // experiment (racy): no waits for the unit requests
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-#endif
-}
-__device__ __forceinline__ void lds_barrier() {
-#ifndef WS_NOBAR  // experiment (racy): no part barriers
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
-}
 
 template <int TH, int FILL, bool ZPAD>
 __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
@@ -188,14 +169,6 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   // epilogue's TH + 1 stores when one lies in between (units 0, 1, 6, 7).  Any extra instruction
   // hipcc adds only makes such a wait stricter.
   const uint32_t stg = (uint32_t)(uintptr_t)(smem + C::STG_OFF) + wv * 1024;
-  auto dma16 = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, uint32_t lds, int soff) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(voff), "s"(lds), "s"(rs), "s"(soff)
-        : "memory");
-  };
   auto request = [&](int n, int u, const Item& it) {
     const uint32_t voff = (it.valid && it.src >= 0) ? (uint32_t)it.src : 0x80000000u;  // pad: reads 0
     const int soff = (2 * u + team) * 16;                                                // the unit's chunk

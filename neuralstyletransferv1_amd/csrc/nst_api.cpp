@@ -28,15 +28,16 @@ const ConvKernelInfo* conv_table_bf16_wl(int* count);
 const ConvKernelInfo* conv_table_f32(int* count);
 const ConvKernelInfo* conv_table_out9(int* count);
 const ConvKernelInfo* conv_table_wstat(int* count);
+const ConvKernelInfo* conv_table_wphase(int* count);
 
 // first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind, int res) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
-  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_out9, conv_table_bf16};
+  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_out9, conv_table_bf16};
   const TableFn tables_f32[] = {conv_table_f32};
   const TableFn* tables = dtype == NST_DT_BF16 ? tables_bf16 : tables_f32;
-  const int ntables = dtype == NST_DT_BF16 ? 4 : 1;
+  const int ntables = dtype == NST_DT_BF16 ? 5 : 1;
   static const bool no_wl = std::getenv("NST_NO_PERSISTENT") != nullptr;  // experiment switch
   for (int ti = (dtype == NST_DT_BF16 && no_wl) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
@@ -212,14 +213,44 @@ uint16_t f32_to_bf16_rne(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// Sub-pixel phase weights of an x2 up-conv: output pixel (2y + a, 2x + b) is a 2x2 conv over the
+// source grid, window tap (ty, tx); its weight is the sum of the 3x3 taps landing on that source
+// pixel: nearest-x2 (a=0: ty0<-{k0}, ty1<-{k1,k2}; a=1: ty0<-{k0,k1}, ty1<-{k2}), or the one
+// ConvTranspose2d(s2,p1) tap (a=0: ty0<-k1; a=1: ty0<-k2, ty1<-k0), per axis.
+// phase_taps: kernel indices (along one axis) that fall on window position t of phase a
+int phase_taps(bool convT, int a, int t, int* ks_out) {
+  if (convT) {  // unflipped ConvTranspose indices
+    if (a == 0) { if (t == 0) { ks_out[0] = 1; return 1; } return 0; }
+    ks_out[0] = t == 0 ? 2 : 0;
+    return 1;
+  }
+  if (a == 0) {
+    if (t == 0) { ks_out[0] = 0; return 1; }
+    ks_out[0] = 1; ks_out[1] = 2; return 2;
+  }
+  if (t == 0) { ks_out[0] = 0; ks_out[1] = 1; return 2; }
+  ks_out[0] = 2;
+  return 1;
+}
+
+// weight of output channel co, input channel ci at phase ph = 2a + b, window tap = 2 ty + tx
+double phase_weight(const LayerDef& d, const float* W, int co, int ci, int ph, int tap) {
+  int ky[2], kx[2];
+  const int ny = phase_taps(d.convT, ph >> 1, tap >> 1, ky), nx = phase_taps(d.convT, ph & 1, tap & 1, kx);
+  double sum = 0.0;
+  for (int yy = 0; yy < ny; ++yy)
+    for (int xx = 0; xx < nx; ++xx)
+      sum += d.convT ? (double)W[(((size_t)ci * d.cout + co) * d.ks + ky[yy]) * d.ks + kx[xx]]
+                     : (double)W[(((size_t)co * d.cin + ci) * d.ks + ky[yy]) * d.ks + kx[xx]];
+  return sum;
+}
+
 // Pack conv weights into MFMA A-fragment order: [cblk][step (nstep_pack; >= nstep zero)][n-subtile][lane][cpc]
 // lane l = (g = l>>4, q = l&15): output channel of row q in subtile t (wave wn, local t):
 //   cb*bn + wn*nsub*16 + 4*nsub*(q>>2) + 4*t + (q&3);  K chunk 4*step+g -> (tap, channel chunk).
 //
 // MODE_PHASE: n-subtile tg = phase*nsub + t (phase (a,b) = (tg/nsub)>>1, &1), tap = (ty,tx) of the
-//   phase's 2x2 window on the source grid; the weight is the sum of the 3x3 taps that land on that
-//   source pixel: nearest-x2 (a=0: ty0<-{k0}, ty1<-{k1,k2}; a=1: ty0<-{k0,k1}, ty1<-{k2}), or the one
-//   ConvTranspose2d(s2,p1) tap (a=0: ty0<-k1; a=1: ty0<-k2, ty1<-k0), per axis.
+//   phase's 2x2 window on the source grid (phase_weight).
 // MODE_XSHIFT: row q = 3*s + c (q < 15) is output channel perm[c] at x-shift s; tap (dy, u) over
 //   13 columns carries W[.][.][dy][u - s] when 0 <= u - s < 9.
 std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W, int coutp,
@@ -231,21 +262,6 @@ std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, cons
     if (d.convT)  // ConvTranspose2d weight [cin][cout][kh][kw], flipped for the zero-inserted conv
       return W[(((size_t)ci * d.cout + co) * d.ks + (d.ks - 1 - dy)) * d.ks + (d.ks - 1 - dx)];
     return W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
-  };
-  // phase taps: kernel indices (along one axis) that fall on window position t of phase a
-  auto phase_taps = [&](int a, int t, int* ks_out) -> int {
-    if (d.convT) {  // unflipped ConvTranspose indices
-      if (a == 0) { if (t == 0) { ks_out[0] = 1; return 1; } return 0; }
-      ks_out[0] = t == 0 ? 2 : 0;
-      return 1;
-    }
-    if (a == 0) {
-      if (t == 0) { ks_out[0] = 0; return 1; }
-      ks_out[0] = 1; ks_out[1] = 2; return 2;
-    }
-    if (t == 0) { ks_out[0] = 0; ks_out[1] = 1; return 2; }
-    ks_out[0] = 2;
-    return 1;
   };
   for (int cb = 0; cb < ncblk; ++cb)
     for (int s = 0; s < k.nstep; ++s)
@@ -263,17 +279,9 @@ std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, cons
             const int ph = tg / k.nsub, t = tg % k.nsub;
             const int co = cb * k.bn + 4 * k.nsub * (q >> 2) + 4 * t + (q & 3);
             if (co >= d.cout) continue;
-            int ky[2], kx[2];
-            const int ny = phase_taps(ph >> 1, tap >> 1, ky), nx = phase_taps(ph & 1, tap & 1, kx);
             for (int j = 0; j < k.cpc; ++j) {
               const int ci = c * k.cpc + j;
-              if (ci >= d.cin) continue;
-              double sum = 0.0;
-              for (int yy = 0; yy < ny; ++yy)
-                for (int xx = 0; xx < nx; ++xx)
-                  sum += d.convT ? (double)W[(((size_t)ci * d.cout + co) * d.ks + ky[yy]) * d.ks + kx[xx]]
-                                 : (double)W[(((size_t)co * d.cin + ci) * d.ks + ky[yy]) * d.ks + kx[xx]];
-              dst[j] = (float)sum;
+              if (ci < d.cin) dst[j] = (float)phase_weight(d, W, co, ci, ph, tap);
             }
           } else if (k.mode == MODE_XSHIFT) {
             if (q >= 15) continue;
@@ -341,6 +349,28 @@ std::vector<float> pack_wstat_weights(const LayerDef& d, const float* W) {
   return out;
 }
 
+// MODE_WPHASE weight registers (conv_wphase.hip): [wave w][step s][subtile t][lane][8 bf16].  Wave w
+// computes phase w & 3 for output channels half w >> 2; step s = 4 q + tap (part q = input channels
+// 32q..32q+31, tap = 2 ty + tx); lane l holds MFMA row l & 15 = output channel
+// (w >> 2) * coutp / 2 + 16 t + (l & 15), K elements = input channels 32 q + 8 (l >> 4) + i.
+std::vector<float> pack_wphase_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
+  const int nstep = 4 * (k.cinp / 32), ns = k.bn / 32;
+  std::vector<float> out((size_t)8 * nstep * ns * 64 * 8, 0.f);
+  for (int w = 0; w < 8; ++w)
+    for (int s = 0; s < nstep; ++s)
+      for (int t = 0; t < ns; ++t)
+        for (int l = 0; l < 64; ++l) {
+          const int q = s / 4, tap = s % 4;
+          const int co = (w >> 2) * (k.bn / 2) + 16 * t + (l & 15);
+          for (int i = 0; i < 8; ++i) {
+            const int ci = 32 * q + 8 * (l >> 4) + i;
+            if (co < d.cout && ci < d.cin)
+              out[((((size_t)w * nstep + s) * ns + t) * 64 + l) * 8 + i] = (float)phase_weight(d, W, co, ci, w & 3, tap);
+          }
+        }
+  return out;
+}
+
 // bias rows of an x-shift layer: row q = 3*s + c -> bias of output channel (perm) c
 std::vector<float> xshift_bias(const float* b, bool reverse_channels) {
   std::vector<float> r(16, 0.f);
@@ -403,7 +433,7 @@ size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 
 // workgroup tiles of a conv launch: phase mode tiles the SOURCE grid (each source pixel -> 4 outputs)
 void tile_grid(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx, int* ty) {
-  if (k.mode == MODE_PHASE) {
+  if (k.mode == MODE_PHASE || k.mode == MODE_WPHASE) {
     *tx = (sw + k.tw - 1) / k.tw;
     *ty = (sh + k.th - 1) / k.th;
   } else {
@@ -581,6 +611,12 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     // conv; the plain mapping is the fallback for shapes without a compiled variant
     const bool up = d.axis_mode == AX_REFLECT_UP2 || d.axis_mode == AX_ZINSERT;
     std::vector<int> modes;
+    // x2 up-convs: weight-stationary phase kernel (conv_wphase.hip) where compiled; its fused join
+    // has no ReLU after the sum (ReCoNet's has), so ReCoNet's residual consumers skip it
+    const char* wp_only = std::getenv("NST_WPHASE_CIN");  // env: debug switch, one input width only
+    if (up && !(res_layer[li] && arch == NST_ARCH_RECONET) && !std::getenv("NST_NO_WPHASE") &&  // env: experiment switch
+        (!wp_only || std::atoi(wp_only) == Ly.cinp))
+      modes.push_back(MODE_WPHASE);
     if (up) modes.push_back(MODE_PHASE);
     if (final_layer && d.cout == 3) {
       if (!std::getenv("NST_NO_KYROT")) modes.push_back(MODE_KYROT);  // experiment switch
@@ -636,6 +672,8 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
       if ((rc = upload_packed(pack_kyrot_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if (Ly.mode == MODE_WSTAT) {
       if ((rc = upload_packed(pack_wstat_weights(d, W), &Ly.wpk)) != NST_OK) break;
+    } else if (Ly.mode == MODE_WPHASE) {
+      if ((rc = upload_packed(pack_wphase_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) {
       break;
     }
@@ -758,7 +796,7 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     p.cs = image_in ? 3 : Ly.cinp;
     p.axis_mode = Ly.d.axis_mode;
     p.pad = Ly.d.axis_mode == AX_ZINSERT ? 1 : Ly.d.pad;
-    if (Ly.mode == MODE_PHASE) {
+    if (Ly.mode == MODE_PHASE || Ly.mode == MODE_WPHASE) {
       // source-grid halo of one pixel; nearest-x2 reflect(1) == clamp on the source grid,
       // ConvTranspose reads zeros past the edge
       p.axis_mode = Ly.d.axis_mode == AX_ZINSERT ? AX_ZERO : AX_CLAMP;
@@ -817,6 +855,10 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
     p.n_cblk = Ly.coutp / k->bn;
     if (Ly.mode == MODE_WSTAT && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out == nullptr || p.res_relu)) {
       set_error("conv " + Ly.d.conv + ": weight-stationary kernel joins IN(y) + r into a residual-stream buffer");
+      return NST_E_SHAPE;
+    }
+    if (Ly.mode == MODE_WPHASE && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out != nullptr || p.res_relu)) {
+      set_error("conv " + Ly.d.conv + ": weight-stationary phase kernel joins IN(y) + r without writing the stream");
       return NST_E_SHAPE;
     }
     if (k->persistent && p.n_cblk != 1) { set_error("conv " + Ly.d.conv + ": persistent kernel needs one channel block"); return NST_E_SHAPE; }

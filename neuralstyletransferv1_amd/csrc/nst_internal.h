@@ -37,7 +37,7 @@ enum OutKind { OUT_ACT = 0, OUT_U8_NHWC = 1, OUT_F32_NCHW = 2 };
 enum AxisMode { AX_REFLECT = 0, AX_REFLECT_UP2 = 1, AX_ZERO = 2, AX_ZERO_PREREFLECT = 3, AX_ZINSERT = 4, AX_CLAMP = 5 };
 
 // conv_kernel mappings (see conv_impl.h)
-enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2, MODE_KYROT = 3, MODE_WSTAT = 4 };  // KYROT: conv_out9.hip, WSTAT: conv_wstat.hip
+enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2, MODE_KYROT = 3, MODE_WSTAT = 4, MODE_WPHASE = 5 };  // KYROT: conv_out9.hip, WSTAT: conv_wstat.hip, WPHASE: conv_wphase.hip
 
 struct ConvParams {
   // input
@@ -76,7 +76,7 @@ struct ConvParams {
   int dec_perm[3];
   int dec_tanh;  // apply tanh to the raw output first (ReCoNet ConvTanhLayer, model.py:77-80)
   int seg_len;    // MODE_KYROT: output rows per work item (set by the launcher)
-  int ph_off[2];  // MODE_PHASE: LDS row/col offset of sub-pixel phase 0/1 ({0,1} nearest-up, {1,1} ConvTranspose)
+  int ph_off[2];  // MODE_PHASE / MODE_WPHASE: LDS row/col offset of sub-pixel phase 0/1 ({0,1} nearest-up, {1,1} ConvTranspose)
 };
 
 // Static description of one compiled conv kernel instantiation.

@@ -246,3 +246,28 @@ def test_weight_stationary_trunk_batch_chunks():
     a = net.stylize_frames(frames, "imagenet_255")
     for i in (0, 15, 16, 19):
         assert torch.equal(net.stylize_frames(frames[i:i + 1].contiguous(), "imagenet_255")[0], a[i]), i
+
+
+@pytest.mark.parametrize("arch,h,w", [
+    ("johnson", 70, 90),      # nearest-x2 up-convs over 18x23 / 35x45 sources: ragged tiles, fused join
+    ("nst", 72, 100),         # ConvTranspose2d phases (zeros past the edge), pre-reflect 40
+    ("reconet", 61, 90),      # 96 -> 48 up-conv padded to 128 -> 64 (the 192-channel one stays generic)
+    ("johnson", 1080, 1920),  # the bench shape (270x480 and 540x960 sources), one frame
+])
+def test_weight_stationary_upconv_vs_generic(arch, h, w, monkeypatch):
+    """The weight-stationary x2 up-convs (conv_wphase.hip: per-wave phase weights in registers,
+    16x16x32 MFMAs, K part-major) against the generic phase-mode kernel on the same bf16 model:
+    same phase-summed bf16 weights and operands, fp32 accumulation in another order, so the bar
+    is the bf16 mode's own (SSIM vs each other well above the 0.98 oracle bar, few-LSB frames)."""
+    frames = torch.from_numpy(synthetic.make_frames(2 if h < 512 else 1, h, w, seed=22)).cuda()
+    x = torch.randn(2, 3, 72, 100, generator=torch.Generator().manual_seed(4)).cuda()
+    fast = _net(arch, 8, "bf16")
+    a, ya = fast.stylize_frames(frames, "imagenet_255").cpu().numpy(), fast(x).cpu().numpy()
+    monkeypatch.setenv("NST_NO_WPHASE", "1")
+    ref = _net(arch, 8, "bf16")
+    b, yb = ref.stylize_frames(frames, "imagenet_255").cpu().numpy(), ref(x).cpu().numpy()
+    for i in range(a.shape[0]):
+        assert O.ssim(a[i], b[i]) >= 0.995
+    d = np.abs(a.astype(int) - b.astype(int))
+    assert d.mean() < 0.5 and (d > 2).mean() < 0.01, (d.mean(), (d > 2).mean(), d.max())
+    assert np.abs(ya - yb).max() <= 3e-2 * np.abs(yb).max(), np.abs(ya - yb).max() / np.abs(yb).max()
