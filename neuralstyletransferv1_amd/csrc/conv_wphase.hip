@@ -27,7 +27,7 @@
 
 namespace nst {
 
-template <int CINP, int COUT, int TH>
+template <int CINP, int COUT, int TH, int NF>
 struct WpCfg {
   static constexpr int NW = 8, NT = 512;          // wave w: phase w & 3, channel half w >> 2
   static constexpr int TW = 16;                   // source columns per tile = MFMA column block
@@ -40,7 +40,7 @@ struct WpCfg {
   static constexpr int NENT = LH * LW;
   static constexpr int EB = (NCH + 2) * 16;       // 2 x odd chunks
   static constexpr int QENT = NENT / 4;           // entries per wave and unit (four waves per chunk)
-  static constexpr int NFMAX = 16;                // frames per launch (IN tables resident in LDS)
+  static constexpr int NFMAX = NF;                // frames per launch (IN tables resident in LDS)
   static constexpr int NSLOT = 4;
   static constexpr int SLOTB = 2 * NW * 1024;     // [y | r] x wave x lane x 16 B
   static constexpr int MAPB = ((LH + LW) * 4 + 15) / 16 * 16;
@@ -50,16 +50,24 @@ struct WpCfg {
   static constexpr int BIAS_OFF = NORM_OFF + 2 * NORM_TAB;
   static constexpr int DUMMY_OFF = BIAS_OFF + COUT * 4;
   static constexpr int STG_OFF = DUMMY_OFF + 64 * 16;
-  static constexpr int LDS = STG_OFF + NSLOT * SLOTB;
+  // output tile staged in LDS for contiguous 16-B stores (when it fits): [row 2TH][pixel 32][COUT
+  // channels + 16 B pad]; NST = 16-B stores per thread
+  static constexpr int OUT_OFF = STG_OFF + NSLOT * SLOTB;
+  static constexpr int PIXB = COUT * 2, PIXP = PIXB + 16, ROWB = 2 * TW * PIXB;
+  static constexpr int OUTB = 2 * TH * 2 * TW * PIXP;
+  static constexpr bool OST = OUT_OFF + OUTB <= 160 * 1024;
+  static constexpr int NST = 2 * TH * ROWB / (NT * 16);
+  static constexpr int LDS = OST ? OUT_OFF + OUTB : OUT_OFF;
+  static_assert(!OST || NST * NT * 16 == 2 * TH * ROWB, "whole 16-B stores per thread");
   static constexpr int WBYTES = NW * NSTEP * NSUBW * 64 * 16;
   static_assert(CINP % 32 == 0 && COUT % 32 == 0 && (NPART == 2 || NPART == 4), "channel shapes");
   static_assert(NENT % 4 == 0 && QENT <= 64, "four waves per unit chunk, one item per lane");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int CINP, int COUT, int TH, int FILL, bool ZPAD>
+template <int CINP, int COUT, int TH, int NF, int FILL, bool ZPAD>
 __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
-  using C = WpCfg<CINP, COUT, TH>;
+  using C = WpCfg<CINP, COUT, TH, NF>;
   constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
   constexpr int U = C::NUNIT, NS = C::NSUBW;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
@@ -159,6 +167,9 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     if constexpr (RES) dma16(frame_rsrc(p.res_r, n), voff, lds + C::NW * 1024, soff);
   };
   auto consume = [&](const Work& wk, int u, const Item& it) {
+#ifdef WS_NOCONSUME  // experiment: no unit transform / halo write
+    return;
+#endif
     const int ch = 2 * u + team;
     const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
     const uint4 y = *(const uint4*)sp;
@@ -203,7 +214,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   // TH * NS output stores and NS partial stores when one lies in between
   constexpr int DPU = RES ? 2 : 1;
   constexpr int KIN = 3 * DPU;
-  constexpr int KEP = KIN + TH * NS + NS;
+  constexpr int KEP = KIN + (C::OST ? C::NST : TH * NS) + NS;
 
   // ---- K loop ----
   typedef f32x4_t Acc[TH][NS];
@@ -258,6 +269,10 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
 
   // ---- epilogue: bias, bf16 NHWC stores of this phase's pixels, one partial row per phase ----
   auto epilogue = [&](const Work& wk, Acc& acc) {
+#ifdef WP_NOEPI  // experiment (racy vmcnt accounting): no stores
+    asm volatile("" ::"v"(acc[0][0]));
+    return;
+#endif
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA results -> VALU reads
     const size_t obytes = (size_t)p.oh * p.ow * p.cout_stride * 2;
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
@@ -281,7 +296,15 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
           const bool valid = decltype(all_valid)::value || (oy0 + 2 * r < p.oh && ox < p.ow);
           const f32x4_t v = acc[r][t] + bias;
           const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
-          __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, 0);
+          if constexpr (C::OST) {  // into the LDS output tile: row 2r + a, pixel 2 px + b
+            *(u32x2_t*)(smem + C::OUT_OFF + ((2 * r + (ph >> 1)) * 2 * C::TW + 2 * px + (ph & 1)) * C::PIXP + c0 * 2) = pk;
+          } else {
+#ifndef WP_NOSTORE  // experiment (racy vmcnt accounting): no output stores
+            __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, 0);
+#else
+            asm volatile("" ::"v"(pk));
+#endif
+          }
           const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
           s1 += x;
           s2 = __builtin_elementwise_fma(x, x, s2);
@@ -291,6 +314,10 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
         rows(std::true_type{});
       else
         rows(std::false_type{});
+#ifdef WP_NOSTATS  // experiment: no InstanceNorm partials
+      asm volatile("" ::"v"(s1), "v"(s2));
+      continue;
+#endif
       const float vv[8] = {s1[0], s2[0], s1[1], s2[1], s1[2], s2[2], s1[3], s2[3]};
       float a4[4], a2[2], a1[1];
       rs_step<4, 0x140>(vv, a4, px >= 8);
@@ -300,6 +327,26 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
       const int idx = (px >= 8 ? 4 : 0) + ((px & 4) ? 2 : 0) + ((px & 2) ? 1 : 0);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv), prs,
                                             (px & 1) ? 0x80000000u : (uint32_t)(((c0 + (idx >> 1)) * 2 + (idx & 1)) * 4), 0, 0);
+    }
+    if constexpr (C::OST) {
+      // the staged tile as whole rows: 2 TW pixels x COUT channels contiguous in HBM (NHWC,
+      // cout_stride == COUT), 16 B per lane
+      lds_barrier();
+      const int ox0 = 2 * wk.tx0, oyb = 2 * wk.ty0;
+#pragma unroll
+      for (int k = 0; k < C::NST; ++k) {
+        const int off = (k * C::NT + tid) * 16;
+        const int row = off / C::ROWB, rem = off - row * C::ROWB;
+        const int pix = rem / C::PIXB, cb = rem - pix * C::PIXB;
+        const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + (row * 2 * C::TW + pix) * C::PIXP + cb);
+        const int oy = oyb + row, ox = ox0 + pix;
+        const bool ok = oy < p.oh && ox < p.ow;
+#ifndef WP_NOSTORE
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, 0);
+#else
+        asm volatile("" ::"v"(v), "v"(ok));
+#endif
+      }
     }
   };
 
@@ -382,9 +429,9 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   vm_wait<0>();  // no LDS-DMA may land after the workgroup has released its LDS
 }
 
-template <int CINP, int COUT, int TH, bool RES>
+template <int CINP, int COUT, int TH, int NF, bool RES>
 struct WphaseInst {
-  using C = WpCfg<CINP, COUT, TH>;
+  using C = WpCfg<CINP, COUT, TH, NF>;
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;
@@ -396,7 +443,7 @@ struct WphaseInst {
   }
   template <int FILL, bool ZPAD>
   static void go(const ConvParams& p, int nb, hipStream_t st) {
-    hipLaunchKernelGGL((wphase_kernel<CINP, COUT, TH, FILL, ZPAD>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((wphase_kernel<CINP, COUT, TH, NF, FILL, ZPAD>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   // grid.x = source tiles per frame, grid.y = frames; chunks of <= NFMAX frames per launch
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
@@ -445,15 +492,18 @@ struct WphaseInst {
 };
 
 #ifndef NST_WP1_TH
-#define NST_WP1_TH 6  // 128 -> 64: 8 rows spill (128 weight + 64 accumulator VGPRs)
+#define NST_WP1_TH 4  // 128 -> 64: 8 rows spill (128 weight + 64 accumulator VGPRs); 4 leaves LDS room for the staged output tile
+#endif
+#ifndef NST_WP1_NF
+#define NST_WP1_NF 8  // frames per launch (IN tables in LDS)
 #endif
 #define E(...) WphaseInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wphase(int* count) {
   static const ConvKernelInfo table[] = {
-      //  CINP COUT TH RES
-      E(128, 64, NST_WP1_TH, false),  // deconv1 / up1
-      E(128, 64, NST_WP1_TH, true),   // deconv1 joining the last residual block (fused join)
-      E(64, 32, 8, false),   // deconv2 / up2
+      //  CINP COUT TH NF RES
+      E(128, 64, NST_WP1_TH, NST_WP1_NF, false),  // deconv1 / up1
+      E(128, 64, NST_WP1_TH, NST_WP1_NF, true),   // deconv1 joining the last residual block (fused join)
+      E(64, 32, 8, 16, false),                    // deconv2 / up2
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

@@ -322,7 +322,11 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         const bool valid = decltype(all_valid)::value || (wk.ty0 + r < p.oh && ox < p.ow);
         const f32x4_t v = acc[r] + bias;
         const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+#ifndef WS_NOSTORE  // experiment (racy vmcnt accounting): no output stores
         __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : 0x80000000u, 0, 0);
+#else
+        asm volatile("" ::"v"(pk));
+#endif
         const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
         s1 += x;
         s2 = __builtin_elementwise_fma(x, x, s2);
