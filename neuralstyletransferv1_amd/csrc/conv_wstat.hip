@@ -36,8 +36,9 @@
 
 namespace nst {
 
-template <int TH>
+template <int TH, int FILL>
 struct WsCfg {
+  static constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
   static constexpr int NW = 8, NT = 512;           // two waves per SIMD, wave w: channels 16w..16w+15
   static constexpr int TW = 16;                    // tile width = MFMA column block
   static constexpr int CINP = 128;
@@ -47,17 +48,23 @@ struct WsCfg {
   static constexpr int NSTEP = 36;                 // 4 parts x 9 taps (K = 32 per step)
   static constexpr int NUNIT = 8;                  // half parts: unit u = chunks 2u (team 0), 2u+1 (team 1)
   static constexpr int QENT = NENT / 4;            // entries per wave and unit (four waves per chunk)
-  static constexpr int NFMAX = 16;                 // frames per launch (IN tables resident in LDS)
+  static constexpr int NFMAX = RES ? 8 : 16;       // frames per launch (IN tables resident in LDS)
   static constexpr int NSLOT = 4;                  // staging slots: units in flight
-  static constexpr int SLOTB = 2 * NW * 1024;      // a slot: [y | r] x wave x lane x 16 B
+  static constexpr int SLOTB = (RES ? 2 : 1) * NW * 1024;  // a slot: [y | r] x wave x lane x 16 B
   static constexpr int MAPB = ((LH + LW) * 4 + 15) / 16 * 16;
   static constexpr int MAP_OFF = NENT * EB;
   static constexpr int NORM_OFF = MAP_OFF + 2 * MAPB;        // [y | r][frame][channel] float2
   static constexpr int NORM_TAB = NFMAX * CINP * 8;
-  static constexpr int BIAS_OFF = NORM_OFF + 2 * NORM_TAB;   // 128 fp32
+  static constexpr int BIAS_OFF = NORM_OFF + (RN ? 2 : 1) * NORM_TAB;  // 128 fp32
   static constexpr int DUMMY_OFF = BIAS_OFF + CINP * 4;      // sink of the lanes without an item
   static constexpr int STG_OFF = DUMMY_OFF + 64 * 16;
-  static constexpr int LDS = STG_OFF + NSLOT * SLOTB;
+  // output tile staged in LDS (when it fits: not the ReLU(IN(r)) join) for whole-pixel 16-B
+  // stores: [row][px][256 B], wave w's 32-byte slot at (w ^ (px & 7)) (bank spread of the writes)
+  static constexpr int OUT_OFF = STG_OFF + NSLOT * SLOTB;
+  static constexpr int OUTB = TH * TW * 256;
+  static constexpr bool OST = OUT_OFF + OUTB <= 160 * 1024;
+  static constexpr int NST = OUTB / (NT * 16);  // 16-B stores per thread
+  static constexpr int LDS = OST ? OUT_OFF + OUTB : OUT_OFF;
   static constexpr int WBYTES = NW * NSTEP * 64 * 16;  // packed weights
   static_assert(NENT % 4 == 0 && QENT <= 64, "four waves per unit chunk, one item per lane");
   static_assert(LDS <= 160 * 1024, "LDS budget");
@@ -65,8 +72,8 @@ struct WsCfg {
 
 template <int TH, int FILL, bool ZPAD>
 __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
-  using C = WsCfg<TH>;
-  constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
+  using C = WsCfg<TH, FILL>;
+  constexpr bool RES = C::RES, RN = C::RN;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -244,7 +251,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   };
   constexpr int DPU = RES ? 2 : 1;                // requests per unit
   constexpr int KIN = 3 * DPU + (RES ? 2 : 0);    // vmcnt before a unit whose wait spans no epilogue
-  constexpr int KEP = KIN + TH + 1;               // ... one that spans the epilogue's stores
+  constexpr int KEP = KIN + (C::OST ? C::NST : TH) + 1;  // ... one that spans the epilogue's stores
 
   // ---- K loop ----
   typedef f32x4_t Acc[TH];
@@ -316,17 +323,24 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const uint32_t row_bytes = (uint32_t)p.ow * p.cout_stride * 2;
     const uint32_t off0 = (uint32_t)(((wk.ty0 * p.ow + ox) * p.cout_stride + c0) * 2);
     f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};  // packed-math statistics
+    // lane-derived LDS addresses recomputed per tile (opaque), not held across the K loop
+    int obase = C::OUT_OFF + px * 256 + ((wv ^ (px & 7)) * 32) + g * 8;
+    asm volatile("" : "+v"(obase));
     auto rows = [&](auto all_valid) {
 #pragma unroll
       for (int r = 0; r < TH; ++r) {
         const bool valid = decltype(all_valid)::value || (wk.ty0 + r < p.oh && ox < p.ow);
         const f32x4_t v = acc[r] + bias;
         const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+        if constexpr (C::OST) {
+          *(u32x2_t*)(smem + obase + r * C::TW * 256) = pk;
+        } else {
 #ifndef WS_NOSTORE  // experiment (racy vmcnt accounting): no output stores
-        __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : 0x80000000u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : 0x80000000u, 0, 0);
 #else
-        asm volatile("" ::"v"(pk));
+          asm volatile("" ::"v"(pk));
 #endif
+        }
         const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
         s1 += x;
         s2 = __builtin_elementwise_fma(x, x, s2);
@@ -352,6 +366,25 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         0x00020000);
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs,
                                           (px & 1) ? 0x80000000u : (uint32_t)(((c0 + (idx >> 1)) * 2 + (idx & 1)) * 4), 0, 0);
+    if constexpr (C::OST) {
+      // the staged tile, 4 whole pixels (1 KB contiguous in a tile row) per store instruction
+      lds_barrier();
+      int t0 = tid;
+      asm volatile("" : "+v"(t0));
+#pragma unroll
+      for (int k = 0; k < C::NST; ++k) {
+        const int off = (k * C::NT + t0) * 16;
+        const int pp = off >> 8, cb = off & 255;
+        const int x = pp & (C::TW - 1), oy = wk.ty0 + pp / C::TW, ox = wk.tx0 + x;
+        const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * 256 + (((cb >> 5) ^ (x & 7)) * 32) + (cb & 31));
+        const bool ok = oy < p.oh && ox < p.ow;
+#ifndef WS_NOSTORE
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * 256 + cb) : 0x80000000u, 0, 0);
+#else
+        asm volatile("" ::"v"(v), "v"(ok));
+#endif
+      }
+    }
   };
 
   // ---- persistent walk ----
@@ -439,7 +472,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
 
 template <int TH, bool RES>
 struct WstatInst {
-  using C = WsCfg<TH>;
+  using C = WsCfg<TH, RES ? WF_RES : WF_NORM>;  // NFMAX, LDS and weight sizes shared by the FILL variants
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;

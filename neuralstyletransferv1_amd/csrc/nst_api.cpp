@@ -857,8 +857,8 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
       set_error("conv " + Ly.d.conv + ": weight-stationary kernel joins IN(y) + r into a residual-stream buffer");
       return NST_E_SHAPE;
     }
-    if (Ly.mode == MODE_WPHASE && p.cout_stride != k->bn) {
-      set_error("conv " + Ly.d.conv + ": weight-stationary phase kernel stores whole pixels of bn channels");
+    if ((Ly.mode == MODE_WPHASE || Ly.mode == MODE_WSTAT) && p.cout_stride != k->bn) {
+      set_error("conv " + Ly.d.conv + ": weight-stationary kernels store whole pixels of bn channels");
       return NST_E_SHAPE;
     }
     if (Ly.mode == MODE_WPHASE && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out != nullptr || p.res_relu)) {
