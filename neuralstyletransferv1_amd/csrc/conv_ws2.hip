@@ -1,0 +1,309 @@
+// conv_ws2.hip — weight-stationary persistent stride-2 3x3 convs (the encoder's down-convs).
+//
+// Replaces ConvLayer(k3, stride 2) = ReflectionPad2d(1) + Conv2d (transformer_net.py:57-66, used at
+// transformer_net.py:11-14 for conv2 32->64 and conv3 64->128) and the zero-padded ConvBlock form
+// of transformer_net_nst.py, with the producer's InstanceNorm + ReLU applied in the fill and this
+// layer's InstanceNorm partial sums in the epilogue.
+//
+// The generic implicit-GEMM kernel re-reads the whole weight tensor from L2 for every 4x16 tile
+// (147 KB per tile for conv3, ~2.4 GB of L2 traffic per launch); here each wave keeps its 16
+// output channels' 3x3xCIN weights in registers for the launch (72 VGPRs for conv3, 36 for conv2):
+//   * workgroup = 8 waves; wave w: channel group w % (COUT/16), output row group w / (COUT/16);
+//   * persistent over (frame, TH x 16 output tiles), XCD-aware tile order; one workgroup per CU;
+//   * the input halo (2TH+1) x 33 in LDS in column-polyphase order ([row][x & 1][x >> 1], entry
+//     stride 2 x odd chunks), so lane px of x-tap dx reads entry px + (dx >> 1) of phase dx & 1 —
+//     consecutive entries, conflict-free ds_read_b128; input row y is the B operand of output rows
+//     (y - dy) / 2 for the y-taps of y's parity;
+//   * the next tile's halo is loaded into registers (16 B per lane and slot, coalesced 33-pixel
+//     row runs) before the current tile's MFMAs and written to LDS after them (IN + ReLU applied),
+//     so its HBM latency hides behind the compute; three barriers per tile;
+//   * output tile staged in LDS (wave slots XOR-swizzled by pixel) and stored as whole pixels,
+//     16 B per lane; one InstanceNorm partial row per tile and row group.
+#include <algorithm>
+#include <cstring>
+
+#include "conv_ws_common.h"
+
+#ifndef W2_RING
+#define W2_RING 3  // operand reads in flight ahead of the MFMAs
+#endif
+
+namespace nst {
+
+template <int CINP, int COUT, int TH>
+struct W2Cfg {
+  static constexpr int NW = 8, NT = 512, TW = 16;
+  static constexpr int NCG = COUT / 16;             // 16-channel groups
+  static constexpr int NRG = NW / NCG;              // output row groups
+  static constexpr int THW = TH / NRG;              // output rows per wave
+  static constexpr int NCH = CINP / 8;              // 16-B chunks per pixel
+  static constexpr int NPART = CINP / 32;           // 32-channel K steps per tap
+  static constexpr int NSTEP = 9 * NPART;           // weight registers (uint4) per wave
+  static constexpr int LH = 2 * TH + 1, LW = 2 * TW + 1;
+  static constexpr int LWE = TW + 1;                // entries per column phase
+  static constexpr int EB = (NCH + 2) * 16;         // entry stride: 2 x odd chunks
+  static constexpr int RS = 2 * LWE * EB;           // bytes per halo row
+  static constexpr int HALO = LH * RS;
+  static constexpr int NCHK = LH * LW * NCH;        // 16-B chunks per halo
+  static constexpr int NPF = (NCHK + NT - 1) / NT;  // fill slots per thread
+  static constexpr int PIXB = COUT * 2;
+  static constexpr int OUT_OFF = HALO;
+  static constexpr int OUTB = TH * TW * PIXB;
+  static constexpr int NST = OUTB / (NT * 16);      // 16-B output stores per thread
+  static constexpr int BIAS_OFF = OUT_OFF + OUTB;
+  static constexpr int LDS = BIAS_OFF + COUT * 4;
+  static constexpr int WBYTES = NCG * NSTEP * 64 * 16;
+  static_assert(CINP % 32 == 0 && COUT % 16 == 0, "channel shapes");
+  static_assert(NT % NCH == 0, "a thread's chunk is the same in every fill slot");
+  static_assert(NW % NCG == 0 && TH % NRG == 0, "waves split channel groups x row groups");
+  static_assert(NST * NT * 16 == OUTB, "whole 16-B stores per thread");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <int CINP, int COUT, int TH, bool ZPAD>
+__global__ __launch_bounds__(512) void ws2_kernel(ConvParams p) {
+  using C = W2Cfg<CINP, COUT, TH>;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cg = wv % C::NCG, rg = wv / C::NCG;
+  const int g = lane >> 4, px = lane & 15;
+
+  struct Work {
+    int n, tile, oy0, ox0;
+  };
+  const int ntile = p.tiles_x * p.tiles_y;
+  auto decode = [&](int wi) {
+    Work r;
+    r.n = wi / ntile;
+    r.tile = wi - r.n * ntile;
+    const int ty = r.tile / p.tiles_x;
+    r.oy0 = ty * TH;
+    r.ox0 = (r.tile - ty * p.tiles_x) * C::TW;
+    return r;
+  };
+  // workgroups b, b+8, ... share an XCD: each XCD takes a contiguous run of tiles per sweep
+  const int G = (int)gridDim.x, b = (int)blockIdx.x;
+  const int w0 = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+  if (w0 >= p.n_work) return;
+
+  // ---- this wave's 16 output channels x 9 x CINP weights, resident for the launch ----
+  uint4 wr[C::NSTEP];
+  {
+    const uint4* wsrc = (const uint4*)p.wpk + (size_t)cg * C::NSTEP * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < C::NSTEP; ++s) wr[s] = wsrc[s * 64];
+  }
+  if (tid < COUT) ((float*)(smem + C::BIAS_OFF))[tid] = p.bias[tid];
+
+  // ---- halo fill: slot k of this thread = chunk j = k NT + tid (entry j / NCH, chunk fc) ----
+  const size_t frame_bytes = (size_t)p.hs * p.ws * p.cs * 2;
+  const int fc = tid % C::NCH;
+  auto src_of = [&](const Work& wk, int k, int& ly, int& lx) -> int {  // byte offset, -1 = zero pad
+    const int e = (k * C::NT + tid) / C::NCH;
+    ly = e / C::LW;
+    lx = e - ly * C::LW;
+    const int sy = map_axis(2 * wk.oy0 - p.pad + ly, p.hs, p.axis_mode, p.pre);
+    const int sx = map_axis(2 * wk.ox0 - p.pad + lx, p.ws, p.axis_mode, p.pre);
+    return (sy < 0 || sx < 0) ? -1 : ((sy * p.ws + sx) * p.cs + fc * 8) * 2;
+  };
+  auto issue = [&](const Work& wk, uint4 (&pf)[C::NPF]) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.in + (size_t)wk.n * frame_bytes), (short)0, (int)frame_bytes, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < C::NPF; ++k) {
+      int ly, lx;
+      const int s = src_of(wk, k, ly, lx);
+      const bool ok = (k + 1) * C::NT <= C::NCHK || k * C::NT + tid < C::NCHK;
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, (ok && s >= 0) ? (uint32_t)s : 0x80000000u, 0, 0);
+      pf[k] = __builtin_bit_cast(uint4, v);
+    }
+  };
+  auto land = [&](const Work& wk, const uint4 (&pf)[C::NPF]) {
+    float2 nm[8];  // the producer's IN {scale, shift} of this thread's 8 channels
+    const float2* ns = p.in_norm + (size_t)wk.n * p.cs + fc * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) nm[i] = ns[i];
+#pragma unroll
+    for (int k = 0; k < C::NPF; ++k) {
+      if ((k + 1) * C::NT > C::NCHK && k * C::NT + tid >= C::NCHK) continue;
+      int ly, lx;
+      const int s = src_of(wk, k, ly, lx);
+      uint4 v = norm_chunk<__bf16>(pf[k], nm);  // IN + ReLU (as the generic kernel's fill)
+      if (ZPAD && s < 0) v = make_uint4(0u, 0u, 0u, 0u);  // zero padding stays zero after IN + ReLU
+      *(uint4*)(smem + ly * C::RS + (lx & 1) * C::LWE * C::EB + (lx >> 1) * C::EB + fc * 16) = v;
+    }
+  };
+
+  // ---- K loop: part q, x-tap dx, halo row y (the wave's 2 THW + 1 rows) ----
+  typedef f32x4_t Acc[C::THW];
+  const int r0 = rg * C::THW;
+  constexpr int NRD = 2 * C::THW + 1;  // reads per (part, dx)
+  constexpr int PRD = 3 * NRD;         // reads per part
+  auto bread = [&](int i) -> uint4 {
+    const int q = i / PRD, rem = i - q * PRD;
+    const int dx = rem / NRD, y = rem % NRD;
+    int base = (2 * r0) * C::RS + px * C::EB + g * 16;
+    asm volatile("" : "+v"(base));
+    return *(const uint4*)(smem + base + y * C::RS + (dx & 1) * C::LWE * C::EB + (dx >> 1) * C::EB + 64 * q);
+  };
+  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
+    const u32x4_t av = __builtin_bit_cast(u32x4_t, a), bv = __builtin_bit_cast(u32x4_t, bop);
+    if (first)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(av), "v"(bv));
+    else
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
+  };
+  auto kloop = [&](Acc& acc) {
+    constexpr int NI = C::NPART * PRD, D = W2_RING;
+    uint4 ring[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) ring[i] = bread(i);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = i / PRD, rem = i - q * PRD;
+      const int dx = rem / NRD, y = rem % NRD;
+      const uint4 bcur = ring[i % D];
+      if (i + D < NI) ring[i % D] = bread(i + D);
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        if ((y - dy) & 1) continue;
+        const int r = (y - dy) / 2;
+        if (y - dy < 0 || r >= C::THW) continue;
+        // row r's first MFMA: q = 0, dx = 0, y = 2r (dy = 0)
+        mfma(acc[r], wr[q * 9 + 3 * dy + dx], bcur, q == 0 && dx == 0 && dy == 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- epilogue: bias, bf16 into the LDS output tile, IN partials from the fp32 values ----
+  auto epilogue = [&](const Work& wk, Acc& acc) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA results -> VALU reads
+    const int c0 = 16 * cg + 4 * g;
+    const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
+    int obase = C::OUT_OFF + px * C::PIXB + ((cg ^ (px & (C::NCG - 1))) * 32) + g * 8;
+    asm volatile("" : "+v"(obase));
+    f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
+    const bool full = wk.oy0 + TH <= p.oh && wk.ox0 + C::TW <= p.ow;
+#pragma unroll
+    for (int r = 0; r < C::THW; ++r) {
+      const int row = r0 + r;
+      const bool valid = full || (wk.oy0 + row < p.oh && wk.ox0 + px < p.ow);
+      const f32x4_t v = acc[r] + bias;
+      const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+      *(u32x2_t*)(smem + obase + row * C::TW * C::PIXB) = pk;
+      const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      s1 += x;
+      s2 = __builtin_elementwise_fma(x, x, s2);
+    }
+    const float vv[8] = {s1[0], s2[0], s1[1], s2[1], s1[2], s2[2], s1[3], s2[3]};
+    float a4[4], a2[2], a1[1];
+    rs_step<4, 0x140>(vv, a4, px >= 8);
+    rs_step<2, 0x141>(a4, a2, (px & 4) != 0);
+    rs_step<1, 0x1b>(a2, a1, (px & 2) != 0);
+    const float t = a1[0] + dpp_f<0xb1>(a1[0]);
+    const int idx = (px >= 8 ? 4 : 0) + ((px & 4) ? 2 : 0) + ((px & 2) ? 1 : 0);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.partial + (((size_t)wk.n * ntile + wk.tile) * C::NRG + rg) * p.cout_stride * 2), (short)0,
+        p.cout_stride * 8, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs,
+                                          (px & 1) ? 0x80000000u : (uint32_t)(((c0 + (idx >> 1)) * 2 + (idx & 1)) * 4), 0, 0);
+  };
+  // the staged tile as whole pixels: 16 B per lane, TW * PIXB contiguous bytes per tile row
+  auto store_out = [&](const Work& wk) {
+    const size_t obytes = (size_t)p.oh * p.ow * C::PIXB;
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)p.out + (size_t)wk.n * obytes), (short)0, (int)obytes, 0x00020000);
+    int t0 = tid;
+    asm volatile("" : "+v"(t0));
+#pragma unroll
+    for (int k = 0; k < C::NST; ++k) {
+      const int off = (k * C::NT + t0) * 16;
+      const int pp = off / C::PIXB, cb = off - pp * C::PIXB;
+      const int x = pp % C::TW, oy = wk.oy0 + pp / C::TW, ox = wk.ox0 + x;
+      const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * C::PIXB + (((cb >> 5) ^ (x & (C::NCG - 1))) * 32) + (cb & 31));
+      const bool ok = oy < p.oh && ox < p.ow;
+      __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, 0);
+    }
+  };
+
+  // ---- persistent walk: B1 halo ready | MFMAs | B2 halo free | epilogue + next halo | B3 | stores ----
+  Work cur = decode(w0);
+  uint4 pf[C::NPF];
+  issue(cur, pf);
+  land(cur, pf);
+  for (int wn = w0 + G;; wn += G) {
+    __syncthreads();
+    const bool more = wn < p.n_work;
+    const Work nxt = decode(more ? wn : w0);
+    if (more) issue(nxt, pf);
+    Acc acc;
+    kloop(acc);
+    __syncthreads();
+    epilogue(cur, acc);
+    if (more) land(nxt, pf);
+    __syncthreads();
+    store_out(cur);
+    if (!more) break;
+    cur = nxt;
+  }
+}
+
+template <int CINP, int COUT, int TH>
+struct Ws2Inst {
+  using C = W2Cfg<CINP, COUT, TH>;
+  static int cus() {
+    static const int v = [] {
+      int dev = 0, c = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        c = 256;
+      return c;
+    }();
+    return v;
+  }
+  // grid.x = output tiles per frame, grid.y = frames
+  static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
+    ConvParams p = p0;
+    p.n_work = (int)grid.x * (int)grid.y;
+    const int nb = std::min(p.n_work, cus());  // one workgroup per CU (LDS)
+    if (p.axis_mode == AX_ZERO || p.axis_mode == AX_ZERO_PREREFLECT)
+      hipLaunchKernelGGL((ws2_kernel<CINP, COUT, TH, true>), dim3(nb), dim3(C::NT), 0, st, p);
+    else
+      hipLaunchKernelGGL((ws2_kernel<CINP, COUT, TH, false>), dim3(nb), dim3(C::NT), 0, st, p);
+  }
+  static ConvKernelInfo info() {
+    ConvKernelInfo k;
+    std::memset(&k, 0, sizeof(k));
+    k.dtype = NST_DT_BF16;
+    k.mode = MODE_WS2;
+    k.ks = 3; k.stride = 2; k.cinp = CINP; k.bn = COUT; k.th = TH; k.tw = C::TW; k.wm = C::NRG; k.wn = C::NCG;
+    k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
+    k.cpc = 8; k.nch = C::NCH; k.lds_bytes = C::LDS;
+    k.wbytes = C::WBYTES;
+    k.persistent = 1;
+    k.part_rows = C::NRG;
+    k.launch = &launch;
+    return k;
+  }
+};
+
+#ifndef NST_W2_C2_TH
+#define NST_W2_C2_TH 16
+#endif
+#ifndef NST_W2_C3_TH
+#define NST_W2_C3_TH 8
+#endif
+#define E(...) Ws2Inst<__VA_ARGS__>::info()
+const ConvKernelInfo* conv_table_ws2(int* count) {
+  static const ConvKernelInfo table[] = {
+      //  CINP COUT TH
+      E(32, 64, NST_W2_C2_TH),   // conv2 / down2
+      E(64, 128, NST_W2_C3_TH),  // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
+  };
+  *count = (int)(sizeof(table) / sizeof(table[0]));
+  return table;
+}
+#undef E
+
+}  // namespace nst

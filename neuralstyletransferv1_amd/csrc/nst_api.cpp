@@ -29,15 +29,17 @@ const ConvKernelInfo* conv_table_f32(int* count);
 const ConvKernelInfo* conv_table_out9(int* count);
 const ConvKernelInfo* conv_table_wstat(int* count);
 const ConvKernelInfo* conv_table_wphase(int* count);
+const ConvKernelInfo* conv_table_ws2(int* count);
 
 // first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind, int res) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
-  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_out9, conv_table_bf16};
+  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_out9,
+                                 conv_table_bf16};
   const TableFn tables_f32[] = {conv_table_f32};
   const TableFn* tables = dtype == NST_DT_BF16 ? tables_bf16 : tables_f32;
-  const int ntables = dtype == NST_DT_BF16 ? 5 : 1;
+  const int ntables = dtype == NST_DT_BF16 ? 6 : 1;
   static const bool no_wl = std::getenv("NST_NO_PERSISTENT") != nullptr;  // experiment switch
   for (int ti = (dtype == NST_DT_BF16 && no_wl) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
@@ -371,6 +373,26 @@ std::vector<float> pack_wphase_weights(const ConvKernelInfo& k, const LayerDef& 
   return out;
 }
 
+// MODE_WS2 weight registers (conv_ws2.hip): [channel group cg][step s][lane][8 bf16].  Step s = 9 q +
+// tap, part q = input channels 32q..32q+31, tap = 3 dy + dx; lane l holds MFMA row l & 15 = output
+// channel 16 cg + (l & 15), K elements = input channels 32 q + 8 (l >> 4) + i.
+std::vector<float> pack_ws2_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
+  const int ncg = k.bn / 16, nstep = 9 * (k.cinp / 32);
+  std::vector<float> out((size_t)ncg * nstep * 64 * 8, 0.f);
+  for (int cg = 0; cg < ncg; ++cg)
+    for (int s = 0; s < nstep; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int q = s / 9, t = s % 9, dy = t / 3, dx = t % 3;
+        const int co = 16 * cg + (l & 15);
+        for (int i = 0; i < 8; ++i) {
+          const int ci = 32 * q + 8 * (l >> 4) + i;
+          if (co < d.cout && ci < d.cin)
+            out[(((size_t)cg * nstep + s) * 64 + l) * 8 + i] = W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
+        }
+      }
+  return out;
+}
+
 // bias rows of an x-shift layer: row q = 3*s + c -> bias of output channel (perm) c
 std::vector<float> xshift_bias(const float* b, bool reverse_channels) {
   std::vector<float> r(16, 0.f);
@@ -627,6 +649,9 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 1 && arch != NST_ARCH_RECONET &&
         !std::getenv("NST_NO_WSTAT"))  // env: experiment switch
       modes.push_back(MODE_WSTAT);
+    // stride-2 down-convs: weight-stationary kernel (conv_ws2.hip) where compiled
+    if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 2 && !std::getenv("NST_NO_WS2"))  // env: experiment switch
+      modes.push_back(MODE_WS2);
     modes.push_back(MODE_STD);
     // image layer: prefer the conv over the pre-padded encoded input (one streaming pre-pass, plain
     // 16-byte fill loads) when it is compiled for this shape; it serves u8 and f32 inputs alike
@@ -674,6 +699,8 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
       if ((rc = upload_packed(pack_wstat_weights(d, W), &Ly.wpk)) != NST_OK) break;
     } else if (Ly.mode == MODE_WPHASE) {
       if ((rc = upload_packed(pack_wphase_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
+    } else if (Ly.mode == MODE_WS2) {
+      if ((rc = upload_packed(pack_ws2_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) {
       break;
     }
@@ -857,7 +884,11 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
       set_error("conv " + Ly.d.conv + ": weight-stationary kernel joins IN(y) + r into a residual-stream buffer");
       return NST_E_SHAPE;
     }
-    if ((Ly.mode == MODE_WPHASE || Ly.mode == MODE_WSTAT) && p.cout_stride != k->bn) {
+    if (Ly.mode == MODE_WS2 && (p.in_norm == nullptr || p.res_r != nullptr || p.crop_x || p.crop_y)) {
+      set_error("conv " + Ly.d.conv + ": weight-stationary down-conv reads a normalized activation, uncropped");
+      return NST_E_SHAPE;
+    }
+    if ((Ly.mode == MODE_WPHASE || Ly.mode == MODE_WSTAT || Ly.mode == MODE_WS2) && p.cout_stride != k->bn) {
       set_error("conv " + Ly.d.conv + ": weight-stationary kernels store whole pixels of bn channels");
       return NST_E_SHAPE;
     }
