@@ -6,7 +6,7 @@ CSRC := $(PKG)/csrc
 BUILD := build/obj
 CXXFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
-SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
+SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
 OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
 LIB := $(PKG)/libnst_hip.so
 
@@ -22,6 +22,7 @@ $(BUILD)/conv_bf16_wl.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=200000
 $(BUILD)/conv_wstat.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 $(BUILD)/conv_wphase.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 $(BUILD)/conv_ws2.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
+$(BUILD)/conv_ws9.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 
 $(BUILD)/%.cpp.o: $(CSRC)/%.cpp $(CSRC)/nst_internal.h include/nst_hip.h
 	@mkdir -p $(BUILD)

@@ -1,0 +1,345 @@
+// conv_ws9.hip — weight-stationary persistent first layer: the 9x9 image conv, 3 -> 32 channels.
+//
+// Replaces ConvLayer(3, 32, kernel 9, stride 1) = ReflectionPad2d(4) + Conv2d
+// (transformer_net.py:8 conv1, transformer_net.py:46-54) and NST's down1 (transformer_net_nst.py:64,
+// zero padding after the 40-pixel pre-reflect), reading the pre-padded encoded frame of
+// conv_prep.hip (bf16 [n][hp][wp][4], channel 3 = 0, padding already resolved) with an identity
+// coordinate map; this layer's InstanceNorm partial sums in the epilogue.
+//
+// The generic implicit-GEMM kernel ran this layer at ~0.5 ms per batch of 8 1080p frames, VALU-
+// and wait-bound (5 VALU per MFMA).  Here the whole weight tensor (32 x 9 x 9 x 4 bf16) lives in
+// every wave's registers (84 VGPRs) and the K loop is LDS reads + MFMAs only:
+//   * K = (ky, kx, c).  For kx 0..7 one 16x16x32 MFMA covers a whole kernel row ky: lane (px, g)
+//     holds the 16 contiguous bytes of padded pixels x + 2g, x + 2g + 1 (4 channels each) of input
+//     row y + ky, so the B operand of input row r serves output rows r - ky for all nine ky.
+//     Column kx = 8 is a 16x16x16 MFMA over 4 kernel rows (lane group g = kernel row 4j + g, one
+//     8-byte pixel): operand K(s) = rows s..s+3 serves output rows s, s - 4, s - 8 (j = 0, 1, 2).
+//     Issued K = 9 x 32 + 3 x 16 = 336 for 324 useful (96 %), at the MFMA cost of 9 + 1.5 steps.
+//   * workgroup = NW waves (4), tile = 8 output rows x 16 NW columns, wave w = 8 rows x columns
+//     16w..16w+15 and all 32 output channels (two M tiles): 16 input-row operands + 16 column-8
+//     operands feed 192 MFMAs per wave and tile;
+//   * persistent over (frame, tile) items, XCD-aware order, two 4-wave workgroups per CU: their
+//     barriers are independent, so one's epilogue and stores overlap the other's MFMAs (one 8-wave
+//     workgroup per CU idled the MFMA pipe through every epilogue: 0.46 ms vs ~0.16 ms of MFMA);
+//   * the next item's 16-row halo (RCH 16-byte chunks per row, contiguous in the padded frame)
+//     travels by LDS-DMA into the second of two halo buffers while the current item computes;
+//   * output tile staged in LDS (8-byte slots XOR-swizzled by pixel) and stored as whole 64-byte
+//     pixels, 16 B per lane; per-wave IN partials (DPP reduce-scatter) combined in fixed order
+//     into one partial row per tile.
+#include <algorithm>
+#include <cstring>
+#include <type_traits>
+
+#include "conv_ws_common.h"
+
+#ifndef NST_WS9_NW
+#define NST_WS9_NW 4  // waves per workgroup: 4 = two workgroups per CU drifting out of phase
+#endif
+
+#ifndef W9_RING
+#define W9_RING 2  // input-row operands in flight ahead of the MFMAs
+#endif
+
+namespace nst {
+
+template <int NW_>
+struct W9Cfg {
+  static constexpr int NW = NW_, NT = 64 * NW, TH = 8, TW = 16 * NW, COUT = 32;
+  static constexpr int HR = TH + 8;                 // halo rows
+  // 16-B chunks per halo row: TW + 8 px used, rounded up so the row stride is == 32 mod 64 dwords
+  // (the column-8 operand's four rows land in disjoint bank halves)
+  static constexpr int RCH = ((TW + 8) / 2 + 7) / 16 * 16 + 8;
+  static constexpr int RS = RCH * 16;
+  static constexpr int HALO = HR * RS;
+  static constexpr int NCHK = HR * RCH;
+  static constexpr int NREQ = (NCHK + NT - 1) / NT; // request slots per thread (the last partial)
+  static constexpr int PIXB = COUT * 2;             // 64 B per output pixel
+  static constexpr int OUT_OFF = 2 * HALO;
+  static constexpr int OUTB = TH * TW * PIXB;
+  static constexpr int NST = OUTB / (NT * 16);      // 16-B stores per thread
+  static constexpr int PART_OFF = OUT_OFF + OUTB;
+  static constexpr int BIAS_OFF = PART_OFF + NW * 64 * 4;
+  static constexpr int LDS = BIAS_OFF + COUT * 4;
+  static constexpr int NWM = 9 * 2;                 // 16x16x32 weight fragments (ky, m)
+  static constexpr int NWK = 3 * 2;                 // 16x16x16 weight fragments (j, m)
+  static constexpr int WBYTES = NWM * 64 * 16 + NWK * 64 * 8;
+  static_assert(NCHK % 64 == 0, "whole-wave DMA requests");
+  static_assert(2 * RCH >= TW + 8 && (RS / 4) % 64 == 32, "halo row");
+  static_assert(NST * NT * 16 == OUTB, "whole 16-B stores per thread");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
+  using C = W9Cfg<NW>;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, px = lane & 15;
+
+  struct Work {
+    int n, tile, oy0, ox0;
+  };
+  const int ntile = p.tiles_x * p.tiles_y;
+  auto decode = [&](int wi) {
+    Work r;
+    r.n = wi / ntile;
+    r.tile = wi - r.n * ntile;
+    const int ty = r.tile / p.tiles_x;
+    r.oy0 = ty * C::TH;
+    r.ox0 = (r.tile - ty * p.tiles_x) * C::TW;
+    return r;
+  };
+  // workgroups b, b+8, ... share an XCD: each XCD takes a contiguous run of tiles per sweep
+  const int G = (int)gridDim.x, b = (int)blockIdx.x;
+  const int w0 = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+  if (w0 >= p.n_work) return;
+
+  // ---- the whole weight tensor, resident for the launch (same in every wave) ----
+  uint4 wm[C::NWM];
+  uint2 wk[C::NWK];
+  {
+    const uint4* src = (const uint4*)p.wpk + lane;
+#pragma unroll
+    for (int s = 0; s < C::NWM; ++s) wm[s] = src[s * 64];
+    const uint2* srck = (const uint2*)((const char*)p.wpk + C::NWM * 64 * 16) + lane;
+#pragma unroll
+    for (int s = 0; s < C::NWK; ++s) wk[s] = srck[s * 64];
+  }
+  if (tid < C::COUT) ((float*)(smem + C::BIAS_OFF))[tid] = p.bias[tid];
+
+  // ---- halo requests: chunk j = k NT + tid -> halo row j / RCH, chunk j % RCH; LDS j * 16 ----
+  const size_t frame_bytes = (size_t)p.hs * p.ws * 8;
+  const uint32_t smem_u = (uint32_t)(uintptr_t)smem;
+  // the tile moves the frame offset only (soffset); a thread's chunk offsets are launch constants.
+  // Rows past the frame read 0 (buffer range check); columns past a row's end read the next row
+  // (finite, only feeding outputs past the frame edge)
+  uint32_t roff[C::NREQ];
+#pragma unroll
+  for (int k = 0; k < C::NREQ; ++k) {
+    const int j = k * C::NT + tid;
+    const int row = j / C::RCH, c = j - row * C::RCH;
+    roff[k] = (uint32_t)((row * p.ws + 2 * c) * 8);
+  }
+  auto request = [&](const Work& wk_, int buf) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.in + (size_t)wk_.n * frame_bytes), (short)0, (int)frame_bytes, 0x00020000);
+    const int soff = (wk_.oy0 * p.ws + wk_.ox0) * 8;
+#pragma unroll
+    for (int k = 0; k < C::NREQ; ++k) {
+      if (k * C::NT + wv * 64 >= C::NCHK) continue;  // wave-uniform
+      dma16(rs, roff[k], smem_u + buf * C::HALO + (k * C::NT + wv * 64) * 16, soff);
+    }
+  };
+
+  typedef f32x4_t Acc[C::TH][2];
+  auto mfma32 = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
+    const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, bop),
+                                                first ? z : c, 0, 0, 0);
+  };
+  auto mfma16 = [&](f32x4_t& c, const uint2& a, const uint2& bop) {
+    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4_t, a), __builtin_bit_cast(s16x4_t, bop), c,
+                                                  0, 0, 0);
+  };
+  // ---- K loop over the wave's 16 halo rows ----
+  auto kloop = [&](Acc& acc, int buf) {
+    int fb = buf * C::HALO + (16 * wv + px + 2 * g) * 8;  // row-r operand: + r * RS
+    int kb = buf * C::HALO + (16 * wv + px + 8) * 8;      // column-8 operand rows r + g (clamped)
+    asm volatile("" : "+v"(fb), "+v"(kb));
+    auto fread = [&](int r) { return *(const uint4*)(smem + fb + r * C::RS); };
+    // rows past the halo only meet zero weights (kernel rows 9..11): read row HR - 1 instead
+    auto kread = [&](int r) {
+      const int kr = (r + 3 < C::HR) ? (r + g) * C::RS : min(r + g, C::HR - 1) * C::RS;
+      return *(const uint2*)(smem + kb + kr);
+    };
+    // operands of row r + D are read while row r's MFMAs issue (register ring, explicit order)
+    constexpr int D = W9_RING;
+    uint4 fr[D];
+    uint2 kf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      fr[i] = fread(i);
+      kf[i] = kread(i);
+    }
+#pragma unroll
+    for (int r = 0; r < C::HR; ++r) {
+      const uint4 f = fr[r % D];
+      const uint2 k8 = kf[r % D];
+      if (r + D < C::HR) {
+        fr[r % D] = fread(r + D);
+        kf[r % D] = kread(r + D);
+      }
+#pragma unroll
+      for (int y = 0; y < C::TH; ++y) {
+        const int ky = r - y;
+        if (ky < 0 || ky > 8) continue;
+        mfma32(acc[y][0], wm[2 * ky + 0], f, ky == 0);
+        mfma32(acc[y][1], wm[2 * ky + 1], f, ky == 0);
+      }
+#pragma unroll
+      for (int y = 0; y < C::TH; ++y) {
+        const int d = r - y;
+        if (d < 0 || d > 8 || (d & 3)) continue;
+        mfma16(acc[y][0], wk[2 * (d >> 2) + 0], k8);
+        mfma16(acc[y][1], wk[2 * (d >> 2) + 1], k8);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- epilogue: bias, bf16 into the LDS output tile, IN partials from the fp32 values ----
+  auto epilogue = [&](const Work& wk_, Acc& acc) {
+    const f32x4_t bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (4 * g) * 4);
+    const f32x4_t bias1 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 + 4 * g) * 4);
+    const int e = 2 * ((px >> 2) & 3);  // slot swizzle of this lane's pixel
+    int obase = C::OUT_OFF + (16 * wv + px) * C::PIXB;
+    asm volatile("" : "+v"(obase));
+    const int o0 = ((0 + g) ^ e) * 8, o1 = ((4 + g) ^ e) * 8;
+    f32x4_t s1a = {0.f, 0.f, 0.f, 0.f}, s2a = s1a, s1b = s1a, s2b = s1a;
+    // interior tiles (all but the frame's last row / column of tiles) take the select-free copy
+    auto rows = [&](auto masked) {
+#pragma unroll
+      for (int y = 0; y < C::TH; ++y) {
+        const f32x4_t va = acc[y][0] + bias0, vb = acc[y][1] + bias1;
+        const u32x2_t pa = {pack_bf16(va[0], va[1]), pack_bf16(va[2], va[3])};
+        const u32x2_t pb = {pack_bf16(vb[0], vb[1]), pack_bf16(vb[2], vb[3])};
+        *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o0) = pa;
+        *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o1) = pb;
+        f32x4_t xa = va, xb = vb;
+        if constexpr (decltype(masked)::value) {
+          const bool valid = wk_.oy0 + y < p.oh && wk_.ox0 + 16 * wv + px < p.ow;
+          const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+          xa = valid ? va : z;
+          xb = valid ? vb : z;
+        }
+        s1a += xa;
+        s2a = __builtin_elementwise_fma(xa, xa, s2a);
+        s1b += xb;
+        s2b = __builtin_elementwise_fma(xb, xb, s2b);
+      }
+    };
+    if (wk_.oy0 + C::TH <= p.oh && wk_.ox0 + C::TW <= p.ow)
+      rows(std::false_type{});
+    else
+      rows(std::true_type{});
+    // value v = 8 m + 2 c + k (channel 16 m + 4 g + c, k = sum / sum of squares); after the
+    // reduce-scatter over the 16 pixel lanes lane px holds the row total of value px
+    const float vv[16] = {s1a[0], s2a[0], s1a[1], s2a[1], s1a[2], s2a[2], s1a[3], s2a[3],
+                          s1b[0], s2b[0], s1b[1], s2b[1], s1b[2], s2b[2], s1b[3], s2b[3]};
+    float a8[8], a4[4], a2[2], a1[1];
+    rs_step<8, 0x140>(vv, a8, px >= 8);
+    rs_step<4, 0x141>(a8, a4, (px & 4) != 0);
+    rs_step<2, 0x1b>(a4, a2, (px & 2) != 0);
+    rs_step<1, 0xb1>(a2, a1, (px & 1) != 0);
+    const int ch = 16 * (px >> 3) + 4 * g + ((px >> 1) & 3);
+    ((float*)(smem + C::PART_OFF))[wv * 64 + ch * 2 + (px & 1)] = a1[0];
+  };
+  // wave 0: the tile's partial row (fixed-order sum over the NW waves); all: whole-pixel stores
+  // store k of thread t: tile row k, pixel column t / 4, bytes 16 (t % 4) .. + 15 (NT / 4 == TW)
+  static_assert(C::NT / 4 == C::TW && C::NST == C::TH, "one tile row per store");
+  const int sx = tid >> 2, scb = (tid & 3) * 16;
+  int srd = C::OUT_OFF + sx * C::PIXB + (((scb >> 3) ^ (2 * ((sx >> 2) & 3))) << 3);
+  asm volatile("" : "+v"(srd));
+  auto store_out = [&](const Work& wk_) {
+    if (wv == 0) {
+      const float* pp = (const float*)(smem + C::PART_OFF) + lane;
+      float t = pp[0];
+#pragma unroll
+      for (int w = 1; w < C::NW; ++w) t += pp[w * 64];
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * 64), (short)0, 256, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (uint32_t)(lane * 4), 0, 0);
+    }
+    const size_t obytes = (size_t)p.oh * p.ow * C::PIXB;
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)p.out + (size_t)wk_.n * obytes), (short)0, (int)obytes, 0x00020000);
+    const uint32_t voff = (wk_.ox0 + sx < p.ow) ? (uint32_t)((wk_.ox0 + sx) * C::PIXB + scb) : 0x80000000u;
+#pragma unroll
+    for (int k = 0; k < C::NST; ++k) {  // store k = tile row k
+      const u32x4_t v = *(const u32x4_t*)(smem + srd + k * C::TW * C::PIXB);
+#ifndef WS9_NOSTORE  // experiment (wrong result): no output stores
+      if (wk_.oy0 + k < p.oh)
+#else
+      if (v[0] == 0x7fc0dead)
+#endif
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + k) * p.ow * C::PIXB, 0);
+    }
+  };
+
+  // ---- persistent walk: [wait own DMA | B1] request next | MFMAs | epilogue | B2 | stores ----
+  // vmcnt: after the next item's requests a wave issues only the stores of store_out (NST, plus
+  // the partial row on wave 0, issued first), so vmcnt(NST) at the top of the next iteration
+  // covers its requests; each wave waits for its own requests, the barrier for everyone's.
+  Work cur = decode(w0);
+  int buf = 0;
+  request(cur, 0);
+  for (int wn = w0 + G;; wn += G) {
+    vm_wait<C::NST>();
+    __syncthreads();
+    const bool more = wn < p.n_work;
+    Work nxt = cur;
+    if (more) {
+      nxt = decode(wn);
+      request(nxt, buf ^ 1);
+    }
+    Acc acc;
+#ifndef WS9_NOMFMA  // experiment (wrong result): no K loop
+    kloop(acc, buf);
+#else
+    for (int y = 0; y < C::TH; ++y) acc[y][0] = acc[y][1] = (f32x4_t){0.f, 0.f, 0.f, (float)buf};
+#endif
+    epilogue(cur, acc);
+    __syncthreads();
+    store_out(cur);
+    if (!more) break;
+    cur = nxt;
+    buf ^= 1;
+  }
+  vm_wait<0>();
+}
+
+template <int NW>
+struct Ws9Inst {
+  using C = W9Cfg<NW>;
+  static int cus() {
+    static const int v = [] {
+      int dev = 0, c = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        c = 256;
+      return c;
+    }();
+    return v;
+  }
+  // grid.x = output tiles per frame, grid.y = frames
+  static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
+    ConvParams p = p0;
+    p.n_work = (int)grid.x * (int)grid.y;
+    const int nb = std::min(p.n_work, cus() * (8 / NW));  // 8 waves per CU (VGPRs)
+    hipLaunchKernelGGL(ws9_kernel<NW>, dim3(nb), dim3(C::NT), 0, st, p);
+  }
+  static ConvKernelInfo info() {
+    ConvKernelInfo k;
+    std::memset(&k, 0, sizeof(k));
+    k.dtype = NST_DT_BF16;
+    k.mode = MODE_WS9;
+    k.ks = 9; k.stride = 1; k.cinp = 4; k.bn = C::COUT; k.th = C::TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
+    k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
+    k.cpc = 4; k.nch = 1; k.lds_bytes = C::LDS;
+    k.wbytes = C::WBYTES;
+    k.persistent = 1;
+    k.part_rows = 1;
+    k.launch = &launch;
+    return k;
+  }
+};
+
+const ConvKernelInfo* conv_table_ws9(int* count) {
+  static const ConvKernelInfo table[] = {Ws9Inst<NST_WS9_NW>::info()};
+  *count = 1;
+  return table;
+}
+
+}  // namespace nst

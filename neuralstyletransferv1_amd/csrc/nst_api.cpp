@@ -30,16 +30,17 @@ const ConvKernelInfo* conv_table_out9(int* count);
 const ConvKernelInfo* conv_table_wstat(int* count);
 const ConvKernelInfo* conv_table_wphase(int* count);
 const ConvKernelInfo* conv_table_ws2(int* count);
+const ConvKernelInfo* conv_table_ws9(int* count);
 
 // first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind, int res) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
-  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_out9,
-                                 conv_table_bf16};
+  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_ws9,
+                                 conv_table_out9, conv_table_bf16};
   const TableFn tables_f32[] = {conv_table_f32};
   const TableFn* tables = dtype == NST_DT_BF16 ? tables_bf16 : tables_f32;
-  const int ntables = dtype == NST_DT_BF16 ? 6 : 1;
+  const int ntables = dtype == NST_DT_BF16 ? 7 : 1;
   static const bool no_wl = std::getenv("NST_NO_PERSISTENT") != nullptr;  // experiment switch
   for (int ti = (dtype == NST_DT_BF16 && no_wl) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
@@ -393,6 +394,28 @@ std::vector<float> pack_ws2_weights(const ConvKernelInfo& k, const LayerDef& d, 
   return out;
 }
 
+// MODE_WS9 weight registers (conv_ws9.hip), the same in every wave.  Kernel columns 0..7: 18
+// 16x16x32 fragments [ky][m][lane][8 bf16], lane l = output channel 16 m + (l & 15), K element
+// i = tap kx = 2 (l >> 4) + (i >> 2), input channel i & 3.  Column 8: 6 16x16x16 fragments
+// [j][m][lane][4 bf16], kernel row 4 j + (l >> 4) (zero past row 8), input channel i.
+std::vector<float> pack_ws9_weights(const LayerDef& d, const float* W) {
+  std::vector<float> out((size_t)18 * 64 * 8 + 6 * 64 * 4, 0.f);
+  auto w = [&](int co, int ci, int ky, int kx) -> float {
+    return (co < d.cout && ci < d.cin && ky < 9) ? W[(((size_t)co * d.cin + ci) * 9 + ky) * 9 + kx] : 0.f;
+  };
+  for (int ky = 0; ky < 9; ++ky)
+    for (int m = 0; m < 2; ++m)
+      for (int l = 0; l < 64; ++l)
+        for (int i = 0; i < 8; ++i)
+          out[(((size_t)ky * 2 + m) * 64 + l) * 8 + i] = w(16 * m + (l & 15), i & 3, ky, 2 * (l >> 4) + (i >> 2));
+  float* k8 = out.data() + (size_t)18 * 64 * 8;
+  for (int j = 0; j < 3; ++j)
+    for (int m = 0; m < 2; ++m)
+      for (int l = 0; l < 64; ++l)
+        for (int i = 0; i < 4; ++i) k8[(((size_t)j * 2 + m) * 64 + l) * 4 + i] = w(16 * m + (l & 15), i, 4 * j + (l >> 4), 8);
+  return out;
+}
+
 // bias rows of an x-shift layer: row q = 3*s + c -> bias of output channel (perm) c
 std::vector<float> xshift_bias(const float* b, bool reverse_channels) {
   std::vector<float> r(16, 0.f);
@@ -656,7 +679,11 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     // image layer: prefer the conv over the pre-padded encoded input (one streaming pre-pass, plain
     // 16-byte fill loads) when it is compiled for this shape; it serves u8 and f32 inputs alike
     if (image_in && !std::getenv("NST_NO_PREPAD")) {  // env: experiment switch
-      Ly.k_main = find_conv_kernel(compute_dtype, MODE_STD, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0);
+      // weight-stationary 9x9 kernel (conv_ws9.hip) where compiled, else the generic one
+      Ly.k_main = std::getenv("NST_NO_WS9") ? nullptr  // env: experiment switch
+                                            : find_conv_kernel(compute_dtype, MODE_WS9, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0);
+      if (Ly.k_main) Ly.mode = MODE_WS9;
+      else Ly.k_main = find_conv_kernel(compute_dtype, MODE_STD, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0);
       if (Ly.k_main && d.stride == 1) { Ly.prepad = true; Ly.k_alt = Ly.k_main; modes.clear(); }
       else Ly.k_main = nullptr;
     }
@@ -701,6 +728,8 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
       if ((rc = upload_packed(pack_wphase_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if (Ly.mode == MODE_WS2) {
       if ((rc = upload_packed(pack_ws2_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
+    } else if (Ly.mode == MODE_WS9) {
+      if ((rc = upload_packed(pack_ws9_weights(d, W), &Ly.wpk)) != NST_OK) break;
     } else if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) {
       break;
     }
@@ -888,7 +917,11 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
       set_error("conv " + Ly.d.conv + ": weight-stationary down-conv reads a normalized activation, uncropped");
       return NST_E_SHAPE;
     }
-    if ((Ly.mode == MODE_WPHASE || Ly.mode == MODE_WSTAT || Ly.mode == MODE_WS2) && p.cout_stride != k->bn) {
+    if (Ly.mode == MODE_WS9 && (!Ly.prepad || p.in_norm != nullptr || p.res_r != nullptr || p.crop_x || p.crop_y || final_out)) {
+      set_error("conv " + Ly.d.conv + ": weight-stationary 9x9 kernel reads the pre-padded frame, uncropped");
+      return NST_E_SHAPE;
+    }
+    if ((Ly.mode == MODE_WPHASE || Ly.mode == MODE_WSTAT || Ly.mode == MODE_WS2 || Ly.mode == MODE_WS9) && p.cout_stride != k->bn) {
       set_error("conv " + Ly.d.conv + ": weight-stationary kernels store whole pixels of bn channels");
       return NST_E_SHAPE;
     }

@@ -37,7 +37,7 @@ enum OutKind { OUT_ACT = 0, OUT_U8_NHWC = 1, OUT_F32_NCHW = 2 };
 enum AxisMode { AX_REFLECT = 0, AX_REFLECT_UP2 = 1, AX_ZERO = 2, AX_ZERO_PREREFLECT = 3, AX_ZINSERT = 4, AX_CLAMP = 5 };
 
 // conv_kernel mappings (see conv_impl.h)
-enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2, MODE_KYROT = 3, MODE_WSTAT = 4, MODE_WPHASE = 5, MODE_WS2 = 6 };  // KYROT: conv_out9.hip, WSTAT: conv_wstat.hip, WPHASE: conv_wphase.hip, WS2: conv_ws2.hip
+enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2, MODE_KYROT = 3, MODE_WSTAT = 4, MODE_WPHASE = 5, MODE_WS2 = 6, MODE_WS9 = 7 };  // KYROT: conv_out9.hip, WSTAT: conv_wstat.hip, WPHASE: conv_wphase.hip, WS2: conv_ws2.hip, WS9: conv_ws9.hip
 
 struct ConvParams {
   // input
