@@ -23,9 +23,12 @@
 //     workgroup per CU idled the MFMA pipe through every epilogue: 0.46 ms vs ~0.16 ms of MFMA);
 //   * the next item's 16-row halo (RCH 16-byte chunks per row, contiguous in the padded frame)
 //     travels by LDS-DMA into the second of two halo buffers while the current item computes;
-//   * output tile staged in LDS (8-byte slots XOR-swizzled by pixel) and stored as whole 64-byte
-//     pixels, 16 B per lane; per-wave IN partials (DPP reduce-scatter) combined in fixed order
-//     into one partial row per tile.
+//   * bf16 outputs stored straight from the accumulators as half pixels (8 B per lane, 32 B runs);
+//     staging the tile in LDS for whole-pixel stores (WS9_STAGED) measured ~1 % slower here;
+//     per-wave IN partials (DPP reduce-scatter) combined in fixed order into one partial row per
+//     tile.  Measured (bench, 8 x 1080p): 0.42-0.46 ms by box vs 0.51 for the generic kernel;
+//     MFMA pipe ~44 % busy (PMC), and removing the MFMAs leaves 0.25 ms of fill / epilogue time
+//     that the two workgroups per CU do not hide behind each other's MFMAs.
 #include <algorithm>
 #include <cstring>
 #include <type_traits>
@@ -199,6 +202,12 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
     asm volatile("" : "+v"(obase));
     const int o0 = ((0 + g) ^ e) * 8, o1 = ((4 + g) ^ e) * 8;
     f32x4_t s1a = {0.f, 0.f, 0.f, 0.f}, s2a = s1a, s1b = s1a, s2b = s1a;
+#ifndef WS9_STAGED
+    const __amdgpu_buffer_rsrc_t dors = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)p.out + (size_t)wk_.n * p.oh * p.ow * C::PIXB), (short)0, (int)(p.oh * p.ow * C::PIXB), 0x00020000);
+    const int dx = wk_.ox0 + 16 * wv + px;
+    const uint32_t dvoff = dx < p.ow ? (uint32_t)(dx * C::PIXB + 8 * g) : 0x80000000u;
+#endif
     // interior tiles (all but the frame's last row / column of tiles) take the select-free copy
     auto rows = [&](auto masked) {
 #pragma unroll
@@ -206,8 +215,15 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
         const f32x4_t va = acc[y][0] + bias0, vb = acc[y][1] + bias1;
         const u32x2_t pa = {pack_bf16(va[0], va[1]), pack_bf16(va[2], va[3])};
         const u32x2_t pb = {pack_bf16(vb[0], vb[1]), pack_bf16(vb[2], vb[3])};
+#ifdef WS9_STAGED
         *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o0) = pa;
         *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o1) = pb;
+#else  // half-pixel stores straight from the accumulators
+        if (wk_.oy0 + y < p.oh) {
+          __builtin_amdgcn_raw_buffer_store_b64(pa, dors, dvoff, (wk_.oy0 + y) * p.ow * C::PIXB, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(pb, dors, dvoff + 32, (wk_.oy0 + y) * p.ow * C::PIXB, 0);
+        }
+#endif
         f32x4_t xa = va, xb = vb;
         if constexpr (decltype(masked)::value) {
           const bool valid = wk_.oy0 + y < p.oh && wk_.ox0 + 16 * wv + px < p.ow;
@@ -257,6 +273,7 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((char*)p.out + (size_t)wk_.n * obytes), (short)0, (int)obytes, 0x00020000);
     const uint32_t voff = (wk_.ox0 + sx < p.ow) ? (uint32_t)((wk_.ox0 + sx) * C::PIXB + scb) : 0x80000000u;
+#ifdef WS9_STAGED
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {  // store k = tile row k
       const u32x4_t v = *(const u32x4_t*)(smem + srd + k * C::TW * C::PIXB);
@@ -267,6 +284,7 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
 #endif
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + k) * p.ow * C::PIXB, 0);
     }
+#endif
   };
 
   // ---- persistent walk: [wait own DMA | B1] request next | MFMAs | epilogue | B2 | stores ----
@@ -277,7 +295,11 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
   int buf = 0;
   request(cur, 0);
   for (int wn = w0 + G;; wn += G) {
+#ifdef WS9_STAGED
     vm_wait<C::NST>();
+#else
+    vm_wait<2 * C::TH>();
+#endif
     __syncthreads();
     const bool more = wn < p.n_work;
     Work nxt = cur;
