@@ -197,10 +197,12 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
   auto epilogue = [&](const Work& wk_, Acc& acc) {
     const f32x4_t bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (4 * g) * 4);
     const f32x4_t bias1 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 + 4 * g) * 4);
+#ifdef WS9_STAGED
     const int e = 2 * ((px >> 2) & 3);  // slot swizzle of this lane's pixel
     int obase = C::OUT_OFF + (16 * wv + px) * C::PIXB;
     asm volatile("" : "+v"(obase));
     const int o0 = ((0 + g) ^ e) * 8, o1 = ((4 + g) ^ e) * 8;
+#endif
     f32x4_t s1a = {0.f, 0.f, 0.f, 0.f}, s2a = s1a, s1b = s1a, s2b = s1a;
 #ifndef WS9_STAGED
     const __amdgpu_buffer_rsrc_t dors = __builtin_amdgcn_make_buffer_rsrc(
@@ -269,11 +271,11 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
           (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * 64), (short)0, 256, 0x00020000);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (uint32_t)(lane * 4), 0, 0);
     }
+#ifdef WS9_STAGED
     const size_t obytes = (size_t)p.oh * p.ow * C::PIXB;
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((char*)p.out + (size_t)wk_.n * obytes), (short)0, (int)obytes, 0x00020000);
     const uint32_t voff = (wk_.ox0 + sx < p.ow) ? (uint32_t)((wk_.ox0 + sx) * C::PIXB + scb) : 0x80000000u;
-#ifdef WS9_STAGED
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {  // store k = tile row k
       const u32x4_t v = *(const u32x4_t*)(smem + srd + k * C::TW * C::PIXB);
