@@ -51,9 +51,14 @@ struct WpCfg {
   static constexpr int DUMMY_OFF = BIAS_OFF + COUT * 4;
   static constexpr int STG_OFF = DUMMY_OFF + 64 * 16;
   // output tile staged in LDS for contiguous 16-B stores (when it fits): [row 2TH][pixel 32][COUT
-  // channels + 16 B pad]; NST = 16-B stores per thread
+  // channels (+ 32 B pad at 32 channels)], 8-byte slots XOR-swizzled by pixel (swz below): the
+  // epilogue's ds_write_b64 and the store pass's ds_read_b128 at most 2-way bank-conflicted (a
+  // 16-B pad without swizzle was 4-way / 3-way); NST = 16-B stores per thread
   static constexpr int OUT_OFF = STG_OFF + NSLOT * SLOTB;
-  static constexpr int PIXB = COUT * 2, PIXP = PIXB + 16, ROWB = 2 * TW * PIXB;
+  static constexpr int PIXB = COUT * 2, PIXP = COUT == 32 ? PIXB + 32 : PIXB, ROWB = 2 * TW * PIXB;
+  static constexpr int SWZ_SH = COUT == 32 ? 2 : 1;
+  // even slot offset (keeps 16-B slot pairs together) of staged pixel q (0 .. 2TW-1 within a row)
+  static __device__ __forceinline__ int swz(int q) { return 2 * ((q ^ (q >> SWZ_SH)) & (PIXB / 16 - 1)); }
   static constexpr int OUTB = 2 * TH * 2 * TW * PIXP;
   static constexpr bool OST = OUT_OFF + OUTB <= 160 * 1024;
   static constexpr int NST = 2 * TH * ROWB / (NT * 16);
@@ -297,7 +302,8 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
           const f32x4_t v = acc[r][t] + bias;
           const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
           if constexpr (C::OST) {  // into the LDS output tile: row 2r + a, pixel 2 px + b
-            *(u32x2_t*)(smem + C::OUT_OFF + ((2 * r + (ph >> 1)) * 2 * C::TW + 2 * px + (ph & 1)) * C::PIXP + c0 * 2) = pk;
+            *(u32x2_t*)(smem + C::OUT_OFF + ((2 * r + (ph >> 1)) * 2 * C::TW + 2 * px + (ph & 1)) * C::PIXP +
+                        (((c0 >> 2) ^ C::swz(2 * px + (ph & 1))) << 3)) = pk;
           } else {
 #ifndef WP_NOSTORE  // experiment (racy vmcnt accounting): no output stores
             __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, 0);
@@ -338,7 +344,8 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
         const int off = (k * C::NT + tid) * 16;
         const int row = off / C::ROWB, rem = off - row * C::ROWB;
         const int pix = rem / C::PIXB, cb = rem - pix * C::PIXB;
-        const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + (row * 2 * C::TW + pix) * C::PIXP + cb);
+        const u32x4_t v =
+            *(const u32x4_t*)(smem + C::OUT_OFF + (row * 2 * C::TW + pix) * C::PIXP + (((cb >> 3) ^ C::swz(pix)) << 3));
         const int oy = oyb + row, ox = ox0 + pix;
         const bool ok = oy < p.oh && ox < p.ow;
 #ifndef WP_NOSTORE
