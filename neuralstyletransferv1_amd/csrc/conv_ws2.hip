@@ -17,7 +17,8 @@
 //   * the next tile's halo is loaded into registers (16 B per lane and slot, coalesced 33-pixel
 //     row runs) before the current tile's MFMAs and written to LDS after them (IN + ReLU applied),
 //     so its HBM latency hides behind the compute; three barriers per tile;
-//   * output tile staged in LDS (wave slots XOR-swizzled by pixel) and stored as whole pixels,
+//   * output tile staged in LDS (8-byte slots XOR-swizzled by pixel: epilogue writes 2-way, store
+//     reads conflict-free; a 32-byte wave-slot swizzle was 4-way on the writes) and stored as whole pixels,
 //     16 B per lane; one InstanceNorm partial row per tile and row group.
 #include <algorithm>
 #include <cstring>
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(512) void ws2_kernel(ConvParams p) {
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA results -> VALU reads
     const int c0 = 16 * cg + 4 * g;
     const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
-    int obase = C::OUT_OFF + px * C::PIXB + ((cg ^ (px & (C::NCG - 1))) * 32) + g * 8;
+    int obase = C::OUT_OFF + px * C::PIXB + (((4 * cg + g) ^ (2 * (px & 7))) * 8);  // 8-B slots swizzled by pixel
     asm volatile("" : "+v"(obase));
     f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
     const bool full = wk.oy0 + TH <= p.oh && wk.ox0 + C::TW <= p.ow;
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(512) void ws2_kernel(ConvParams p) {
       const int off = (k * C::NT + t0) * 16;
       const int pp = off / C::PIXB, cb = off - pp * C::PIXB;
       const int x = pp % C::TW, oy = wk.oy0 + pp / C::TW, ox = wk.ox0 + x;
-      const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * C::PIXB + (((cb >> 5) ^ (x & (C::NCG - 1))) * 32) + (cb & 31));
+      const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * C::PIXB + (((cb >> 3) ^ (2 * (x & 7))) << 3));
       const bool ok = oy < p.oh && ox < p.ow;
       __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, 0);
     }
