@@ -59,7 +59,8 @@ struct WsCfg {
   static constexpr int DUMMY_OFF = BIAS_OFF + CINP * 4;      // sink of the lanes without an item
   static constexpr int STG_OFF = DUMMY_OFF + 64 * 16;
   // output tile staged in LDS (when it fits: not the ReLU(IN(r)) join) for whole-pixel 16-B
-  // stores: [row][px][256 B], wave w's 32-byte slot at (w ^ (px & 7)) (bank spread of the writes)
+  // stores: [row][px][256 B], 8-byte slot s (wave w, lane group g: s = 4w + g) at s ^ 2 (px & 7): the
+  // epilogue's ds_write_b64 2-way bank-conflicted (the former 32-byte wave-slot swizzle: 4-way)
   static constexpr int OUT_OFF = STG_OFF + NSLOT * SLOTB;
   static constexpr int OUTB = TH * TW * 256;
   static constexpr bool OST = OUT_OFF + OUTB <= 160 * 1024;
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const uint32_t off0 = (uint32_t)(((wk.ty0 * p.ow + ox) * p.cout_stride + c0) * 2);
     f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};  // packed-math statistics
     // lane-derived LDS addresses recomputed per tile (opaque), not held across the K loop
-    int obase = C::OUT_OFF + px * 256 + ((wv ^ (px & 7)) * 32) + g * 8;
+    int obase = C::OUT_OFF + px * 256 + (((4 * wv + g) ^ (2 * (px & 7))) * 8);
     asm volatile("" : "+v"(obase));
     auto rows = [&](auto all_valid) {
 #pragma unroll
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         const int off = (k * C::NT + t0) * 16;
         const int pp = off >> 8, cb = off & 255;
         const int x = pp & (C::TW - 1), oy = wk.ty0 + pp / C::TW, ox = wk.tx0 + x;
-        const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * 256 + (((cb >> 5) ^ (x & 7)) * 32) + (cb & 31));
+        const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * 256 + (((cb >> 3) ^ (2 * (x & 7))) << 3));
         const bool ok = oy < p.oh && ox < p.ow;
 #ifndef WS_NOSTORE
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * 256 + cb) : 0x80000000u, 0, 0);
