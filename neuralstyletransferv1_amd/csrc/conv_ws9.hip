@@ -39,6 +39,10 @@
 #define NST_WS9_NW 4  // waves per workgroup: 4 = two workgroups per CU drifting out of phase
 #endif
 
+#ifndef W9_K8PAIR
+#define W9_K8PAIR 0  // 1: kernel column 8 as 16x16x32 over kernel-row pairs (11 instead of 12 MFMAs per row and
+                     // M tile, but twice the column-8 LDS reads: measured 2 % slower)
+#endif
 #ifndef W9_RING
 #define W9_RING 2  // input-row operands in flight ahead of the MFMAs
 #endif
@@ -64,8 +68,13 @@ struct W9Cfg {
   static constexpr int BIAS_OFF = PART_OFF + NW * 64 * 4;
   static constexpr int LDS = BIAS_OFF + COUT * 4;
   static constexpr int NWM = 9 * 2;                 // 16x16x32 weight fragments (ky, m)
+#if W9_K8PAIR
+  static constexpr int NWK = 2 * 2;                 // column-8 16x16x32 weight fragments (j, m)
+  static constexpr int WBYTES = NWM * 64 * 16 + NWK * 64 * 16;
+#else
   static constexpr int NWK = 3 * 2;                 // 16x16x16 weight fragments (j, m)
   static constexpr int WBYTES = NWM * 64 * 16 + NWK * 64 * 8;
+#endif
   static_assert(NCHK % 64 == 0, "whole-wave DMA requests");
   static_assert(2 * RCH >= TW + 8 && (RS / 4) % 64 == 32, "halo row");
   static_assert(NST * NT * 16 == OUTB, "whole 16-B stores per thread");
@@ -102,12 +111,20 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
 
   // ---- the whole weight tensor, resident for the launch (same in every wave) ----
   uint4 wm[C::NWM];
+#if W9_K8PAIR
+  uint4 wk[C::NWK];
+#else
   uint2 wk[C::NWK];
+#endif
   {
     const uint4* src = (const uint4*)p.wpk + lane;
 #pragma unroll
     for (int s = 0; s < C::NWM; ++s) wm[s] = src[s * 64];
+#if W9_K8PAIR
+    const uint4* srck = (const uint4*)((const char*)p.wpk + C::NWM * 64 * 16) + lane;
+#else
     const uint2* srck = (const uint2*)((const char*)p.wpk + C::NWM * 64 * 16) + lane;
+#endif
 #pragma unroll
     for (int s = 0; s < C::NWK; ++s) wk[s] = srck[s * 64];
   }
@@ -143,10 +160,12 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, bop),
                                                 first ? z : c, 0, 0, 0);
   };
+#if !W9_K8PAIR
   auto mfma16 = [&](f32x4_t& c, const uint2& a, const uint2& bop) {
     c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4_t, a), __builtin_bit_cast(s16x4_t, bop), c,
                                                   0, 0, 0);
   };
+#endif
   // ---- K loop over the wave's 16 halo rows ----
   auto kloop = [&](Acc& acc, int buf) {
     int fb = buf * C::HALO + (16 * wv + px + 2 * g) * 8;  // row-r operand: + r * RS
@@ -154,14 +173,27 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
     asm volatile("" : "+v"(fb), "+v"(kb));
     auto fread = [&](int r) { return *(const uint4*)(smem + fb + r * C::RS); };
     // rows past the halo only meet zero weights (kernel rows 9..11): read row HR - 1 instead
+#if W9_K8PAIR
+    // column-8 operand P(s): lane group g = kernel rows 2g, 2g + 1 (input rows s + 2g, s + 2g + 1);
+    // rows past the halo only meet zero weights (P(s) for s >= 8 serves kernel row 8 = lane group 0)
+    typedef uint4 KOp;
+    auto kread = [&](int r) {
+      const int r0 = (r + 7 < C::HR) ? (r + 2 * g) * C::RS : min(r + 2 * g, C::HR - 1) * C::RS;
+      const int r1 = (r + 7 < C::HR) ? (r + 2 * g + 1) * C::RS : min(r + 2 * g + 1, C::HR - 1) * C::RS;
+      const uint2 a = *(const uint2*)(smem + kb + r0), b2 = *(const uint2*)(smem + kb + r1);
+      return make_uint4(a.x, a.y, b2.x, b2.y);
+    };
+#else
+    typedef uint2 KOp;
     auto kread = [&](int r) {
       const int kr = (r + 3 < C::HR) ? (r + g) * C::RS : min(r + g, C::HR - 1) * C::RS;
       return *(const uint2*)(smem + kb + kr);
     };
+#endif
     // operands of row r + D are read while row r's MFMAs issue (register ring, explicit order)
     constexpr int D = W9_RING;
     uint4 fr[D];
-    uint2 kf[D];
+    KOp kf[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       fr[i] = fread(i);
@@ -170,7 +202,7 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
 #pragma unroll
     for (int r = 0; r < C::HR; ++r) {
       const uint4 f = fr[r % D];
-      const uint2 k8 = kf[r % D];
+      const KOp k8 = kf[r % D];
       if (r + D < C::HR) {
         fr[r % D] = fread(r + D);
         kf[r % D] = kread(r + D);
@@ -182,6 +214,17 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
         mfma32(acc[y][0], wm[2 * ky + 0], f, ky == 0);
         mfma32(acc[y][1], wm[2 * ky + 1], f, ky == 0);
       }
+#if W9_K8PAIR
+      // P(r) serves output row r (kernel rows 0..7, j = 0) and output row r - 8 (kernel row 8, j = 1)
+      if (r < C::TH) {
+        mfma32(acc[r][0], wk[0], k8, false);
+        mfma32(acc[r][1], wk[1], k8, false);
+      }
+      if (r >= 8 && r - 8 < C::TH) {
+        mfma32(acc[r - 8][0], wk[2], k8, false);
+        mfma32(acc[r - 8][1], wk[3], k8, false);
+      }
+#else
 #pragma unroll
       for (int y = 0; y < C::TH; ++y) {
         const int d = r - y;
@@ -189,6 +232,7 @@ __global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
         mfma16(acc[y][0], wk[2 * (d >> 2) + 0], k8);
         mfma16(acc[y][1], wk[2 * (d >> 2) + 1], k8);
       }
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -355,6 +399,7 @@ struct Ws9Inst {
     k.wbytes = C::WBYTES;
     k.persistent = 1;
     k.part_rows = 1;
+    k.korder = W9_K8PAIR;  // column-8 packing (pack_ws9_weights)
     k.launch = &launch;
     return k;
   }

@@ -396,10 +396,13 @@ std::vector<float> pack_ws2_weights(const ConvKernelInfo& k, const LayerDef& d, 
 
 // MODE_WS9 weight registers (conv_ws9.hip), the same in every wave.  Kernel columns 0..7: 18
 // 16x16x32 fragments [ky][m][lane][8 bf16], lane l = output channel 16 m + (l & 15), K element
-// i = tap kx = 2 (l >> 4) + (i >> 2), input channel i & 3.  Column 8: 6 16x16x16 fragments
-// [j][m][lane][4 bf16], kernel row 4 j + (l >> 4) (zero past row 8), input channel i.
-std::vector<float> pack_ws9_weights(const LayerDef& d, const float* W) {
-  std::vector<float> out((size_t)18 * 64 * 8 + 6 * 64 * 4, 0.f);
+// i = tap kx = 2 (l >> 4) + (i >> 2), input channel i & 3.  Column 8 (k.korder == 1): 4 16x16x32
+// fragments [j][m][lane][8 bf16], j = 0: kernel row 2 (l >> 4) + (i >> 2); j = 1: kernel row 8 in
+// lane group 0, elements 0..3 only; input channel i & 3.  (k.korder == 0: 6 16x16x16 fragments
+// [j][m][lane][4 bf16], kernel row 4 j + (l >> 4), input channel i.)
+std::vector<float> pack_ws9_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
+  const bool pair = k.korder == 1;
+  std::vector<float> out((size_t)18 * 64 * 8 + (pair ? 4 * 64 * 8 : 6 * 64 * 4), 0.f);
   auto w = [&](int co, int ci, int ky, int kx) -> float {
     return (co < d.cout && ci < d.cin && ky < 9) ? W[(((size_t)co * d.cin + ci) * 9 + ky) * 9 + kx] : 0.f;
   };
@@ -409,10 +412,20 @@ std::vector<float> pack_ws9_weights(const LayerDef& d, const float* W) {
         for (int i = 0; i < 8; ++i)
           out[(((size_t)ky * 2 + m) * 64 + l) * 8 + i] = w(16 * m + (l & 15), i & 3, ky, 2 * (l >> 4) + (i >> 2));
   float* k8 = out.data() + (size_t)18 * 64 * 8;
-  for (int j = 0; j < 3; ++j)
+  if (pair) {
     for (int m = 0; m < 2; ++m)
       for (int l = 0; l < 64; ++l)
-        for (int i = 0; i < 4; ++i) k8[(((size_t)j * 2 + m) * 64 + l) * 4 + i] = w(16 * m + (l & 15), i, 4 * j + (l >> 4), 8);
+        for (int i = 0; i < 8; ++i) {
+          const int co = 16 * m + (l & 15);
+          k8[(((size_t)0 * 2 + m) * 64 + l) * 8 + i] = w(co, i & 3, 2 * (l >> 4) + (i >> 2), 8);
+          k8[(((size_t)1 * 2 + m) * 64 + l) * 8 + i] = ((l >> 4) == 0 && i < 4) ? w(co, i & 3, 8, 8) : 0.f;
+        }
+  } else {
+    for (int j = 0; j < 3; ++j)
+      for (int m = 0; m < 2; ++m)
+        for (int l = 0; l < 64; ++l)
+          for (int i = 0; i < 4; ++i) k8[(((size_t)j * 2 + m) * 64 + l) * 4 + i] = w(16 * m + (l & 15), i, 4 * j + (l >> 4), 8);
+  }
   return out;
 }
 
@@ -729,7 +742,7 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     } else if (Ly.mode == MODE_WS2) {
       if ((rc = upload_packed(pack_ws2_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if (Ly.mode == MODE_WS9) {
-      if ((rc = upload_packed(pack_ws9_weights(d, W), &Ly.wpk)) != NST_OK) break;
+      if ((rc = upload_packed(pack_ws9_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) {
       break;
     }
