@@ -35,6 +35,15 @@
 
 #include "conv_ws_common.h"
 
+#ifndef NST_WS9_TH
+#define NST_WS9_TH 8  // output rows per tile (each wave's rows)
+#endif
+#ifndef WS9_DIRECT  // half-pixel stores straight from the accumulators instead (~3 % slower)
+#define WS9_STAGED
+#endif
+#ifndef NST_WS9_OCC
+#define NST_WS9_OCC 2  // waves per SIMD the register allocation must allow (two 4-wave workgroups per CU)
+#endif
 #ifndef NST_WS9_NW
 #define NST_WS9_NW 4  // waves per workgroup: 4 = two workgroups per CU drifting out of phase
 #endif
@@ -51,7 +60,7 @@ namespace nst {
 
 template <int NW_>
 struct W9Cfg {
-  static constexpr int NW = NW_, NT = 64 * NW, TH = 8, TW = 16 * NW, COUT = 32;
+  static constexpr int NW = NW_, NT = 64 * NW, TH = NST_WS9_TH, TW = 16 * NW, COUT = 32;
   static constexpr int HR = TH + 8;                 // halo rows
   // 16-B chunks per halo row: TW + 8 px used, rounded up so the row stride is == 32 mod 64 dwords
   // (the column-8 operand's four rows land in disjoint bank halves)
@@ -62,8 +71,12 @@ struct W9Cfg {
   static constexpr int NREQ = (NCHK + NT - 1) / NT; // request slots per thread (the last partial)
   static constexpr int PIXB = COUT * 2;             // 64 B per output pixel
   static constexpr int OUT_OFF = 2 * HALO;
-  static constexpr int OUTB = TH * TW * PIXB;
-  static constexpr int NST = OUTB / (NT * 16);      // 16-B stores per thread
+#ifdef WS9_STAGED
+  static constexpr int OUTB = TH * TW * PIXB;       // the LDS output tile
+#else
+  static constexpr int OUTB = 0;
+#endif
+  static constexpr int NST = TH * TW * PIXB / (NT * 16);  // 16-B stores per thread
   static constexpr int PART_OFF = OUT_OFF + OUTB;
   static constexpr int BIAS_OFF = PART_OFF + NW * 64 * 4;
   static constexpr int LDS = BIAS_OFF + COUT * 4;
@@ -77,14 +90,14 @@ struct W9Cfg {
 #endif
   static_assert(NCHK % 64 == 0, "whole-wave DMA requests");
   static_assert(2 * RCH >= TW + 8 && (RS / 4) % 64 == 32, "halo row");
-  static_assert(NST * NT * 16 == OUTB, "whole 16-B stores per thread");
+  static_assert(NST * NT * 16 == TH * TW * PIXB, "whole 16-B stores per thread");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void ws9_kernel(ConvParams p) {
+__global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p) {
   using C = W9Cfg<NW>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
