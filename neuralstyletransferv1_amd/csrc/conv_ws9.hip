@@ -18,17 +18,16 @@
 //   * workgroup = NW waves (4), tile = 8 output rows x 16 NW columns, wave w = 8 rows x columns
 //     16w..16w+15 and all 32 output channels (two M tiles): 16 input-row operands + 16 column-8
 //     operands feed 192 MFMAs per wave and tile;
-//   * persistent over (frame, tile) items, XCD-aware order, two 4-wave workgroups per CU: their
-//     barriers are independent, so one's epilogue and stores overlap the other's MFMAs (one 8-wave
-//     workgroup per CU idled the MFMA pipe through every epilogue: 0.46 ms vs ~0.16 ms of MFMA);
+//   * persistent over (frame, tile) items, XCD-aware order, two 4-wave workgroups per CU (register
+//     allocation bounded to two waves per SIMD): their barriers are independent, so one's epilogue
+//     and stores overlap the other's MFMAs.  Unbounded, hipcc spilled the accumulators to AGPRs at
+//     one wave per SIMD and only one workgroup per CU was resident (0.465 vs 0.367 ms);
 //   * the next item's 16-row halo (RCH 16-byte chunks per row, contiguous in the padded frame)
 //     travels by LDS-DMA into the second of two halo buffers while the current item computes;
-//   * bf16 outputs stored straight from the accumulators as half pixels (8 B per lane, 32 B runs);
-//     staging the tile in LDS for whole-pixel stores (WS9_STAGED) measured ~1 % slower here;
+//   * output tile staged in LDS (8-byte slots XOR-swizzled by pixel) and stored as whole 64-byte
+//     pixels, 16 B per lane (WS9_DIRECT: half-pixel stores from the accumulators, ~3 % slower);
 //     per-wave IN partials (DPP reduce-scatter) combined in fixed order into one partial row per
-//     tile.  Measured (bench, 8 x 1080p): 0.42-0.46 ms by box vs 0.51 for the generic kernel;
-//     MFMA pipe ~44 % busy (PMC), and removing the MFMAs leaves 0.25 ms of fill / epilogue time
-//     that the two workgroups per CU do not hide behind each other's MFMAs.
+//     tile.  Measured (bench, 8 x 1080p): 0.367 ms vs 0.51 for the generic kernel.
 #include <algorithm>
 #include <cstring>
 #include <type_traits>
