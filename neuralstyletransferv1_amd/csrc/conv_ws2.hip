@@ -9,7 +9,9 @@
 // (147 KB per tile for conv3, ~2.4 GB of L2 traffic per launch); here each wave keeps its 16
 // output channels' 3x3xCIN weights in registers for the launch (72 VGPRs for conv3, 36 for conv2):
 //   * workgroup = 8 waves; wave w: channel group w % (COUT/16), output row group w / (COUT/16);
-//   * persistent over (frame, TH x 16 output tiles), XCD-aware tile order; one workgroup per CU;
+//   * persistent over (frame, TH x 16 output tiles), XCD-aware tile order; conv2 (8-row tiles, 126
+//     VGPRs, 72 KB LDS) runs two workgroups per CU, so one's fill / epilogue / stores overlap the
+//     other's MFMAs and loads (16-row tiles at one per CU: 0.447 vs 0.393 ms); conv3 one per CU;
 //   * the input halo (2TH+1) x 33 in LDS in column-polyphase order ([row][x & 1][x >> 1], entry
 //     stride 2 x odd chunks), so lane px of x-tap dx reads entry px + (dx >> 1) of phase dx & 1 —
 //     consecutive entries, conflict-free ds_read_b128; input row y is the B operand of output rows
@@ -61,8 +63,10 @@ struct W2Cfg {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int CINP, int COUT, int TH, bool ZPAD>
-__global__ __launch_bounds__(512) void ws2_kernel(ConvParams p) {
+// OCC = waves per SIMD the register allocation must allow: 4 = two workgroups per CU (conv2's
+// 8-row tiles fit 126 VGPRs and 72 KB of LDS), 2 = one
+template <int CINP, int COUT, int TH, bool ZPAD, int OCC>
+__global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
   using C = W2Cfg<CINP, COUT, TH>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -251,7 +255,7 @@ __global__ __launch_bounds__(512) void ws2_kernel(ConvParams p) {
   }
 }
 
-template <int CINP, int COUT, int TH>
+template <int CINP, int COUT, int TH, int OCC>
 struct Ws2Inst {
   using C = W2Cfg<CINP, COUT, TH>;
   static int cus() {
@@ -267,11 +271,11 @@ struct Ws2Inst {
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
     ConvParams p = p0;
     p.n_work = (int)grid.x * (int)grid.y;
-    const int nb = std::min(p.n_work, cus());  // one workgroup per CU (LDS)
+    const int nb = std::min(p.n_work, cus() * (OCC / 2));  // workgroups resident per CU
     if (p.axis_mode == AX_ZERO || p.axis_mode == AX_ZERO_PREREFLECT)
-      hipLaunchKernelGGL((ws2_kernel<CINP, COUT, TH, true>), dim3(nb), dim3(C::NT), 0, st, p);
+      hipLaunchKernelGGL((ws2_kernel<CINP, COUT, TH, true, OCC>), dim3(nb), dim3(C::NT), 0, st, p);
     else
-      hipLaunchKernelGGL((ws2_kernel<CINP, COUT, TH, false>), dim3(nb), dim3(C::NT), 0, st, p);
+      hipLaunchKernelGGL((ws2_kernel<CINP, COUT, TH, false, OCC>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
@@ -290,7 +294,7 @@ struct Ws2Inst {
 };
 
 #ifndef NST_W2_C2_TH
-#define NST_W2_C2_TH 16
+#define NST_W2_C2_TH 8  // 8 rows: two workgroups per CU (16 rows, one per CU: 0.447 vs 0.393 ms)
 #endif
 #ifndef NST_W2_C3_TH
 #define NST_W2_C3_TH 8
@@ -298,9 +302,9 @@ struct Ws2Inst {
 #define E(...) Ws2Inst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_ws2(int* count) {
   static const ConvKernelInfo table[] = {
-      //  CINP COUT TH
-      E(32, 64, NST_W2_C2_TH),   // conv2 / down2
-      E(64, 128, NST_W2_C3_TH),  // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
+      //  CINP COUT TH OCC
+      E(32, 64, NST_W2_C2_TH, NST_W2_C2_TH <= 8 ? 4 : 2),  // conv2 / down2
+      E(64, 128, NST_W2_C3_TH, 2),  // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;
