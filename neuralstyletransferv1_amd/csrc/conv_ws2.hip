@@ -304,7 +304,7 @@ const ConvKernelInfo* conv_table_ws2(int* count) {
   static const ConvKernelInfo table[] = {
       //  CINP COUT TH OCC
       E(32, 64, NST_W2_C2_TH, NST_W2_C2_TH <= 8 ? 4 : 2),  // conv2 / down2
-      E(64, 128, NST_W2_C3_TH, 2),  // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
+      E(64, 128, NST_W2_C3_TH, NST_W2_C3_TH <= 4 ? 4 : 2),  // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;
