@@ -33,9 +33,10 @@ __global__ __launch_bounds__(256) void prepad_encode_f32_kernel(ConvParams p, in
 
 // uint8 frames: the encoded bf16 value of a channel depends only on its byte, so each block first
 // tabulates the 3 x 256 values with the exact per-element formula (768 evaluations, amortised
-// over the block's 1024 pixels), then every pixel is 3 byte loads + 3 LDS lookups; 4 consecutive
-// output pixels per thread (32-byte contiguous stores).
+// over the block's 8 rows x 1024 pixels), then every pixel is 3 bytes (3 dword loads per 4 interior
+// pixels) + 3 LDS lookups; 4 consecutive output pixels per thread (32-byte contiguous stores).
 constexpr int PREP_PX = 4;
+constexpr int PREP_ROWS = 8;  // padded rows per block: the 768-entry table is built once per 8 rows
 __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int hp, int wp, uint4* __restrict__ out) {
   __shared__ uint16_t lut[3][256];
   for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
@@ -46,37 +47,57 @@ __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int
   }
   __syncthreads();
   const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * PREP_PX;
-  const int y = blockIdx.y, n = blockIdx.z;
+  const int n = blockIdx.z;
   if (x0 >= wp) return;
-  const int sy = map_axis(y - p.pad, p.hs, p.axis_mode, p.pre);
-  const uint8_t* row = (const uint8_t*)p.in + ((size_t)n * p.hs + (sy < 0 ? 0 : sy)) * p.ws * 3;
-  uint32_t w[2 * PREP_PX];
+  // the 4 source columns of this thread (same for every row): consecutive and dword-aligned in the
+  // interior, so the 12 bytes come as 3 dword loads; reflected / padded edges take byte loads
+  int sxs[PREP_PX];
 #pragma unroll
-  for (int j = 0; j < PREP_PX; ++j) {
-    const int sx = map_axis(x0 + j - p.pad, p.ws, p.axis_mode, p.pre);
-    uint32_t lo = 0u, hi = 0u;
-    if (sy >= 0 && sx >= 0 && x0 + j < wp) {
-      const uint8_t* px = row + (size_t)sx * 3;
-      lo = (uint32_t)lut[0][px[p.enc_perm[0]]] | ((uint32_t)lut[1][px[p.enc_perm[1]]] << 16);
-      hi = (uint32_t)lut[2][px[p.enc_perm[2]]] | ((uint32_t)pack_bf16(0.f, 0.f) & 0xffff0000u);
+  for (int j = 0; j < PREP_PX; ++j) sxs[j] = x0 + j < wp ? map_axis(x0 + j - p.pad, p.ws, p.axis_mode, p.pre) : -1;
+  const bool run = sxs[0] >= 0 && sxs[PREP_PX - 1] == sxs[0] + PREP_PX - 1;
+  const int pr0 = p.enc_perm[0], pr1 = p.enc_perm[1], pr2 = p.enc_perm[2];
+  for (int y = blockIdx.y * PREP_ROWS; y < min(hp, (int)(blockIdx.y + 1) * PREP_ROWS); ++y) {
+    const int sy = map_axis(y - p.pad, p.hs, p.axis_mode, p.pre);
+    const uint8_t* row = (const uint8_t*)p.in + ((size_t)n * p.hs + (sy < 0 ? 0 : sy)) * p.ws * 3;
+    uint32_t w[2 * PREP_PX];
+    if (run && sy >= 0 && (((uintptr_t)row + (size_t)sxs[0] * 3) & 3) == 0) {
+      const uint32_t* d = (const uint32_t*)(row + (size_t)sxs[0] * 3);
+      const uint32_t dw[3] = {d[0], d[1], d[2]};
+      auto byte = [&](int k) { return (dw[k >> 2] >> (8 * (k & 3))) & 255u; };
+#pragma unroll
+      for (int j = 0; j < PREP_PX; ++j) {
+        w[2 * j] = (uint32_t)lut[0][byte(3 * j + pr0)] | ((uint32_t)lut[1][byte(3 * j + pr1)] << 16);
+        w[2 * j + 1] = (uint32_t)lut[2][byte(3 * j + pr2)] | ((uint32_t)pack_bf16(0.f, 0.f) & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < PREP_PX; ++j) {
+        uint32_t lo = 0u, hi = 0u;
+        if (sy >= 0 && sxs[j] >= 0) {
+          const uint8_t* px = row + (size_t)sxs[j] * 3;
+          lo = (uint32_t)lut[0][px[pr0]] | ((uint32_t)lut[1][px[pr1]] << 16);
+          hi = (uint32_t)lut[2][px[pr2]] | ((uint32_t)pack_bf16(0.f, 0.f) & 0xffff0000u);
+        }
+        w[2 * j] = lo;
+        w[2 * j + 1] = hi;
+      }
     }
-    w[2 * j] = lo;
-    w[2 * j + 1] = hi;
-  }
-  uint2* o = (uint2*)out + ((size_t)n * hp + y) * wp + x0;
-  if (x0 + PREP_PX <= wp && ((((size_t)n * hp + y) * wp + x0) & 1) == 0) {
-    ((uint4*)o)[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    ((uint4*)o)[1] = make_uint4(w[4], w[5], w[6], w[7]);
-  } else {
+    uint2* o = (uint2*)out + ((size_t)n * hp + y) * wp + x0;
+    if (x0 + PREP_PX <= wp && ((((size_t)n * hp + y) * wp + x0) & 1) == 0) {
+      ((uint4*)o)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      ((uint4*)o)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    } else {
 #pragma unroll
-    for (int j = 0; j < PREP_PX; ++j)
-      if (x0 + j < wp) o[j] = make_uint2(w[2 * j], w[2 * j + 1]);
+      for (int j = 0; j < PREP_PX; ++j)
+        if (x0 + j < wp) o[j] = make_uint2(w[2 * j], w[2 * j + 1]);
+    }
   }
 }
 
 hipError_t launch_prepad_encode(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st) {
   if (in_kind == IN_U8_NHWC) {
-    const dim3 grid((unsigned)((wp + 256 * PREP_PX - 1) / (256 * PREP_PX)), (unsigned)hp, (unsigned)n);
+    const dim3 grid((unsigned)((wp + 256 * PREP_PX - 1) / (256 * PREP_PX)), (unsigned)((hp + PREP_ROWS - 1) / PREP_ROWS),
+                    (unsigned)n);
     hipLaunchKernelGGL(prepad_encode_u8_kernel, grid, dim3(256), 0, st, p, hp, wp, (uint4*)out);
   } else {
     const dim3 grid((unsigned)((wp + 255) / 256), (unsigned)hp, (unsigned)n);
