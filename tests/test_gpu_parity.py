@@ -304,7 +304,8 @@ def test_weight_stationary_downconv_vs_generic(arch, h, w, monkeypatch):
 
 
 @pytest.mark.parametrize("arch,h,w", [
-    ("johnson", 70, 90),      # ragged 8x128 tiles in both directions, reflection padding
+    ("johnson", 70, 90),      # ragged 8x64 tiles in both directions, reflection padding
+    ("johnson", 33, 47),      # frame smaller than one tile's halo in x, 5 ragged tile rows
     ("nst", 72, 100),         # pre-reflect 40 + zero padding resolved by the pre-pass (152x180 conv)
     ("johnson", 1080, 1920),  # the bench shape, one frame
 ])
