@@ -80,6 +80,25 @@ const char* nst_version(void);
  */
 int nst_create(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                nst_handle** out);
+
+/*
+ * nst_create with kernel-selection flags (0 = the default, fastest mapping for every layer).  Each
+ * NST_KSEL_NO_* bit removes one specialised bf16 kernel family so the layer falls back to the
+ * generic implicit-GEMM mapping; the tests use this to check the specialised kernels against the
+ * generic ones on the same model.  NST_KSEL_UNFUSED_RESIDUAL runs the residual add as its own
+ * kernel instead of fusing it into the next conv's fill.  Unknown bits -> NST_E_INVALID.
+ */
+#define NST_KSEL_NO_WSTAT 0x1             /* residual-trunk weight-stationary conv (conv_wstat.hip) */
+#define NST_KSEL_NO_WPHASE 0x2            /* x2 up-conv phase kernel (conv_wphase.hip) */
+#define NST_KSEL_NO_WS2 0x4               /* stride-2 down-conv kernel (conv_ws2.hip) */
+#define NST_KSEL_NO_WS9 0x8               /* 9x9 first-layer kernel (conv_ws9.hip) */
+#define NST_KSEL_NO_KYROT 0x10            /* 9x9 output-conv row-streaming kernel (conv_out9.hip) */
+#define NST_KSEL_NO_PREPAD 0x20           /* first layer over the pre-padded encoded frame (conv_prep.hip) */
+#define NST_KSEL_NO_PERSISTENT 0x40       /* generic persistent LDS-weight-ring kernels */
+#define NST_KSEL_UNFUSED_RESIDUAL 0x80    /* residual add as a separate kernel */
+#define NST_KSEL_ALL 0xff
+int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
+                  unsigned flags, nst_handle** out);
 void nst_destroy(nst_handle* h);
 
 /* Output spatial size the architecture produces for an h x w input
@@ -99,6 +118,42 @@ int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* 
  */
 int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset,
                 void* y, int y_fmt, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Per-layer inspection (parity tests): the handle runs its architecture as a program of ops, each a
+ * conv (with the producer's InstanceNorm + ReLU, or the residual join, applied in its fill) or a
+ * separate residual add.  nst_op_describe gives op i's wiring and geometry for an n x h x w batch;
+ * nst_forward_capture is nst_forward that also copies, after each op i, the activation it wrote
+ * (act[i]: [n][out_h][out_w][cout_stride] in the compute dtype, the raw conv output before its
+ * InstanceNorm), the joined residual stream it wrote (res[i]: [n][in_h][in_w][cin_stride]) and its
+ * layer's InstanceNorm {scale, shift} pairs (stats[i]: [n][cout_stride] float2) into caller-owned
+ * device buffers; NULL arrays or NULL entries skip a copy.  The final op writes y and captures nothing.
+ * Replaces inspecting intermediate tensors of the reference's module graph (transformer_net.py:29-41).
+ */
+#define NST_BUF_INPUT (-1)  /* nst_op_desc src: the input frames / tensor */
+#define NST_BUF_OUTPUT (-2) /* nst_op_desc dst: y */
+typedef struct nst_op_desc {
+  int kind;         /* 0 conv, 1 residual add (out = IN_in_norm(src) + r) */
+  int layer;        /* conv layer index (nst_layer_name); for a residual add the layer whose IN applies */
+  int src, dst;     /* activation buffer ids (0..6) or NST_BUF_INPUT / NST_BUF_OUTPUT */
+  int in_norm;      /* layer whose InstanceNorm the fill applies to src, -1 = none */
+  int in_relu;      /* ReLU after that InstanceNorm */
+  int res_buf;      /* residual stream r joined in (-1 none): operand = IN(src) + r' */
+  int res_norm;     /* r' = ReLU(IN_res_norm(r)) if >= 0, else r */
+  int res_out;      /* buffer that receives the joined stream (-1 none) */
+  int relu_out;     /* ReLU after the join (ReCoNet ResLayer) */
+  int in_h, in_w;   /* source extent */
+  int conv_h, conv_w; /* conv output extent (before the NST centre crop) */
+  int out_h, out_w; /* stored output extent */
+  int cin_stride, cout_stride;
+  int kernel_mode;  /* internal kernel family (0 generic, 1 phase, 2 x-shift, 3 out9, 4 wstat, 5 wphase, 6 ws2, 7 ws9) */
+  int elem_bytes;   /* 2 (bf16) or 4 (fp32) */
+} nst_op_desc;
+int nst_num_ops(const nst_handle* h);
+int nst_op_describe(const nst_handle* h, int n, int in_h, int in_w, int op, nst_op_desc* out);
+int nst_forward_capture(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset,
+                        void* y, int y_fmt, void* workspace, size_t workspace_bytes, void* const* act,
+                        void* const* res, void* const* stats, void* stream);
 
 /*
  * Decode a raw model output (f32 NCHW [n,3,h,w]) with `preset` + clamp(0,1), resize

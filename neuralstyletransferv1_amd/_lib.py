@@ -34,12 +34,29 @@ EXPORTED_SYMBOLS = (
     "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8", "nst_lab_create",
     "nst_lab_destroy", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
     "nst_profile_end", "nst_num_layers", "nst_layer_name", "nst_blend_models_u8", "nst_blend_models_lab_u8",
-    "nst_mask_feather",
+    "nst_mask_feather", "nst_create_ex", "nst_num_ops", "nst_op_describe", "nst_forward_capture",
 )
+
+# nst_create_ex kernel-selection flags (include/nst_hip.h NST_KSEL_*)
+KSEL = {
+    "no_wstat": 0x1, "no_wphase": 0x2, "no_ws2": 0x4, "no_ws9": 0x8, "no_kyrot": 0x10, "no_prepad": 0x20,
+    "no_persistent": 0x40, "unfused_residual": 0x80,
+}
+NST_BUF_INPUT, NST_BUF_OUTPUT = -1, -2
 
 
 class NstParam(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.POINTER(ctypes.c_float)), ("numel", ctypes.c_int64)]
+
+
+class NstOpDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "kind", "layer", "src", "dst", "in_norm", "in_relu", "res_buf", "res_norm", "res_out", "relu_out",
+        "in_h", "in_w", "conv_h", "conv_w", "out_h", "out_w", "cin_stride", "cout_stride", "kernel_mode",
+        "elem_bytes")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 
 _lib = None
@@ -66,6 +83,12 @@ def lib() -> ctypes.CDLL:
         L.nst_last_error.restype = ctypes.c_char_p
         L.nst_version.restype = ctypes.c_char_p
         L.nst_create.argtypes = [i, ctypes.POINTER(NstParam), i, i, i, ctypes.POINTER(vp)]
+        L.nst_create_ex.argtypes = [i, ctypes.POINTER(NstParam), i, i, i, ctypes.c_uint, ctypes.POINTER(vp)]
+        L.nst_num_ops.argtypes = [vp]
+        L.nst_num_ops.restype = i
+        L.nst_op_describe.argtypes = [vp, i, i, i, i, ctypes.POINTER(NstOpDesc)]
+        L.nst_forward_capture.argtypes = [vp, vp, i, i, i, i, i, vp, i, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                          ctypes.POINTER(vp), vp]
         L.nst_destroy.argtypes = [vp]
         L.nst_destroy.restype = None
         L.nst_output_hw.argtypes = [vp, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
@@ -89,7 +112,7 @@ def lib() -> ctypes.CDLL:
         L.nst_num_layers.restype = i
         L.nst_layer_name.argtypes = [vp, i]
         L.nst_layer_name.restype = ctypes.c_char_p
-        for name in ("nst_create", "nst_output_hw", "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8",
+        for name in ("nst_create", "nst_create_ex", "nst_op_describe", "nst_forward_capture", "nst_output_hw", "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8",
                      "nst_lab_create", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
                      "nst_profile_end"):
             getattr(L, name).restype = i

@@ -3,21 +3,12 @@
 #include "conv_impl.h"
 
 // Tile shapes (TH, TW, WM, WN) of the Johnson/NST layers; overridable at build time for tile sweeps
-#ifndef NST_C1_TILE
+// tile shapes (TH, TW, WM, WN) of the generic instantiations
 #define NST_C1_TILE 8, 32, 4, 1
-#endif
-#ifndef NST_C2_TILE
 #define NST_C2_TILE 4, 16, 2, 2
-#endif
-#ifndef NST_C3_TILE
 #define NST_C3_TILE 4, 16, 2, 2
-#endif
-#ifndef NST_D1_TILE
 #define NST_D1_TILE 4, 16, 1, 4
-#endif
-#ifndef NST_D2_TILE
 #define NST_D2_TILE 4, 16, 1, 4
-#endif
 
 namespace nst {
 typedef __bf16 B;

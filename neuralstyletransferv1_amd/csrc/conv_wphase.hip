@@ -21,11 +21,9 @@
 
 #include "conv_ws_common.h"
 
-#ifndef WP_RING
-#define WP_RING 3  // operand reads in flight ahead of the MFMAs
-#endif
-
 namespace nst {
+
+constexpr int WP_RING = 3;  // operand reads in flight ahead of the MFMAs
 
 template <int CINP, int COUT, int TH, int NF>
 struct WpCfg {
@@ -172,9 +170,6 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     if constexpr (RES) dma16(frame_rsrc(p.res_r, n), voff, lds + C::NW * 1024, soff);
   };
   auto consume = [&](const Work& wk, int u, const Item& it) {
-#ifdef WS_NOCONSUME  // experiment: no unit transform / halo write
-    return;
-#endif
     const int ch = 2 * u + team;
     const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
     const uint4 y = *(const uint4*)sp;
@@ -274,10 +269,6 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
 
   // ---- epilogue: bias, bf16 NHWC stores of this phase's pixels, one partial row per phase ----
   auto epilogue = [&](const Work& wk, Acc& acc) {
-#ifdef WP_NOEPI  // experiment (racy vmcnt accounting): no stores
-    asm volatile("" ::"v"(acc[0][0]));
-    return;
-#endif
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA results -> VALU reads
     const size_t obytes = (size_t)p.oh * p.ow * p.cout_stride * 2;
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
@@ -305,11 +296,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
             *(u32x2_t*)(smem + C::OUT_OFF + ((2 * r + (ph >> 1)) * 2 * C::TW + 2 * px + (ph & 1)) * C::PIXP +
                         (((c0 >> 2) ^ C::swz(2 * px + (ph & 1))) << 3)) = pk;
           } else {
-#ifndef WP_NOSTORE  // experiment (racy vmcnt accounting): no output stores
             __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, 0);
-#else
-            asm volatile("" ::"v"(pk));
-#endif
           }
           const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
           s1 += x;
@@ -320,10 +307,6 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
         rows(std::true_type{});
       else
         rows(std::false_type{});
-#ifdef WP_NOSTATS  // experiment: no InstanceNorm partials
-      asm volatile("" ::"v"(s1), "v"(s2));
-      continue;
-#endif
       const float vv[8] = {s1[0], s2[0], s1[1], s2[1], s1[2], s2[2], s1[3], s2[3]};
       float a4[4], a2[2], a1[1];
       rs_step<4, 0x140>(vv, a4, px >= 8);
@@ -348,11 +331,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
             *(const u32x4_t*)(smem + C::OUT_OFF + (row * 2 * C::TW + pix) * C::PIXP + (((cb >> 3) ^ C::swz(pix)) << 3));
         const int oy = oyb + row, ox = ox0 + pix;
         const bool ok = oy < p.oh && ox < p.ow;
-#ifndef WP_NOSTORE
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, 0);
-#else
-        asm volatile("" ::"v"(v), "v"(ok));
-#endif
       }
     }
   };
@@ -498,18 +477,14 @@ struct WphaseInst {
   }
 };
 
-#ifndef NST_WP1_TH
-#define NST_WP1_TH 4  // 128 -> 64: 8 rows spill (128 weight + 64 accumulator VGPRs); 4 leaves LDS room for the staged output tile
-#endif
-#ifndef NST_WP1_NF
-#define NST_WP1_NF 8  // frames per launch (IN tables in LDS)
-#endif
+constexpr int WP1_TH = 4;  // 128 -> 64: 8 rows spill (128 weight + 64 accumulator VGPRs); 4 leaves LDS room for the staged output tile
+constexpr int WP1_NF = 8;  // frames per launch (IN tables in LDS)
 #define E(...) WphaseInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wphase(int* count) {
   static const ConvKernelInfo table[] = {
       //  CINP COUT TH NF RES
-      E(128, 64, NST_WP1_TH, NST_WP1_NF, false),  // deconv1 / up1
-      E(128, 64, NST_WP1_TH, NST_WP1_NF, true),   // deconv1 joining the last residual block (fused join)
+      E(128, 64, WP1_TH, WP1_NF, false),  // deconv1 / up1
+      E(128, 64, WP1_TH, WP1_NF, true),   // deconv1 joining the last residual block (fused join)
       E(64, 32, 8, 16, false),                    // deconv2 / up2
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));

@@ -27,11 +27,9 @@
 
 #include "conv_ws_common.h"
 
-#ifndef W2_RING
-#define W2_RING 3  // operand reads in flight ahead of the MFMAs
-#endif
-
 namespace nst {
+
+constexpr int W2_RING = 3;  // operand reads in flight ahead of the MFMAs
 
 template <int CINP, int COUT, int TH>
 struct W2Cfg {
@@ -293,18 +291,14 @@ struct Ws2Inst {
   }
 };
 
-#ifndef NST_W2_C2_TH
-#define NST_W2_C2_TH 8  // 8 rows: two workgroups per CU (16 rows, one per CU: 0.447 vs 0.393 ms)
-#endif
-#ifndef NST_W2_C3_TH
-#define NST_W2_C3_TH 8
-#endif
+constexpr int W2_C2_TH = 8;  // 8 rows: two workgroups per CU (16 rows, one per CU: 0.447 vs 0.393 ms)
+constexpr int W2_C3_TH = 8;
 #define E(...) Ws2Inst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_ws2(int* count) {
   static const ConvKernelInfo table[] = {
       //  CINP COUT TH OCC
-      E(32, 64, NST_W2_C2_TH, NST_W2_C2_TH <= 8 ? 4 : 2),  // conv2 / down2
-      E(64, 128, NST_W2_C3_TH, NST_W2_C3_TH <= 4 ? 4 : 2),  // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
+      E(32, 64, W2_C2_TH, W2_C2_TH <= 8 ? 4 : 2),  // conv2 / down2
+      E(64, 128, W2_C3_TH, W2_C3_TH <= 4 ? 4 : 2),  // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

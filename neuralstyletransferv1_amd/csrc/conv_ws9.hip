@@ -25,7 +25,7 @@
 //   * the next item's 16-row halo (RCH 16-byte chunks per row, contiguous in the padded frame)
 //     travels by LDS-DMA into the second of two halo buffers while the current item computes;
 //   * output tile staged in LDS (8-byte slots XOR-swizzled by pixel) and stored as whole 64-byte
-//     pixels, 16 B per lane (WS9_DIRECT: half-pixel stores from the accumulators, ~3 % slower);
+//     pixels, 16 B per lane (half-pixel stores from the accumulators measured ~3 % slower);
 //     per-wave IN partials (DPP reduce-scatter) combined in fixed order into one partial row per
 //     tile.  Measured (bench, 8 x 1080p): 0.367 ms vs 0.51 for the generic kernel.
 #include <algorithm>
@@ -34,32 +34,16 @@
 
 #include "conv_ws_common.h"
 
-#ifndef NST_WS9_TH
-#define NST_WS9_TH 8  // output rows per tile (each wave's rows)
-#endif
-#ifndef WS9_DIRECT  // half-pixel stores straight from the accumulators instead (~3 % slower)
-#define WS9_STAGED
-#endif
-#ifndef NST_WS9_OCC
-#define NST_WS9_OCC 2  // waves per SIMD the register allocation must allow (two 4-wave workgroups per CU)
-#endif
-#ifndef NST_WS9_NW
-#define NST_WS9_NW 4  // waves per workgroup: 4 = two workgroups per CU drifting out of phase
-#endif
-
-#ifndef W9_K8PAIR
-#define W9_K8PAIR 0  // 1: kernel column 8 as 16x16x32 over kernel-row pairs (11 instead of 12 MFMAs per row and
-                     // M tile, but twice the column-8 LDS reads: measured 2 % slower)
-#endif
-#ifndef W9_RING
-#define W9_RING 2  // input-row operands in flight ahead of the MFMAs
-#endif
-
 namespace nst {
+
+constexpr int WS9_TH = 8;    // output rows per tile (each wave's rows)
+constexpr int WS9_OCC = 2;   // waves per SIMD the register allocation must allow (two 4-wave workgroups per CU)
+constexpr int WS9_NW = 4;    // waves per workgroup: 4 = two workgroups per CU drifting out of phase
+constexpr int WS9_RING = 2;  // input-row operands in flight ahead of the MFMAs
 
 template <int NW_>
 struct W9Cfg {
-  static constexpr int NW = NW_, NT = 64 * NW, TH = NST_WS9_TH, TW = 16 * NW, COUT = 32;
+  static constexpr int NW = NW_, NT = 64 * NW, TH = WS9_TH, TW = 16 * NW, COUT = 32;
   static constexpr int HR = TH + 8;                 // halo rows
   // 16-B chunks per halo row: TW + 8 px used, rounded up so the row stride is == 32 mod 64 dwords
   // (the column-8 operand's four rows land in disjoint bank halves)
@@ -70,23 +54,14 @@ struct W9Cfg {
   static constexpr int NREQ = (NCHK + NT - 1) / NT; // request slots per thread (the last partial)
   static constexpr int PIXB = COUT * 2;             // 64 B per output pixel
   static constexpr int OUT_OFF = 2 * HALO;
-#ifdef WS9_STAGED
   static constexpr int OUTB = TH * TW * PIXB;       // the LDS output tile
-#else
-  static constexpr int OUTB = 0;
-#endif
   static constexpr int NST = TH * TW * PIXB / (NT * 16);  // 16-B stores per thread
   static constexpr int PART_OFF = OUT_OFF + OUTB;
   static constexpr int BIAS_OFF = PART_OFF + NW * 64 * 4;
   static constexpr int LDS = BIAS_OFF + COUT * 4;
   static constexpr int NWM = 9 * 2;                 // 16x16x32 weight fragments (ky, m)
-#if W9_K8PAIR
-  static constexpr int NWK = 2 * 2;                 // column-8 16x16x32 weight fragments (j, m)
-  static constexpr int WBYTES = NWM * 64 * 16 + NWK * 64 * 16;
-#else
   static constexpr int NWK = 3 * 2;                 // 16x16x16 weight fragments (j, m)
   static constexpr int WBYTES = NWM * 64 * 16 + NWK * 64 * 8;
-#endif
   static_assert(NCHK % 64 == 0, "whole-wave DMA requests");
   static_assert(2 * RCH >= TW + 8 && (RS / 4) % 64 == 32, "halo row");
   static_assert(NST * NT * 16 == TH * TW * PIXB, "whole 16-B stores per thread");
@@ -96,7 +71,7 @@ struct W9Cfg {
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 template <int NW>
-__global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p) {
+__global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   using C = W9Cfg<NW>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -123,20 +98,12 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
 
   // ---- the whole weight tensor, resident for the launch (same in every wave) ----
   uint4 wm[C::NWM];
-#if W9_K8PAIR
-  uint4 wk[C::NWK];
-#else
   uint2 wk[C::NWK];
-#endif
   {
     const uint4* src = (const uint4*)p.wpk + lane;
 #pragma unroll
     for (int s = 0; s < C::NWM; ++s) wm[s] = src[s * 64];
-#if W9_K8PAIR
-    const uint4* srck = (const uint4*)((const char*)p.wpk + C::NWM * 64 * 16) + lane;
-#else
     const uint2* srck = (const uint2*)((const char*)p.wpk + C::NWM * 64 * 16) + lane;
-#endif
 #pragma unroll
     for (int s = 0; s < C::NWK; ++s) wk[s] = srck[s * 64];
   }
@@ -146,8 +113,10 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
   const size_t frame_bytes = (size_t)p.hs * p.ws * 8;
   const uint32_t smem_u = (uint32_t)(uintptr_t)smem;
   // the tile moves the frame offset only (soffset); a thread's chunk offsets are launch constants.
-  // Rows past the frame read 0 (buffer range check); columns past a row's end read the next row
-  // (finite, only feeding outputs past the frame edge)
+  // The last tile row's halo and the columns past a row's end read finite data of the next rows or
+  // frame, or the workspace's tail slack behind the last frame (make_plan sizes it for the 16 halo
+  // rows), whether or not the range check covers soffset; such reads only feed outputs past the
+  // frame edge, which are masked
   uint32_t roff[C::NREQ];
 #pragma unroll
   for (int k = 0; k < C::NREQ; ++k) {
@@ -172,12 +141,10 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, bop),
                                                 first ? z : c, 0, 0, 0);
   };
-#if !W9_K8PAIR
   auto mfma16 = [&](f32x4_t& c, const uint2& a, const uint2& bop) {
     c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4_t, a), __builtin_bit_cast(s16x4_t, bop), c,
                                                   0, 0, 0);
   };
-#endif
   // ---- K loop over the wave's 16 halo rows ----
   auto kloop = [&](Acc& acc, int buf) {
     int fb = buf * C::HALO + (16 * wv + px + 2 * g) * 8;  // row-r operand: + r * RS
@@ -185,25 +152,13 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
     asm volatile("" : "+v"(fb), "+v"(kb));
     auto fread = [&](int r) { return *(const uint4*)(smem + fb + r * C::RS); };
     // rows past the halo only meet zero weights (kernel rows 9..11): read row HR - 1 instead
-#if W9_K8PAIR
-    // column-8 operand P(s): lane group g = kernel rows 2g, 2g + 1 (input rows s + 2g, s + 2g + 1);
-    // rows past the halo only meet zero weights (P(s) for s >= 8 serves kernel row 8 = lane group 0)
-    typedef uint4 KOp;
-    auto kread = [&](int r) {
-      const int r0 = (r + 7 < C::HR) ? (r + 2 * g) * C::RS : min(r + 2 * g, C::HR - 1) * C::RS;
-      const int r1 = (r + 7 < C::HR) ? (r + 2 * g + 1) * C::RS : min(r + 2 * g + 1, C::HR - 1) * C::RS;
-      const uint2 a = *(const uint2*)(smem + kb + r0), b2 = *(const uint2*)(smem + kb + r1);
-      return make_uint4(a.x, a.y, b2.x, b2.y);
-    };
-#else
     typedef uint2 KOp;
     auto kread = [&](int r) {
       const int kr = (r + 3 < C::HR) ? (r + g) * C::RS : min(r + g, C::HR - 1) * C::RS;
       return *(const uint2*)(smem + kb + kr);
     };
-#endif
     // operands of row r + D are read while row r's MFMAs issue (register ring, explicit order)
-    constexpr int D = W9_RING;
+    constexpr int D = WS9_RING;
     uint4 fr[D];
     KOp kf[D];
 #pragma unroll
@@ -226,17 +181,6 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
         mfma32(acc[y][0], wm[2 * ky + 0], f, ky == 0);
         mfma32(acc[y][1], wm[2 * ky + 1], f, ky == 0);
       }
-#if W9_K8PAIR
-      // P(r) serves output row r (kernel rows 0..7, j = 0) and output row r - 8 (kernel row 8, j = 1)
-      if (r < C::TH) {
-        mfma32(acc[r][0], wk[0], k8, false);
-        mfma32(acc[r][1], wk[1], k8, false);
-      }
-      if (r >= 8 && r - 8 < C::TH) {
-        mfma32(acc[r - 8][0], wk[2], k8, false);
-        mfma32(acc[r - 8][1], wk[3], k8, false);
-      }
-#else
 #pragma unroll
       for (int y = 0; y < C::TH; ++y) {
         const int d = r - y;
@@ -244,7 +188,6 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
         mfma16(acc[y][0], wk[2 * (d >> 2) + 0], k8);
         mfma16(acc[y][1], wk[2 * (d >> 2) + 1], k8);
       }
-#endif
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -253,19 +196,11 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
   auto epilogue = [&](const Work& wk_, Acc& acc) {
     const f32x4_t bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (4 * g) * 4);
     const f32x4_t bias1 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 + 4 * g) * 4);
-#ifdef WS9_STAGED
     const int e = 2 * ((px >> 2) & 3);  // slot swizzle of this lane's pixel
     int obase = C::OUT_OFF + (16 * wv + px) * C::PIXB;
     asm volatile("" : "+v"(obase));
     const int o0 = ((0 + g) ^ e) * 8, o1 = ((4 + g) ^ e) * 8;
-#endif
     f32x4_t s1a = {0.f, 0.f, 0.f, 0.f}, s2a = s1a, s1b = s1a, s2b = s1a;
-#ifndef WS9_STAGED
-    const __amdgpu_buffer_rsrc_t dors = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((char*)p.out + (size_t)wk_.n * p.oh * p.ow * C::PIXB), (short)0, (int)(p.oh * p.ow * C::PIXB), 0x00020000);
-    const int dx = wk_.ox0 + 16 * wv + px;
-    const uint32_t dvoff = dx < p.ow ? (uint32_t)(dx * C::PIXB + 8 * g) : 0x80000000u;
-#endif
     // interior tiles (all but the frame's last row / column of tiles) take the select-free copy
     auto rows = [&](auto masked) {
 #pragma unroll
@@ -273,15 +208,8 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
         const f32x4_t va = acc[y][0] + bias0, vb = acc[y][1] + bias1;
         const u32x2_t pa = {pack_bf16(va[0], va[1]), pack_bf16(va[2], va[3])};
         const u32x2_t pb = {pack_bf16(vb[0], vb[1]), pack_bf16(vb[2], vb[3])};
-#ifdef WS9_STAGED
         *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o0) = pa;
         *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o1) = pb;
-#else  // half-pixel stores straight from the accumulators
-        if (wk_.oy0 + y < p.oh) {
-          __builtin_amdgcn_raw_buffer_store_b64(pa, dors, dvoff, (wk_.oy0 + y) * p.ow * C::PIXB, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(pb, dors, dvoff + 32, (wk_.oy0 + y) * p.ow * C::PIXB, 0);
-        }
-#endif
         f32x4_t xa = va, xb = vb;
         if constexpr (decltype(masked)::value) {
           const bool valid = wk_.oy0 + y < p.oh && wk_.ox0 + 16 * wv + px < p.ow;
@@ -327,7 +255,6 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
           (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * 64), (short)0, 256, 0x00020000);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (uint32_t)(lane * 4), 0, 0);
     }
-#ifdef WS9_STAGED
     const size_t obytes = (size_t)p.oh * p.ow * C::PIXB;
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((char*)p.out + (size_t)wk_.n * obytes), (short)0, (int)obytes, 0x00020000);
@@ -335,14 +262,9 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {  // store k = tile row k
       const u32x4_t v = *(const u32x4_t*)(smem + srd + k * C::TW * C::PIXB);
-#ifndef WS9_NOSTORE  // experiment (wrong result): no output stores
       if (wk_.oy0 + k < p.oh)
-#else
-      if (v[0] == 0x7fc0dead)
-#endif
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + k) * p.ow * C::PIXB, 0);
     }
-#endif
   };
 
   // ---- persistent walk: [wait own DMA | B1] request next | MFMAs | epilogue | B2 | stores ----
@@ -353,11 +275,7 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
   int buf = 0;
   request(cur, 0);
   for (int wn = w0 + G;; wn += G) {
-#ifdef WS9_STAGED
     vm_wait<C::NST>();
-#else
-    vm_wait<2 * C::TH>();
-#endif
     __syncthreads();
     const bool more = wn < p.n_work;
     Work nxt = cur;
@@ -366,11 +284,7 @@ __global__ __launch_bounds__(64 * NW, NST_WS9_OCC) void ws9_kernel(ConvParams p)
       request(nxt, buf ^ 1);
     }
     Acc acc;
-#ifndef WS9_NOMFMA  // experiment (wrong result): no K loop
     kloop(acc, buf);
-#else
-    for (int y = 0; y < C::TH; ++y) acc[y][0] = acc[y][1] = (f32x4_t){0.f, 0.f, 0.f, (float)buf};
-#endif
     epilogue(cur, acc);
     __syncthreads();
     store_out(cur);
@@ -411,14 +325,14 @@ struct Ws9Inst {
     k.wbytes = C::WBYTES;
     k.persistent = 1;
     k.part_rows = 1;
-    k.korder = W9_K8PAIR;  // column-8 packing (pack_ws9_weights)
+    k.korder = 0;  // column-8 packing: 16x16x16 fragments over kernel-row quads (pack_ws9_weights)
     k.launch = &launch;
     return k;
   }
 };
 
 const ConvKernelInfo* conv_table_ws9(int* count) {
-  static const ConvKernelInfo table[] = {Ws9Inst<NST_WS9_NW>::info()};
+  static const ConvKernelInfo table[] = {Ws9Inst<WS9_NW>::info()};
   *count = 1;
   return table;
 }

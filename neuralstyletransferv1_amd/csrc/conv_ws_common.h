@@ -14,14 +14,10 @@ enum WsFill { WF_NORM = 0, WF_RAW = 1, WF_RES = 2, WF_RESRN = 3 };  // IN+ReLU /
 // s_waitcnt vmcnt(N) / the part barrier, as statements hipcc cannot move memory operations across
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-#ifndef WS_NOWAIT  // experiment (racy): no waits for the unit requests
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-#endif
 }
 __device__ __forceinline__ void lds_barrier() {
-#ifndef WS_NOBAR  // experiment (racy): no part barriers
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
 }
 
 // One 16-byte LDS-DMA request: 64 lanes x 16 B from per-lane buffer offsets into LDS at

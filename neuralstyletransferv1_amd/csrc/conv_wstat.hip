@@ -30,11 +30,9 @@
 
 #include "conv_ws_common.h"
 
-#ifndef WS_RING
-#define WS_RING 3  // operand reads in flight ahead of the MFMAs
-#endif
-
 namespace nst {
+
+constexpr int WS_RING = 3;  // operand reads in flight ahead of the MFMAs
 
 template <int TH, int FILL>
 struct WsCfg {
@@ -182,16 +180,11 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const int soff = (2 * u + team) * 16;                                                // the unit's chunk
     const uint32_t lds = stg + (u % C::NSLOT) * C::SLOTB;
     dma16(frame_rsrc(p.in, n), voff, lds, soff);
-#ifndef WS_NORLOAD  // experiment: no residual loads (wrong result; vmcnt count stays conservative)
     if constexpr (RES) dma16(frame_rsrc(p.res_r, n), voff, lds + C::NW * 1024, soff);
-#endif
   };
   // consume unit u of tile wk: IN + ReLU / residual join of the staged chunk into the halo.
   // live = false: a restaging pass past the last work item (LDS only, no residual-stream stores)
   auto consume = [&](const Work& wk, int u, const Item& it, bool live) {
-#ifdef WS_NOCONSUME  // experiment: no unit transform / halo write
-    return;
-#endif
     const int ch = 2 * u + team;
     const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
     const uint4 y = *(const uint4*)sp;
@@ -242,9 +235,6 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const int pix = tid >> 2, c = 4 * q + (tid & 3);  // 128 pixels x 4 chunks
     const int r = pix >> 4, x = pix & 15;
     const int oy = wk.ty0 + r, ox = wk.tx0 + x;
-#ifdef WS_NOREGION  // experiment: no residual-stream stores
-    return;
-#endif
     const u32x4_t v = *(const u32x4_t*)(smem + ((r + 1) * C::LW + x + 1) * C::EB + c * 16);
     const bool ok = oy < p.oh && ox < p.ow;
     __builtin_amdgcn_raw_buffer_store_b128(v, frame_rsrc(p.res_out, wk.n),
@@ -296,9 +286,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         const int s = q * 9 + 3 * dy + dx;  // packed weight step
         mfma(acc[r], wr[s], bcur, q == 0 && dx == 0 && dy == 0);  // row r's first: y = r, dx = dy = 0
       }
-#ifndef WS_NOHOOK  // experiment: no unit work at all
       hook(q, rem);
-#endif
       if (rem == PRD - 1) {
         lds_barrier();  // every wave is past its reads of part q (in-flight unit requests stay in flight)
         bound(q);
@@ -336,11 +324,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         if constexpr (C::OST) {
           *(u32x2_t*)(smem + obase + r * C::TW * 256) = pk;
         } else {
-#ifndef WS_NOSTORE  // experiment (racy vmcnt accounting): no output stores
           __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : 0x80000000u, 0, 0);
-#else
-          asm volatile("" ::"v"(pk));
-#endif
         }
         const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
         s1 += x;
@@ -379,11 +363,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         const int x = pp & (C::TW - 1), oy = wk.ty0 + pp / C::TW, ox = wk.tx0 + x;
         const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * 256 + (((cb >> 3) ^ (2 * (x & 7))) << 3));
         const bool ok = oy < p.oh && ox < p.ow;
-#ifndef WS_NOSTORE
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * 256 + cb) : 0x80000000u, 0, 0);
-#else
-        asm volatile("" ::"v"(v), "v"(ok));
-#endif
       }
     }
   };
@@ -535,14 +515,12 @@ struct WstatInst {
   }
 };
 
-#ifndef NST_WSTAT_TH
-#define NST_WSTAT_TH 8
-#endif
+constexpr int WSTAT_TH = 8;  // tile rows
 #define E(...) WstatInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wstat(int* count) {
   static const ConvKernelInfo table[] = {
-      E(NST_WSTAT_TH, false),  // residual trunk
-      E(NST_WSTAT_TH, true),   // + residual join in the fill
+      E(WSTAT_TH, false),  // residual trunk
+      E(WSTAT_TH, true),   // + residual join in the fill
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

@@ -34,15 +34,14 @@ const ConvKernelInfo* conv_table_ws9(int* count);
 
 // first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
-                                       int out_kind, int res) {
+                                       int out_kind, int res, bool no_persistent) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
   const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_ws9,
                                  conv_table_out9, conv_table_bf16};
   const TableFn tables_f32[] = {conv_table_f32};
   const TableFn* tables = dtype == NST_DT_BF16 ? tables_bf16 : tables_f32;
   const int ntables = dtype == NST_DT_BF16 ? 7 : 1;
-  static const bool no_wl = std::getenv("NST_NO_PERSISTENT") != nullptr;  // experiment switch
-  for (int ti = (dtype == NST_DT_BF16 && no_wl) ? 1 : 0; ti < ntables; ++ti) {
+  for (int ti = (dtype == NST_DT_BF16 && no_persistent) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
     const ConvKernelInfo* t = tables[ti](&count);
     for (int i = 0; i < count; ++i) {
@@ -519,7 +518,10 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
       }
       const int ch = conv_out_dim(Ly.d, sh), cw = conv_out_dim(Ly.d, sw);
       if (op.src == B_IMG && Ly.prepad) {  // bf16 x4 per pixel over the conv's padded input extent
-        const size_t pb = (size_t)n * (ch + Ly.d.ks - 1) * (cw + Ly.d.ks - 1) * 8;
+        // + tail slack: the 9x9 kernel's last tile row reads up to 16 halo rows (and a row of column
+        // wrap) from its tile origin, which may lie past the last frame's padded extent
+        const int wpad = cw + Ly.d.ks - 1;
+        const size_t pb = (size_t)n * (ch + Ly.d.ks - 1) * wpad * 8 + (size_t)18 * wpad * 8 + 8192;
         if (pb > P.pre_bytes) P.pre_bytes = pb;
       }
       if (op.res_out >= 0) {  // the joined residual stream: same geometry as the conv input
@@ -620,10 +622,17 @@ const char* nst_version(void) { return "nst_hip 0.1.0 (gfx950)"; }
 
 int nst_create(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                nst_handle** out) {
-  if (!out || arch < 0 || arch > 2 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16)) {
+  return nst_create_ex(arch, params, n_params, compute_dtype, device, 0u, out);
+}
+
+int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
+                  unsigned flags, nst_handle** out) {
+  if (!out || arch < 0 || arch > 2 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16) ||
+      (flags & ~(unsigned)NST_KSEL_ALL) != 0) {
     set_error("nst_create: invalid arguments");
     return NST_E_INVALID;
   }
+  const bool no_pers = (flags & NST_KSEL_NO_PERSISTENT) != 0;
   *out = nullptr;
   std::map<std::string, const nst_param*> byname;
   for (int i = 0; i < n_params; ++i)
@@ -643,7 +652,7 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
   auto* h = new nst_handle();
   h->arch = arch; h->dtype = compute_dtype; h->device = device;
   std::vector<LayerDef> defs;
-  build_program(arch, std::getenv("NST_NO_RESFUSE") == nullptr, defs, h->prog);  // env: experiment switch
+  build_program(arch, (flags & NST_KSEL_UNFUSED_RESIDUAL) == 0, defs, h->prog);
   // layers whose fill joins the residual stream run the VAR_RES instantiation
   std::vector<int> res_layer(defs.size(), 0);
   for (const Op& op : h->prog)
@@ -671,40 +680,39 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
     std::vector<int> modes;
     // x2 up-convs: weight-stationary phase kernel (conv_wphase.hip) where compiled; its fused join
     // has no ReLU after the sum (ReCoNet's has), so ReCoNet's residual consumers skip it
-    const char* wp_only = std::getenv("NST_WPHASE_CIN");  // env: debug switch, one input width only
-    if (up && !(res_layer[li] && arch == NST_ARCH_RECONET) && !std::getenv("NST_NO_WPHASE") &&  // env: experiment switch
-        (!wp_only || std::atoi(wp_only) == Ly.cinp))
+    if (up && !(res_layer[li] && arch == NST_ARCH_RECONET) && !(flags & NST_KSEL_NO_WPHASE))
       modes.push_back(MODE_WPHASE);
     if (up) modes.push_back(MODE_PHASE);
     if (final_layer && d.cout == 3) {
-      if (!std::getenv("NST_NO_KYROT")) modes.push_back(MODE_KYROT);  // experiment switch
+      if (!(flags & NST_KSEL_NO_KYROT)) modes.push_back(MODE_KYROT);
       modes.push_back(MODE_XSHIFT);
     }
     // residual-trunk convs (128 -> 128, 3x3): weight-stationary kernel (conv_wstat.hip); ReCoNet's
     // trunk is 192 channels and its join has a ReLU after the sum, so it never matches
     if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 1 && arch != NST_ARCH_RECONET &&
-        !std::getenv("NST_NO_WSTAT"))  // env: experiment switch
+        !(flags & NST_KSEL_NO_WSTAT))
       modes.push_back(MODE_WSTAT);
     // stride-2 down-convs: weight-stationary kernel (conv_ws2.hip) where compiled
-    if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 2 && !std::getenv("NST_NO_WS2"))  // env: experiment switch
+    if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 2 && !(flags & NST_KSEL_NO_WS2))
       modes.push_back(MODE_WS2);
     modes.push_back(MODE_STD);
     // image layer: prefer the conv over the pre-padded encoded input (one streaming pre-pass, plain
     // 16-byte fill loads) when it is compiled for this shape; it serves u8 and f32 inputs alike
-    if (image_in && !std::getenv("NST_NO_PREPAD")) {  // env: experiment switch
+    if (image_in && !(flags & NST_KSEL_NO_PREPAD)) {
       // weight-stationary 9x9 kernel (conv_ws9.hip) where compiled, else the generic one
-      Ly.k_main = std::getenv("NST_NO_WS9") ? nullptr  // env: experiment switch
-                                            : find_conv_kernel(compute_dtype, MODE_WS9, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0);
+      Ly.k_main = (flags & NST_KSEL_NO_WS9)
+                      ? nullptr
+                      : find_conv_kernel(compute_dtype, MODE_WS9, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0, no_pers);
       if (Ly.k_main) Ly.mode = MODE_WS9;
-      else Ly.k_main = find_conv_kernel(compute_dtype, MODE_STD, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0);
+      else Ly.k_main = find_conv_kernel(compute_dtype, MODE_STD, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0, no_pers);
       if (Ly.k_main && d.stride == 1) { Ly.prepad = true; Ly.k_alt = Ly.k_main; modes.clear(); }
       else Ly.k_main = nullptr;
     }
     for (int mode : modes) {
-      Ly.k_main = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk, res_layer[li]);
+      Ly.k_main = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk, res_layer[li], no_pers);
       Ly.k_alt = nullptr;
-      if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk);
-      if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW);
+      if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk, 0, no_pers);
+      if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW, 0, no_pers);
       const bool tanh_ok = mode != MODE_KYROT || !Ly.k_main ||
                            (Ly.k_main->tanh_out == (arch == NST_ARCH_RECONET ? 1 : 0) && Ly.k_alt &&
                             Ly.k_alt->tanh_out == Ly.k_main->tanh_out);
@@ -804,8 +812,19 @@ int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* 
   return NST_OK;
 }
 
-int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset, void* y,
-                int y_fmt, void* workspace, size_t workspace_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// per-op device copies of what an op produced (nst_forward_capture)
+struct Capture {
+  void* const* act;
+  void* const* res;
+  void* const* stats;
+};
+
+int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset, void* y, int y_fmt,
+                 void* workspace, size_t workspace_bytes, void* stream, const Capture* cap) {
   if (!h || !x || !y || n <= 0 || in_h <= 0 || in_w <= 0 ||
       (x_fmt != NST_IO_F32_NCHW && x_fmt != NST_IO_U8_NHWC) || (y_fmt != NST_IO_F32_NCHW && y_fmt != NST_IO_U8_NHWC)) {
     set_error("nst_forward: invalid arguments");
@@ -830,6 +849,7 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
   }
   DeviceGuard guard(h->device);
   hipStream_t st = (hipStream_t)stream;
+  const size_t esz = h->dtype == NST_DT_BF16 ? 2 : 4;
   char* ws = (char*)workspace;
   void* bufs[NBUF];
   for (int b = 0; b < NBUF; ++b) bufs[b] = ws + P.off_buf[b];
@@ -851,6 +871,8 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
                                      op.r_norm >= 0 ? stats[op.r_norm] : nullptr, op.r_relu, op.relu_out,
                                      bufs[op.dst], n, hw, Ly.coutp, st);
       if (e != hipSuccess) { set_error(std::string("residual launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+      if (cap && cap->act && cap->act[i])
+        NST_HIP_CHECK(hipMemcpyAsync(cap->act[i], bufs[op.dst], (size_t)n * hw * Ly.coutp * esz, hipMemcpyDeviceToDevice, st));
       continue;
     }
     const bool image_in = op.src == B_IMG, final_out = op.dst == B_OUT;
@@ -963,7 +985,77 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
                              Ly.gamma, Ly.beta, 1e-5f, stats[op.layer], ws + P.off_seg, st);
       if (e != hipSuccess) { set_error(std::string("finalize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
     }
+    if (cap && !final_out) {
+      if (cap->act && cap->act[i])
+        NST_HIP_CHECK(hipMemcpyAsync(cap->act[i], bufs[op.dst], (size_t)n * P.oh[i] * P.ow[i] * Ly.coutp * esz,
+                                     hipMemcpyDeviceToDevice, st));
+      if (cap->res && cap->res[i] && op.res_out >= 0)
+        NST_HIP_CHECK(hipMemcpyAsync(cap->res[i], bufs[op.res_out], (size_t)n * P.ih[i] * P.iw[i] * Ly.cinp * esz,
+                                     hipMemcpyDeviceToDevice, st));
+      if (cap->stats && cap->stats[i])
+        NST_HIP_CHECK(hipMemcpyAsync(cap->stats[i], stats[op.layer], (size_t)n * Ly.coutp * 8, hipMemcpyDeviceToDevice, st));
+    }
   }
+  return NST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset, void* y,
+                int y_fmt, void* workspace, size_t workspace_bytes, void* stream) {
+  return forward_impl(h, x, x_fmt, n, in_h, in_w, preset, y, y_fmt, workspace, workspace_bytes, stream, nullptr);
+}
+
+int nst_forward_capture(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset, void* y,
+                        int y_fmt, void* workspace, size_t workspace_bytes, void* const* act, void* const* res,
+                        void* const* stats, void* stream) {
+  const Capture cap{act, res, stats};
+  return forward_impl(h, x, x_fmt, n, in_h, in_w, preset, y, y_fmt, workspace, workspace_bytes, stream, &cap);
+}
+
+int nst_num_ops(const nst_handle* h) { return h ? (int)h->prog.size() : 0; }
+
+int nst_op_describe(const nst_handle* h, int n, int in_h, int in_w, int op_index, nst_op_desc* out) {
+  if (!h || !out || n <= 0 || in_h <= 0 || in_w <= 0 || op_index < 0 || op_index >= (int)h->prog.size()) {
+    set_error("nst_op_describe: invalid arguments");
+    return NST_E_INVALID;
+  }
+  Plan P = make_plan(h, n, in_h, in_w);
+  if (!P.ok) { set_error(P.err); return NST_E_SHAPE; }
+  const Op& op = h->prog[op_index];
+  const Layer& Ly = h->layers[op.layer];
+  std::memset(out, 0, sizeof(*out));
+  out->kind = op.kind;
+  out->layer = op.layer;
+  out->src = op.src;
+  out->dst = op.dst;
+  if (op.kind == OP_CONV) {
+    out->in_norm = op.in_norm;
+    out->in_relu = op.in_norm >= 0 && op.res_buf < 0 ? 1 : 0;
+    out->res_buf = op.res_buf;
+    out->res_norm = op.res_buf >= 0 ? op.r_norm : -1;
+    out->res_out = op.res_out;
+    out->relu_out = op.res_buf >= 0 ? op.relu_out : 0;
+  } else {
+    out->in_norm = op.layer;  // out = IN_layer(src) + r
+    out->in_relu = 0;
+    out->res_buf = op.r_buf;
+    out->res_norm = op.r_norm;
+    out->res_out = -1;
+    out->relu_out = op.relu_out;
+  }
+  out->in_h = P.ih[op_index];
+  out->in_w = P.iw[op_index];
+  out->out_h = P.oh[op_index];
+  out->out_w = P.ow[op_index];
+  out->conv_h = P.ch[op_index];
+  out->conv_w = P.cw[op_index];
+  out->cin_stride = op.src == B_IMG ? 3 : Ly.cinp;
+  out->cout_stride = Ly.coutp;
+  out->kernel_mode = Ly.mode;
+  out->elem_bytes = h->dtype == NST_DT_BF16 ? 2 : 4;
   return NST_OK;
 }
 

@@ -97,7 +97,7 @@ struct ConvKernelInfo {
 
 // Look up a compiled instantiation; nullptr if the combination was not built.
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
-                                       int out_kind, int res = 0);
+                                       int out_kind, int res = 0, bool no_persistent = false);
 
 // ---- elementwise / reduction launchers (nst_ops.hip) ----
 constexpr int IN_MAX_SEGMENTS = 128;

@@ -23,7 +23,8 @@ _DTYPES = {"fp32": _lib.NST_DT_F32, "float32": _lib.NST_DT_F32, "bf16": _lib.NST
 class Engine:
     """One packed checkpoint on one device (owns an nst_handle and a reusable workspace)."""
 
-    def __init__(self, arch: int, state: Dict[str, torch.Tensor], dtype: str, device: torch.device):
+    def __init__(self, arch: int, state: Dict[str, torch.Tensor], dtype: str, device: torch.device,
+                 kernel_flags: int = 0):
         if device.type != "cuda":
             raise NstError("libnst_hip runs on MI355X (cuda) devices only; there is no CPU path")
         self.arch = arch
@@ -41,7 +42,8 @@ class Engine:
             arr[i].numel = host[k].numel()
         h = ctypes.c_void_p()
         dev_index = device.index if device.index is not None else torch.cuda.current_device()
-        check(lib().nst_create(arch, arr, len(names), self.dtype, dev_index, ctypes.byref(h)), "nst_create")
+        check(lib().nst_create_ex(arch, arr, len(names), self.dtype, dev_index, kernel_flags, ctypes.byref(h)),
+              "nst_create")
         self._h = h
         self._keep = None
         self._ws: Optional[torch.Tensor] = None
@@ -76,11 +78,66 @@ class Engine:
         return oh.value, ow.value
 
     def workspace(self, n: int, h: int, w: int) -> torch.Tensor:
+        """The cached workspace, grown on demand.  It is handed to kernels on whichever stream is
+        current, so it is recorded on that stream (the caching allocator then never reuses its bytes
+        while work queued there may still touch them, also after it is replaced)."""
         need = ctypes.c_size_t()
         check(lib().nst_workspace_bytes(self._h, n, h, w, ctypes.byref(need)), "nst_workspace_bytes")
         if self._ws is None or self._ws.numel() < need.value:
             self._ws = torch.empty(max(need.value, 256), dtype=torch.uint8, device=self.device)
+        self._ws.record_stream(torch.cuda.current_stream(self.device))
         return self._ws
+
+    def op_descs(self, n: int, h: int, w: int):
+        """Wiring and geometry of every op of the handle's program (nst_op_describe)."""
+        out = []
+        for i in range(lib().nst_num_ops(self._h)):
+            d = _lib.NstOpDesc()
+            check(lib().nst_op_describe(self._h, n, h, w, i, ctypes.byref(d)), "nst_op_describe")
+            out.append(d.as_dict())
+        return out
+
+    def forward_capture(self, x: torch.Tensor, x_fmt: str, preset: str, y_fmt: str):
+        """nst_forward_capture: run the batch and return (y, ops, captures); captures[i] =
+        {"act": raw conv output of op i [n,oh,ow,cout_stride] (bf16/fp32), "res": joined residual
+        stream it wrote or None, "stats": [n,cout_stride,2] fp32 {scale, shift} or None}."""
+        _lib.require_gpu_tensor(x, "input")
+        x = x.contiguous()
+        if x_fmt == "u8":
+            n, h, w, _ = x.shape
+            xf = _lib.NST_IO_U8_NHWC
+        else:
+            n, _, h, w = x.shape
+            xf = _lib.NST_IO_F32_NCHW
+        oh, ow = self.output_hw(h, w)
+        if y_fmt == "u8":
+            y = torch.empty((n, oh, ow, 3), dtype=torch.uint8, device=self.device)
+            yf = _lib.NST_IO_U8_NHWC
+        else:
+            y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=self.device)
+            yf = _lib.NST_IO_F32_NCHW
+        ops = self.op_descs(n, h, w)
+        dt = torch.bfloat16 if self.dtype == _lib.NST_DT_BF16 else torch.float32
+        caps = []
+        k = len(ops)
+        act, res, st = (ctypes.c_void_p * k)(), (ctypes.c_void_p * k)(), (ctypes.c_void_p * k)()
+        for i, d in enumerate(ops):
+            c = {"act": None, "res": None, "stats": None}
+            if d["dst"] != _lib.NST_BUF_OUTPUT:
+                c["act"] = torch.empty((n, d["out_h"], d["out_w"], d["cout_stride"]), dtype=dt, device=self.device)
+                act[i] = c["act"].data_ptr()
+                if d["kind"] == 0:
+                    c["stats"] = torch.empty((n, d["cout_stride"], 2), dtype=torch.float32, device=self.device)
+                    st[i] = c["stats"].data_ptr()
+                if d["res_out"] >= 0:
+                    c["res"] = torch.empty((n, d["in_h"], d["in_w"], d["cin_stride"]), dtype=dt, device=self.device)
+                    res[i] = c["res"].data_ptr()
+            caps.append(c)
+        ws = self.workspace(n, h, w)
+        check(lib().nst_forward_capture(self._h, x.data_ptr(), xf, n, h, w, _lib.PRESETS[preset], y.data_ptr(), yf,
+                                        ws.data_ptr(), ws.numel(), act, res, st, _lib.stream_ptr(self.device)),
+              "nst_forward_capture")
+        return y, ops, caps
 
     def forward_tensor(self, x: torch.Tensor) -> torch.Tensor:
         """Raw model tensor in, raw model tensor out: [n,3,h,w] fp32 -> [n,3,oh,ow] fp32."""
@@ -137,7 +194,10 @@ class StylizationNet(nn.Module):
         super().__init__()
         # "fp32": parity mode (exact-f32 MFMA); "bf16": throughput mode (bf16 MFMA, fp32 accumulate)
         self.compute_dtype = "fp32"
-        self._engines: Dict[Tuple[str, int, str], Tuple[tuple, Engine]] = {}
+        # kernel selection (names of _lib.KSEL): e.g. {"no_wstat"} runs the residual trunk on the
+        # generic kernel instead of the weight-stationary one; empty = the fastest mapping
+        self.kernel_select = frozenset()
+        self._engines: Dict[Tuple[str, int, str, int], Tuple[tuple, Engine]] = {}
 
     def _param_key(self) -> tuple:
         return tuple((p.data_ptr(), p._version) for p in self.state_dict().values())
@@ -154,12 +214,17 @@ class StylizationNet(nn.Module):
         dtype = dtype or self.compute_dtype
         if dtype not in _DTYPES:
             raise NstError(f"compute_dtype must be fp32 or bf16, got {dtype!r}")
-        key = (device.type, device.index, dtype)
+        flags = 0
+        for name in self.kernel_select:
+            if name not in _lib.KSEL:
+                raise NstError(f"unknown kernel_select entry {name!r} (known: {sorted(_lib.KSEL)})")
+            flags |= _lib.KSEL[name]
+        key = (device.type, device.index, dtype, flags)
         pk = self._param_key()
         hit = self._engines.get(key)
         if hit is not None and hit[0] == pk:
             return hit[1]
-        eng = Engine(self.ARCH, self.state_dict(), dtype, device)
+        eng = Engine(self.ARCH, self.state_dict(), dtype, device, flags)
         self._engines[key] = (pk, eng)
         return eng
 

@@ -14,10 +14,13 @@ Additions: --gpus N (frames round-robin over N GPUs, ordered gather to rank 0 ov
 arithmetic, default; bf16 = throughput mode), --synthetic WxH / --synthetic_frames N (an
 in-memory synthetic frame stream instead of files; config 4 of BASELINE.json).
 
-Out of scope for this engine (rejected with a clear message if requested):
-region blending (--region_*), optical-flow EMA / motion blend (--flow_ema, --motion_blend),
-Magenta (TF-Hub) and Torch7 (OpenCV DNN) backends, LAB multi-model blend (--blend_models_lab),
-mask feathering (needs OpenCV's GaussianBlur; --mask_feather/--mask_feather_pct).
+Also on the GPU: the LAB multi-model blend (--blend_models_lab, pipeline.py:1841-1870) and the
+Gaussian mask feather (--mask_feather / --mask_feather_pct, pipeline.py:349-351; cv2's blur
+restated, parity unpinned because cv2 is absent here).
+
+Not built (rejected with a clear message if requested): region blending
+(--region_*), optical-flow EMA / motion blend (--flow_ema, --motion_blend), Magenta (TF-Hub) and
+Torch7 (OpenCV DNN) backends.
 """
 from __future__ import annotations
 
@@ -31,6 +34,7 @@ import sys
 import time
 import uuid
 from concurrent.futures import ThreadPoolExecutor
+from datetime import timedelta
 from pathlib import Path
 from typing import Dict, List, Optional
 
@@ -132,6 +136,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("GPUS", "1")),
                     help="frames round-robin over N GPUs (one process per GPU), ordered gather to rank 0")
     ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
+    ap.add_argument("--dist_backend", choices=["nccl", "gloo"], default="nccl",
+                    help="--gpus > 1 process group: nccl (RCCL over xGMI, one GPU per rank) or gloo (host-staged "
+                         "exchange; ranks may share a GPU, used by the tests)")
+    ap.add_argument("--dist_timeout", type=float, default=600.0, help="seconds before a blocked exchange aborts")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
                     help="fp32 = parity with the reference arithmetic; bf16 = throughput mode")
     ap.add_argument("--synthetic", type=str, default=None, help="WxH: stylize an in-memory synthetic frame stream")
@@ -161,23 +169,19 @@ def reject_out_of_scope(args) -> None:
 
 
 # ----------------------------------------------------------------------------- host I/O helpers
+# EXIF Orientation (tag 0x0112) -> counter-clockwise PIL rotation that uprights the image
+_EXIF_UPRIGHT = {3: 180, 6: 270, 8: 90}
+
+
 def _get_image_with_exif_pil(image_path: str):
-    """pipeline.py:171-187."""
-    from PIL import ExifTags, Image
+    """EXIF-normalised RGB image (pipeline.py:171-187: orientations 3/6/8 rotated upright, others
+    untouched; JPEG's legacy _getexif table, absent on other formats)."""
+    from PIL import Image
     img = Image.open(image_path)
-    exif = getattr(img, "_getexif", lambda: None)()
-    orientation = None
-    if exif:
-        for tag, value in exif.items():
-            if ExifTags.TAGS.get(tag) == "Orientation":
-                orientation = value
-                break
-    if orientation == 3:
-        img = img.rotate(180, expand=True)
-    elif orientation == 6:
-        img = img.rotate(270, expand=True)
-    elif orientation == 8:
-        img = img.rotate(90, expand=True)
+    tags = getattr(img, "_getexif", lambda: None)() or {}
+    angle = _EXIF_UPRIGHT.get(tags.get(0x0112))
+    if angle is not None:
+        img = img.rotate(angle, expand=True)
     return img.convert("RGB")
 
 
@@ -397,7 +401,8 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     from .frames import plan_groups, run_sharded
     from .postproc import LabSmoother, blend_frames
 
-    dev = torch.device("cuda", rank if world > 1 else torch.cuda.current_device())
+    # one GPU per rank (several ranks may share a device with --dist_backend gloo: tests)
+    dev = torch.device("cuda", rank % torch.cuda.device_count() if world > 1 else torch.cuda.current_device())
     torch.cuda.set_device(dev)
     blend = float(max(0.0, min(1.0, blend)))
     save_map = save_map or {}
@@ -567,7 +572,7 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             out_img.save(out_path)
         return str(out_path)
 
-    run_sharded(groups, world, rank, stylize, consume)
+    run_sharded(groups, world, rank, stylize, consume, dev)
     for p in pending:
         p.result()
     pool.shutdown()
@@ -730,11 +735,16 @@ def _worker(rank: int, world: int, argv: List[str], port: int, prep):
     import torch
     import torch.distributed as dist
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    torch.cuda.set_device(rank)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
-                            device_id=torch.device("cuda", rank))
+    args = build_parser().parse_args(argv)
+    dev = torch.device("cuda", rank % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    if args.dist_backend == "nccl":  # RCCL over xGMI, one GPU per rank
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                                device_id=dev, timeout=timedelta(seconds=args.dist_timeout))
+    else:  # gloo: frames travel through host memory (ranks may share a GPU)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                                timeout=timedelta(seconds=args.dist_timeout))
     try:
-        args = build_parser().parse_args(argv)
         frames_dir, model_path, save_map, image_mode, _ = prep
         _run_style(args, frames_dir, model_path, save_map, image_mode, rank, world)
     finally:

@@ -1,0 +1,149 @@
+"""Teacher-forced per-layer parity of the bf16 engine (helper of tests/test_gpu_layers.py).
+
+Runs one batch through nst_forward_capture, then recomputes every op on the CPU from the engine's
+own stored inputs (oracle/bf16_layers.py) and compares:
+  * each conv's stored bf16 output element-wise, in bf16 ulps;
+  * each conv's InstanceNorm {scale, shift} (from the engine's fp32 values) against the statistics
+    of the oracle's fp32 values;
+  * each joined residual stream bit for bit;
+  * the output conv's raw fp32 values and its decoded u8 frames.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from oracle import bf16_layers as B
+
+# bars (tests state them; see oracle/bf16_layers.py for why they are not zero)
+ULP_MAX = 1              # stored bf16 outputs: at most one bf16 ulp apart ...
+ATOL_REL = 4e-6          # ... or within this fraction of the layer's max |value| (sums that cancel to ~0)
+ULP1_FRAC_MAX = 1e-3     # at most 0.1 % of the elements one ulp apart (accumulation-order rounding flips)
+STATS_REL = 1e-5         # IN scale/shift vs the oracle's statistics of its fp32 values (measured <= 4e-7)
+RAW_REL = 5e-6           # output conv raw fp32, relative to max |y| (measured <= 1.1e-6)
+U8_EXACT_MIN = 0.9999    # decoded u8 frames: >= 99.99 % identical, the rest 1 LSB (truncation boundary)
+
+
+def _nchw(t: torch.Tensor, c: int) -> torch.Tensor:
+    return t[..., :c].float().cpu().permute(0, 3, 1, 2).contiguous()
+
+
+def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequence[Tuple[float, int]]] = None,
+                 acc: torch.dtype = torch.float32) -> List[Dict]:
+    """-> one record per op.  bands: None = every output row; else [(fraction, rows)] row bands
+    (start = fraction of the output height, rounded down to even) checked per op (4K frames)."""
+    arch = {0: "johnson", 1: "nst", 2: "reconet"}[net.ARCH]
+    sd = {k: v.detach().float().cpu() for k, v in net.state_dict().items()}
+    eng = net.engine()
+    fr_dev = torch.from_numpy(frames_u8).to(eng.device)
+    n, H0, W0, _ = frames_u8.shape
+    oh, ow = eng.output_hw(H0, W0)
+    y_raw, ops, caps = eng.forward_capture(fr_dev, "u8", preset, "f32")
+    y_raw = y_raw.cpu()
+    y_u8 = None
+    if (oh, ow) == (H0, W0):
+        y_u8, _, _ = eng.forward_capture(fr_dev, "u8", preset, "u8")
+        y_u8 = y_u8.cpu().numpy()
+    torch.cuda.synchronize()
+    layers = B.LAYERS[arch]
+    host = [{k: (v.cpu() if v is not None else None) for k, v in c.items()} for c in caps]
+    writer: Dict[int, Tuple[int, str]] = {}   # buffer -> (op, "act" | "res")
+    layer_op: Dict[int, int] = {}            # layer -> conv op that ran it (its stats capture)
+    recs = []
+    x_enc = None
+    for i, d in enumerate(ops):
+        if d["kind"] != 0:
+            raise AssertionError("unfused residual ops are not part of the default program")
+        conv, norm, cin, cout, ks, st, axis, pad, pre = layers[d["layer"]]
+
+        def stats_of(layer):
+            return host[layer_op[layer]]["stats"][:, :, :]
+
+        def buf_rows(buf):
+            j, kind = writer[buf]
+            return _nchw(host[j][kind], cin)
+
+        if d["src"] == -1:
+            if x_enc is None:
+                x_enc = B.encode_operand(frames_u8, preset)
+            src = x_enc
+
+            def get_rows(idx, src=src):
+                return src.index_select(2, idx)
+            Hs = src.shape[2]
+        else:
+            ysrc = buf_rows(d["src"])
+            ys = stats_of(d["in_norm"])[:, :cin] if d["in_norm"] >= 0 else None
+            r = rs = None
+            if d["res_buf"] >= 0:
+                r = buf_rows(d["res_buf"])
+                rs = stats_of(d["res_norm"])[:, :cin] if d["res_norm"] >= 0 else None
+
+            def get_rows(idx, ysrc=ysrc, ys=ys, r=r, rs=rs, d=d):
+                return B.fill_operand(ysrc.index_select(2, idx), ys, bool(d["in_relu"]),
+                                      None if r is None else r.index_select(2, idx), rs, bool(d["relu_out"]))
+            Hs = ysrc.shape[2]
+            if d["res_out"] >= 0:  # the joined stream the op wrote for its own pixels: bit-exact
+                joined = get_rows(torch.arange(Hs))
+                got = _nchw(host[i]["res"], cin)
+                assert torch.equal(got, joined), f"op {i} ({conv}): joined residual stream differs"
+        final = d["dst"] == -2
+        ch = d["conv_h"]
+        row_sets = [(0, ch)] if bands is None else sorted({
+            (r0, min(ch, r0 + k)) for f, k in bands for r0 in [min(max(0, int(f * ch)) // 2 * 2, max(0, ch - k) // 2 * 2)]})
+        rec = {"op": i, "layer": conv, "mode": d["kernel_mode"], "elements": 0}
+        W, bias = sd[conv + ".weight"], sd[conv + ".bias"]
+        for (r0, r1) in row_sets:
+            z = B.conv_layer(get_rows, Hs, n, cin, W, bias, ks, st, axis, pad, pre, True, (r0, r1), acc)
+            if final:
+                if arch == "reconet":
+                    z = torch.tanh(z)
+                cy, cx = (d["conv_h"] - d["out_h"]) // 2, (d["conv_w"] - d["out_w"]) // 2
+                lo, hi = max(r0, cy), min(r1, cy + d["out_h"])
+                if hi <= lo:
+                    continue
+                zc = z[:, :, lo - r0:hi - r0, cx:cx + d["out_w"]]
+                yc = y_raw[:, :, lo - cy:hi - cy, :]
+                rel = float((yc - zc).abs().max() / zc.abs().max().clamp_min(1e-12))
+                rec["raw_rel"] = max(rec.get("raw_rel", 0.0), rel)
+                assert rel <= RAW_REL, f"op {i} ({conv}) raw output rel err {rel:.2e} rows {r0}:{r1}"
+                if y_u8 is not None:
+                    ref = B.decode_u8(zc, preset)
+                    got = y_u8[:, lo - cy:hi - cy]
+                    dd = np.abs(got.astype(int) - ref.astype(int))
+                    rec["u8_max"] = max(rec.get("u8_max", 0), int(dd.max()))
+                    rec["u8_exact"] = min(rec.get("u8_exact", 1.0), float((dd == 0).mean()))
+                    assert dd.max() <= 1 and (dd == 0).mean() >= U8_EXACT_MIN, (i, conv, dd.max(), (dd == 0).mean())
+                rec["elements"] += zc.numel()
+                continue
+            got_full = host[i]["act"]
+            got = got_full[:, r0:r1].permute(0, 3, 1, 2)[:, :cout].contiguous()
+            pad_ch = got_full[:, r0:r1, :, cout:]
+            assert (pad_ch.float() == 0).all(), f"op {i} ({conv}): padded channels not zero"
+            ref = z.to(torch.bfloat16)
+            ulp = B.bf16_ulp_diff(got, ref)
+            diff = (got.float() - ref.float()).abs()
+            atol = ATOL_REL * float(ref.float().abs().max())
+            bad = (ulp > ULP_MAX) & (diff > atol)
+            rec["elements"] += ref.numel()
+            rec["ulp1_frac"] = max(rec.get("ulp1_frac", 0.0), float((ulp >= 1).float().mean()))
+            rec["ulp_max"] = max(rec.get("ulp_max", 0), int(ulp.max()))
+            rec["bad"] = rec.get("bad", 0) + int(bad.sum())
+            assert not bad.any(), (f"op {i} ({conv}) rows {r0}:{r1}: {int(bad.sum())} elements beyond "
+                                   f"{ULP_MAX} ulp / atol {atol:.2e}; first at {tuple(bad.nonzero()[0].tolist())}")
+            assert rec["ulp1_frac"] <= ULP1_FRAC_MAX, (i, conv, rec["ulp1_frac"])
+            if bands is None:  # statistics need the whole frame
+                s_ref = B.in_stats(z, sd[norm + ".weight"], sd[norm + ".bias"])
+                s_got = host[i]["stats"][:, :cout]
+                err = (s_got - s_ref).abs() / s_ref.abs().amax(dim=1, keepdim=True).clamp_min(1e-6)
+                rec["stats_rel"] = float(err.max())
+                assert rec["stats_rel"] <= STATS_REL, (i, conv, rec["stats_rel"])
+        if not final:
+            writer[d["dst"]] = (i, "act")
+            layer_op[d["layer"]] = i
+            if d["res_out"] >= 0:
+                writer[d["res_out"]] = (i, "res")
+        recs.append(rec)
+    return recs

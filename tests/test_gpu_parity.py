@@ -27,11 +27,12 @@ def _arch(path):
     return os.path.basename(path).split("_")[1]
 
 
-def _net(arch, seed, dtype):
+def _net(arch, seed, dtype, ksel=()):
     m = synthetic.build_module(arch)
     m.load_state_dict(synthetic.make_state_dict(arch, seed))
     m = m.to("cuda").eval()
     m.compute_dtype = dtype
+    m.kernel_select = frozenset(ksel)
     return m
 
 
@@ -157,7 +158,7 @@ def test_gram_vs_reference_golden():
     ("nst", 72, 100, "raw_01"),             # zero padding + centre crop
     ("reconet", 48, 84, "tanh"),            # 48 -> 64 padded channels, tanh output
 ])
-def test_bf16_output_conv_mappings_agree(arch, h, w, preset, monkeypatch):
+def test_bf16_output_conv_mappings_agree(arch, h, w, preset):
     """The row-streaming ky-rotation output conv (conv_out9.hip) against the x-shift / plain
     implicit-GEMM mapping of the same layer: same bf16 operands, fp32 accumulation in another
     order, so u8 frames agree to 1 LSB and raw outputs to fp32 rounding."""
@@ -167,8 +168,7 @@ def test_bf16_output_conv_mappings_agree(arch, h, w, preset, monkeypatch):
     a = fast.stylize_frames(frames, preset).cpu().numpy()
     x = torch.randn(2, 3, h, w, generator=torch.Generator().manual_seed(0)).cuda()
     ya = fast(x).cpu().numpy()
-    monkeypatch.setenv("NST_NO_KYROT", "1")
-    slow = _net(arch, sd_seed, "bf16")
+    slow = _net(arch, sd_seed, "bf16", {"no_kyrot"})
     b = slow.stylize_frames(frames, preset).cpu().numpy()
     yb = slow(x).cpu().numpy()
     d = np.abs(a.astype(int) - b.astype(int))
@@ -178,7 +178,7 @@ def test_bf16_output_conv_mappings_agree(arch, h, w, preset, monkeypatch):
 
 @pytest.mark.parametrize("arch", ["johnson", "nst", "reconet"])
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
-def test_fused_residual_join_bit_exact(arch, dtype, monkeypatch):
+def test_fused_residual_join_bit_exact(arch, dtype):
     """The residual add fused into the next conv's fill (VAR_RES, x_{k+1} written by that conv for
     its own pixels) against the separate residual kernel: identical fp32 arithmetic, so the
     outputs are bit-identical (u8 frames and the raw tensor output)."""
@@ -187,27 +187,24 @@ def test_fused_residual_join_bit_exact(arch, dtype, monkeypatch):
     x = torch.randn(2, 3, h, w, generator=torch.Generator().manual_seed(1)).cuda()
     fused = _net(arch, 2, dtype)
     a, ya = fused.stylize_frames(frames, "imagenet_255"), fused(x)
-    monkeypatch.setenv("NST_NO_RESFUSE", "1")
-    plain = _net(arch, 2, dtype)
+    plain = _net(arch, 2, dtype, {"unfused_residual"})
     b, yb = plain.stylize_frames(frames, "imagenet_255"), plain(x)
     assert torch.equal(a, b)
     assert torch.equal(ya, yb)
 
 
 @pytest.mark.parametrize("arch", ["johnson", "nst", "reconet"])
-def test_prepadded_image_layer_bit_exact(arch, monkeypatch):
+def test_prepadded_image_layer_bit_exact(arch):
     """bf16 first layer over the pre-padded encoded input (conv_prep.hip) against the encode fused
     into the conv's fill: same per-element arithmetic and the same LDS image, so bit-identical
     (both through the generic kernel; the weight-stationary 9x9 kernel is tested below)."""
-    monkeypatch.setenv("NST_NO_WS9", "1")
     h, w = (72, 100) if arch == "nst" else (61, 90)
     frames = torch.from_numpy(synthetic.make_frames(2, h, w, seed=12)).cuda()
     x = torch.randn(2, 3, h, w, generator=torch.Generator().manual_seed(2)).cuda()
-    fast = _net(arch, 5, "bf16")
+    fast = _net(arch, 5, "bf16", {"no_ws9"})
     outs_a = [fast.stylize_frames(frames, p) for p in ("imagenet_255", "caffe_bgr", "tanh")]
     ya = fast(x)
-    monkeypatch.setenv("NST_NO_PREPAD", "1")
-    ref = _net(arch, 5, "bf16")
+    ref = _net(arch, 5, "bf16", {"no_ws9", "no_prepad"})
     outs_b = [ref.stylize_frames(frames, p) for p in ("imagenet_255", "caffe_bgr", "tanh")]
     yb = ref(x)
     for a, b in zip(outs_a, outs_b):
@@ -220,17 +217,16 @@ def test_prepadded_image_layer_bit_exact(arch, monkeypatch):
     ("nst", 72, 100),         # zero padding (transformer_net_nst.py ConvBlock), pre-reflect 40
     ("johnson", 1080, 1920),  # the bench shape (270x480 trunk), one frame
 ])
-def test_weight_stationary_trunk_vs_generic(arch, h, w, monkeypatch):
+def test_weight_stationary_trunk_vs_generic(arch, h, w):
     """The weight-stationary residual-trunk conv (conv_wstat.hip: 32x32x16 MFMAs, bias-initialised
     accumulators, its own K order) against the generic persistent kernel on the same bf16 model:
     every trunk layer's bf16 rounding may land differently, so the bar is the bf16 mode's own
     (SSIM vs each other well above the 0.98 oracle bar, few-LSB frames, raw outputs close)."""
     frames = torch.from_numpy(synthetic.make_frames(2 if h < 512 else 1, h, w, seed=21)).cuda()
-    x = torch.randn(2, 3, 72, 100, generator=torch.Generator().manual_seed(3)).cuda()
+    x = torch.randn(frames.shape[0], 3, h, w, generator=torch.Generator().manual_seed(3)).cuda()
     fast = _net(arch, 6, "bf16")
     a, ya = fast.stylize_frames(frames, "imagenet_255").cpu().numpy(), fast(x).cpu().numpy()
-    monkeypatch.setenv("NST_NO_WSTAT", "1")
-    ref = _net(arch, 6, "bf16")
+    ref = _net(arch, 6, "bf16", {"no_wstat"})
     b, yb = ref.stylize_frames(frames, "imagenet_255").cpu().numpy(), ref(x).cpu().numpy()
     for i in range(a.shape[0]):
         assert O.ssim(a[i], b[i]) >= 0.995
@@ -256,17 +252,16 @@ def test_weight_stationary_trunk_batch_chunks():
     ("reconet", 61, 90),      # 96 -> 48 up-conv padded to 128 -> 64 (the 192-channel one stays generic)
     ("johnson", 1080, 1920),  # the bench shape (270x480 and 540x960 sources), one frame
 ])
-def test_weight_stationary_upconv_vs_generic(arch, h, w, monkeypatch):
+def test_weight_stationary_upconv_vs_generic(arch, h, w):
     """The weight-stationary x2 up-convs (conv_wphase.hip: per-wave phase weights in registers,
     16x16x32 MFMAs, K part-major) against the generic phase-mode kernel on the same bf16 model:
     same phase-summed bf16 weights and operands, fp32 accumulation in another order, so the bar
     is the bf16 mode's own (SSIM vs each other well above the 0.98 oracle bar, few-LSB frames)."""
     frames = torch.from_numpy(synthetic.make_frames(2 if h < 512 else 1, h, w, seed=22)).cuda()
-    x = torch.randn(2, 3, 72, 100, generator=torch.Generator().manual_seed(4)).cuda()
+    x = torch.randn(frames.shape[0], 3, h, w, generator=torch.Generator().manual_seed(4)).cuda()
     fast = _net(arch, 8, "bf16")
     a, ya = fast.stylize_frames(frames, "imagenet_255").cpu().numpy(), fast(x).cpu().numpy()
-    monkeypatch.setenv("NST_NO_WPHASE", "1")
-    ref = _net(arch, 8, "bf16")
+    ref = _net(arch, 8, "bf16", {"no_wphase"})
     b, yb = ref.stylize_frames(frames, "imagenet_255").cpu().numpy(), ref(x).cpu().numpy()
     for i in range(a.shape[0]):
         assert O.ssim(a[i], b[i]) >= 0.995
@@ -281,7 +276,7 @@ def test_weight_stationary_upconv_vs_generic(arch, h, w, monkeypatch):
     ("reconet", 61, 90),      # 48 -> 96 down-conv padded to 64 -> 128 (the 96 -> 192 one stays generic)
     ("johnson", 1080, 1920),  # the bench shape, one frame
 ])
-def test_weight_stationary_downconv_vs_generic(arch, h, w, monkeypatch):
+def test_weight_stationary_downconv_vs_generic(arch, h, w):
     """The weight-stationary stride-2 convs (conv_ws2.hip: per-wave weights in registers,
     column-polyphase LDS halo, register-prefetched fill) against the generic implicit-GEMM kernel on
     the same bf16 model: same operands, fp32 accumulation in another order, so the bar is the bf16
@@ -289,11 +284,10 @@ def test_weight_stationary_downconv_vs_generic(arch, h, w, monkeypatch):
     output is far more sensitive to bf16 rounding (the generic bf16 path is ~10 % max-relative off
     the fp32 path on these synthetic weights, tools/dbg_w2.py), so its raw bar is wider."""
     frames = torch.from_numpy(synthetic.make_frames(2 if h < 512 else 1, h, w, seed=23)).cuda()
-    x = torch.randn(2, 3, 72, 100, generator=torch.Generator().manual_seed(5)).cuda()
+    x = torch.randn(frames.shape[0], 3, h, w, generator=torch.Generator().manual_seed(5)).cuda()
     fast = _net(arch, 9, "bf16")
     a, ya = fast.stylize_frames(frames, "imagenet_255").cpu().numpy(), fast(x).cpu().numpy()
-    monkeypatch.setenv("NST_NO_WS2", "1")
-    ref = _net(arch, 9, "bf16")
+    ref = _net(arch, 9, "bf16", {"no_ws2"})
     b, yb = ref.stylize_frames(frames, "imagenet_255").cpu().numpy(), ref(x).cpu().numpy()
     for i in range(a.shape[0]):
         assert O.ssim(a[i], b[i]) >= 0.995
@@ -309,18 +303,17 @@ def test_weight_stationary_downconv_vs_generic(arch, h, w, monkeypatch):
     ("nst", 72, 100),         # pre-reflect 40 + zero padding resolved by the pre-pass (152x180 conv)
     ("johnson", 1080, 1920),  # the bench shape, one frame
 ])
-def test_weight_stationary_image_conv_vs_generic(arch, h, w, monkeypatch):
+def test_weight_stationary_image_conv_vs_generic(arch, h, w):
     """The weight-stationary 9x9 first layer (conv_ws9.hip: the whole 3 -> 32 weight tensor in
     registers, 16x16x32 MFMAs over kernel columns 0..7 and 16x16x16 over column 8, LDS-DMA halo)
     against the generic kernel over the same pre-padded bf16 input: same operands, fp32
     accumulation in another order, so the bar is the bf16 mode's own (SSIM vs each other well
     above the 0.98 oracle bar, few-LSB frames, raw outputs close)."""
     frames = torch.from_numpy(synthetic.make_frames(2 if h < 512 else 1, h, w, seed=24)).cuda()
-    x = torch.randn(2, 3, 72, 100, generator=torch.Generator().manual_seed(6)).cuda()
+    x = torch.randn(frames.shape[0], 3, h, w, generator=torch.Generator().manual_seed(6)).cuda()
     fast = _net(arch, 10, "bf16")
     a, ya = fast.stylize_frames(frames, "imagenet_255").cpu().numpy(), fast(x).cpu().numpy()
-    monkeypatch.setenv("NST_NO_WS9", "1")
-    ref = _net(arch, 10, "bf16")
+    ref = _net(arch, 10, "bf16", {"no_ws9"})
     b, yb = ref.stylize_frames(frames, "imagenet_255").cpu().numpy(), ref(x).cpu().numpy()
     for i in range(a.shape[0]):
         assert O.ssim(a[i], b[i]) >= 0.995

@@ -154,3 +154,109 @@ def test_cli_lab_blend_and_feathered_mask(tmp_path):
         ref = O.blend_u8(lab, fr, alpha[..., None], "keep", 1.0)
         got = np.array(Image.open(outs[i]))
         _close(got, ref, frac=0.01)
+
+
+def _lsb_report(got, ref):
+    d = np.abs(got.astype(int) - ref.astype(int))
+    return d, float((d <= 2).mean()), int(d.max())
+
+
+def test_1080p_mask_blend_cli_vs_oracle(tmp_path):
+    """configs[4] without DeepLab: 1080p frames, a per-frame mask directory (mask_####.png, the
+    sky_swap.py output layout), --composite_mode keep, --blend 0.9, LAB smoothing 0.65 (run_videos.py
+    defaults) through the CLI, fp32 parity mode against the oracle chain: u8 values within 2 LSB on
+    >= 99.99 % of them; and the bf16 throughput mode (the bench kernels) at SSIM >= 0.98."""
+    ck, sd = _ckpt(tmp_path, "johnson", 0)
+    frames = synthetic.make_frames(2, 1080, 1920, seed=77)
+    d_in, d_m = tmp_path / "in", tmp_path / "masks"
+    d_in.mkdir()
+    d_m.mkdir()
+    src_mask = Image.open(os.path.join(GOLDEN, "masks", "center_circle.png")).convert("L")
+    for i, f in enumerate(frames):
+        Image.fromarray(f).save(d_in / f"frame_{i + 1:04d}.png")
+        src_mask.rotate(15 * i).save(d_m / f"mask_{i + 1:04d}.png")
+    masks = [P.load_mask_fit(str(d_m / f"mask_{i + 1:04d}.png"), (1080, 1920), False) for i in range(2)]
+    ref = _oracle_chain([("johnson", sd)], [1.0], list(frames), "imagenet_255", alpha=0.65, blend=0.9,
+                        masks=masks, mode="keep")
+    for dtype in ("fp32", "bf16"):
+        d_out = tmp_path / f"out_{dtype}"
+        rc = P.main(["--input_dir", str(d_in), "--output_dir", str(d_out), "--model", ck, "--io_preset", "imagenet_255",
+                     "--mask_dir", str(d_m), "--composite_mode", "keep", "--blend", "0.9", "--smooth_alpha", "0.65",
+                     "--dtype", dtype, "--batch", "2", "--work_dir", str(tmp_path / f"w_{dtype}")])
+        assert rc == 0
+        for i in range(2):
+            got = np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png"))
+            d, within2, dmax = _lsb_report(got, ref[i])
+            print(dtype, i, "within 2 LSB", within2, "max", dmax, "ssim", O.ssim(got, ref[i]))
+            if dtype == "fp32":
+                assert within2 >= 0.9999, (within2, dmax)
+            else:
+                assert O.ssim(got, ref[i]) >= 0.98
+
+
+def test_single_256_jpeg_cli_config0(tmp_path):
+    """configs[0]: one 256x256 JPEG through the Johnson TransformerNet via the single-image CLI
+    (io_preset auto -> imagenet_255 for transformer models, LAB smoothing on by default)."""
+    ck, sd = _ckpt(tmp_path, "johnson", 3)
+    fr = synthetic.make_frames(1, 256, 256, seed=256)[0]
+    inp, outp = tmp_path / "in.jpg", tmp_path / "out.png"
+    Image.fromarray(fr).save(inp, format="JPEG", quality=95)
+    # the CLI stages the image EXIF-normalised and re-saved at --jpeg_quality (85), pipeline.py:2552-2561
+    import io
+    buf = io.BytesIO()
+    Image.open(inp).convert("RGB").save(buf, format="JPEG", quality=85)
+    decoded = np.array(Image.open(io.BytesIO(buf.getvalue())).convert("RGB"))
+    rc = P.main(["--input_image", str(inp), "--output_image", str(outp), "--model", ck, "--model_type", "transformer",
+                 "--work_dir", str(tmp_path / "w")])
+    assert rc == 0
+    got = np.array(Image.open(outp))
+    ref = _oracle_chain([("johnson", sd)], [1.0], [decoded], "imagenet_255")[0]
+    d, within2, dmax = _lsb_report(got, ref)
+    assert got.shape == (256, 256, 3) and within2 >= 0.9999, (within2, dmax)
+
+
+def test_inference_res_lanczos_cli(tmp_path):
+    """--inference_res (pipeline.py:1089-1097): frames whose long side exceeds it are LANCZOS-downscaled
+    for the model, the output is fitted back to the content size (pipeline.py:1512-1516, bilinear)."""
+    ck, sd = _ckpt(tmp_path, "johnson", 4)
+    fr = synthetic.make_frames(1, 120, 162, seed=31)[0]
+    inp, outp = tmp_path / "in.png", tmp_path / "out.png"
+    Image.fromarray(fr).save(inp)
+    rc = P.main(["--input_image", str(inp), "--output_image", str(outp), "--model", ck, "--io_preset", "raw_255",
+                 "--inference_res", "100", "--work_dir", str(tmp_path / "w")])
+    assert rc == 0
+    pil = Image.fromarray(fr)
+    r = 100 / 162.0
+    small = np.array(pil.resize((int(round(162 * r)), int(round(120 * r))), Image.Resampling.LANCZOS))
+    with torch.no_grad():
+        y = O.FORWARDS["johnson"](sd, O.encode(O.to_tensor01(small[None]), "raw_255"))
+        o = O.fit_to_content(O.decode(y, "raw_255"), 120, 162)
+    ref = O.LabEMA(True, 0.7)(O.to_pil_u8(o.clamp(0, 1))[0])
+    got = np.array(Image.open(outp))
+    d, within2, dmax = _lsb_report(got, ref)
+    assert got.shape == (120, 162, 3) and within2 >= 0.999, (within2, dmax)
+
+
+def test_multi_gpu_orchestration_gloo_matches_single(tmp_path):
+    """The --gpus N orchestration (pipeline.py main -> one spawned process per rank, round-robin
+    frames, ordered gather to rank 0, rank-0 LAB EMA + mask/blend + save) with the gloo backend and
+    both ranks on this box's one GPU: outputs byte-identical to --gpus 1 (frame order and the EMA's
+    sequential state survive the sharding)."""
+    ck, _ = _ckpt(tmp_path, "johnson", 2)
+    frames = synthetic.make_frames(7, 48, 64, seed=90)
+    d_in = tmp_path / "in"
+    d_in.mkdir()
+    for i, f in enumerate(frames):
+        Image.fromarray(f).save(d_in / f"frame_{i + 1:04d}.png")
+    outs = {}
+    for gpus in (1, 2):
+        d_out = tmp_path / f"out{gpus}"
+        argv = ["--input_dir", str(d_in), "--output_dir", str(d_out), "--model", ck, "--io_preset", "imagenet_255",
+                "--blend", "0.9", "--smooth_alpha", "0.65", "--batch", "2", "--dtype", "bf16",
+                "--work_dir", str(tmp_path / f"w{gpus}")]
+        if gpus > 1:
+            argv += ["--gpus", "2", "--dist_backend", "gloo", "--dist_timeout", "120"]
+        assert P.main(argv) == 0
+        outs[gpus] = [np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png")) for i in range(7)]
+    for i in range(7):
+        assert np.array_equal(outs[1][i], outs[2][i]), i

@@ -96,6 +96,58 @@ def test_ordered_gather_gloo(world):
         assert vals == g  # frame j of each group is the frame itself, in order
 
 
+def _failing_worker(rank, world, port, fail_rank, fail_in, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    groups = F.plan_groups([(2, 3)] * 8, world, batch=2)
+    consumed = []
+
+    def stylize(idx):
+        if fail_in == "stylize" and rank == fail_rank and idx and idx[0] >= 4:
+            raise ValueError("bad frame")
+        if not idx:
+            return torch.empty((0, 2, 3, 3), dtype=torch.uint8)
+        return torch.stack([torch.full((2, 3, 3), f, dtype=torch.uint8) for f in idx])
+
+    def consume(g, full):
+        if fail_in == "consume" and g[0] >= 4:
+            raise OSError("disk full")
+        consumed.append(list(g))
+
+    try:
+        F.run_sharded(groups, world, rank, stylize, consume)
+        outcome = "ok"
+    except F.RankFailed:
+        outcome = "RankFailed"
+    except (ValueError, OSError) as e:
+        outcome = type(e).__name__
+    dist.destroy_process_group()
+    q.put((rank, outcome, consumed))
+
+
+@pytest.mark.parametrize("fail_in,fail_rank", [("stylize", 1), ("stylize", 0), ("consume", 0)])
+def test_sharded_failure_reaches_every_rank(fail_in, fail_rank):
+    """A rank whose stylize (or rank 0 whose consume) raises must not leave the others blocked in the
+    point-to-point exchange: every rank stops (the failing one with its own error)."""
+    import torch.multiprocessing as mp
+    world = 3
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, fail_rank, fail_in, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (o, c) for r, o, c in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+    own = "ValueError" if fail_in == "stylize" else "OSError"
+    for r in range(world):
+        assert res[r][0] == (own if r == fail_rank else "RankFailed"), (r, res[r])
+    assert res[0][1] == [[0, 1, 2, 3, 4, 5]]  # the group before the failure was consumed, nothing after
+
+
 def test_run_videos_env_mapping(monkeypatch):
     for k in list(os.environ):
         if k.startswith(("MODEL_", "IO_PRESET", "BLEND", "GPUS", "SMOOTH", "MAX_FRAMES")):

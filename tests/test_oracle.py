@@ -91,3 +91,35 @@ def test_ssim_sanity():
     assert O.ssim(a, a) == pytest.approx(1.0)
     b = np.clip(a.astype(int) + 40, 0, 255).astype(np.uint8)
     assert O.ssim(a, b) < 0.99
+
+
+@pytest.mark.parametrize("arch,h,w", [("johnson", 37, 61), ("nst", 50, 70), ("reconet", 48, 84)])
+def test_bf16_layer_restatement_matches_reference_forward(arch, h, w):
+    """oracle/bf16_layers.py (the per-layer checker of the bf16 kernels) with its rounding switched
+    off restates the reference forward: sub-pixel phase up-convs, padding modes, residual joins and
+    statistics all agree with nst_oracle.forward (itself bit-exact to the reference goldens)."""
+    from oracle import bf16_layers as B
+    sd = synthetic.make_state_dict(arch, 1)
+    x = O.encode(O.to_tensor01(synthetic.make_frames(2, h, w, seed=3)), "imagenet_255")
+    ref = O.forward(arch, sd, x)
+    with torch.no_grad():
+        y = B.forward_layers(arch, sd, x, round_bf16=False, acc=torch.float64)
+    assert y.shape == ref.shape
+    assert float((y - ref).abs().max() / ref.abs().max()) < 3e-5
+
+
+def test_bf16_layer_bands_equal_full_rows():
+    from oracle import bf16_layers as B
+    sd = synthetic.make_state_dict("nst", 2)
+    g = torch.Generator().manual_seed(0)
+    for name, cin, axis, ks, st, pad, pre, H in (("down2.conv", 32, B.ZERO, 3, 2, 1, 0, 37),
+                                                 ("up1.conv", 128, B.ZINSERT, 3, 1, 1, 0, 13),
+                                                 ("down1.conv", 3, B.ZERO_PREREFLECT, 9, 1, 4, 40, 45)):
+        x = torch.randn(1, cin, H, 47, generator=g)
+        get = lambda idx: x.index_select(2, idx)  # noqa: E731
+        W, b = sd[name + ".weight"], sd[name + ".bias"]
+        oh = 2 * H if axis == B.ZINSERT else (H + 2 * pre + 2 * pad - ks) // st + 1
+        full = B.conv_layer(get, H, 1, cin, W, b, ks, st, axis, pad, pre, True, (0, oh))
+        for r0 in (0, 6, oh - 6 - oh % 2):
+            part = B.conv_layer(get, H, 1, cin, W, b, ks, st, axis, pad, pre, True, (r0, r0 + 6))
+            assert torch.allclose(part, full[:, :, r0:r0 + 6], atol=1e-5), (name, r0)

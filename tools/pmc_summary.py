@@ -1,6 +1,6 @@
 """Per-kernel summary of tools/prof_pass.sh output (rocprofv3 CSV), averaged over dispatches.
 
-  python tools/pmc_summary.py gpurun_out/<tag> [--json out.json]
+  python tools/pmc_summary.py gpurun_out/<tag> [--json out.json] [--res-json profiles/pmc_res_conv.json]
 
 Prints per kernel: average duration (kernel-trace pass), every PMC counter averaged over its
 dispatches, and derived figures: HBM bytes (gfx950 correction: 2*FETCH_SIZE + WRITE_SIZE, KiB;
@@ -62,6 +62,29 @@ def main():
     if "--json" in sys.argv:
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
             json.dump(out, f, indent=1)
+    if "--res-json" in sys.argv:  # the dominant kernel's summary bench.py reads (keyed by the library build)
+        import hashlib
+        lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "neuralstyletransferv1_amd",
+                           "libnst_hip.so")
+        key = next(k for k in out if "wstat_kernel<8, 0," in k)
+        r = out[key]
+        res = {
+            "source": f"tools/prof_pass.sh {os.path.basename(d.rstrip('/'))} (rocprofv3 --kernel-trace --stats, then "
+                      "--pmc passes in separate runs of bench.py)",
+            "units": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half of a wide "
+                     "coalesced read stream, MI355X_MICROARCH.md HBM section)",
+            "lib_sha16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16],
+            "res_conv_kernel": key,
+            "hbm_bytes_per_launch": r.get("hbm_bytes"),
+            "fetch_size_kib": r.get("FETCH_SIZE"),
+            "write_size_kib": r.get("WRITE_SIZE"),
+            "avg_us_profiled": r.get("avg_us"),
+            "eff_clock_ghz": r.get("eff_clock_ghz"),
+            "mfma_insts_per_launch": r.get("SQ_INSTS_MFMA"),
+            "algorithmic_bytes_per_launch": 530841600,
+        }
+        with open(sys.argv[sys.argv.index("--res-json") + 1], "w") as f:
+            json.dump(res, f, indent=1)
 
 
 if __name__ == "__main__":
