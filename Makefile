@@ -4,7 +4,10 @@ ARCH ?= gfx950
 PKG := neuralstyletransferv1_amd
 CSRC := $(PKG)/csrc
 BUILD := build/obj
-CXXFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+# SLP: -fno-slp-vectorize keeps scalar f32 VALU scalar (packed f32 beside MFMAs costs extra cycles,
+# conv_ws_common.h); the VALU-heavy up-conv file measured faster with packed consume math
+SLP ?= -fno-slp-vectorize
+CXXFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off $(SLP) -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
 SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
 OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
@@ -21,6 +24,7 @@ $(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h $(C
 $(BUILD)/conv_bf16_wl.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=200000
 $(BUILD)/conv_wstat.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 $(BUILD)/conv_wphase.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
+$(BUILD)/conv_wphase.hip.o: SLP =
 $(BUILD)/conv_ws2.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 $(BUILD)/conv_ws9.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 

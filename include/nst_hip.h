@@ -236,8 +236,17 @@ int nst_profile_end(nst_handle* h, int n_layers, float* total_ms, int* launches)
 int nst_num_layers(const nst_handle* h);
 const char* nst_layer_name(const nst_handle* h, int layer);
 
-/* Gram matrix G[b] = F[b] F[b]^T / (c*hw) (utils.py:80-83), F [n,c,hw] f32 or bf16. fp32 out. */
-int nst_gram(const void* F, int dtype, int n, int c, int hw, float* G, void* stream);
+/*
+ * Gram matrix G[b] = F[b] F[b]^T / (c*hw) (utils.py:80-83 gram_matrix), F f32 or bf16, G fp32 [n,c,c].
+ * layout NST_GRAM_CHW: F [n][c][hw] (the reference's NCHW feature map); NST_GRAM_HWC: F [n][hw][c]
+ * (NHWC activations).  MFMA tiles over K slices of hw, slices summed in fixed order: bit-identical
+ * across runs.  workspace: nst_gram_workspace_bytes (0 for a single slice).
+ */
+#define NST_GRAM_CHW 0
+#define NST_GRAM_HWC 1
+int nst_gram_workspace_bytes(int n, int c, int hw, size_t* out);
+int nst_gram(const void* F, int dtype, int layout, int n, int c, int hw, float* G, void* workspace,
+             size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -35,7 +35,9 @@ EXPORTED_SYMBOLS = (
     "nst_lab_destroy", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
     "nst_profile_end", "nst_num_layers", "nst_layer_name", "nst_blend_models_u8", "nst_blend_models_lab_u8",
     "nst_mask_feather", "nst_create_ex", "nst_num_ops", "nst_op_describe", "nst_forward_capture",
+    "nst_gram_workspace_bytes",
 )
+NST_GRAM_CHW, NST_GRAM_HWC = 0, 1
 
 # nst_create_ex kernel-selection flags (include/nst_hip.h NST_KSEL_*)
 KSEL = {
@@ -100,7 +102,9 @@ def lib() -> ctypes.CDLL:
         L.nst_lab_destroy.restype = None
         L.nst_lab_ema_u8.argtypes = [vp, vp, vp, i, i, i, i, f, f, i, f, f, vp, i, vp]
         L.nst_blend_u8.argtypes = [vp, vp, vp, i, f, f, vp, i, i, i, vp]
-        L.nst_gram.argtypes = [vp, i, i, i, i, vp, vp]
+        L.nst_gram.argtypes = [vp, i, i, i, i, i, vp, vp, sz, vp]
+        L.nst_gram_workspace_bytes.argtypes = [i, i, i, ctypes.POINTER(sz)]
+        L.nst_gram_workspace_bytes.restype = i
         L.nst_blend_models_u8.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(i), ctypes.POINTER(f), i, i, i, i, vp,
                                           i, i, vp]
         L.nst_blend_models_u8.restype = i

@@ -193,12 +193,11 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
     for (int r = 0; r < C::THW; ++r) {
       const int row = r0 + r;
       const bool valid = full || (wk.oy0 + row < p.oh && wk.ox0 + px < p.ow);
-      const f32x4_t v = acc[r] + bias;
+      const f32x4_t v = add4(acc[r], bias);
       const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
       *(u32x2_t*)(smem + obase + row * C::TW * C::PIXB) = pk;
       const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
-      s1 += x;
-      s2 = __builtin_elementwise_fma(x, x, s2);
+      stat4(s1, s2, x);
     }
     const float vv[8] = {s1[0], s2[0], s1[1], s2[1], s1[2], s2[2], s1[3], s2[3]};
     float a4[4], a2[2], a1[1];

@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
     auto rows = [&](auto masked) {
 #pragma unroll
       for (int y = 0; y < C::TH; ++y) {
-        const f32x4_t va = acc[y][0] + bias0, vb = acc[y][1] + bias1;
+        const f32x4_t va = add4(acc[y][0], bias0), vb = add4(acc[y][1], bias1);
         const u32x2_t pa = {pack_bf16(va[0], va[1]), pack_bf16(va[2], va[3])};
         const u32x2_t pb = {pack_bf16(vb[0], vb[1]), pack_bf16(vb[2], vb[3])};
         *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o0) = pa;
@@ -217,10 +217,8 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
           xa = valid ? va : z;
           xb = valid ? vb : z;
         }
-        s1a += xa;
-        s2a = __builtin_elementwise_fma(xa, xa, s2a);
-        s1b += xb;
-        s2b = __builtin_elementwise_fma(xb, xb, s2b);
+        stat4(s1a, s2a, xa);
+        stat4(s1b, s2b, xb);
       }
     };
     if (wk_.oy0 + C::TH <= p.oh && wk_.ox0 + C::TW <= p.ow)

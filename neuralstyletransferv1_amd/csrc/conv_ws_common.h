@@ -8,6 +8,25 @@ namespace nst {
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
+// f32x4 epilogue arithmetic as four scalar VALU instructions.  Packed f32 VALU (v_pk_add_f32,
+// v_pk_fma_f32) costs ~22-26 extra cycles per instruction when issued beside MFMAs, scalar f32 ~0
+// (MI355X_MICROARCH.md, 'price of one filler beside MFMAs'); the library is built with
+// -fno-slp-vectorize so scalar code stays scalar.  Same per-element roundings as the vector forms.
+__device__ __forceinline__ f32x4_t add4(const f32x4_t& a, const f32x4_t& b) {
+  f32x4_t r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = a[i] + b[i];
+  return r;
+}
+// s1 += x, s2 += x * x (one fused rounding, as __builtin_elementwise_fma)
+__device__ __forceinline__ void stat4(f32x4_t& s1, f32x4_t& s2, const f32x4_t& x) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s1[i] = s1[i] + x[i];
+    s2[i] = __builtin_fmaf(x[i], x[i], s2[i]);
+  }
+}
+
 // what the fill applies to a staged input chunk
 enum WsFill { WF_NORM = 0, WF_RAW = 1, WF_RES = 2, WF_RESRN = 3 };  // IN+ReLU / identity / join / join of ReLU(IN(r))
 

@@ -319,7 +319,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
 #pragma unroll
       for (int r = 0; r < TH; ++r) {
         const bool valid = decltype(all_valid)::value || (wk.ty0 + r < p.oh && ox < p.ow);
-        const f32x4_t v = acc[r] + bias;
+        const f32x4_t v = add4(acc[r], bias);
         const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
         if constexpr (C::OST) {
           *(u32x2_t*)(smem + obase + r * C::TW * 256) = pk;
@@ -327,8 +327,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
           __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : 0x80000000u, 0, 0);
         }
         const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
-        s1 += x;
-        s2 = __builtin_elementwise_fma(x, x, s2);
+        stat4(s1, s2, x);
       }
     };
     // every tile but those on the bottom / right edge: no per-row validity

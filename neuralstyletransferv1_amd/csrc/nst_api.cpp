@@ -201,8 +201,8 @@ struct nst_handle {
 
 struct nst_lab {
   int device;
-  uint8_t* rgb2lab = nullptr;
-  uint8_t* lab2rgb = nullptr;
+  uint32_t* rgb2lab = nullptr;  // 2^24 x {L, a, b, 0}
+  uint32_t* lab2rgb = nullptr;  // 2^24 x {r, g, b, 0}
 };
 
 namespace {
@@ -1139,9 +1139,19 @@ int nst_lab_create(const uint8_t* rgb2lab, const uint8_t* lab2rgb, int device, n
   DeviceGuard guard(device);
   auto* l = new nst_lab();
   l->device = device;
-  const size_t bytes = (size_t)3 << 24;
-  int rc = upload(rgb2lab, bytes, (void**)&l->rgb2lab);
-  if (rc == NST_OK) rc = upload(lab2rgb, bytes, (void**)&l->lab2rgb);
+  // widen the 3-byte entries to one dword each (a lookup is one aligned 4-byte load on the device)
+  const size_t entries = (size_t)1 << 24;
+  std::vector<uint32_t> wide(entries);
+  auto widen = [&](const uint8_t* t) {
+    for (size_t i = 0; i < entries; ++i)
+      wide[i] = (uint32_t)t[3 * i] | ((uint32_t)t[3 * i + 1] << 8) | ((uint32_t)t[3 * i + 2] << 16);
+  };
+  widen(rgb2lab);
+  int rc = upload(wide.data(), entries * 4, (void**)&l->rgb2lab);
+  if (rc == NST_OK) {
+    widen(lab2rgb);
+    rc = upload(wide.data(), entries * 4, (void**)&l->lab2rgb);
+  }
   if (rc != NST_OK) { nst_lab_destroy(l); return rc; }
   *out = l;
   return NST_OK;
@@ -1208,17 +1218,32 @@ int nst_blend_u8(const uint8_t* styled, const uint8_t* orig, const float* mask, 
   return NST_OK;
 }
 
-int nst_gram(const void* F, int dtype, int n, int c, int hw, float* G, void* stream) {
-  if (!F || !G || n <= 0 || c <= 0 || hw <= 0 || (dtype != NST_DT_F32 && dtype != NST_DT_BF16)) {
+int nst_gram_workspace_bytes(int n, int c, int hw, size_t* out) {
+  if (n <= 0 || c <= 0 || hw <= 0 || !out) { set_error("nst_gram_workspace_bytes: invalid arguments"); return NST_E_INVALID; }
+  *out = gram_workspace_bytes(n, c, hw);
+  return NST_OK;
+}
+
+int nst_gram(const void* F, int dtype, int layout, int n, int c, int hw, float* G, void* workspace,
+             size_t workspace_bytes, void* stream) {
+  if (!F || !G || n <= 0 || c <= 0 || hw <= 0 || (dtype != NST_DT_F32 && dtype != NST_DT_BF16) ||
+      (layout != NST_GRAM_CHW && layout != NST_GRAM_HWC)) {
     set_error("nst_gram: invalid arguments");
     return NST_E_INVALID;
   }
   const int vec = dtype == NST_DT_BF16 ? 8 : 4;
-  if (hw % vec != 0 || ((uintptr_t)F % 16) != 0) {
-    set_error("nst_gram: h*w must be a multiple of " + std::to_string(vec) + " and F 16-byte aligned");
+  const int minor = layout == NST_GRAM_CHW ? hw : c;  // the contiguous axis of F's 16-byte loads
+  if (minor % vec != 0 || ((uintptr_t)F % 16) != 0) {
+    set_error("nst_gram: the contiguous axis (" + std::string(layout == NST_GRAM_CHW ? "h*w" : "c") +
+              ") must be a multiple of " + std::to_string(vec) + " and F 16-byte aligned");
     return NST_E_SHAPE;
   }
-  hipError_t e = launch_gram(F, dtype, n, c, hw, G, (hipStream_t)stream);
+  const size_t need = gram_workspace_bytes(n, c, hw);
+  if (need > 0 && (!workspace || workspace_bytes < need)) {
+    set_error("nst_gram: workspace too small (" + std::to_string(workspace_bytes) + " < " + std::to_string(need) + ")");
+    return NST_E_WORKSPACE;
+  }
+  hipError_t e = launch_gram(F, dtype, layout == NST_GRAM_HWC, n, c, hw, G, workspace, (hipStream_t)stream);
   if (e != hipSuccess) { set_error(std::string("gram launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
   return NST_OK;
 }

@@ -116,10 +116,11 @@ constexpr int NST_MAX_MODELS = 8;  // slots A..H (pipeline.py model_b..model_h)
 hipError_t launch_blend_models_u8(const float* const* ys, const float (*dp)[3], const float (*dq)[3],
                                   const float (*dr)[3], const float (*ds)[3], const int (*perm)[3], const float* wts,
                                   int m, int n, int h, int w, uint8_t* out, int oh, int ow, hipStream_t st);
-hipError_t launch_lab_ema(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* in,
+// LAB tables on the device: 2^24 entries of {x, y, z, 0} bytes (one dword per lookup)
+hipError_t launch_lab_ema(const uint32_t* rgb2lab, const uint32_t* lab2rgb, const uint8_t* in,
                           uint8_t* out, int n, int hw, int sl, float a, float oma, int sc, float ca,
                           float coma, float* state, int first, hipStream_t st);
-hipError_t launch_lab_blend(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* const* frames,
+hipError_t launch_lab_blend(const uint32_t* rgb2lab, const uint32_t* lab2rgb, const uint8_t* const* frames,
                             const float* wrest, int nrest, float wL, float wab, size_t npix, uint8_t* out,
                             hipStream_t st);
 hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigma, float* tmp, float* alpha,
@@ -127,6 +128,8 @@ hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigm
 hipError_t launch_prepad_encode(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st);
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,
                         float omb, uint8_t* out, int n, int hw, hipStream_t st);
-hipError_t launch_gram(const void* F, int dtype, int n, int c, int hw, float* G, hipStream_t st);
+size_t gram_workspace_bytes(int n, int c, int hw);
+hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, int hw, float* G, void* ws,
+                       hipStream_t st);
 
 }  // namespace nst

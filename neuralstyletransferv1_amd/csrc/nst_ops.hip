@@ -2,6 +2,8 @@
 // output decode + bilinear fit, LAB temporal smoothing, original/mask blend, Gram matrix.
 // All fp32 elementwise arithmetic is written op-by-op in the reference's order and the
 // library is built with -ffp-contract=off, so no FMA contraction changes a rounding.
+#include <algorithm>
+
 #include "nst_internal.h"
 #include "nst_hip.h"
 
@@ -370,34 +372,27 @@ hipError_t launch_blend_models_u8(const float* const* ys, const float (*dp)[3], 
 // ---------------------------------------------------------------------------------------
 // LAB temporal smoothing (pipeline.py:1942-1978): Pillow RGB->LAB, float32 EMA of L (and
 // optionally a/b bytes), np.clip(0,255), astype(uint8) truncation, LAB->RGB.  The two
-// LittleCMS transforms are exact 2^24-entry LUT gathers (tables made from Pillow itself).
-// One thread per pixel walks the batch in frame order (the EMA state is per pixel).
-// Byte triples are read through volatile pointers: with ordinary loads hipcc (ROCm 7.2) merges
-// adjacent bytes into one 16-bit load and then shifts the pair left by 16 without masking the
-// upper byte ((uint32_t)b[0] << 16 came out as (b[0] | b[1] << 8) << 16), corrupting the
-// 24-bit table index (an out-of-range gather).
-__device__ __forceinline__ void load3(const uint8_t* q, uint32_t& x, uint32_t& y, uint32_t& z) {
-  const volatile uint8_t* v = q;
-  x = v[0];
-  y = v[1];
-  z = v[2];
+// LittleCMS transforms are exact 2^24-entry LUT gathers (tables made from Pillow itself), held on
+// the device as 4-byte entries {x, y, z, 0} so one dword load is one lookup.
+// A thread owns 4 consecutive pixels (three aligned dwords of each frame) and walks the batch in
+// frame order in chunks of LAB_NF frames: the chunk's loads and rgb->lab gathers are issued
+// together (independent across frames), then the sequential EMA (registers only), then the
+// lab->rgb gathers and stores together -- three dependent memory rounds per chunk instead of two
+// per frame.  The ragged tail (hw % 4) takes the same arithmetic one pixel at a time.
+constexpr int LAB_NF = 8;
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[3], int i) {  // byte i of 12 packed bytes
+  return (w[i >> 2] >> (8 * (i & 3))) & 0xffu;
 }
-__global__ __launch_bounds__(256) void lab_ema_kernel(const uint8_t* __restrict__ rgb2lab,
-                                                      const uint8_t* __restrict__ lab2rgb,
-                                                      const uint8_t* in, uint8_t* out, int n, int hw,
-                                                      int sl, float a, float oma, int sc, float ca,
-                                                      float coma, float* __restrict__ state, int first) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= hw) return;
-  float pL = state[p], pa = state[hw + p], pb = state[2 * hw + p];
-  for (int f = 0; f < n; ++f) {
-    const size_t idx = ((size_t)f * hw + p) * 3;
-    uint32_t r, g, b, l0, l1, l2;
-    load3(in + idx, r, g, b);
-    load3(rgb2lab + (size_t)((r << 16) | (g << 8) | b) * 3, l0, l1, l2);
-    float L = (float)l0, A = (float)l1, Bc = (float)l2;
+
+struct LabEma {
+  int sl, sc;
+  float a, oma, ca, coma;
+  // one pixel, one frame: lab (x = L, y = a, z = b bytes) -> smoothed lab index; state updated
+  __device__ __forceinline__ uint32_t step(uint32_t lab, bool seed, float& pL, float& pa, float& pb) const {
+    float L = (float)(lab & 0xffu), A = (float)((lab >> 8) & 0xffu), Bc = (float)((lab >> 16) & 0xffu);
     if (sl) {
-      if (first && f == 0) pL = L;
+      if (seed) pL = L;
       const float t0 = a * L;
       const float t1 = oma * pL;
       const float Ls = t0 + t1;
@@ -405,7 +400,7 @@ __global__ __launch_bounds__(256) void lab_ema_kernel(const uint8_t* __restrict_
       L = fminf(fmaxf(Ls, 0.f), 255.f);
     }
     if (sc) {
-      if (first && f == 0) { pa = A; pb = Bc; }
+      if (seed) { pa = A; pb = Bc; }
       const float as = ca * A + coma * pa;
       const float bs = ca * Bc + coma * pb;
       pa = as;
@@ -413,22 +408,106 @@ __global__ __launch_bounds__(256) void lab_ema_kernel(const uint8_t* __restrict_
       A = fminf(fmaxf(as, 0.f), 255.f);
       Bc = fminf(fmaxf(bs, 0.f), 255.f);
     }
-    const uint32_t li = ((uint32_t)(uint8_t)L << 16) | ((uint32_t)(uint8_t)A << 8) | (uint32_t)(uint8_t)Bc;
-    const uint8_t* o = lab2rgb + (size_t)li * 3;
-    out[idx] = o[0];
-    out[idx + 1] = o[1];
-    out[idx + 2] = o[2];
+    return ((uint32_t)(uint8_t)L << 16) | ((uint32_t)(uint8_t)A << 8) | (uint32_t)(uint8_t)Bc;
   }
-  state[p] = pL;
-  state[hw + p] = pa;
-  state[2 * hw + p] = pb;
-}
+};
 
-hipError_t launch_lab_ema(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* in, uint8_t* out,
+__global__ __launch_bounds__(256) void lab_ema_kernel(const uint32_t* __restrict__ rgb2lab,
+                                                      const uint32_t* __restrict__ lab2rgb, const uint8_t* in,
+                                                      uint8_t* out, int n, int hw, LabEma e,
+                                                      float* __restrict__ state, int first) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p0 = 4 * t;
+  if (p0 >= hw) return;
+  const int np = min(4, hw - p0);
+  float pL[4], pa[4], pb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = min(p0 + k, hw - 1);
+    pL[k] = e.sl ? state[p] : 0.f;
+    pa[k] = e.sc ? state[hw + p] : 0.f;
+    pb[k] = e.sc ? state[2 * hw + p] : 0.f;
+  }
+  if (np == 4 && (hw & 3) == 0) {  // every frame's 4-pixel groups dword-aligned
+    for (int f0 = 0; f0 < n; f0 += LAB_NF) {
+      const int nf = min(LAB_NF, n - f0);
+      uint32_t w[LAB_NF][3], lab[LAB_NF][4];
+#pragma unroll
+      for (int f = 0; f < LAB_NF; ++f) {
+        if (f < nf) {
+          const uint32_t* src = (const uint32_t*)(in + ((size_t)(f0 + f) * hw + p0) * 3);
+          w[f][0] = src[0]; w[f][1] = src[1]; w[f][2] = src[2];
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < LAB_NF; ++f) {
+        if (f < nf) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            lab[f][k] = rgb2lab[(byte_of(w[f], 3 * k) << 16) | (byte_of(w[f], 3 * k + 1) << 8) | byte_of(w[f], 3 * k + 2)];
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < LAB_NF; ++f) {
+        if (f < nf) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) lab[f][k] = e.step(lab[f][k], first && f0 + f == 0, pL[k], pa[k], pb[k]);
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < LAB_NF; ++f) {
+        if (f < nf) {
+          uint32_t rgb[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) rgb[k] = lab2rgb[lab[f][k]];
+          // 4 pixels x {r, g, b} -> 12 bytes
+          uint32_t o[3] = {0u, 0u, 0u};
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const int i = 3 * k + c;
+              o[i >> 2] |= ((rgb[k] >> (8 * c)) & 0xffu) << (8 * (i & 3));
+            }
+          uint32_t* dst = (uint32_t*)(out + ((size_t)(f0 + f) * hw + p0) * 3);
+          dst[0] = o[0]; dst[1] = o[1]; dst[2] = o[2];
+        }
+      }
+    }
+  } else {
+    for (int k = 0; k < np; ++k) {
+      for (int f = 0; f < n; ++f) {
+        const size_t idx = ((size_t)f * hw + p0 + k) * 3;
+        const volatile uint8_t* v = in + idx;  // single bytes (see the note on byte merging below)
+        const uint32_t r = v[0], g = v[1], b = v[2];
+        const uint32_t li = e.step(rgb2lab[(r << 16) | (g << 8) | b], first && f == 0, pL[k], pa[k], pb[k]);
+        const uint32_t rgb = lab2rgb[li];
+        out[idx] = (uint8_t)(rgb & 0xffu);
+        out[idx + 1] = (uint8_t)((rgb >> 8) & 0xffu);
+        out[idx + 2] = (uint8_t)((rgb >> 16) & 0xffu);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < np) {
+      if (e.sl) state[p0 + k] = pL[k];
+      if (e.sc) { state[hw + p0 + k] = pa[k]; state[2 * hw + p0 + k] = pb[k]; }
+    }
+  }
+}
+// Note on byte merging: with ordinary uint8_t loads of adjacent bytes hipcc (ROCm 7.2) once merged
+// them into one 16-bit load and shifted the pair left by 16 without masking the upper byte,
+// corrupting a 24-bit table index; the tail reads single bytes through volatile pointers, the main
+// path extracts bytes from dwords explicitly.
+
+hipError_t launch_lab_ema(const uint32_t* rgb2lab, const uint32_t* lab2rgb, const uint8_t* in, uint8_t* out,
                           int n, int hw, int sl, float a, float oma, int sc, float ca, float coma,
                           float* state, int first, hipStream_t st) {
-  hipLaunchKernelGGL(lab_ema_kernel, dim3((unsigned)((hw + 255) / 256)), dim3(256), 0, st, rgb2lab, lab2rgb,
-                     in, out, n, hw, sl, a, oma, sc, ca, coma, state, first);
+  const LabEma e{sl, sc, a, oma, ca, coma};
+  const int threads = (hw + 3) / 4;
+  hipLaunchKernelGGL(lab_ema_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, rgb2lab, lab2rgb,
+                     in, out, n, hw, e, state, first);
   return hipGetLastError();
 }
 
@@ -441,15 +520,18 @@ struct LabBlendArgs {
   const uint8_t* f[NST_MAX_MODELS];  // f[0] = model A's uint8 frame, f[1..] = the others
   float w[NST_MAX_MODELS];           // w[i] multiplies f[i + 1]
 };
-__global__ __launch_bounds__(256) void lab_blend_kernel(const uint8_t* __restrict__ rgb2lab,
-                                                        const uint8_t* __restrict__ lab2rgb, LabBlendArgs a,
+__global__ __launch_bounds__(256) void lab_blend_kernel(const uint32_t* __restrict__ rgb2lab,
+                                                        const uint32_t* __restrict__ lab2rgb, LabBlendArgs a,
                                                         int nrest, float wL, float wab, size_t npix, uint8_t* out) {
   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npix) return;
   auto lab_of = [&](const uint8_t* f, uint32_t& L, uint32_t& A, uint32_t& B) {
-    uint32_t r, g, b;
-    load3(f + p * 3, r, g, b);
-    load3(rgb2lab + (size_t)((r << 16) | (g << 8) | b) * 3, L, A, B);
+    const volatile uint8_t* v = f + p * 3;
+    const uint32_t r = v[0], g = v[1], b = v[2];
+    const uint32_t lab = rgb2lab[(r << 16) | (g << 8) | b];
+    L = lab & 0xffu;
+    A = (lab >> 8) & 0xffu;
+    B = (lab >> 16) & 0xffu;
   };
   uint32_t La, Aa, Ba;
   lab_of(a.f[0], La, Aa, Ba);
@@ -463,21 +545,21 @@ __global__ __launch_bounds__(256) void lab_blend_kernel(const uint8_t* __restric
   const float A = fminf(fmaxf(wL * (float)Aa + wab * am, 0.f), 255.f);
   const float B = fminf(fmaxf(wL * (float)Ba + wab * bm, 0.f), 255.f);
   const uint32_t li = (La << 16) | ((uint32_t)(uint8_t)A << 8) | (uint32_t)(uint8_t)B;
-  uint32_t r, g, b;
-  load3(lab2rgb + (size_t)li * 3, r, g, b);
-  out[p * 3] = (uint8_t)r;
-  out[p * 3 + 1] = (uint8_t)g;
-  out[p * 3 + 2] = (uint8_t)b;
+  const uint32_t rgb = lab2rgb[li];
+  out[p * 3] = (uint8_t)(rgb & 0xffu);
+  out[p * 3 + 1] = (uint8_t)((rgb >> 8) & 0xffu);
+  out[p * 3 + 2] = (uint8_t)((rgb >> 16) & 0xffu);
 }
 
-hipError_t launch_lab_blend(const uint8_t* rgb2lab, const uint8_t* lab2rgb, const uint8_t* const* frames,
+hipError_t launch_lab_blend(const uint32_t* rgb2lab, const uint32_t* lab2rgb, const uint8_t* const* frames,
                             const float* wrest, int nrest, float wL, float wab, size_t npix, uint8_t* out,
                             hipStream_t st) {
   if (nrest < 0 || nrest + 1 > NST_MAX_MODELS) return hipErrorInvalidValue;
   LabBlendArgs a;
-  for (int i = 0; i < NST_MAX_MODELS; ++i) { a.f[i] = nullptr; a.w[i] = 0.f; }
-  for (int i = 0; i <= nrest; ++i) a.f[i] = frames[i];
-  for (int i = 0; i < nrest; ++i) a.w[i] = wrest[i];
+  for (int i = 0; i < NST_MAX_MODELS; ++i) {
+    a.f[i] = i <= nrest ? frames[i] : nullptr;
+    a.w[i] = i < nrest ? wrest[i] : 0.f;
+  }
   hipLaunchKernelGGL(lab_blend_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, rgb2lab, lab2rgb, a,
                      nrest, wL, wab, npix, out);
   return hipGetLastError();
@@ -595,78 +677,211 @@ hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, i
 }
 
 // ---------------------------------------------------------------------------------------
-// Gram matrix G = F F^T / (c*h*w)  (utils.py:80-83) on MFMA.
-// F [n][c][hw] row-major.  One workgroup = one 32x32 tile of G (4 waves = 2x2 16x16 tiles)
-// over a KCH-long slice of hw; slices accumulate with fp32 atomics into G (zeroed first),
-// then a scale pass divides by c*hw.
+// Gram matrix G = F F^T / (c*h*w)  (utils.py:80-83) on MFMA, deterministic.
+// F per batch element: [c][hw] (GRAM_CHW, the reference's layout) or [hw][c] (GRAM_HWC, the engine's
+// NHWC activations).  Workgroup = one TI x TI tile of G over one K slice (hw range) of KB-pixel
+// fills: the fill is staged channel-major in LDS ([row][KB pixels], padded rows: conflict-free
+// fragment reads; an HWC fill is transposed on its way in), the next fill prefetched into
+// registers during the MFMAs.  8 waves in a 2 x 4 grid of (TI/2) x (TI/4) sub-blocks.  K slices
+// write fp32 partial tiles; a second pass sums the slices in fixed order and divides by c*hw (one
+// slice: the first pass writes G directly).  No atomics: bit-identical across runs.
 template <typename T>
-__global__ __launch_bounds__(256) void gram_kernel(const T* __restrict__ F, int c, int hw, int kchunk,
-                                                   float* __restrict__ G) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+struct GramT;
+template <>
+struct GramT<__bf16> {
+  static constexpr int KM = 32, VEC = 8, KB = 64, RS = 160;  // MFMA K, elements per 16 B, pixels per fill, row bytes
+};
+template <>
+struct GramT<float> {
+  static constexpr int KM = 4, VEC = 4, KB = 64, RS = 272;
+};
+
+template <typename T, int TI, bool HWC>
+__global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int c, int hw, int kslice,
+                                                   float* __restrict__ out, size_t slice_stride) {
+  using GT = GramT<T>;
+  constexpr int KB = GT::KB, RS = GT::RS, VEC = GT::VEC, KM = GT::KM;
+  constexpr int MI = TI / 32, MJ = TI / 64;                // 16 x 16 fragments per wave
+  constexpr int CPS = TI * KB / VEC;                        // 16-B chunks per side and fill
+  constexpr int CPT = (CPS + 511) / 512;                    // per thread
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tt = (c + TI - 1) / TI;
+  const int ti = blockIdx.x / tt, tj = blockIdx.x % tt;
   const int b = blockIdx.z;
-  const int ti = blockIdx.x / ((c + 31) / 32), tj = blockIdx.x % ((c + 31) / 32);
-  const int i0 = ti * 32 + (wave >> 1) * 16, j0 = tj * 32 + (wave & 1) * 16;
-  const int row = lane & 15, g = lane >> 4;
-  const int ri = min(i0 + row, c - 1), rj = min(j0 + row, c - 1);
-  const T* Fi = F + ((size_t)b * c + ri) * hw;
-  const T* Fj = F + ((size_t)b * c + rj) * hw;
-  const int k0 = blockIdx.y * kchunk, k1 = min(hw, k0 + kchunk);
-  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (sizeof(T) == 2) {
-    int k = k0;
-    for (; k + 32 <= k1; k += 32) {
-      const uint4 a = *(const uint4*)(Fi + k + 8 * g), bb = *(const uint4*)(Fj + k + 8 * g);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, bb), acc, 0, 0, 0);
-    }
-    for (; k < k1; k += 4) {  // tail (hw % 32): 4 at a time through the f32 MFMA
-      const int kk = k + g;
-      const float av = kk < k1 ? (float)Fi[kk] : 0.f, bv = kk < k1 ? (float)Fj[kk] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-    }
-  } else {
-    int k = k0;
-    for (; k + 16 <= k1; k += 16) {
-      const float4 a = *(const float4*)(Fi + k + 4 * g), bb = *(const float4*)(Fj + k + 4 * g);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bb.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bb.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bb.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bb.w, acc, 0, 0, 0);
-    }
-    for (; k < k1; k += 4) {
-      const int kk = k + g;
-      const float av = kk < k1 ? Fi[kk] : 0.f, bv = kk < k1 ? Fj[kk] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-    }
-  }
-  // C[row = 4g + r][col = lane&15]: row -> i, col -> j
-  const int j = j0 + (lane & 15);
+  const bool diag = ti == tj;
+  const int i0 = ti * TI, j0 = tj * TI;
+  const int k0 = blockIdx.y * kslice, k1 = min(hw, k0 + kslice);
+  const T* Fb = F + (size_t)b * c * hw;
+  char* sa = gsm;
+  char* sb = diag ? gsm : gsm + TI * RS;
+
+  // chunk q of a side: CHW: row q / (KB/VEC), pixels (q % (KB/VEC)) * VEC ..; HWC: pixel q / (TI/VEC),
+  // channels (q % (TI/VEC)) * VEC ..
+  auto load = [&](int r0, int k, int q) -> uint4 {
+    int row, px;
+    if constexpr (HWC) { px = q / (TI / VEC); row = (q % (TI / VEC)) * VEC; }
+    else { row = q / (KB / VEC); px = (q % (KB / VEC)) * VEC; }
+    const int gr = r0 + row, gk = k + px;
+    if (q >= CPS || gr >= c || gk >= k1) return make_uint4(0u, 0u, 0u, 0u);  // hw % VEC == 0 (checked)
+    const T* src = HWC ? Fb + (size_t)gk * c + gr : Fb + (size_t)gr * hw + gk;
+    return *(const uint4*)src;
+  };
+  auto store = [&](char* side, int q, const uint4& v) {
+    if (q >= CPS) return;
+    if constexpr (HWC) {
+      const int px = q / (TI / VEC), row = (q % (TI / VEC)) * VEC;
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      if constexpr (sizeof(T) == 2) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = i0 + 4 * g + r;
-    if (i < c && j < c) atomicAdd(&G[((size_t)b * c + i) * c + j], acc[r]);
+        for (int e = 0; e < 8; ++e)
+          *(uint16_t*)(side + (row + e) * RS + px * 2) = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) *(uint32_t*)(side + (row + e) * RS + px * 4) = w[e];
+      }
+    } else {
+      const int row = q / (KB / VEC), px = (q % (KB / VEC)) * VEC;
+      *(uint4*)(side + row * RS + px * (int)sizeof(T)) = v;
+    }
+  };
+
+  const int wr = wv >> 2, wc = wv & 3;
+  const int ra = wr * (TI / 2), cb = wc * (TI / 4);  // this wave's rows / cols inside the tile
+  const int row = lane & 15, g = lane >> 4;
+  f32x4_t acc[MI][MJ];
+#pragma unroll
+  for (int m = 0; m < MI; ++m)
+#pragma unroll
+    for (int n = 0; n < MJ; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  uint4 pa[CPT], pb[CPT];
+#pragma unroll
+  for (int t = 0; t < CPT; ++t) {
+    pa[t] = load(i0, k0, t * 512 + tid);
+    if (!diag) pb[t] = load(j0, k0, t * 512 + tid);
   }
+  for (int k = k0; k < k1; k += KB) {
+    __syncthreads();  // the previous fill's fragment reads are done
+#pragma unroll
+    for (int t = 0; t < CPT; ++t) {
+      store(sa, t * 512 + tid, pa[t]);
+      if (!diag) store(sb, t * 512 + tid, pb[t]);
+    }
+    __syncthreads();
+    if (k + KB < k1) {
+#pragma unroll
+      for (int t = 0; t < CPT; ++t) {
+        pa[t] = load(i0, k + KB, t * 512 + tid);
+        if (!diag) pb[t] = load(j0, k + KB, t * 512 + tid);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < KB; kk += KM) {
+      if constexpr (sizeof(T) == 2) {
+        uint4 fa[MI], fb[MJ];
+#pragma unroll
+        for (int m = 0; m < MI; ++m) fa[m] = *(const uint4*)(sa + (ra + 16 * m + row) * RS + (kk + 8 * g) * 2);
+#pragma unroll
+        for (int n = 0; n < MJ; ++n) fb[n] = *(const uint4*)(sb + (cb + 16 * n + row) * RS + (kk + 8 * g) * 2);
+#pragma unroll
+        for (int m = 0; m < MI; ++m)
+#pragma unroll
+          for (int n = 0; n < MJ; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[m]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[n]), acc[m][n], 0, 0, 0);
+      } else {
+        float fa[MI], fb[MJ];
+#pragma unroll
+        for (int m = 0; m < MI; ++m) fa[m] = *(const float*)(sa + (ra + 16 * m + row) * RS + (kk + g) * 4);
+#pragma unroll
+        for (int n = 0; n < MJ; ++n) fb[n] = *(const float*)(sb + (cb + 16 * n + row) * RS + (kk + g) * 4);
+#pragma unroll
+        for (int m = 0; m < MI; ++m)
+#pragma unroll
+          for (int n = 0; n < MJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[m], fb[n], acc[m][n], 0, 0, 0);
+      }
+    }
+  }
+  // C[4g + r][lane & 15] of fragment (m, n): G row i0 + ra + 16m + 4g + r, col j0 + cb + 16n + (lane & 15)
+  float* o = out + (size_t)blockIdx.y * slice_stride + (size_t)b * c * c;
+#pragma unroll
+  for (int m = 0; m < MI; ++m)
+#pragma unroll
+    for (int n = 0; n < MJ; ++n) {
+      const int j = j0 + cb + 16 * n + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + ra + 16 * m + 4 * g + r;
+        if (i < c && j < c) o[(size_t)i * c + j] = acc[m][n][r];
+      }
+    }
 }
 
-__global__ void gram_scale_kernel(float* G, size_t total, float denom) {
+// G = (sum over the K slices, in slice order) / (c*hw)
+__global__ void gram_reduce_kernel(const float* __restrict__ part, int slices, size_t slice_stride, float denom,
+                                   float* __restrict__ G) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < total) G[i] = G[i] / denom;
+  if (i >= slice_stride) return;
+  float s = part[i];
+  for (int k = 1; k < slices; ++k) s += part[(size_t)k * slice_stride + i];
+  G[i] = s / denom;
 }
 
-hipError_t launch_gram(const void* F, int dtype, int n, int c, int hw, float* G, hipStream_t st) {
-  const size_t total = (size_t)n * c * c;
-  hipError_t e = hipMemsetAsync(G, 0, total * sizeof(float), st);
+namespace {
+struct GramPlan {
+  int ti, tt, slices, kslice;
+  size_t ws_bytes;
+};
+GramPlan gram_plan(int n, int c, int hw) {
+  GramPlan g;
+  g.ti = c <= 64 ? 64 : (c <= 128 ? 128 : 256);
+  g.tt = (c + g.ti - 1) / g.ti;
+  const int blocks = g.tt * g.tt * n;
+  const int fills = (hw + 63) / 64;
+  g.slices = std::max(1, std::min(fills, (512 + blocks - 1) / blocks));
+  g.kslice = ((fills + g.slices - 1) / g.slices) * 64;
+  g.slices = (hw + g.kslice - 1) / g.kslice;
+  g.ws_bytes = g.slices > 1 ? (size_t)g.slices * n * c * c * sizeof(float) : 0;
+  return g;
+}
+}  // namespace
+
+size_t gram_workspace_bytes(int n, int c, int hw) { return gram_plan(n, c, hw).ws_bytes; }
+
+hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, int hw, float* G, void* ws,
+                       hipStream_t st) {
+  const GramPlan g = gram_plan(n, c, hw);
+  const size_t slice = (size_t)n * c * c;
+  const float denom = (float)((double)c * (double)hw);
+  float* dst = g.slices > 1 ? (float*)ws : G;  // one slice: the reduce pass divides G in place
+  dim3 grid(g.tt * g.tt, g.slices, n);
+  const int rs = dtype == NST_DT_BF16 ? GramT<__bf16>::RS : GramT<float>::RS;
+  const size_t lds = (size_t)2 * g.ti * rs;
+#define NST_GRAM_GO(T, TI, HWC)                                                                          \
+  do {                                                                                                   \
+    static const hipError_t attr = hipFuncSetAttribute((const void*)gram_kernel<T, TI, HWC>,            \
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+    (void)attr;                                                                                          \
+    hipLaunchKernelGGL((gram_kernel<T, TI, HWC>), grid, dim3(512), lds, st, (const T*)F, c, hw, g.kslice, dst, slice); \
+  } while (0)
+#define NST_GRAM_TI(T, HWC)                      \
+  do {                                           \
+    if (g.ti == 64) NST_GRAM_GO(T, 64, HWC);     \
+    else if (g.ti == 128) NST_GRAM_GO(T, 128, HWC); \
+    else NST_GRAM_GO(T, 256, HWC);               \
+  } while (0)
+  if (dtype == NST_DT_BF16) {
+    if (layout_hwc) NST_GRAM_TI(__bf16, true); else NST_GRAM_TI(__bf16, false);
+  } else {
+    if (layout_hwc) NST_GRAM_TI(float, true); else NST_GRAM_TI(float, false);
+  }
+#undef NST_GRAM_TI
+#undef NST_GRAM_GO
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int tiles = ((c + 31) / 32) * ((c + 31) / 32);
-  const int kchunk = 2048;
-  dim3 grid(tiles, (hw + kchunk - 1) / kchunk, n);
-  if (dtype == NST_DT_BF16)
-    hipLaunchKernelGGL(gram_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)F, c, hw, kchunk, G);
-  else
-    hipLaunchKernelGGL(gram_kernel<float>, grid, dim3(256), 0, st, (const float*)F, c, hw, kchunk, G);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(gram_scale_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, G, total,
-                     (float)((double)c * (double)hw));
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((slice + 255) / 256)), dim3(256), 0, st, dst, g.slices, slice,
+                     denom, G);
   return hipGetLastError();
 }
 

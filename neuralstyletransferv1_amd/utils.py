@@ -23,8 +23,18 @@ def gram_matrix(feature_map: torch.Tensor) -> torch.Tensor:
         feature_map = feature_map.to(torch.float32)
         dt = _lib.NST_DT_F32
     f = feature_map.contiguous()
+    return gram_raw(f, dt, _lib.NST_GRAM_CHW, n, c, h * w)
+
+
+def gram_raw(f: torch.Tensor, dt: int, layout: int, n: int, c: int, hw: int) -> torch.Tensor:
+    """nst_gram on a contiguous device buffer (CHW or HWC per batch element) -> [n,c,c] fp32."""
+    import ctypes
     G = torch.empty((n, c, c), dtype=torch.float32, device=f.device)
-    check(lib().nst_gram(f.data_ptr(), dt, n, c, h * w, G.data_ptr(), _lib.stream_ptr(f.device)), "nst_gram")
+    need = ctypes.c_size_t()
+    check(lib().nst_gram_workspace_bytes(n, c, hw, ctypes.byref(need)), "nst_gram_workspace_bytes")
+    ws = torch.empty(max(need.value, 16), dtype=torch.uint8, device=f.device)
+    check(lib().nst_gram(f.data_ptr(), dt, layout, n, c, hw, G.data_ptr(), ws.data_ptr(), ws.numel(),
+                         _lib.stream_ptr(f.device)), "nst_gram")
     return G
 
 

@@ -32,7 +32,7 @@ def test_argument_validation_without_gpu():
     oh, ow = ctypes.c_int(), ctypes.c_int()
     assert lib.nst_output_hw(None, 8, 8, ctypes.byref(oh), ctypes.byref(ow)) == -1
     assert lib.nst_forward(None, None, 0, 1, 8, 8, 0, None, 0, None, 0, None) == -1
-    assert lib.nst_gram(None, 0, 1, 1, 1, None, None) == -1
+    assert lib.nst_gram(None, 0, 0, 1, 1, 1, None, None, 0, None) == -1
 
 
 def test_presets_table_matches_header():

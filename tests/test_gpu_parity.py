@@ -124,6 +124,19 @@ def test_lab_ema_bit_exact_sequence():
         out = np.concatenate(out)
         for i in range(5):
             assert np.array_equal(out[i], ref(frames[i])), (sl, a, sc, ca, i)
+    # a ragged frame (h*w % 4 == 1: the per-pixel tail path) and 11 frames in one call (two chunks)
+    frames = synthetic.make_frames(11, 37, 61, seed=19)
+    for sl, a, sc, ca in ((True, 0.65, True, 0.85), (True, 0.7, False, 0.85)):
+        gpu = LabSmoother("cuda", sl, a, sc, ca)
+        ref = O.LabEMA(sl, a, sc, ca)
+        out = gpu(torch.from_numpy(frames).cuda()).cpu().numpy()
+        for i in range(11):
+            assert np.array_equal(out[i], ref(frames[i])), ("ragged", sl, a, sc, ca, i)
+    frames = synthetic.make_frames(11, 40, 64, seed=20)  # aligned: the 4-pixel path over two chunks
+    gpu, ref = LabSmoother("cuda", True, 0.65, True, 0.85), O.LabEMA(True, 0.65, True, 0.85)
+    out = gpu(torch.from_numpy(frames).cuda()).cpu().numpy()
+    for i in range(11):
+        assert np.array_equal(out[i], ref(frames[i])), ("chunks", i)
 
 
 def test_blend_and_mask_bit_exact():
@@ -150,6 +163,36 @@ def test_gram_vs_reference_golden():
     assert np.abs(G - z["G"]).max() / np.abs(z["G"]).max() < 1e-5
     Gb = gram_matrix(F.to(torch.bfloat16)).cpu().numpy()
     assert np.abs(Gb - z["G"]).max() / np.abs(z["G"]).max() < 2e-2
+
+
+@pytest.mark.parametrize("c,hw", [(64, 512 * 512), (128, 256 * 256), (256, 128 * 128), (512, 64 * 64), (512, 32 * 32),
+                                  (48, 384), (200, 1000)])
+def test_gram_vgg_shapes_deterministic(c, hw):
+    """nst_gram at the VGG-19 style layers of a 512x512 image (relu1_1..relu5_1: c = 64..512, hw =
+    512^2 / 4^k) and ragged shapes: fp32 within 1e-5 of an fp64 Gram (utils.py:80-83 arithmetic);
+    bf16 within 1e-5 of the fp64 Gram of the bf16-rounded features (products exact, fp32
+    accumulation); bit-identical across runs and between the CHW and HWC layouts."""
+    from neuralstyletransferv1_amd import _lib
+    from neuralstyletransferv1_amd.utils import gram_matrix, gram_raw
+    g = torch.Generator().manual_seed(c + hw)
+    F = torch.relu(torch.randn(2, c, hw, generator=g))  # post-ReLU features
+    ref = (F.double() @ F.double().transpose(1, 2)) / (c * hw)
+    Fd = F.cuda().view(2, c, hw, 1)
+    G32 = gram_matrix(Fd)
+    rel = float((G32.cpu().double() - ref).abs().max() / ref.abs().max())
+    assert rel < 1e-5, rel
+    Fb = F.to(torch.bfloat16)
+    refb = (Fb.double() @ Fb.double().transpose(1, 2)) / (c * hw)
+    Gb = gram_matrix(Fb.cuda().view(2, c, hw, 1))
+    relb = float((Gb.cpu().double() - refb).abs().max() / refb.abs().max())
+    assert relb < 1e-5, relb
+    assert torch.equal(Gb, gram_matrix(Fb.cuda().view(2, c, hw, 1)))  # deterministic
+    assert torch.equal(G32, gram_matrix(Fd))
+    if c % 8 == 0:  # the NHWC activation layout gives the same fills, so the same bits
+        hwc = Fb.transpose(1, 2).contiguous().cuda()
+        assert torch.equal(gram_raw(hwc, _lib.NST_DT_BF16, _lib.NST_GRAM_HWC, 2, c, hw), Gb)
+        hwc32 = F.transpose(1, 2).contiguous().cuda()
+        assert torch.equal(gram_raw(hwc32, _lib.NST_DT_F32, _lib.NST_GRAM_HWC, 2, c, hw), G32)
 
 
 @pytest.mark.parametrize("arch,h,w,preset", [
