@@ -9,7 +9,7 @@ BUILD := build/obj
 SLP ?= -fno-slp-vectorize
 CXXFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off $(SLP) -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
-SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/nst_ops.hip $(CSRC)/nst_api.cpp
+SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp
 OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
 LIB := $(PKG)/libnst_hip.so
 

@@ -248,6 +248,44 @@ int nst_gram_workspace_bytes(int n, int c, int hw, size_t* out);
 int nst_gram(const void* F, int dtype, int layout, int n, int c, int hw, float* G, void* workspace,
              size_t workspace_bytes, void* stream);
 
+/* ---- Gatys optimisation loop (BASELINE.json configs[2]) ----
+ * The reference provides only gram_matrix (utils.py:80-83) and preprocess_for_vgg (utils.py:93-96);
+ * it has no VGG network, loss or optimiser.  These entry points build the loop the
+ * configuration names around them: VGG-19 features (torchvision layout, state_dict keys
+ * "features.N.weight"/"features.N.bias", N in {0,2,5,7,10,12,14,16,19,21,23,25,28}), style =
+ * MSE of Grams of relu1_1..relu5_1, content = MSE of relu4_2, gradient with respect to the image,
+ * Adam on the image.  Images: [1,3,h,w] fp32 in [0,1], h and w multiples of 16; bf16 activations
+ * with fp32 accumulation. */
+typedef struct nst_vgg nst_vgg;
+int nst_vgg_create(const nst_param* params, int n_params, int device, nst_vgg** out);
+void nst_vgg_destroy(nst_vgg* v);
+/* caller-owned device buffers: workspace (activations, gradients, Grams) and state (targets) */
+int nst_gatys_buffer_bytes(const nst_vgg* v, int h, int w, size_t* workspace, size_t* state);
+/* forward only: the pre-activations of relu1_1, relu2_1, relu3_1, relu4_1, relu5_1, relu4_2 (bf16
+ * NHWC [h_l][w_l][c_l]) into feats[0..5] (NULL entries skipped) */
+int nst_vgg_features(nst_vgg* v, const float* image, int h, int w, void* const* feats, void* workspace,
+                     size_t workspace_bytes, void* stream);
+/* targets into state: style Grams of `style` (same size as content) and relu4_2 of `content` */
+int nst_gatys_targets(nst_vgg* v, const float* content, const float* style, int h, int w, void* state,
+                      void* workspace, size_t workspace_bytes, void* stream);
+/* losses (device float[3]: total, content, style) of `image` and grad = dL/d(normalised image),
+ * fp32 [1,3,h,w]; L = content_weight * mean((F - P)^2) + style_weight * sum_l w_l mean((G_l - A_l)^2),
+ * style_layer_weights: host float[5] (NULL = all 1) */
+int nst_gatys_grad(nst_vgg* v, const float* image, int h, int w, const float* style_layer_weights,
+                   float content_weight, float style_weight, const void* state, float* grad, float* losses,
+                   void* workspace, size_t workspace_bytes, void* stream);
+/* nst_gatys_grad that also copies dL/dz of each of the 13 convs (z = its pre-activation; bf16 NHWC
+ * [h_i][w_i][c_i]) into dz[i] (NULL entries skipped): per-layer checks of the backward pass */
+int nst_gatys_grad_capture(nst_vgg* v, const float* image, int h, int w, const float* style_layer_weights,
+                           float content_weight, float style_weight, const void* state, float* grad,
+                           float* losses, void* workspace, size_t workspace_bytes, void* const* dz,
+                           void* stream);
+/* torch.optim.Adam step on an image [c=3][hw] (step >= 1 counts updates; bias corrections from it);
+ * grad_is_normalised: the gradient is with respect to (x - mean) / std (nst_gatys_grad's), so it is
+ * divided by std per channel; clamp01 clamps the image to [0, 1] after the update */
+int nst_adam_step(float* x, const float* grad, float* m, float* v, int c, int hw, float lr, float beta1,
+                  float beta2, float eps, int step, int clamp01, int grad_is_normalised, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,7 +35,8 @@ EXPORTED_SYMBOLS = (
     "nst_lab_destroy", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
     "nst_profile_end", "nst_num_layers", "nst_layer_name", "nst_blend_models_u8", "nst_blend_models_lab_u8",
     "nst_mask_feather", "nst_create_ex", "nst_num_ops", "nst_op_describe", "nst_forward_capture",
-    "nst_gram_workspace_bytes",
+    "nst_gram_workspace_bytes", "nst_vgg_create", "nst_vgg_destroy", "nst_gatys_buffer_bytes", "nst_vgg_features",
+    "nst_gatys_targets", "nst_gatys_grad", "nst_adam_step", "nst_gatys_grad_capture",
 )
 NST_GRAM_CHW, NST_GRAM_HWC = 0, 1
 
@@ -91,6 +92,17 @@ def lib() -> ctypes.CDLL:
         L.nst_op_describe.argtypes = [vp, i, i, i, i, ctypes.POINTER(NstOpDesc)]
         L.nst_forward_capture.argtypes = [vp, vp, i, i, i, i, i, vp, i, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(vp),
                                           ctypes.POINTER(vp), vp]
+        L.nst_vgg_create.argtypes = [ctypes.POINTER(NstParam), i, i, ctypes.POINTER(vp)]
+        L.nst_vgg_destroy.argtypes = [vp]
+        L.nst_vgg_destroy.restype = None
+        L.nst_gatys_buffer_bytes.argtypes = [vp, i, i, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        L.nst_vgg_features.argtypes = [vp, vp, i, i, ctypes.POINTER(vp), vp, sz, vp]
+        L.nst_gatys_targets.argtypes = [vp, vp, vp, i, i, vp, vp, sz, vp]
+        L.nst_gatys_grad.argtypes = [vp, vp, i, i, ctypes.POINTER(f), f, f, vp, vp, vp, vp, sz, vp]
+        L.nst_gatys_grad_capture.argtypes = [vp, vp, i, i, ctypes.POINTER(f), f, f, vp, vp, vp, vp, sz,
+                                             ctypes.POINTER(vp), vp]
+        L.nst_gatys_grad_capture.restype = i
+        L.nst_adam_step.argtypes = [vp, vp, vp, vp, i, i, f, f, f, f, i, i, i, vp]
         L.nst_destroy.argtypes = [vp]
         L.nst_destroy.restype = None
         L.nst_output_hw.argtypes = [vp, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
@@ -116,7 +128,8 @@ def lib() -> ctypes.CDLL:
         L.nst_num_layers.restype = i
         L.nst_layer_name.argtypes = [vp, i]
         L.nst_layer_name.restype = ctypes.c_char_p
-        for name in ("nst_create", "nst_create_ex", "nst_op_describe", "nst_forward_capture", "nst_output_hw", "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8",
+        for name in ("nst_vgg_create", "nst_gatys_buffer_bytes", "nst_vgg_features", "nst_gatys_targets",
+                     "nst_gatys_grad", "nst_adam_step", "nst_create", "nst_create_ex", "nst_op_describe", "nst_forward_capture", "nst_output_hw", "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8",
                      "nst_lab_create", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
                      "nst_profile_end"):
             getattr(L, name).restype = i

@@ -1,0 +1,32 @@
+// conv_vgg.hip — bf16 instantiations of the generic implicit-GEMM conv (conv_impl.h) for the
+// VGG-19 feature extractor of the Gatys loop (configs[2]; vgg_gatys.cpp): 3x3, stride 1, zero
+// padding 1.  Forward: the image layer reads the fp32 NCHW image with the ImageNet normalisation
+// (utils.py:93-96 preprocess_for_vgg) as the fill's encode; every other layer reads the stored
+// pre-activation of its producer with the ReLU applied in the fill (unit InstanceNorm table) or the
+// already-rectified pooled map.  Backward (input gradients only: the image is the variable): the
+// same kernel over the masked output gradient with the flipped, transposed weights; the image
+// layer's gradient leaves as fp32 NCHW.
+#include "conv_impl.h"
+
+namespace nst {
+typedef __bf16 B;
+#define E(...) ConvInst<__VA_ARGS__>::info()
+constexpr int SD = MODE_STD;
+const ConvKernelInfo* conv_table_vgg(int* count) {
+  static const ConvKernelInfo table[] = {
+      //  T  MODE KS S CINP BN TH TW WM WN  IN           OUT
+      // forward
+      E(B, SD, 3, 1, 4, 64, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),   // conv1_1 (normalised image)
+      E(B, SD, 3, 1, 64, 64, 8, 16, 2, 2, IN_ACT, OUT_ACT),       // conv1_2
+      E(B, SD, 3, 1, 64, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),      // conv2_1
+      E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // conv2_2, conv3_1 (2 channel blocks); backward 2_2
+      E(B, SD, 3, 1, 256, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // conv3_2..3_4, conv4_1; backward 3_1..3_4
+      E(B, SD, 3, 1, 512, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),     // conv4_2..5_1; backward 4_1..5_1
+      // backward
+      E(B, SD, 3, 1, 128, 64, 8, 16, 2, 2, IN_ACT, OUT_ACT),      // conv2_1 -> 64 input channels
+      E(B, SD, 3, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_F32_NCHW),  // conv1_1 -> the image gradient (3 of 16)
+  };
+  *count = (int)(sizeof(table) / sizeof(table[0]));
+  return table;
+}
+}  // namespace nst

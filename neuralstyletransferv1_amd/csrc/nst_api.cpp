@@ -615,6 +615,25 @@ bool preset_consts(int preset, PresetConsts& c) {
 
 }  // namespace
 
+namespace nst {
+// pack a plain conv weight [cout][cin][ks][ks] (fp32, host) for a generic-kernel instantiation and
+// upload it (bf16 or fp32 per the kernel); used by the VGG program (vgg_gatys.cpp)
+int pack_upload_conv(const ConvKernelInfo& k, int cin, int cout, int ks, const float* W, int coutp, void** dev) {
+  LayerDef d{"", "", cin, cout, ks, 1, AX_ZERO, ks / 2, 0, false};
+  const std::vector<float> pk = pack_weights(k, d, W, coutp);
+  if (k.dtype == NST_DT_BF16) {
+    std::vector<uint16_t> pb(pk.size());
+    for (size_t i = 0; i < pk.size(); ++i) pb[i] = f32_to_bf16_rne(pk[i]);
+    return upload(pb.data(), pb.size() * 2, dev);
+  }
+  return upload(pk.data(), pk.size() * 4, dev);
+}
+int upload_floats(const float* host, size_t n, float** dev) { return upload(host, n * 4, (void**)dev); }
+void tile_grid_of(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx, int* ty) {
+  tile_grid(k, sh, sw, oh, ow, tx, ty);
+}
+}  // namespace nst
+
 extern "C" {
 
 const char* nst_last_error(void) { return g_last_error.c_str(); }

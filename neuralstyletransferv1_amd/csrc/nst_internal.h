@@ -99,6 +99,27 @@ struct ConvKernelInfo {
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind, int res = 0, bool no_persistent = false);
 
+// ---- host helpers shared with the VGG program (nst_api.cpp) ----
+int pack_upload_conv(const ConvKernelInfo& k, int cin, int cout, int ks, const float* W, int coutp, void** dev);
+int upload_floats(const float* host, size_t n, float** dev);
+void tile_grid_of(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx, int* ty);
+const ConvKernelInfo* conv_table_vgg(int* count);
+
+// ---- VGG / Gatys kernels (vgg_ops.hip) ----
+hipError_t launch_vgg_pool(const void* z, int h, int w, int c, void* out, hipStream_t st);
+hipError_t launch_vgg_pool_bwd(const void* z, const void* gp, int h, int w, int c, void* gz, hipStream_t st);
+hipError_t launch_vgg_relu_bwd(const void* z, const void* ga, const void* P, float cw, size_t elems, void* gz,
+                               hipStream_t st);
+hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, float cw, const float* M, int hw, int c,
+                               void* gz, hipStream_t st);
+hipError_t launch_vgg_style_delta(const float* G, const float* A, int c, float k, float* M, float* loss_out,
+                                  hipStream_t st);
+int vgg_content_parts(size_t elems);
+hipError_t launch_vgg_losses(const void* z, const void* P, size_t elems, float* part, const float* style_raw,
+                             float cscale, const float* sscale, float* losses, hipStream_t st);
+hipError_t launch_adam(float* x, const float* g, float* m, float* v, int hw, int n, const float* inv_std, float lr,
+                       float b1, float b2, float eps, float bc1, float bc2, int clamp01, hipStream_t st);
+
 // ---- elementwise / reduction launchers (nst_ops.hip) ----
 constexpr int IN_MAX_SEGMENTS = 128;
 int in_finalize_segments(int tiles);
@@ -129,7 +150,8 @@ hipError_t launch_prepad_encode(const ConvParams& p, int in_kind, int n, int hp,
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,
                         float omb, uint8_t* out, int n, int hw, hipStream_t st);
 size_t gram_workspace_bytes(int n, int c, int hw);
+// relu: Gram of ReLU(F) (bf16 HWC only: the VGG program's stored pre-activations)
 hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, int hw, float* G, void* ws,
-                       hipStream_t st);
+                       hipStream_t st, int relu = 0);
 
 }  // namespace nst

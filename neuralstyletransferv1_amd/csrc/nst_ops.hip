@@ -696,7 +696,7 @@ struct GramT<float> {
   static constexpr int KM = 4, VEC = 4, KB = 64, RS = 272;
 };
 
-template <typename T, int TI, bool HWC>
+template <typename T, int TI, bool HWC, bool RELU>
 __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int c, int hw, int kslice,
                                                    float* __restrict__ out, size_t slice_stride) {
   using GT = GramT<T>;
@@ -727,8 +727,21 @@ __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int 
     const T* src = HWC ? Fb + (size_t)gk * c + gr : Fb + (size_t)gr * hw + gk;
     return *(const uint4*)src;
   };
-  auto store = [&](char* side, int q, const uint4& v) {
+  auto store = [&](char* side, int q, uint4 v) {
     if (q >= CPS) return;
+    if constexpr (RELU) {  // Gram of ReLU(F) (the VGG program stores pre-activations)
+      if constexpr (sizeof(T) == 2) {
+        typedef short s2 __attribute__((ext_vector_type(2)));
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          w[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, w[j]), (s2){0, 0}));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        v = make_uint4(__float_as_uint(fmaxf(__uint_as_float(v.x), 0.f)), __float_as_uint(fmaxf(__uint_as_float(v.y), 0.f)),
+                       __float_as_uint(fmaxf(__uint_as_float(v.z), 0.f)), __float_as_uint(fmaxf(__uint_as_float(v.w), 0.f)));
+      }
+    }
     if constexpr (HWC) {
       const int px = q / (TI / VEC), row = (q % (TI / VEC)) * VEC;
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -850,7 +863,7 @@ GramPlan gram_plan(int n, int c, int hw) {
 size_t gram_workspace_bytes(int n, int c, int hw) { return gram_plan(n, c, hw).ws_bytes; }
 
 hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, int hw, float* G, void* ws,
-                       hipStream_t st) {
+                       hipStream_t st, int relu) {
   const GramPlan g = gram_plan(n, c, hw);
   const size_t slice = (size_t)n * c * c;
   const float denom = (float)((double)c * (double)hw);
@@ -858,23 +871,27 @@ hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, i
   dim3 grid(g.tt * g.tt, g.slices, n);
   const int rs = dtype == NST_DT_BF16 ? GramT<__bf16>::RS : GramT<float>::RS;
   const size_t lds = (size_t)2 * g.ti * rs;
-#define NST_GRAM_GO(T, TI, HWC)                                                                          \
+#define NST_GRAM_GO(T, TI, HWC, RL)                                                                      \
   do {                                                                                                   \
-    static const hipError_t attr = hipFuncSetAttribute((const void*)gram_kernel<T, TI, HWC>,            \
+    static const hipError_t attr = hipFuncSetAttribute((const void*)gram_kernel<T, TI, HWC, RL>,        \
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
     (void)attr;                                                                                          \
-    hipLaunchKernelGGL((gram_kernel<T, TI, HWC>), grid, dim3(512), lds, st, (const T*)F, c, hw, g.kslice, dst, slice); \
+    hipLaunchKernelGGL((gram_kernel<T, TI, HWC, RL>), grid, dim3(512), lds, st, (const T*)F, c, hw, g.kslice, dst, slice); \
   } while (0)
-#define NST_GRAM_TI(T, HWC)                      \
-  do {                                           \
-    if (g.ti == 64) NST_GRAM_GO(T, 64, HWC);     \
-    else if (g.ti == 128) NST_GRAM_GO(T, 128, HWC); \
-    else NST_GRAM_GO(T, 256, HWC);               \
+#define NST_GRAM_TI(T, HWC, RL)                      \
+  do {                                               \
+    if (g.ti == 64) NST_GRAM_GO(T, 64, HWC, RL);     \
+    else if (g.ti == 128) NST_GRAM_GO(T, 128, HWC, RL); \
+    else NST_GRAM_GO(T, 256, HWC, RL);               \
   } while (0)
   if (dtype == NST_DT_BF16) {
-    if (layout_hwc) NST_GRAM_TI(__bf16, true); else NST_GRAM_TI(__bf16, false);
+    if (layout_hwc) {
+      if (relu) NST_GRAM_TI(__bf16, true, true); else NST_GRAM_TI(__bf16, true, false);
+    } else {
+      NST_GRAM_TI(__bf16, false, false);
+    }
   } else {
-    if (layout_hwc) NST_GRAM_TI(float, true); else NST_GRAM_TI(float, false);
+    if (layout_hwc) NST_GRAM_TI(float, true, false); else NST_GRAM_TI(float, false, false);
   }
 #undef NST_GRAM_TI
 #undef NST_GRAM_GO

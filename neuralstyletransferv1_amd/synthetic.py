@@ -91,3 +91,22 @@ def make_frames(n: int, h: int, w: int, seed: int = 0) -> np.ndarray:
         img += rng.normal(0.0, 0.02, (h, w, 3)).astype(np.float32)
         frames[f] = np.clip(img * 255.0, 0, 255).astype(np.uint8)
     return frames
+
+
+# VGG-19 `features` convs up to conv5_1 (torchvision indices) for the Gatys loop (configs[2]); the
+# ImageNet weights cannot be fetched offline, so seeded He-initialised weights stand in
+VGG19_CONVS = ((0, 3, 64), (2, 64, 64), (5, 64, 128), (7, 128, 128), (10, 128, 256), (12, 256, 256),
+               (14, 256, 256), (16, 256, 256), (19, 256, 512), (21, 512, 512), (23, 512, 512), (25, 512, 512),
+               (28, 512, 512))
+
+
+def make_vgg19_state_dict(seed: int = 0) -> Dict[str, torch.Tensor]:
+    """{features.N.weight, features.N.bias} fp32, N(0, 2/fan_in) weights, small uniform biases."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out: Dict[str, torch.Tensor] = {}
+    for idx, cin, cout in VGG19_CONVS:
+        w = rng.standard_normal((cout, cin, 3, 3)) * np.sqrt(2.0 / (cin * 9))
+        b = rng.uniform(-0.02, 0.02, cout)
+        out[f"features.{idx}.weight"] = torch.from_numpy(np.ascontiguousarray(w, dtype=np.float32))
+        out[f"features.{idx}.bias"] = torch.from_numpy(np.ascontiguousarray(b, dtype=np.float32))
+    return out
