@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--gather", action="store_true",
                     help="time the ordered gather to rank 0 + rank-0 LAB EMA with the forward (configs[3])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode timing (profiling runs)")
     ap.add_argument("--cpu-frames", type=int, default=3, help="timed 1080p frames per CPU configuration")
     return ap.parse_args()
 
@@ -288,7 +289,7 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_fp32:
         # the fp32 parity mode (exact-f32 MFMA), same frames
         net.compute_dtype = "fp32"
         e32 = net.engine(dev)

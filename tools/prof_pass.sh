@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 export TMPDIR=/tmp
 TAG=$1; shift
-ARGS=${*:---steps 3 --warmup 1 --no-cpu-baseline}
+ARGS=${*:---steps 3 --warmup 1 --no-cpu-baseline --no-fp32}
 O=gpurun_out/$TAG
 mkdir -p "$O"
 run() {  # name, then rocprofv3 options
@@ -21,4 +21,6 @@ run stats --kernel-trace --stats &&
 run sq1 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE &&
 run sq2 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR &&
 run fetch --pmc FETCH_SIZE &&
-run write --pmc WRITE_SIZE
+run write --pmc WRITE_SIZE &&
+python3 tools/pmc_summary.py "$O" --json "$O/pmc.json" --res-json "$O/pmc_res_conv.json" > "$O/summary.txt" &&
+echo "summary ok"
