@@ -194,7 +194,8 @@ __device__ __forceinline__ uint4 norm_chunk(uint4 raw, const float2* nm) {
 // Residual join, fused into the consumer conv's fill (ResidualBlock.forward transformer_net.py:71-76,
 // transformer_net_nst.py:138-142; ReCoNet ResLayer model.py:55-60 adds the ReLU after the sum):
 //   v = IN_y(y) + (rn ? ReLU(IN_r(r)) : r)  [then ReLU if relu_out]
-// in the residual kernel's fp32 arithmetic (product, then sum: no contraction) with one rounding.
+// in the residual kernel's fp32 arithmetic (product, then sum: no contraction) with one rounding;
+// ReLU(IN_r(r)) is the value a normalising fill would stage (bf16: rounded, as the stored x_0).
 template <typename T>
 __device__ __forceinline__ uint4 res_chunk(uint4 y, uint4 r, const float2* yn, const float2* rn, bool has_rn,
                                            bool relu_out) {
@@ -214,7 +215,13 @@ __device__ __forceinline__ uint4 res_chunk(uint4 y, uint4 r, const float2* yn, c
 #pragma unroll
   for (int j = 0; j < CPC; ++j) {
     float rr = fr[j];
-    if (has_rn) rr = fmaxf(rr * rn[j].x + rn[j].y, 0.f);
+    if (has_rn) {
+      // r' = ReLU(IN_r(r)) exactly as a normalising fill stages it (norm_chunk): bf16 of one fma
+      if constexpr (sizeof(T) == 2)
+        rr = fmaxf(bf16_lo(pack_bf16(__builtin_fmaf(rr, rn[j].x, rn[j].y), 0.f)), 0.f);
+      else
+        rr = fmaxf(rr * rn[j].x + rn[j].y, 0.f);
+    }
     float v = fy[j] * yn[j].x + yn[j].y;
     v = rr + v;
     o[j] = relu_out ? fmaxf(v, 0.f) : v;

@@ -184,9 +184,11 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float r0 = bf16_lo(w2[j]), r1 = bf16_hi(w2[j]);
-        if (RN) {
-          r0 = fmaxf(r0 * nr[2 * j] + nr[8 + 2 * j], 0.f);
-          r1 = fmaxf(r1 * nr[2 * j + 1] + nr[8 + 2 * j + 1], 0.f);
+        if (RN) {  // ReLU(IN_r(r)) as a normalising fill stages it: bf16 of one fma
+          const uint32_t rn = pack_bf16(__builtin_fmaf(r0, nr[2 * j], nr[8 + 2 * j]),
+                                        __builtin_fmaf(r1, nr[2 * j + 1], nr[8 + 2 * j + 1]));
+          r0 = fmaxf(bf16_lo(rn), 0.f);
+          r1 = fmaxf(bf16_hi(rn), 0.f);
         }
         const float a = bf16_lo(w[j]) * ny[2 * j] + ny[8 + 2 * j];
         const float bb = bf16_hi(w[j]) * ny[2 * j + 1] + ny[8 + 2 * j + 1];

@@ -28,6 +28,7 @@ __device__ __forceinline__ void stat4(f32x4_t& s1, f32x4_t& s2, const f32x4_t& x
 }
 
 // what the fill applies to a staged input chunk
+// (join of ReLU(IN(r)): r normalised as a WF_NORM fill stages it, bf16-rounded)
 enum WsFill { WF_NORM = 0, WF_RAW = 1, WF_RES = 2, WF_RESRN = 3 };  // IN+ReLU / identity / join / join of ReLU(IN(r))
 
 // s_waitcnt vmcnt(N) / the part barrier, as statements hipcc cannot move memory operations across

@@ -33,10 +33,12 @@
 namespace nst {
 
 constexpr int WS_RING = 3;  // operand reads in flight ahead of the MFMAs
+constexpr int WS_SPLIT = 1;  // read steps between a unit's staging read and its transform (0: back to back)
+constexpr uint32_t OOB = 0xFFFFFF00u;  // buffer offset past every launch's records: loads 0, stores dropped
 
 template <int TH, int FILL>
 struct WsCfg {
-  static constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
+  static constexpr bool RES = FILL == WF_RES;
   static constexpr int NW = 8, NT = 512;           // two waves per SIMD, wave w: channels 16w..16w+15
   static constexpr int TW = 16;                    // tile width = MFMA column block
   static constexpr int CINP = 128;
@@ -53,7 +55,7 @@ struct WsCfg {
   static constexpr int MAP_OFF = NENT * EB;
   static constexpr int NORM_OFF = MAP_OFF + 2 * MAPB;        // [y | r][frame][channel] float2
   static constexpr int NORM_TAB = NFMAX * CINP * 8;
-  static constexpr int BIAS_OFF = NORM_OFF + (RN ? 2 : 1) * NORM_TAB;  // 128 fp32
+  static constexpr int BIAS_OFF = NORM_OFF + NORM_TAB;  // 128 fp32
   static constexpr int DUMMY_OFF = BIAS_OFF + CINP * 4;      // sink of the lanes without an item
   static constexpr int STG_OFF = DUMMY_OFF + 64 * 16;
   // output tile staged in LDS (when it fits: not the ReLU(IN(r)) join) for whole-pixel 16-B
@@ -69,10 +71,14 @@ struct WsCfg {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int TH, int FILL, bool ZPAD>
+// XO: a WF_NORM fill also writes what it staged for the tile's own pixels (ReLU(IN(y)), the first
+// residual block's input x_0) to res_out, so the next join reads x_0 instead of re-normalising
+template <int TH, int FILL, bool ZPAD, bool XO>
 __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   using C = WsCfg<TH, FILL>;
-  constexpr bool RES = C::RES, RN = C::RN;
+  constexpr bool RES = C::RES;
+  static_assert(!XO || FILL == WF_NORM, "x_0 export is a normalising fill");
+  constexpr bool SOUT = RES || XO;  // residual-stream stores from the halo
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -83,6 +89,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     int n, tile, ty0, tx0;
   };
   const int ntile = p.tiles_x * p.tiles_y;
+  const int nfr = p.n_work / ntile;  // frames in this launch
   auto decode = [&](int wi) {
     Work r;
     r.n = wi / ntile;
@@ -106,32 +113,28 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     for (int s = 0; s < C::NSTEP; ++s) wr[s] = wsrc[s * 64];
   }
   // ---- the launch's IN constants (<= NFMAX frames) and bias, resident in LDS ----
-  // per frame and 8-channel chunk: scale[8], shift[8] (planar, so a packed FMA takes its scale and
-  // shift pairs straight from one ds_read_b128 each)
+  // per frame and 8-channel chunk: 4 x {scale lo, scale hi, shift lo, shift hi} (one ds_read_b128 per
+  // channel pair, read right before its use: few registers live in the fill)
   float* norm_y = (float*)(smem + C::NORM_OFF);
-  float* norm_r = norm_y + C::NFMAX * C::CINP * 2;
   if (FILL != WF_RAW) {
-    const int nfr = p.n_work / ntile;
     for (int t = tid; t < nfr * C::CINP; t += C::NT) {
       const int f = t / C::CINP, c = t - f * C::CINP;
-      const int o = (f * 16 + (c >> 3)) * 16 + (c & 7);
+      // chunk layout: per channel pair j = (c & 7) >> 1: {scale lo, scale hi, shift lo, shift hi}
+      const int o = (f * 16 + (c >> 3)) * 16 + 4 * ((c & 7) >> 1) + (c & 1);
       const float2 v = p.in_norm[(size_t)f * p.cs + c];
       norm_y[o] = v.x;
-      norm_y[o + 8] = v.y;
-      if (RN) {
-        const float2 r = p.res_rnorm[(size_t)f * p.cs + c];
-        norm_r[o] = r.x;
-        norm_r[o + 8] = r.y;
-      }
+      norm_y[o + 2] = v.y;
     }
   }
   if (tid < C::CINP) ((float*)(smem + C::BIAS_OFF))[tid] = p.bias[tid];
 
   // ---- halo staging ----
-  const size_t frame_bytes = (size_t)p.hs * p.ws * p.cs * 2;
-  auto frame_rsrc = [&](const void* base, int n) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (size_t)n * frame_bytes), (short)0,
-                                             (int)frame_bytes, 0x00020000);
+  // one buffer resource per tensor for the whole launch (the launcher keeps a launch's frames within
+  // 32-bit offsets): a frame is a 32-bit offset, nothing per request is 64-bit scalar math
+  const uint32_t fb = (uint32_t)p.hs * p.ws * p.cs * 2;          // bytes per frame: in, res_r, res_out
+  const uint32_t ob = (uint32_t)p.oh * p.ow * p.cout_stride * 2;  // ... out
+  auto launch_rsrc = [&](const void* base, uint32_t frame) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(frame * (uint32_t)nfr), 0x00020000);
   };
   auto build_maps = [&](const Work& wk, int slot) {
     int* rowmap = (int*)(smem + C::MAP_OFF + slot * C::MAPB);
@@ -148,11 +151,11 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
       }
     }
   };
-  // this lane's item in every unit of a tile: entry ebase of chunk 2u + team.  src = its byte offset
-  // in the frame (chunk 0), -1 = zero padding; valid: the entry exists
+  // this lane's item in every unit of a tile: entry ebase of chunk 2u + team.  voff = its byte offset
+  // in the launch's input (chunk 0), OOB = zero padding (reads 0); valid: the entry exists
   const int ebase = (wv & 3) * C::QENT + lane;
   struct Item {
-    int src;
+    uint32_t voff;
     bool valid;
   };
   auto items = [&](const Work& wk, int slot) {
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const int e = it.valid ? ebase : 0;
     const int ly = e / C::LW, lx = e - ly * C::LW;
     const int ro = rowmap[ly], co = colmap[lx];
-    it.src = (ro >= 0 && co >= 0) ? ro + co : -1;
+    it.voff = (it.valid && ro >= 0 && co >= 0) ? (uint32_t)(ro + co) + (uint32_t)wk.n * fb : OOB;
     return it;
   };
   // Units travel by LDS-DMA (buffer_load ... lds: no VGPR destination) into a 4-slot staging ring:
@@ -175,22 +178,31 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   // epilogue's TH + 1 stores when one lies in between (units 0, 1, 6, 7).  Any extra instruction
   // hipcc adds only makes such a wait stricter.
   const uint32_t stg = (uint32_t)(uintptr_t)(smem + C::STG_OFF) + wv * 1024;
-  auto request = [&](int n, int u, const Item& it) {
-    const uint32_t voff = (it.valid && it.src >= 0) ? (uint32_t)it.src : 0x80000000u;  // pad: reads 0
-    const int soff = (2 * u + team) * 16;                                                // the unit's chunk
+  const __amdgpu_buffer_rsrc_t rs_in = launch_rsrc(p.in, fb);
+  const __amdgpu_buffer_rsrc_t rs_r = launch_rsrc(RES ? p.res_r : p.in, fb);
+  auto request = [&](int u, const Item& it) {
+    const int soff = (2 * u + team) * 16;  // the unit's chunk
     const uint32_t lds = stg + (u % C::NSLOT) * C::SLOTB;
-    dma16(frame_rsrc(p.in, n), voff, lds, soff);
-    if constexpr (RES) dma16(frame_rsrc(p.res_r, n), voff, lds + C::NW * 1024, soff);
+    dma16(rs_in, it.voff, lds, soff);
+    if constexpr (RES) dma16(rs_r, it.voff, lds + C::NW * 1024, soff);
+  };
+  // unit u's staged chunk (this lane's 16 B of the input, and of the residual stream for RES), read
+  // WS_SPLIT read steps before its transform so the LDS latency runs under MFMAs
+  struct Staged {
+    uint4 y, r;
+  };
+  auto stage_read = [&](int u) {
+    const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
+    Staged st;
+    st.y = *(const uint4*)sp;
+    st.r = RES ? *(const uint4*)(sp + C::NW * 1024) : make_uint4(0u, 0u, 0u, 0u);
+    return st;
   };
   // consume unit u of tile wk: IN + ReLU / residual join of the staged chunk into the halo.
-  // live = false: a restaging pass past the last work item (LDS only, no residual-stream stores)
-  auto consume = [&](const Work& wk, int u, const Item& it, bool live) {
+  auto consume = [&](const Work& wk, int u, const Item& it, const Staged& st) {
     const int ch = 2 * u + team;
-    const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
-    const uint4 y = *(const uint4*)sp;
-    const uint4 rr = RES ? *(const uint4*)(sp + C::NW * 1024) : make_uint4(0u, 0u, 0u, 0u);
-    const float* ny = norm_y + (wk.n * 16 + ch) * 16;  // scale[8], shift[8]
-    const float* nr = norm_r + (wk.n * 16 + ch) * 16;
+    const uint4 y = st.y, rr = st.r;
+    const float4* ny = (const float4*)(norm_y + (wk.n * 16 + ch) * 16);  // per pair: {scale lo, hi, shift lo, hi}
     const uint32_t w[4] = {y.x, y.y, y.z, y.w};
     uint32_t o[4];
     if constexpr (RES) {
@@ -200,12 +212,9 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float r0 = bf16_lo(w2[j]), r1 = bf16_hi(w2[j]);
-        if (RN) {
-          r0 = fmaxf(r0 * nr[2 * j] + nr[8 + 2 * j], 0.f);
-          r1 = fmaxf(r1 * nr[2 * j + 1] + nr[8 + 2 * j + 1], 0.f);
-        }
-        const float a = bf16_lo(w[j]) * ny[2 * j] + ny[8 + 2 * j];
-        const float bb = bf16_hi(w[j]) * ny[2 * j + 1] + ny[8 + 2 * j + 1];
+        const float4 n = ny[j];
+        const float a = bf16_lo(w[j]) * n.x + n.z;
+        const float bb = bf16_hi(w[j]) * n.y + n.w;
         o[j] = pack_bf16(r0 + a, r1 + bb);
       }
     } else if constexpr (FILL == WF_RAW) {
@@ -215,19 +224,20 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
       // producer IN apply + ReLU, as norm_chunk
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float a = __builtin_fmaf(bf16_lo(w[j]), ny[2 * j], ny[8 + 2 * j]);
-        const float bb = __builtin_fmaf(bf16_hi(w[j]), ny[2 * j + 1], ny[8 + 2 * j + 1]);
+        const float4 n = ny[j];
+        const float a = __builtin_fmaf(bf16_lo(w[j]), n.x, n.z);
+        const float bb = __builtin_fmaf(bf16_hi(w[j]), n.y, n.w);
         const i16x2_t r = __builtin_bit_cast(i16x2_t, pack_bf16(a, bb));
         o[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
       }
     }
-    const bool pad = ZPAD && it.src < 0;  // zero padding stays zero (pad after IN + ReLU); reflection never pads
+    const bool pad = ZPAD && it.voff == OOB;  // zero padding stays zero (pad after IN + ReLU); reflection never pads
     const u32x4_t v = {pad ? 0u : o[0], pad ? 0u : o[1], pad ? 0u : o[2], pad ? 0u : o[3]};
     int eb = ebase * C::EB + ch * 16;  // recomputed per unit, not held across the loop
     asm volatile("" : "+v"(eb));
     *(u32x4_t*)(smem + (it.valid ? eb : C::DUMMY_OFF + lane * 16)) = v;
   };
-  // RES: the joined residual stream x_{k+1} of the tile's own pixels goes to res_out from the halo,
+  // RES / XO: the joined residual stream x_{k+1} (x_0) of the tile's own pixels goes to res_out from the halo,
   // region by region (region q during part q: complete since unit 2q+1 was consumed, overwritten
   // only in part q+1), as 64-byte pixel quarters — one store per lane and part, instead of 16-byte
   // pieces per unit (which cost as much as the rest of the join)
@@ -237,11 +247,11 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const int oy = wk.ty0 + r, ox = wk.tx0 + x;
     const u32x4_t v = *(const u32x4_t*)(smem + ((r + 1) * C::LW + x + 1) * C::EB + c * 16);
     const bool ok = oy < p.oh && ox < p.ow;
-    __builtin_amdgcn_raw_buffer_store_b128(v, frame_rsrc(p.res_out, wk.n),
-                                           ok ? (uint32_t)(((oy * p.ws + ox) * p.cs + c * 8) * 2) : 0x80000000u, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, launch_rsrc(p.res_out, fb),
+                                           ok ? (uint32_t)wk.n * fb + (uint32_t)(((oy * p.ws + ox) * p.cs + c * 8) * 2) : OOB, 0, 0);
   };
   constexpr int DPU = RES ? 2 : 1;                // requests per unit
-  constexpr int KIN = 3 * DPU + (RES ? 2 : 0);    // vmcnt before a unit whose wait spans no epilogue
+  constexpr int KIN = 3 * DPU + (SOUT ? 2 : 0);   // vmcnt before a unit whose wait spans no epilogue
   constexpr int KEP = KIN + (C::OST ? C::NST : TH) + 1;  // ... one that spans the epilogue's stores
 
   // ---- K loop ----
@@ -305,12 +315,11 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     const int c0 = 16 * wv + 4 * g;
     const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
-    const size_t obytes = (size_t)p.oh * p.ow * p.cout_stride * 2;
-    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((char*)p.out + (size_t)wk.n * obytes), (short)0, (int)obytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ors = launch_rsrc(p.out, ob);
     const int ox = wk.tx0 + px;
     const uint32_t row_bytes = (uint32_t)p.ow * p.cout_stride * 2;
-    const uint32_t off0 = (uint32_t)(((wk.ty0 * p.ow + ox) * p.cout_stride + c0) * 2);
+    const uint32_t fo = (uint32_t)wk.n * ob;
+    const uint32_t off0 = fo + (uint32_t)(((wk.ty0 * p.ow + ox) * p.cout_stride + c0) * 2);
     f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};  // packed-math statistics
     // lane-derived LDS addresses recomputed per tile (opaque), not held across the K loop
     int obase = C::OUT_OFF + px * 256 + (((4 * wv + g) ^ (2 * (px & 7))) * 8);
@@ -324,7 +333,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         if constexpr (C::OST) {
           *(u32x2_t*)(smem + obase + r * C::TW * 256) = pk;
         } else {
-          __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : 0x80000000u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : OOB, 0, 0);
         }
         const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
         stat4(s1, s2, x);
@@ -362,7 +371,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         const int x = pp & (C::TW - 1), oy = wk.ty0 + pp / C::TW, ox = wk.tx0 + x;
         const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * 256 + (((cb >> 3) ^ (2 * (x & 7))) << 3));
         const bool ok = oy < p.oh && ox < p.ow;
-        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * 256 + cb) : 0x80000000u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? fo + (uint32_t)((oy * p.ow + ox) * 256 + cb) : OOB, 0, 0);
       }
     }
   };
@@ -379,18 +388,18 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   Item xx = items(cur, 0);  // sources of the tile being consumed
   Item xd = xx;             // ... and of the tile being requested
 #pragma unroll
-  for (int u = 0; u < C::NSLOT; ++u) request(cur.n, u, xd);
+  for (int u = 0; u < C::NSLOT; ++u) request(u, xd);
   {
     const Work n1 = decode(min(wn, last));
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
       vm_wait<0>();
-      consume(cur, u, xx, true);
+      consume(cur, u, xx, stage_read(u));
       if (u + 4 < C::NUNIT) {
-        request(cur.n, u + 4, xd);
+        request(u + 4, xd);
       } else {
         if (u + 4 == C::NUNIT) xd = items(n1, 1);
-        request(n1.n, u + 4 - C::NUNIT, xd);
+        request(u + 4 - C::NUNIT, xd);
       }
     }
   }
@@ -405,6 +414,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   // behind team 0 so the two waves of a SIMD never stage at the same time.
   constexpr int POS_A = 0, POS_B = PRD / 2, DT = PRD / 4;
   Acc acc;
+  Staged stg_u;  // the unit between its staging read and its transform
   for (int it = 0;; ++it) {
     // past the last work item the hooks restage LDS with whatever they are given (never read
     // again) and store nothing, so they need no branch
@@ -415,26 +425,39 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     kloop(
         acc,
         [&](int q, int rem) {  // after read rem of part q
+          // unit work at pa / pb (staging read) and WS_SPLIT reads later (transform + next request)
           const int pa = POS_A + (team ? DT : 0), pb = POS_B + (team ? DT : 0);
-          if (rem != pa && rem != pb) return;
-          const int half = rem == pa ? 0 : 1;
+          const bool rd = rem == pa || rem == pb;
+          const bool wr = rem == pa + WS_SPLIT || rem == pb + WS_SPLIT;
+          if (!rd && !wr) return;
+          const int half = (rem == pa || rem == pa + WS_SPLIT) ? 0 : 1;
           if (q == 0) {
-            vm_wait<KEP>();
-            consume(cur, 6 + half, xx, true);
-            request(nxt.n, 2 + half, xd);
-            if (RES && half == 0) store_region(cur, 0);
+            if (rd) {
+              vm_wait<KEP>();
+              stg_u = stage_read(6 + half);
+            }
+            if (wr) {
+              consume(cur, 6 + half, xx, stg_u);
+              request(2 + half, xd);
+              if (SOUT && half == 0) store_region(cur, 0);
+            }
           } else {
             const int u = 2 * (q - 1) + half;
-            if (u == 0) xx = items(nxt, ns);
-            if (u <= 1) vm_wait<KEP>(); else vm_wait<KIN>();
-            consume(nxt, u, xx, more);
-            if (u + 4 < C::NUNIT) {
-              request(nxt.n, u + 4, xd);
-            } else {
-              if (u == 4) xd = items(nxt2, cs);
-              request(nxt2.n, u - 4, xd);
+            if (rd) {
+              if (u == 0) xx = items(nxt, ns);
+              if (u <= 1) vm_wait<KEP>(); else vm_wait<KIN>();
+              stg_u = stage_read(u);
             }
-            if (RES && half == 0) store_region(cur, q);
+            if (wr) {
+              consume(nxt, u, xx, stg_u);
+              if (u + 4 < C::NUNIT) {
+                request(u + 4, xd);
+              } else {
+                if (u == 4) xd = items(nxt2, cs);
+                request(u - 4, xd);
+              }
+              if (SOUT && half == 0) store_region(cur, q);
+            }
           }
         },
         [&](int q) {  // after the barrier that ends part q
@@ -462,35 +485,38 @@ struct WstatInst {
     }();
     return v;
   }
-  template <int FILL, bool ZPAD>
+  template <int FILL, bool ZPAD, bool XO = false>
   static void go(const ConvParams& p, int nb, hipStream_t st) {
-    hipLaunchKernelGGL((wstat_kernel<TH, FILL, ZPAD>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((wstat_kernel<TH, FILL, ZPAD, XO>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   // grid.x = tiles per frame, grid.y = frames; launched in chunks of <= NFMAX frames (the IN tables
   // of a launch's frames live in LDS)
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
     const int ntile = (int)grid.x, n = (int)grid.y;
     const size_t fin = (size_t)p0.hs * p0.ws * p0.cs * 2, fout = (size_t)p0.oh * p0.ow * p0.cout_stride * 2;
-    for (int f0 = 0; f0 < n; f0 += C::NFMAX) {
-      const int nf = std::min(C::NFMAX, n - f0);
+    // frames per launch: the LDS IN tables' capacity, and every offset (frame * bytes) below OOB
+    const int fmax = (int)std::min<size_t>(C::NFMAX, (size_t)OOB / std::max(fin, fout));
+    if (fmax < 1) return;  // nst_api validates sizes before launching
+    for (int f0 = 0; f0 < n; f0 += fmax) {
+      const int nf = std::min(fmax, n - f0);
       ConvParams p = p0;
       p.in = (const char*)p0.in + f0 * fin;
       p.out = (char*)p0.out + f0 * fout;
       if (p0.res_r) p.res_r = (const char*)p0.res_r + f0 * fin;
       if (p0.res_out) p.res_out = (char*)p0.res_out + f0 * fin;
       if (p0.in_norm) p.in_norm = p0.in_norm + (size_t)f0 * p0.cs;
-      if (p0.res_rnorm) p.res_rnorm = p0.res_rnorm + (size_t)f0 * p0.cs;
       p.partial = p0.partial + (size_t)f0 * ntile * p0.cout_stride * 2;
       p.n_work = nf * ntile;
       const int nb = std::min(p.n_work, cus());  // one workgroup per CU (registers, LDS)
       const bool zp = p.axis_mode != AX_REFLECT;  // zero-padded trunk (transformer_net_nst.py ConvBlock)
       if constexpr (RES) {
-        if (p.res_rnorm != nullptr)  // block 1's join: the residual is ReLU(IN(conv3)), applied here
-          zp ? go<WF_RESRN, true>(p, nb, st) : go<WF_RESRN, false>(p, nb, st);
-        else
-          zp ? go<WF_RES, true>(p, nb, st) : go<WF_RES, false>(p, nb, st);
+        // joins a stored residual stream (block 1's conv1 exports x_0; nst_api rejects a
+        // normalised residual here)
+        zp ? go<WF_RES, true>(p, nb, st) : go<WF_RES, false>(p, nb, st);
       } else {
-        if (p.in_norm != nullptr)
+        if (p.in_norm != nullptr && p.res_out != nullptr)  // block 1's conv1, exporting x_0
+          zp ? go<WF_NORM, true, true>(p, nb, st) : go<WF_NORM, false, true>(p, nb, st);
+        else if (p.in_norm != nullptr)
           zp ? go<WF_NORM, true>(p, nb, st) : go<WF_NORM, false>(p, nb, st);
         else  // the residual stream itself (unfused joins)
           zp ? go<WF_RAW, true>(p, nb, st) : go<WF_RAW, false>(p, nb, st);

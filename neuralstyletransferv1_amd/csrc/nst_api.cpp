@@ -94,7 +94,11 @@ struct Op {
 
 static int round_up(int v, int a) { return (v + a - 1) / a * a; }
 
-static void build_program(int arch, bool fuse_res, std::vector<LayerDef>& L, std::vector<Op>& P) {
+// x0_export (with fuse_res): block 1's conv1 also writes x_0 = ReLU(IN_2(C)) from its fill (only the
+// weight-stationary trunk kernel does), so block 2's join reads a stored x_0 like every later join
+static void build_program(int arch, bool fuse_res, bool x0_export, std::vector<LayerDef>& L, std::vector<Op>& P) {
+  L.clear();
+  P.clear();
   auto conv = [&](int layer, int src, int dst, int in_norm) {
     P.push_back(Op{OP_CONV, layer, src, dst, in_norm, 0, 0, 0, 0});
   };
@@ -165,14 +169,16 @@ static void build_program(int arch, bool fuse_res, std::vector<LayerDef>& L, std
     conv(u1, B_C, B_A, -1);
   } else {
     // the residual add x_{k+1} = IN(y_k) + x_k runs inside the NEXT conv's fill, which also writes
-    // x_{k+1} (ping-pong F/G) for its own pixels; x_0 = ReLU(IN_2(C)) is never materialised
-    int xbuf = B_C, xnorm = 2;
+    // x_{k+1} (ping-pong F/G) for its own pixels; x_0 = ReLU(IN_2(C)) is either written by block 1's
+    // conv1 (x0_export, into F) or applied lazily in block 2's join
+    int xbuf = x0_export ? B_F : B_C, xnorm = x0_export ? -1 : 2;
     for (int r = 0; r < nres; ++r) {
       const int l1 = 3 + 2 * r, l2 = 4 + 2 * r;
       if (r == 0) {
         conv(l1, B_C, B_D, 2);
+        if (x0_export) P.back().res_out = B_F;
       } else {
-        const int xout = (r & 1) ? B_F : B_G;
+        const int xout = ((r & 1) != 0) != x0_export ? B_F : B_G;
         convres(l1, B_E, l2 - 2, xbuf, xnorm, xout, relu_out, B_D);
         xbuf = xout;
         xnorm = -1;
@@ -671,7 +677,8 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
   auto* h = new nst_handle();
   h->arch = arch; h->dtype = compute_dtype; h->device = device;
   std::vector<LayerDef> defs;
-  build_program(arch, (flags & NST_KSEL_UNFUSED_RESIDUAL) == 0, defs, h->prog);
+  const bool fuse_res = (flags & NST_KSEL_UNFUSED_RESIDUAL) == 0;
+  build_program(arch, fuse_res, fuse_res, defs, h->prog);
   // layers whose fill joins the residual stream run the VAR_RES instantiation
   std::vector<int> res_layer(defs.size(), 0);
   for (const Op& op : h->prog)
@@ -796,6 +803,9 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     nst_destroy(h);
     return rc;
   }
+  // x_0 export needs block 1's conv1 on the weight-stationary kernel; otherwise block 2's join
+  // normalises conv3's output itself (the same layers and residual layers either way)
+  if (fuse_res && h->layers[3].mode != MODE_WSTAT) build_program(arch, true, false, defs, h->prog);
   *out = h;
   return NST_OK;
 }
@@ -920,9 +930,9 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     if (op.res_buf >= 0) {
       p.res_r = bufs[op.res_buf];
       p.res_rnorm = op.r_norm >= 0 ? stats[op.r_norm] : nullptr;
-      p.res_out = op.res_out >= 0 ? bufs[op.res_out] : nullptr;
       p.res_relu = op.relu_out;
     }
+    p.res_out = op.res_out >= 0 ? bufs[op.res_out] : nullptr;
     for (int c = 0; c < 3; ++c) {
       p.enc_a[c] = pc.ea[c]; p.enc_b[c] = pc.eb[c]; p.enc_d[c] = pc.ed[c]; p.enc_perm[c] = pc.eperm[c];
       p.dec_p[c] = pc.dp[c]; p.dec_q[c] = pc.dq[c]; p.dec_r[c] = pc.dr[c]; p.dec_s[c] = pc.ds[c]; p.dec_perm[c] = pc.dperm[c];
@@ -963,6 +973,10 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     p.cout_stride = Ly.coutp;
     tile_grid(*k, p.hs, p.ws, p.oh, p.ow, &p.tiles_x, &p.tiles_y);
     p.n_cblk = Ly.coutp / k->bn;
+    if (p.res_out != nullptr && p.res_r == nullptr && (Ly.mode != MODE_WSTAT || p.in_norm == nullptr)) {
+      set_error("conv " + Ly.d.conv + ": only the weight-stationary trunk kernel writes its normalised input");
+      return NST_E_SHAPE;
+    }
     if (Ly.mode == MODE_WSTAT && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out == nullptr || p.res_relu)) {
       set_error("conv " + Ly.d.conv + ": weight-stationary kernel joins IN(y) + r into a residual-stream buffer");
       return NST_E_SHAPE;

@@ -167,7 +167,11 @@ __global__ __launch_bounds__(256) void residual_kernel(const T* __restrict__ y, 
     for (int j = 0; j < CPC; ++j) {
       float rr = vr[j];
       if (rs) {
-        rr = rr * rsc[j] + rsh[j];
+        // as a normalising fill stages it (conv_impl.h norm_chunk): bf16 of one fma
+        if constexpr (sizeof(T) == 2)
+          rr = (float)(__bf16)__builtin_fmaf(rr, rsc[j], rsh[j]);
+        else
+          rr = rr * rsc[j] + rsh[j];
         if (r_relu) rr = fmaxf(rr, 0.f);
       }
       float v = vy[j] * ysc[j] + ysh[j];

@@ -108,7 +108,9 @@ def fill_operand(y: torch.Tensor, ys: Optional[torch.Tensor], in_relu: bool, r: 
                  rs: Optional[torch.Tensor] = None, relu_out: bool = False, round_bf16: bool = True) -> torch.Tensor:
     """The conv input the engine stages: y [n,c,h,w] (stored values), ys [n,c,2] {scale, shift}.
     No residual: fma(y, scale, shift) rounded once to fp32 (then bf16), ReLU.  Residual join
-    (ResidualBlock): r' + (y*scale + shift) in unfused fp32, r' = relu(r*scale_r + shift_r) if rs."""
+    (ResidualBlock): r' + (y*scale + shift) in unfused fp32, r' = relu(r*scale_r + shift_r) if rs
+    (bf16: r' = the normalised fill of r, rounded to bf16 — block 1's input x_0 as the trunk stores
+    it, conv_wstat.hip XO)."""
     rnd = bf16 if round_bf16 else (lambda t: t)
     if r is None:
         if ys is None:
@@ -121,7 +123,10 @@ def fill_operand(y: torch.Tensor, ys: Optional[torch.Tensor], in_relu: bool, r: 
     sc, sh = ys[..., 0][:, :, None, None], ys[..., 1][:, :, None, None]
     rr = r
     if rs is not None:
-        rr = (r * rs[..., 0][:, :, None, None] + rs[..., 1][:, :, None, None]).clamp_min(0.0)
+        if round_bf16:  # r' exactly as a normalising fill stages it (the stored x_0 of the fused trunk)
+            rr = fill_operand(r, rs, True, round_bf16=True)
+        else:
+            rr = (r * rs[..., 0][:, :, None, None] + rs[..., 1][:, :, None, None]).clamp_min(0.0)
     v = rr + (y * sc + sh)
     if relu_out:
         v = v.clamp_min(0.0)
