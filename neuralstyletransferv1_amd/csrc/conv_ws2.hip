@@ -18,7 +18,10 @@
 //     (y - dy) / 2 for the y-taps of y's parity;
 //   * the next tile's halo is loaded into registers (16 B per lane and slot, coalesced 33-pixel
 //     row runs) before the current tile's MFMAs and written to LDS after them (IN + ReLU applied),
-//     so its HBM latency hides behind the compute; three barriers per tile;
+//     so its HBM latency hides behind the compute; three barriers per tile.  Its source offsets
+//     come from per-tile row / column maps in LDS (built a tile ahead) and its IN constants from
+//     an LDS table (loaded with the halo, written after the MFMAs), so no address or padding math
+//     and no dependent global load sits in the fill;
 //   * output tile staged in LDS (8-byte slots XOR-swizzled by pixel: epilogue writes 2-way, store
 //     reads conflict-free; a 32-byte wave-slot swizzle was 4-way on the writes) and stored as whole pixels,
 //     16 B per lane; one InstanceNorm partial row per tile and row group.
@@ -52,7 +55,10 @@ struct W2Cfg {
   static constexpr int OUTB = TH * TW * PIXB;
   static constexpr int NST = OUTB / (NT * 16);      // 16-B output stores per thread
   static constexpr int BIAS_OFF = OUT_OFF + OUTB;
-  static constexpr int LDS = BIAS_OFF + COUT * 4;
+  static constexpr int NORM_OFF = BIAS_OFF + COUT * 4;     // the landing tile's IN {scale, shift} per channel
+  static constexpr int MAPB = ((LH + LW) * 4 + 15) / 16 * 16;
+  static constexpr int MAP_OFF = NORM_OFF + CINP * 8;       // 2 slots: halo row / column source offsets
+  static constexpr int LDS = MAP_OFF + 2 * MAPB;
   static constexpr int WBYTES = NCG * NSTEP * 64 * 16;
   static_assert(CINP % 32 == 0 && COUT % 16 == 0, "channel shapes");
   static_assert(NT % NCH == 0, "a thread's chunk is the same in every fill slot");
@@ -102,38 +108,63 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
   // ---- halo fill: slot k of this thread = chunk j = k NT + tid (entry j / NCH, chunk fc) ----
   const size_t frame_bytes = (size_t)p.hs * p.ws * p.cs * 2;
   const int fc = tid % C::NCH;
-  auto src_of = [&](const Work& wk, int k, int& ly, int& lx) -> int {  // byte offset, -1 = zero pad
+  auto build_maps = [&](const Work& wk, int slot) {  // source byte offsets of the halo rows / columns, -1 = pad
+    int* map = (int*)(smem + C::MAP_OFF + slot * C::MAPB);
+    for (int t = tid; t < C::LH + C::LW; t += C::NT) {
+      if (t < C::LH) {
+        const int sy = map_axis(2 * wk.oy0 - p.pad + t, p.hs, p.axis_mode, p.pre);
+        map[t] = sy < 0 ? -1 : sy * p.ws * p.cs * 2;
+      } else {
+        const int sx = map_axis(2 * wk.ox0 - p.pad + t - C::LH, p.ws, p.axis_mode, p.pre);
+        map[t] = sx < 0 ? -1 : sx * p.cs * 2;
+      }
+    }
+  };
+  auto entry_of = [&](int k, int& ly, int& lx) {
     const int e = (k * C::NT + tid) / C::NCH;
     ly = e / C::LW;
     lx = e - ly * C::LW;
-    const int sy = map_axis(2 * wk.oy0 - p.pad + ly, p.hs, p.axis_mode, p.pre);
-    const int sx = map_axis(2 * wk.ox0 - p.pad + lx, p.ws, p.axis_mode, p.pre);
-    return (sy < 0 || sx < 0) ? -1 : ((sy * p.ws + sx) * p.cs + fc * 8) * 2;
   };
-  auto issue = [&](const Work& wk, uint4 (&pf)[C::NPF]) {
+  float2 nv = make_float2(0.f, 0.f);  // this thread's channel of the landing tile's IN constants (tid < CINP)
+  uint32_t padm = 0;                   // bit k: slot k is zero padding
+  auto issue = [&](const Work& wk, int slot, uint4 (&pf)[C::NPF]) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)p.in + (size_t)wk.n * frame_bytes), (short)0, (int)frame_bytes, 0x00020000);
+    const int* map = (const int*)(smem + C::MAP_OFF + slot * C::MAPB);
+    padm = 0;
 #pragma unroll
     for (int k = 0; k < C::NPF; ++k) {
       int ly, lx;
-      const int s = src_of(wk, k, ly, lx);
+      entry_of(k, ly, lx);
       const bool ok = (k + 1) * C::NT <= C::NCHK || k * C::NT + tid < C::NCHK;
-      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, (ok && s >= 0) ? (uint32_t)s : 0x80000000u, 0, 0);
+      const int ro = map[ok ? ly : 0], co = map[C::LH + (ok ? lx : 0)];
+      const bool pad = ro < 0 || co < 0;
+      padm |= pad ? 1u << k : 0u;
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, (ok && !pad) ? (uint32_t)(ro + co + fc * 16) : 0x80000000u, 0, 0);
       pf[k] = __builtin_bit_cast(uint4, v);
     }
+    if (tid < CINP) nv = p.in_norm[(size_t)wk.n * p.cs + tid];
   };
-  auto land = [&](const Work& wk, const uint4 (&pf)[C::NPF]) {
+  auto put_norm = [&]() {  // after the MFMAs: the landing tile's IN constants into LDS
+    if (tid < CINP) *(float2*)(smem + C::NORM_OFF + tid * 8) = nv;
+  };
+  auto land = [&](const uint4 (&pf)[C::NPF]) {
     float2 nm[8];  // the producer's IN {scale, shift} of this thread's 8 channels
-    const float2* ns = p.in_norm + (size_t)wk.n * p.cs + fc * 8;
+    const float4* nl = (const float4*)(smem + C::NORM_OFF + fc * 64);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) nm[i] = ns[i];
+    for (int i = 0; i < 4; ++i) {
+      const float4 v = nl[i];
+      nm[2 * i] = make_float2(v.x, v.y);
+      nm[2 * i + 1] = make_float2(v.z, v.w);
+    }
 #pragma unroll
     for (int k = 0; k < C::NPF; ++k) {
       if ((k + 1) * C::NT > C::NCHK && k * C::NT + tid >= C::NCHK) continue;
       int ly, lx;
-      const int s = src_of(wk, k, ly, lx);
+      entry_of(k, ly, lx);
       uint4 v = norm_chunk<__bf16>(pf[k], nm);  // IN + ReLU (as the generic kernel's fill)
-      if (ZPAD && s < 0) v = make_uint4(0u, 0u, 0u, 0u);  // zero padding stays zero after IN + ReLU
+      if (ZPAD && ((padm >> k) & 1u)) v = make_uint4(0u, 0u, 0u, 0u);  // zero padding stays zero after IN + ReLU
       *(uint4*)(smem + ly * C::RS + (lx & 1) * C::LWE * C::EB + (lx >> 1) * C::EB + fc * 16) = v;
     }
   };
@@ -231,20 +262,28 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
   };
 
   // ---- persistent walk: B1 halo ready | MFMAs | B2 halo free | epilogue + next halo | B3 | stores ----
+  // map slot of the tile being issued: it & 1 (the maps of the tile after it are built before B3)
   Work cur = decode(w0);
   uint4 pf[C::NPF];
-  issue(cur, pf);
-  land(cur, pf);
-  for (int wn = w0 + G;; wn += G) {
+  build_maps(cur, 0);
+  build_maps(decode(min(w0 + G, p.n_work - 1)), 1);
+  __syncthreads();
+  issue(cur, 0, pf);
+  put_norm();
+  __syncthreads();
+  land(pf);
+  for (int wn = w0 + G, it = 1;; wn += G, ++it) {
     __syncthreads();
     const bool more = wn < p.n_work;
     const Work nxt = decode(more ? wn : w0);
-    if (more) issue(nxt, pf);
+    if (more) issue(nxt, it & 1, pf);
     Acc acc;
     kloop(acc);
+    put_norm();
     __syncthreads();
     epilogue(cur, acc);
-    if (more) land(nxt, pf);
+    if (more) land(pf);
+    build_maps(decode(min(wn + G, p.n_work - 1)), (it + 1) & 1);
     __syncthreads();
     store_out(cur);
     if (!more) break;
