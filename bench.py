@@ -26,7 +26,6 @@ SSIM / max |d| of the GPU output vs the CPU output.
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import os
 import sys
@@ -126,10 +125,9 @@ def cpu_baseline(frames_u8: np.ndarray, sd, nframes: int):
     }, outs
 
 
-def _lib_sha() -> str:
+def _kernel_sha() -> str:
     from neuralstyletransferv1_amd import _lib
-    with open(_lib.LIB_PATH, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+    return _lib.trunk_kernel_sha()
 
 
 def main():
@@ -221,19 +219,19 @@ def main():
     layer_ms = {n: round(ms / max(c, 1), 4) for (n, ms, c) in prof}
     conv_ms_per_step = sum(ms for _, ms, _ in prof) / kp
 
-    # HBM traffic of the dominant kernel from the rocprofv3 PMC pass of this same library build
-    # (tools/prof_pass.sh + tools/pmc_summary.py write it with the library's hash); a summary of an
-    # older build is not used
-    traffic, traffic_note = None, "no PMC summary for this library build"
+    # HBM traffic of the dominant kernel from the rocprofv3 PMC pass of this same kernel build
+    # (tools/prof_pass.sh + tools/pmc_summary.py write it keyed by the hash of the kernel's sources and
+    # build flags, _lib.TRUNK_KERNEL_SOURCES); a summary of another version of the kernel is not used
+    traffic, traffic_note = None, "no PMC summary for this kernel build"
     pmc_path = os.path.join(REPO, "profiles", "pmc_res_conv.json")
     if os.path.exists(pmc_path) and (H, W) == (1080, 1920):
         try:
             with open(pmc_path) as f:
                 pm = json.load(f)
-            if pm.get("lib_sha16") == _lib_sha():
+            if pm.get("kernel_src_sha16") == _kernel_sha():
                 traffic, traffic_note = pm.get("hbm_bytes_per_launch"), pm.get("source")
             else:
-                traffic_note = f"PMC summary is of library {pm.get('lib_sha16')}, not this build"
+                traffic_note = f"PMC summary is of kernel sources {pm.get('kernel_src_sha16')}, not this build"
         except Exception as e:  # noqa: BLE001
             traffic_note = f"unreadable PMC summary: {e}"
 

@@ -70,6 +70,24 @@ class NstError(RuntimeError):
     """Raised for any non-zero status from libnst_hip (message from nst_last_error)."""
 
 
+# Sources (and build flags) that determine the residual-trunk kernel's machine code: the key under
+# which tools/pmc_summary.py files that kernel's PMC traffic and bench.py looks it up, so unrelated
+# library changes do not orphan the measurement (and any change to the kernel does).
+TRUNK_KERNEL_SOURCES = ("csrc/conv_wstat.hip", "csrc/conv_ws_common.h", "csrc/conv_impl.h")
+
+
+def trunk_kernel_sha() -> str:
+    import hashlib
+    import re
+    h = hashlib.sha256()
+    for rel in TRUNK_KERNEL_SOURCES:
+        with open(os.path.join(_HERE, rel), "rb") as f:
+            h.update(f.read())
+    with open(os.path.join(_HERE, "..", "Makefile")) as f:  # the compiler and flags the kernel is built with
+        h.update("".join(l for l in f if re.match(r"(HIPCC|ARCH|SLP|CXXFLAGS) |.*conv_wstat", l)).encode())
+    return h.hexdigest()[:16]
+
+
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is not None:

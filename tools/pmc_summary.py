@@ -63,9 +63,8 @@ def main():
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
             json.dump(out, f, indent=1)
     if "--res-json" in sys.argv:  # the dominant kernel's summary bench.py reads (keyed by the library build)
-        import hashlib
-        lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "neuralstyletransferv1_amd",
-                           "libnst_hip.so")
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from neuralstyletransferv1_amd._lib import trunk_kernel_sha
         key = next(k for k in out if "wstat_kernel<8, 0," in k)
         r = out[key]
         res = {
@@ -73,7 +72,7 @@ def main():
                       "--pmc passes in separate runs of bench.py)",
             "units": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half of a wide "
                      "coalesced read stream, MI355X_MICROARCH.md HBM section)",
-            "lib_sha16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16],
+            "kernel_src_sha16": trunk_kernel_sha(),
             "res_conv_kernel": key,
             "hbm_bytes_per_launch": r.get("hbm_bytes"),
             "fetch_size_kib": r.get("FETCH_SIZE"),
