@@ -286,6 +286,54 @@ int nst_gatys_grad_capture(nst_vgg* v, const float* image, int h, int w, const f
 int nst_adam_step(float* x, const float* grad, float* m, float* v, int c, int hw, float lr, float beta1,
                   float beta2, float eps, int step, int clamp01, int grad_is_normalised, void* stream);
 
+/* ---- DeepLab v3+ mask program (BASELINE.json configs[4]) ----
+ * The network of modeling/deeplab.py:9-33 as sky_swap.py:143-177 load_deeplab builds it: backbone
+ * 'resnet' (ResNet-101, modeling/backbone/resnet.py:45-124), output stride 16, BatchNorm2d in eval mode,
+ * ASPP (modeling/aspp.py:34-78), decoder (modeling/decoder.py:7-43).  Parameters by their state_dict
+ * names without the "module." prefix (sky_swap.py:150 strips it), e.g. "backbone.layer3.22.conv2.weight",
+ * "aspp.global_avg_pool.1.weight", "decoder.last_conv.8.bias"; running_mean / running_var are used,
+ * num_batches_tracked is ignored.  NHWC activations in the compute dtype, fp32 accumulation. */
+typedef struct nst_seg nst_seg;
+int nst_seg_create(const nst_param* params, int n_params, int num_classes, int compute_dtype, int device,
+                   nst_seg** out);
+void nst_seg_destroy(nst_seg* s);
+int nst_seg_num_classes(const nst_seg* s);
+int nst_seg_workspace_bytes(const nst_seg* s, int n, int h, int w, size_t* out);
+/*
+ * DeepLab.forward (deeplab.py:27-33) on a batch.  x: NST_IO_F32_NCHW = the module input [n,3,h,w]
+ * (already normalised), or NST_IO_U8_NHWC = frames [n,h,w,3] with sky_swap.py:179-183 preprocess_pil
+ * fused.  logits (optional): f32 NCHW [n,nc,h,w] = the module output (bilinear, align_corners=True);
+ * pred (optional): u8 [n,h,w] = logits.argmax(1) (sky_swap.py:189-193: the second interpolate to the
+ * same size is the identity).
+ */
+int nst_seg_forward(nst_seg* s, const void* x, int x_fmt, int n, int h, int w, float* logits, uint8_t* pred,
+                    void* workspace, size_t workspace_bytes, void* stream);
+/*
+ * infer_mask's post-processing (sky_swap.py:196-215) on class maps pred [n,h,w] -> mask u8 [n,h,w]:
+ * 255 where pred is one of target_ids, MORPH_CLOSE with ones(close_ks, close_ks) (5 in the reference;
+ * 0 skips), dilate ones(2e+1), erode ones(2c+1), GaussianBlur(sigma = feather_px / 2) (cv2 restated:
+ * parity unpinned).  scratch: nst_seg_mask_scratch_bytes.
+ */
+int nst_seg_mask_scratch_bytes(int n, int h, int w, size_t* out);
+int nst_seg_mask(const uint8_t* pred, int n, int h, int w, const int* target_ids, int n_ids, int close_ks,
+                 int expand_px, int contract_px, int feather_px, uint8_t* mask, void* scratch, size_t scratch_bytes,
+                 void* stream);
+
+/* ---- image resamplers of the mask / inference_res paths ----
+ * NST_RESIZE_PIL_LANCZOS: Pillow Image.resize((ow, oh), Image.LANCZOS) of RGB frames (sky_swap.py:294-301,
+ *   pipeline.py:1089-1097 --inference_res): Resample.c's two integer passes, bit-exact.
+ * NST_RESIZE_CV_LINEAR: cv2.resize(m, (ow, oh), interpolation=INTER_LINEAR) of u8 images with c channels
+ *   (sky_swap.py:321-324 mask upscale): OpenCV's fixed-point taps restated (cv2 absent: parity unpinned).
+ * A resampler is made once per (h, w) -> (oh, ow) geometry: its tap tables live on the device. */
+#define NST_RESIZE_PIL_LANCZOS 0
+#define NST_RESIZE_CV_LINEAR 1
+typedef struct nst_resize nst_resize;
+int nst_resize_create(int kind, int h, int w, int oh, int ow, int device, nst_resize** out);
+void nst_resize_destroy(nst_resize* r);
+int nst_resize_scratch_bytes(const nst_resize* r, int n, size_t* out);
+int nst_resize_u8(const nst_resize* r, const uint8_t* in, int n, int c, uint8_t* out, void* scratch,
+                  size_t scratch_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,6 +37,9 @@ EXPORTED_SYMBOLS = (
     "nst_mask_feather", "nst_create_ex", "nst_num_ops", "nst_op_describe", "nst_forward_capture",
     "nst_gram_workspace_bytes", "nst_vgg_create", "nst_vgg_destroy", "nst_gatys_buffer_bytes", "nst_vgg_features",
     "nst_gatys_targets", "nst_gatys_grad", "nst_adam_step", "nst_gatys_grad_capture",
+    "nst_seg_create", "nst_seg_destroy", "nst_seg_num_classes", "nst_seg_workspace_bytes", "nst_seg_forward",
+    "nst_seg_mask_scratch_bytes", "nst_seg_mask", "nst_resize_create", "nst_resize_destroy",
+    "nst_resize_scratch_bytes", "nst_resize_u8",
 )
 NST_GRAM_CHW, NST_GRAM_HWC = 0, 1
 
@@ -84,7 +87,7 @@ def trunk_kernel_sha() -> str:
         with open(os.path.join(_HERE, rel), "rb") as f:
             h.update(f.read())
     with open(os.path.join(_HERE, "..", "Makefile")) as f:  # the compiler and flags the kernel is built with
-        h.update("".join(l for l in f if re.match(r"(HIPCC|ARCH|SLP|CXXFLAGS) |.*conv_wstat", l)).encode())
+        h.update("".join(l for l in f if re.match(r"(HIPCC|ARCH|SLP|CXXFLAGS) |\$\(BUILD\)/conv_wstat", l)).encode())
     return h.hexdigest()[:16]
 
 
@@ -123,6 +126,19 @@ def lib() -> ctypes.CDLL:
         L.nst_adam_step.argtypes = [vp, vp, vp, vp, i, i, f, f, f, f, i, i, i, vp]
         L.nst_destroy.argtypes = [vp]
         L.nst_destroy.restype = None
+        L.nst_seg_create.argtypes = [ctypes.POINTER(NstParam), i, i, i, i, ctypes.POINTER(vp)]
+        L.nst_seg_destroy.argtypes = [vp]
+        L.nst_seg_destroy.restype = None
+        L.nst_seg_num_classes.argtypes = [vp]
+        L.nst_seg_workspace_bytes.argtypes = [vp, i, i, i, ctypes.POINTER(sz)]
+        L.nst_seg_forward.argtypes = [vp, vp, i, i, i, i, vp, vp, vp, sz, vp]
+        L.nst_seg_mask_scratch_bytes.argtypes = [i, i, i, ctypes.POINTER(sz)]
+        L.nst_seg_mask.argtypes = [vp, i, i, i, ctypes.POINTER(i), i, i, i, i, i, vp, vp, sz, vp]
+        L.nst_resize_create.argtypes = [i, i, i, i, i, i, ctypes.POINTER(vp)]
+        L.nst_resize_destroy.argtypes = [vp]
+        L.nst_resize_destroy.restype = None
+        L.nst_resize_scratch_bytes.argtypes = [vp, i, ctypes.POINTER(sz)]
+        L.nst_resize_u8.argtypes = [vp, vp, i, i, vp, vp, sz, vp]
         L.nst_output_hw.argtypes = [vp, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
         L.nst_workspace_bytes.argtypes = [vp, i, i, i, ctypes.POINTER(sz)]
         L.nst_forward.argtypes = [vp, vp, i, i, i, i, i, vp, i, vp, sz, vp]
@@ -146,7 +162,9 @@ def lib() -> ctypes.CDLL:
         L.nst_num_layers.restype = i
         L.nst_layer_name.argtypes = [vp, i]
         L.nst_layer_name.restype = ctypes.c_char_p
-        for name in ("nst_vgg_create", "nst_gatys_buffer_bytes", "nst_vgg_features", "nst_gatys_targets",
+        for name in ("nst_seg_create", "nst_seg_num_classes", "nst_seg_workspace_bytes", "nst_seg_forward",
+                     "nst_seg_mask_scratch_bytes", "nst_seg_mask", "nst_resize_create", "nst_resize_scratch_bytes",
+                     "nst_resize_u8", "nst_vgg_create", "nst_gatys_buffer_bytes", "nst_vgg_features", "nst_gatys_targets",
                      "nst_gatys_grad", "nst_adam_step", "nst_create", "nst_create_ex", "nst_op_describe", "nst_forward_capture", "nst_output_hw", "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8",
                      "nst_lab_create", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
                      "nst_profile_end"):

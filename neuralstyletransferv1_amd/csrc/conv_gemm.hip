@@ -1,0 +1,220 @@
+// conv_gemm.hip — K-streaming implicit-GEMM convolution for the DeepLab v3+ ResNet-101 mask network
+// (modeling/backbone/resnet.py:6-43 Bottleneck, :61-65 stem; modeling/aspp.py:7-78; modeling/decoder.py:19-43).
+//
+// The stylization kernels stage a tile's whole input halo (all channels) in LDS once; ResNet-101's
+// 1024/2048-channel layers do not fit that, so this kernel streams K instead: one STAGE = one tap x
+// 128 bytes of input channels (64 bf16 or 32 fp32), double-buffered in LDS through registers (the
+// next stage's global loads are in flight while the current stage's MFMAs run; one barrier per stage).
+//
+//   * GEMM rows = output channels (A = packed weights, one contiguous 8 KiB piece per 64 rows and
+//     stage: [cout/64][stage][64][128 B]); columns = output pixels (B = an im2col row gathered on the
+//     fly: pixel (n,oy,ox), tap (ky,kx) -> source (oy*s - pad + ky*d, ox*s - pad + kx*d), zero outside
+//     the image: Conv2d zero padding, any stride and dilation — the atrous convs of layer4 / ASPP).
+//   * 4 waves in 2x2, each (BM/2)x(BN/2) of the BMxBN tile; bf16: v_mfma_f32_16x16x32_bf16, one per
+//     16x16 sub-tile and half-stage; fp32 (parity mode): v_mfma_f32_16x16x4_f32, 4 per half-stage over
+//     a 16-byte operand read (the K permutation is the same for A and B, so the sum is over the same
+//     products).
+//   * LDS image per stage: [half][row][4 x 16-B chunks] with the chunk index XOR (((row >> 3) & 1) << 1):
+//     each of ds_read_b128's four 16-lane groups (lanes {0-3,12-15,20-27}, ...) then touches 16
+//     distinct 16-B bank slots (MI355X_MICROARCH.md §LDS).
+//   * epilogue: eval BatchNorm as y = acc * scale + shift (torch's inference form: alpha = gamma /
+//     sqrt(var + eps), beta = bias - mean * alpha), + residual, ReLU, NHWC store at a channel offset.
+#include <hip/hip_runtime.h>
+
+#include "nst_hip.h"
+#include "seg_internal.h"
+
+namespace nst {
+
+namespace {
+
+typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
+typedef float f32x4_g __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_g __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int chunk_swz(int row) { return ((row >> 3) & 1) << 1; }
+
+__device__ __forceinline__ float bf_to_f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ uint16_t f_to_bf(float f) {  // round to nearest even (finite inputs)
+  const uint32_t u = __float_as_uint(f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+template <int BM, int BN, bool F32>
+__global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
+  constexpr int MI = BM / 32, NI = BN / 32;      // 16x16 sub-tiles per wave along rows / columns
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, BUF = A_BYTES + B_BYTES;
+  constexpr int A_TPR = 256 / BM, A_CPT = 8 / A_TPR;  // loader threads per row, 16-B chunks per thread
+  constexpr int B_TPR = 256 / BN, B_CPT = 8 / B_TPR;
+  constexpr int ESZ = F32 ? 4 : 2;
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int pix0 = blockIdx.x * BN, row0 = blockIdx.y * BM;
+
+  // ---- loader roles ----
+  const int a_row = tid / A_TPR, a_c0 = (tid % A_TPR) * A_CPT;
+  const int b_pix = tid / B_TPR, b_c0 = (tid % B_TPR) * B_CPT;
+  const int gp = pix0 + b_pix;
+  const bool pvalid = gp < p.npix;
+  int img = 0, oy = 0, ox = 0;
+  if (pvalid) {
+    const int hw = p.ho * p.wo;
+    img = gp / hw;
+    const int r = gp - img * hw;
+    oy = r / p.wo;
+    ox = r - oy * p.wo;
+  }
+  const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
+  const char* in_img = (const char*)p.in + (size_t)img * p.hi * p.wi * p.cs * ESZ + b_c0 * 16;
+  const int nck = p.cin / (128 / ESZ);
+  const int nstage = p.kh * p.kw * nck;
+  const int ablk = (row0 + a_row) >> 6;
+  const char* wsrc = (const char*)p.wpk + ((size_t)ablk * nstage * 64 + (a_row & 63)) * 128 + a_c0 * 16;
+  const size_t wstage = 64 * 128;
+
+  u32x4_g ra[A_CPT], rb[B_CPT];
+  auto load_stage = [&](int s) {
+    const char* wa = wsrc + (size_t)s * wstage;
+#pragma unroll
+    for (int j = 0; j < A_CPT; ++j) ra[j] = *(const u32x4_g*)(wa + j * 16);
+    const int tap = s / nck, cc = s - tap * nck;
+    const int ky = tap / p.kw, kx = tap - ky * p.kw;
+    const int iy = iy0 + ky * p.dil, ix = ix0 + kx * p.dil;
+    const bool ok = pvalid && (unsigned)iy < (unsigned)p.hi && (unsigned)ix < (unsigned)p.wi;
+    const char* src = in_img + ((size_t)iy * p.wi + ix) * p.cs * ESZ + cc * 128;
+#pragma unroll
+    for (int j = 0; j < B_CPT; ++j) {
+      u32x4_g v = {0u, 0u, 0u, 0u};
+      if (ok) v = *(const u32x4_g*)(src + j * 16);
+      rb[j] = v;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    char* A = lds + buf * BUF;
+    char* B = A + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < A_CPT; ++j) {
+      const int c = a_c0 + j, half = c >> 2, q = c & 3;
+      *(u32x4_g*)(A + half * (BM * 64) + a_row * 64 + ((q ^ chunk_swz(a_row)) << 4)) = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < B_CPT; ++j) {
+      const int c = b_c0 + j, half = c >> 2, q = c & 3;
+      *(u32x4_g*)(B + half * (BN * 64) + b_pix * 64 + ((q ^ chunk_swz(b_pix)) << 4)) = rb[j];
+    }
+  };
+
+  // ---- fragment addressing: lane (r16, g) reads row r16 of a 16-row sub-tile, chunk g (swizzled) ----
+  const int r16 = lane & 15, g = lane >> 4;
+  const int frag_off = r16 * 64 + ((g ^ chunk_swz(r16)) << 4);
+  const int a_off = (wm * (BM / 2)) * 64 + frag_off;
+  const int b_off = A_BYTES + (wn * (BN / 2)) * 64 + frag_off;
+
+  f32x4_g acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4_g{0.f, 0.f, 0.f, 0.f};
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  for (int s = 0; s < nstage; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < nstage;
+    if (more) load_stage(s + 1);
+    const char* base = lds + cur * BUF;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      u32x4_g a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = *(const u32x4_g*)(base + half * (BM * 64) + a_off + i * 16 * 64);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = *(const u32x4_g*)(base + half * (BN * 64) + b_off + j * 16 * 64);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          if constexpr (F32) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].x), __uint_as_float(b[j].x), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].y), __uint_as_float(b[j].y), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].z), __uint_as_float(b[j].z), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].w), __uint_as_float(b[j].w), acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_g, a[i]),
+                                                                __builtin_bit_cast(bf16x8_g, b[j]), acc[i][j], 0, 0, 0);
+          }
+        }
+    }
+    if (more) store_stage(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns output channels co..co+3 of one pixel per sub-tile ----
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int px = pix0 + wn * (BN / 2) + j * 16 + r16;
+    if (px >= p.npix) continue;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int co = row0 + wm * (BM / 2) + i * 16 + 4 * g;
+      if (co >= p.cout_store) continue;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = acc[i][j][q] * p.scale[co + q] + p.shift[co + q];
+      if (p.res) {
+        if constexpr (F32) {
+          const float4 r = *(const float4*)((const float*)p.res + (size_t)px * p.res_cs + co);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        } else {
+          const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
+          v[0] += bf_to_f((uint16_t)(r.x & 0xffff)); v[1] += bf_to_f((uint16_t)(r.x >> 16));
+          v[2] += bf_to_f((uint16_t)(r.y & 0xffff)); v[3] += bf_to_f((uint16_t)(r.y >> 16));
+        }
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      }
+      const size_t o = (size_t)px * p.out_cs + p.out_off + co;
+      if (F32 || p.out_f32) {
+        *(float4*)((float*)p.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 w;
+        w.x = (uint32_t)f_to_bf(v[0]) | ((uint32_t)f_to_bf(v[1]) << 16);
+        w.y = (uint32_t)f_to_bf(v[2]) | ((uint32_t)f_to_bf(v[3]) << 16);
+        *(uint2*)((uint16_t*)p.out + o) = w;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, bool F32>
+void launch_tile(const GemmConvParams& p, hipStream_t st) {
+  const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM));
+  hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, F32>), grid, dim3(256), 0, st, p);
+}
+
+}  // namespace
+
+hipError_t launch_gemm_conv(int dtype, const GemmConvParams& p, hipStream_t st) {
+  const int ck = gemm_stage_channels(dtype);
+  if (p.npix <= 0 || p.cin <= 0 || p.cin % ck || p.cs % 8 || p.cout_store % 4 || p.out_off % 4 ||
+      p.out_cs % 4 || (p.res && p.res_cs % 4))
+    return hipErrorInvalidValue;
+  // 128x128 tiles when they alone give the chip a few waves of workgroups; 64x64 otherwise
+  const long big = (long)((p.npix + 127) / 128) * ((p.cout_store + 127) / 128);
+  const bool f32 = dtype == NST_DT_F32;
+  if (big >= 512) {
+    if (f32) launch_tile<128, 128, true>(p, st);
+    else launch_tile<128, 128, false>(p, st);
+  } else {
+    if (f32) launch_tile<64, 64, true>(p, st);
+    else launch_tile<64, 64, false>(p, st);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace nst

@@ -5,6 +5,7 @@
 #include <algorithm>
 
 #include "nst_internal.h"
+#include "seg_internal.h"
 #include "nst_hip.h"
 
 namespace nst {
@@ -614,7 +615,8 @@ __global__ __launch_bounds__(256) void feather_rows_kernel(const uint8_t* __rest
   tmp[f + (size_t)y * w + x] = s;
 }
 __global__ __launch_bounds__(256) void feather_cols_kernel(const float* __restrict__ tmp, int h, int w, int r,
-                                                           double sigma, float* __restrict__ alpha) {
+                                                           double sigma, float* __restrict__ alpha,
+                                                           uint8_t* __restrict__ out_u8) {
   __shared__ float k[2 * FEATHER_MAX_R + 1];
   feather_taps(k, r, sigma);
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
@@ -623,7 +625,8 @@ __global__ __launch_bounds__(256) void feather_cols_kernel(const float* __restri
   float s = 0.f;
   for (int i = -r; i <= r; ++i) s += k[i + r] * tmp[f + (size_t)reflect101(y + i, h) * w + x];
   const float u8 = fminf(fmaxf(rintf(s), 0.f), 255.f);  // saturate_cast<uchar>
-  alpha[f + (size_t)y * w + x] = u8 / 255.0f;
+  if (out_u8) out_u8[f + (size_t)y * w + x] = (uint8_t)u8;  // the blurred mask itself (sky_swap.py:213-215)
+  else alpha[f + (size_t)y * w + x] = u8 / 255.0f;
 }
 
 int feather_radius(float sigma) {
@@ -639,7 +642,20 @@ hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigm
   hipLaunchKernelGGL(feather_rows_kernel, grid, dim3(256), 0, st, m, h, w, r, (double)sigma, tmp);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(feather_cols_kernel, grid, dim3(256), 0, st, tmp, h, w, r, (double)sigma, alpha);
+  hipLaunchKernelGGL(feather_cols_kernel, grid, dim3(256), 0, st, tmp, h, w, r, (double)sigma, alpha, nullptr);
+  return hipGetLastError();
+}
+
+// the same blur with the uint8 result kept (the DeepLab mask's feather, sky_swap.py:213-215)
+hipError_t launch_seg_gauss_u8(const uint8_t* m, int n, int h, int w, float sigma, float* tmp, uint8_t* out,
+                               hipStream_t st) {
+  const int r = feather_radius(sigma);
+  if (r > FEATHER_MAX_R || !(sigma > 0.f)) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((w + 255) / 256), (unsigned)h, (unsigned)n);
+  hipLaunchKernelGGL(feather_rows_kernel, grid, dim3(256), 0, st, m, h, w, r, (double)sigma, tmp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(feather_cols_kernel, grid, dim3(256), 0, st, tmp, h, w, r, (double)sigma, nullptr, out);
   return hipGetLastError();
 }
 

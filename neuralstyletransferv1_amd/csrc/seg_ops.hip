@@ -1,0 +1,356 @@
+// seg_ops.hip — the non-GEMM stages of the DeepLab v3+ mask program (configs[4]):
+// the stem's normalised im2col, max / average pooling, align_corners=True bilinear resizes written
+// into concatenation buffers, the final upsample + argmax, the class-id selection, the binary
+// morphology and the two image resamplers of the mask path (Pillow LANCZOS for the working-size
+// downscale, OpenCV INTER_LINEAR for the mask's upscale).  All NHWC, one thread per output element
+// or 16-byte channel group; HBM-bound streaming kernels.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "nst_hip.h"
+#include "seg_internal.h"
+
+namespace nst {
+
+namespace {
+
+__device__ __forceinline__ float ld_act(const void* p, size_t i, bool f32) {
+  return f32 ? ((const float*)p)[i] : __uint_as_float((uint32_t)((const uint16_t*)p)[i] << 16);
+}
+__device__ __forceinline__ uint16_t bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ void st_act(void* p, size_t i, float v, bool f32) {
+  if (f32) ((float*)p)[i] = v;
+  else ((uint16_t*)p)[i] = bf16_rne(v);
+}
+inline unsigned blocks_for(size_t n, int per = 256) { return (unsigned)((n + per - 1) / per); }
+
+// ---- stem im2col (sky_swap.py:179-183 preprocess_pil fused for u8 frames) ----
+// u8: float32(u8) / 255 in float32, then (x - mean) / std in float64 (numpy promotes the float32
+// array against the float64 tuples), then .float() -> float32 — reproduced operation for operation.
+__global__ __launch_bounds__(256) void stem_im2col_kernel(const void* __restrict__ x, int x_u8, int f32, int n, int h,
+                                                          int w, int ho, int wo, int kp, void* __restrict__ col) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)n * ho * wo * kp;
+  if (e >= total) return;
+  const int k = (int)(e % kp);
+  const size_t px = e / kp;
+  const int ox = (int)(px % wo);
+  const int oy = (int)((px / wo) % ho);
+  const int img = (int)(px / ((size_t)wo * ho));
+  float v = 0.f;
+  if (k < 147) {
+    const int c = k % 3, tap = k / 3, ky = tap / 7, kx = tap % 7;
+    const int iy = oy * 2 - 3 + ky, ix = ox * 2 - 3 + kx;
+    if (iy >= 0 && iy < h && ix >= 0 && ix < w) {
+      if (x_u8) {
+        const double mean[3] = {0.485, 0.456, 0.406}, sd[3] = {0.229, 0.224, 0.225};
+        const float x01 = (float)((const uint8_t*)x)[(((size_t)img * h + iy) * w + ix) * 3 + c] / 255.0f;
+        v = (float)(((double)x01 - mean[c]) / sd[c]);
+      } else {
+        v = ((const float*)x)[(((size_t)img * 3 + c) * h + iy) * w + ix];
+      }
+    }
+  }
+  st_act(col, e, v, f32);
+}
+
+// ---- MaxPool2d(3, stride 2, padding 1) (resnet.py:65), NHWC ----
+__global__ __launch_bounds__(256) void maxpool_kernel(const void* __restrict__ in, int f32, int n, int h, int w, int c,
+                                                      void* __restrict__ out, int ho, int wo) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)n * ho * wo * c;
+  if (e >= total) return;
+  const int ch = (int)(e % c);
+  const size_t px = e / c;
+  const int ox = (int)(px % wo), oy = (int)((px / wo) % ho), img = (int)(px / ((size_t)wo * ho));
+  float m = -FLT_MAX;
+  bool any = false;
+  for (int dy = 0; dy < 3; ++dy) {
+    const int iy = oy * 2 - 1 + dy;
+    if (iy < 0 || iy >= h) continue;
+    for (int dx = 0; dx < 3; ++dx) {
+      const int ix = ox * 2 - 1 + dx;
+      if (ix < 0 || ix >= w) continue;
+      const float v = ld_act(in, (((size_t)img * h + iy) * w + ix) * c + ch, f32);
+      m = any ? fmaxf(m, v) : v;
+      any = true;
+    }
+  }
+  st_act(out, e, m, f32);
+}
+
+// ---- AdaptiveAvgPool2d(1) (aspp.py:55): torch takes mean over (h, w); summed here in fp64 ----
+__global__ __launch_bounds__(256) void avgpool_kernel(const void* __restrict__ in, int f32, int hw, int c, int cs,
+                                                      void* __restrict__ out) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x, img = blockIdx.y;
+  if (ch >= c) return;
+  double s = 0.0;
+  const size_t base = (size_t)img * hw * cs + ch;
+  for (int i = 0; i < hw; ++i) s += (double)ld_act(in, base + (size_t)i * cs, f32);
+  st_act(out, (size_t)img * cs + ch, (float)(s / hw), f32);
+}
+
+// ---- bilinear, align_corners=True (deeplab.py:31, aspp.py:71, decoder.py:39): torch's CPU
+// arithmetic — scale = (in-1)/(out-1) in float, src = scale*dst, i0 = floor, lambda in float,
+// v = (v00*l0x + v01*l1x)*l0y + (v10*l0x + v11*l1x)*l1y ----
+struct AcAxis {
+  int i0, i1;
+  float l0, l1;
+};
+__device__ __forceinline__ AcAxis ac_axis(int dst, int in, int out) {
+  const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  const float real = scale * (float)dst;
+  int i0 = min((int)floorf(real), in - 1);
+  const float lam = fminf(fmaxf(real - (float)i0, 0.f), 1.f);
+  AcAxis a;
+  a.i0 = i0;
+  a.i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  a.l1 = lam;
+  a.l0 = 1.f - lam;
+  return a;
+}
+
+__global__ __launch_bounds__(256) void resize_ac_kernel(const void* __restrict__ in, int f32, int n, int h, int w,
+                                                        int c, int cs_in, void* __restrict__ out, int oh, int ow,
+                                                        int cs_out, int off) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)n * oh * ow * c;
+  if (e >= total) return;
+  const int ch = (int)(e % c);
+  const size_t px = e / c;
+  const int ox = (int)(px % ow), oy = (int)((px / ow) % oh), img = (int)(px / ((size_t)ow * oh));
+  const AcAxis ay = ac_axis(oy, h, oh), ax = ac_axis(ox, w, ow);
+  const size_t b = (size_t)img * h * w;
+  const float v00 = ld_act(in, (b + (size_t)ay.i0 * w + ax.i0) * cs_in + ch, f32);
+  const float v01 = ld_act(in, (b + (size_t)ay.i0 * w + ax.i1) * cs_in + ch, f32);
+  const float v10 = ld_act(in, (b + (size_t)ay.i1 * w + ax.i0) * cs_in + ch, f32);
+  const float v11 = ld_act(in, (b + (size_t)ay.i1 * w + ax.i1) * cs_in + ch, f32);
+  const float t0 = v00 * ax.l0 + v01 * ax.l1;
+  const float t1 = v10 * ax.l0 + v11 * ax.l1;
+  st_act(out, px * cs_out + off + ch, t0 * ay.l0 + t1 * ay.l1, f32);
+}
+
+// ---- final upsample (deeplab.py:31) + argmax over classes (sky_swap.py:193: first maximum wins) ----
+__global__ __launch_bounds__(256) void upsample_argmax_kernel(const float* __restrict__ lg, int n, int h4, int w4,
+                                                              int nc, int ncs, int h, int w, uint8_t* __restrict__ pred,
+                                                              float* __restrict__ lout) {
+  const size_t px = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (px >= (size_t)n * h * w) return;
+  const int ox = (int)(px % w), oy = (int)((px / w) % h), img = (int)(px / ((size_t)w * h));
+  const AcAxis ay = ac_axis(oy, h4, h), ax = ac_axis(ox, w4, w);
+  const size_t b = (size_t)img * h4 * w4;
+  const float* p00 = lg + (b + (size_t)ay.i0 * w4 + ax.i0) * ncs;
+  const float* p01 = lg + (b + (size_t)ay.i0 * w4 + ax.i1) * ncs;
+  const float* p10 = lg + (b + (size_t)ay.i1 * w4 + ax.i0) * ncs;
+  const float* p11 = lg + (b + (size_t)ay.i1 * w4 + ax.i1) * ncs;
+  float best = 0.f;
+  int arg = 0;
+  for (int c = 0; c < nc; ++c) {
+    const float t0 = p00[c] * ax.l0 + p01[c] * ax.l1;
+    const float t1 = p10[c] * ax.l0 + p11[c] * ax.l1;
+    const float v = t0 * ay.l0 + t1 * ay.l1;
+    if (c == 0 || v > best) {
+      best = v;
+      arg = c;
+    }
+    if (lout) lout[(((size_t)img * nc + c) * h + oy) * w + ox] = v;
+  }
+  if (pred) pred[px] = (uint8_t)arg;
+}
+
+__global__ __launch_bounds__(256) void select_kernel(const uint8_t* __restrict__ pred, size_t npix, SegIdSet ids,
+                                                     uint8_t* __restrict__ mask) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const int c = pred[p];
+  mask[p] = ((ids.bits[c >> 5] >> (c & 31)) & 1u) ? 255 : 0;
+}
+
+// ---- rectangle morphology (cv2.dilate / cv2.erode with ones(k, k), anchor at the centre, default
+// border = ignored): separable, rows then columns ----
+__global__ __launch_bounds__(256) void morph_pass_kernel(const uint8_t* __restrict__ in, int n, int h, int w, int k,
+                                                         int op, int vertical, uint8_t* __restrict__ out) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (size_t)n * h * w) return;
+  const int x = (int)(p % w), y = (int)((p / w) % h);
+  const size_t img = p / ((size_t)w * h);
+  const int a = k / 2;
+  int m = op == 0 ? 0 : 255;
+  const int lo = (vertical ? y : x) - a, len = vertical ? h : w;
+  for (int i = 0; i < k; ++i) {
+    const int q = lo + i;
+    if (q < 0 || q >= len) continue;
+    const int v = vertical ? in[(img * h + q) * w + x] : in[(img * h + y) * w + q];
+    m = op == 0 ? max(m, v) : min(m, v);
+  }
+  out[p] = (uint8_t)m;
+}
+
+// ---- cv2.resize INTER_LINEAR on u8 (OpenCV's fixed-point path: 11-bit taps, horizontal sums as
+// int, vertical ((b0*(S0>>4))>>16 + (b1*(S1>>4))>>16 + 2) >> 2) ----
+__global__ __launch_bounds__(256) void resize_linear_cv_kernel(const uint8_t* __restrict__ in, int n, int h, int w,
+                                                               int c, uint8_t* __restrict__ out, int oh, int ow,
+                                                               const int* __restrict__ xofs,
+                                                               const short* __restrict__ xa,
+                                                               const int* __restrict__ yofs,
+                                                               const short* __restrict__ yb) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)n * oh * ow * c) return;
+  const int ch = (int)(e % c);
+  const size_t px = e / c;
+  const int dx = (int)(px % ow), dy = (int)((px / ow) % oh);
+  const size_t img = px / ((size_t)ow * oh);
+  const int sx = xofs[dx], sx1 = min(sx + 1, w - 1);
+  const int a0 = xa[2 * dx], a1 = xa[2 * dx + 1];
+  const int sy = yofs[dy];
+  const int r0 = min(max(sy, 0), h - 1), r1 = min(max(sy + 1, 0), h - 1);
+  const uint8_t* row0 = in + (img * h + r0) * (size_t)w * c;
+  const uint8_t* row1 = in + (img * h + r1) * (size_t)w * c;
+  const int S0 = row0[sx * c + ch] * a0 + row0[sx1 * c + ch] * a1;
+  const int S1 = row1[sx * c + ch] * a0 + row1[sx1 * c + ch] * a1;
+  const int b0 = yb[2 * dy], b1 = yb[2 * dy + 1];
+  const int v = (((b0 * (S0 >> 4)) >> 16) + ((b1 * (S1 >> 4)) >> 16) + 2) >> 2;
+  out[e] = (uint8_t)min(max(v, 0), 255);
+}
+
+// ---- Pillow Image.resize(LANCZOS) on RGB (libImaging/Resample.c 8bpc passes: 22-bit integer taps,
+// accumulator seeded with 1 << 21, >> 22, clip to 0..255) ----
+__device__ __forceinline__ uint8_t clip8_pil(int ss) {
+  const int v = ss >> 22;
+  return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+__global__ __launch_bounds__(256) void pil_h_kernel(const uint8_t* __restrict__ in, int h, int w, int y0, int th,
+                                                    uint8_t* __restrict__ out, int ow, const int* __restrict__ xb,
+                                                    const int* __restrict__ xk, int kx, int n) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (size_t)n * th * ow) return;
+  const int xx = (int)(p % ow), yy = (int)((p / ow) % th);
+  const size_t img = p / ((size_t)ow * th);
+  const int xmin = xb[2 * xx], xmax = xb[2 * xx + 1];
+  const int* k = xk + (size_t)xx * kx;
+  const uint8_t* row = in + ((img * h) + y0 + yy) * (size_t)w * 3;
+  int s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+  for (int x = 0; x < xmax; ++x) {
+    const uint8_t* q = row + (size_t)(x + xmin) * 3;
+    s0 += q[0] * k[x];
+    s1 += q[1] * k[x];
+    s2 += q[2] * k[x];
+  }
+  uint8_t* o = out + p * 3;
+  o[0] = clip8_pil(s0);
+  o[1] = clip8_pil(s1);
+  o[2] = clip8_pil(s2);
+}
+__global__ __launch_bounds__(256) void pil_v_kernel(const uint8_t* __restrict__ in, int h, int w,
+                                                    uint8_t* __restrict__ out, int oh, const int* __restrict__ yb,
+                                                    const int* __restrict__ yk, int ky, int n) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (size_t)n * oh * w) return;
+  const int xx = (int)(p % w), yy = (int)((p / w) % oh);
+  const size_t img = p / ((size_t)w * oh);
+  const int ymin = yb[2 * yy], ymax = yb[2 * yy + 1];
+  const int* k = yk + (size_t)yy * ky;
+  int s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+  for (int y = 0; y < ymax; ++y) {
+    const uint8_t* q = in + ((img * h + ymin + y) * (size_t)w + xx) * 3;
+    s0 += q[0] * k[y];
+    s1 += q[1] * k[y];
+    s2 += q[2] * k[y];
+  }
+  uint8_t* o = out + p * 3;
+  o[0] = clip8_pil(s0);
+  o[1] = clip8_pil(s1);
+  o[2] = clip8_pil(s2);
+}
+
+}  // namespace
+
+hipError_t launch_seg_stem_im2col(int dtype, const void* x, int x_u8, int n, int h, int w, int ho, int wo, int kp,
+                                  void* col, hipStream_t st) {
+  const size_t total = (size_t)n * ho * wo * kp;
+  hipLaunchKernelGGL(stem_im2col_kernel, dim3(blocks_for(total)), dim3(256), 0, st, x, x_u8, dtype == NST_DT_F32 ? 1 : 0,
+                     n, h, w, ho, wo, kp, col);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_maxpool(int dtype, const void* in, int n, int h, int w, int c, void* out, int ho, int wo,
+                              hipStream_t st) {
+  const size_t total = (size_t)n * ho * wo * c;
+  hipLaunchKernelGGL(maxpool_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, dtype == NST_DT_F32 ? 1 : 0, n, h,
+                     w, c, out, ho, wo);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_avgpool(int dtype, const void* in, int n, int hw, int c, int cs, void* out, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_kernel, dim3(blocks_for((size_t)c), (unsigned)n), dim3(256), 0, st, in,
+                     dtype == NST_DT_F32 ? 1 : 0, hw, c, cs, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_resize_ac(int dtype, const void* in, int n, int h, int w, int c, int cs_in, void* out, int oh,
+                                int ow, int cs_out, int off, hipStream_t st) {
+  const size_t total = (size_t)n * oh * ow * c;
+  hipLaunchKernelGGL(resize_ac_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, dtype == NST_DT_F32 ? 1 : 0, n,
+                     h, w, c, cs_in, out, oh, ow, cs_out, off);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_upsample_argmax(const float* logits, int n, int h4, int w4, int nc, int ncs, int h, int w,
+                                      uint8_t* pred, float* logits_out, hipStream_t st) {
+  const size_t total = (size_t)n * h * w;
+  hipLaunchKernelGGL(upsample_argmax_kernel, dim3(blocks_for(total)), dim3(256), 0, st, logits, n, h4, w4, nc, ncs, h,
+                     w, pred, logits_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_select(const uint8_t* pred, size_t npix, SegIdSet ids, uint8_t* mask, hipStream_t st) {
+  hipLaunchKernelGGL(select_kernel, dim3(blocks_for(npix)), dim3(256), 0, st, pred, npix, ids, mask);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_morph(const uint8_t* in, int n, int h, int w, int k, int op, uint8_t* tmp, uint8_t* out,
+                            hipStream_t st) {
+  const size_t total = (size_t)n * h * w;
+  hipLaunchKernelGGL(morph_pass_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, n, h, w, k, op, 0, tmp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(morph_pass_kernel, dim3(blocks_for(total)), dim3(256), 0, st, (const uint8_t*)tmp, n, h, w, k, op,
+                     1, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_resize_linear_cv_u8(const uint8_t* in, int n, int h, int w, int c, uint8_t* out, int oh, int ow,
+                                      const int* xofs, const short* xalpha, const int* yofs, const short* ybeta,
+                                      hipStream_t st) {
+  const size_t total = (size_t)n * oh * ow * c;
+  hipLaunchKernelGGL(resize_linear_cv_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, n, h, w, c, out, oh, ow,
+                     xofs, xalpha, yofs, ybeta);
+  return hipGetLastError();
+}
+
+hipError_t launch_resize_pil_u8(const uint8_t* in, int n, int h, int w, uint8_t* tmp, int y0, int th, uint8_t* out,
+                                int oh, int ow, const int* xb, const int* xk, int kx, const int* yb, const int* yk,
+                                int ky, int need_h, int need_v, hipStream_t st) {
+  const uint8_t* vsrc = in;
+  int vh = h;
+  if (need_h) {
+    uint8_t* hdst = need_v ? tmp : out;
+    hipLaunchKernelGGL(pil_h_kernel, dim3(blocks_for((size_t)n * th * ow)), dim3(256), 0, st, in, h, w, y0, th, hdst,
+                       ow, xb, xk, kx, n);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !need_v) return e;
+    vsrc = tmp;
+    vh = th;
+  }
+  if (need_v) {
+    hipLaunchKernelGGL(pil_v_kernel, dim3(blocks_for((size_t)n * oh * ow)), dim3(256), 0, st, vsrc, vh, ow, out, oh,
+                       yb, yk, ky, n);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace nst

@@ -1,0 +1,171 @@
+"""configs[4] mask producer: DeepLab v3+ ResNet-101 on libnst_hip against the reference.
+
+Pinned pieces and their bars:
+  * the network (modeling/deeplab.py:27-33 in eval mode): tests/golden/deeplab_*.npz hold the REFERENCE
+    module's logits on seeded inputs (tests/golden/make_golden_deeplab.py); fp32 parity mode within 1e-4
+    of max |logit| and the same argmax wherever the reference's top-2 margin exceeds 1e-4 (elsewhere the
+    order of fp32 accumulation decides a near-tie); bf16 mode within 3e-2 of max |logit|.
+  * preprocess_pil fused into the stem (sky_swap.py:179-183): u8 frames -> same logits as the oracle's
+    numpy preprocessing + forward.
+  * Pillow LANCZOS (sky_swap.py:294-301): bit-exact against Pillow itself.
+Restated (cv2 is absent here, parity unpinned): morphology (exact, binary masks), GaussianBlur (+-1 LSB),
+cv2.resize INTER_LINEAR (bit-exact to the restatement)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from neuralstyletransferv1_amd import deeplab, synthetic
+from oracle import deeplab_oracle as D
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = ("deeplab_s0_33x47.npz", "deeplab_s1_40x56.npz")
+DEV = torch.device("cuda", 0)
+
+_models = {}
+
+
+def _model(nc, seed, dtype):
+    key = (nc, seed)
+    if key not in _models:
+        m = deeplab.DeepLab(num_classes=nc)
+        m.load_state_dict(deeplab.make_state_dict(nc, seed))
+        _models[key] = m.eval().to(DEV)
+    m = _models[key]
+    m.compute_dtype = dtype
+    return m
+
+
+def _margin(y):
+    s = np.sort(y, axis=1)
+    return s[:, -1] - s[:, -2]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_forward_fp32_vs_reference(case):
+    z = np.load(os.path.join(GOLDEN, case))
+    m = _model(int(z["num_classes"]), int(z["seed"]), "fp32")
+    y = m(torch.from_numpy(z["x"]).to(DEV)).cpu().numpy()
+    ref = z["y"]
+    assert y.shape == ref.shape
+    rel = float(np.abs(y - ref).max() / np.abs(ref).max())
+    decided = _margin(ref) > 1e-4 * np.abs(ref).max()
+    agree = (y.argmax(1) == ref.argmax(1))
+    print(case, f"fp32 max rel {rel:.2e}, argmax agreement {agree.mean():.6f}, on decided pixels {agree[decided].mean()}")
+    assert rel <= 1e-4, rel
+    assert agree[decided].all()
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_forward_bf16_vs_reference(case):
+    z = np.load(os.path.join(GOLDEN, case))
+    m = _model(int(z["num_classes"]), int(z["seed"]), "bf16")
+    y = m(torch.from_numpy(z["x"]).to(DEV)).cpu().numpy()
+    ref = z["y"]
+    rel = float(np.abs(y - ref).max() / np.abs(ref).max())
+    agree = float((y.argmax(1) == ref.argmax(1)).mean())
+    print(case, f"bf16 max rel {rel:.2e}, argmax agreement {agree:.4f}")
+    assert rel <= 3e-2, rel
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_forward_deterministic(dtype):
+    m = _model(19, 0, dtype)
+    x = torch.randn(2, 3, 72, 96, generator=torch.Generator().manual_seed(5)).to(DEV)
+    a = m(x)
+    b = m(x)
+    assert torch.equal(a, b)
+
+
+def test_u8_frames_preprocess_fused():
+    """nst_seg_forward on uint8 frames == the module on preprocess_pil(frames) (sky_swap.py:179-183)."""
+    m = _model(19, 0, "fp32")
+    frames = synthetic.make_frames(2, 54, 96, seed=41)
+    eng = m.engine(DEV, "fp32")
+    lg, pred = eng.run(torch.from_numpy(frames).to(DEV), logits=True, pred=True)
+    sd = {k: v for k, v in m.state_dict().items()}
+    sd = {k: v.cpu() for k, v in sd.items()}
+    for i in range(2):
+        x = D.preprocess_u8(frames[i])
+        ref = D.forward(sd, x)[0].numpy()
+        got = lg[i].cpu().numpy()
+        rel = float(np.abs(got - ref).max() / np.abs(ref).max())
+        decided = _margin(ref[None])[0] > 1e-4 * np.abs(ref).max()
+        p = pred[i].cpu().numpy()
+        print(f"frame {i}: rel {rel:.2e}, pred agreement {(p == ref.argmax(0)).mean():.6f}")
+        assert rel <= 1e-4, rel
+        assert (p == ref.argmax(0))[decided].all()
+        assert (p == got.argmax(0)).all()  # the fused argmax is the argmax of the returned logits
+
+
+@pytest.mark.parametrize("geom", [((1080, 1920), (144, 256)), ((1080, 1920), (143, 256)), ((37, 53), (20, 29)),
+                                  ((40, 30), (40, 17)), ((40, 30), (21, 30)), ((24, 32), (50, 61))])
+def test_lanczos_bit_exact_vs_pillow(geom):
+    (h, w), (oh, ow) = geom
+    frames = synthetic.make_frames(2, h, w, seed=7)
+    rs = deeplab.Resampler("lanczos", h, w, oh, ow, DEV)
+    got = rs(torch.from_numpy(frames).to(DEV)).cpu().numpy()
+    for i in range(2):
+        ref = D.lanczos(frames[i], ow, oh)
+        assert np.array_equal(got[i], ref), (geom, i, int(np.abs(got[i].astype(int) - ref).max()))
+
+
+@pytest.mark.parametrize("geom", [((144, 256), (1080, 1920)), ((143, 256), (1080, 1920)), ((20, 29), (37, 53)),
+                                  ((50, 61), (24, 32)), ((9, 9), (9, 9))])
+@pytest.mark.parametrize("c", [1, 3])
+def test_cv_resize_linear_vs_restatement(geom, c):
+    (h, w), (oh, ow) = geom
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (2, h, w, c), dtype=np.uint8)
+    if c == 1:
+        img = img[..., 0]
+    rs = deeplab.Resampler("cv_linear", h, w, oh, ow, DEV)
+    got = rs(torch.from_numpy(img).to(DEV)).cpu().numpy()
+    for i in range(2):
+        assert np.array_equal(got[i], D.cv_resize_linear_u8(img[i], ow, oh)), (geom, c, i)
+
+
+@pytest.mark.parametrize("params", [(0, 0, 0), (0, 0, 3), (2, 0, 0), (0, 3, 0), (1, 2, 5)])
+def test_mask_post_vs_oracle(params):
+    expand, contract, feather = params
+    rng = np.random.default_rng(11)
+    # blocky class maps (like a segmentation) with isolated specks so close/open have work to do
+    pred = np.kron(rng.integers(0, 6, (3, 9, 12)), np.ones((1, 6, 6), dtype=np.int64)).astype(np.uint8)
+    pred[rng.random(pred.shape) < 0.02] = 2
+    ids = [2, 4]
+    got = deeplab.mask_from_pred(torch.from_numpy(pred).to(DEV), ids, 5, expand, contract, feather).cpu().numpy()
+    for i in range(pred.shape[0]):
+        ref = D.infer_post(pred[i], ids, expand, contract, feather)
+        d = np.abs(got[i].astype(int) - ref.astype(int))
+        if feather:
+            assert d.max() <= 1, d.max()
+        else:
+            assert d.max() == 0
+
+
+def test_mask_engine_1080p_vs_oracle():
+    """configs[4]'s mask producer on two 1080p frames (working size 256x144): GPU (fp32) vs the oracle chain
+    (Pillow LANCZOS -> preprocess -> DeepLab -> argmax -> select / close / feather -> INTER_LINEAR)."""
+    m = _model(19, 0, "fp32")
+    frames = synthetic.make_frames(2, 1080, 1920, seed=21)
+    me = deeplab.MaskEngine(m, DEV, resolution=256, dtype="fp32")
+    ids = [8, 11, 18]
+    masks, pred = me.masks(torch.from_numpy(frames).to(DEV), ids, feather_px=3, return_pred=True)
+    masks, pred = masks.cpu().numpy(), pred.cpu().numpy()
+    sd = {k: v.cpu() for k, v in m.state_dict().items()}
+    ref_m, ref_p, ref_lg = D.masks_from_frames(sd, frames, ids, resolution=256, feather_px=3)
+    assert pred.shape == ref_p.shape == (2, 144, 256)
+    decided = _margin(ref_lg) > 1e-4 * np.abs(ref_lg).max()
+    assert (pred == ref_p)[decided].all()
+    if (pred == ref_p).all():
+        d = np.abs(masks.astype(int) - ref_m.astype(int))
+        print("mask max |d|", d.max(), "pixels off", (d > 0).mean())
+        assert d.max() <= 1
+    else:  # a near-tie flipped a class: compare the masks made from the GPU's own class maps
+        print("near-tie flips:", int((pred != ref_p).sum()))
+        for i in range(2):
+            mm = D.cv_resize_linear_u8(D.infer_post(pred[i], ids, 0, 0, 3), 1920, 1080)
+            assert np.abs(masks[i].astype(int) - mm.astype(int)).max() <= 1
