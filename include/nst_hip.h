@@ -222,6 +222,10 @@ int nst_mask_feather(const uint8_t* mask, int n, int h, int w, float sigma, floa
 int nst_blend_u8(const uint8_t* styled, const uint8_t* orig, const float* mask, int composite_mode,
                  float blend, float one_minus_blend, uint8_t* out, int n, int h, int w,
                  void* stream);
+/* nst_blend_u8 with an 8-bit mask [n,h,w] (alpha = m / 255 in fp32, pipeline.py:353): the DeepLab masks of
+ * nst_seg_mask / nst_resize_u8 composited straight from HBM (configs[4]) */
+int nst_blend_mask8_u8(const uint8_t* styled, const uint8_t* orig, const uint8_t* mask, int composite_mode, float blend,
+                       float one_minus_blend, uint8_t* out, int n, int h, int w, void* stream);
 
 /*
  * Live per-layer kernel timing (bench.py roofline): between nst_profile_begin and

@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "nst_gatys_targets", "nst_gatys_grad", "nst_adam_step", "nst_gatys_grad_capture",
     "nst_seg_create", "nst_seg_destroy", "nst_seg_num_classes", "nst_seg_workspace_bytes", "nst_seg_forward",
     "nst_seg_mask_scratch_bytes", "nst_seg_mask", "nst_resize_create", "nst_resize_destroy",
-    "nst_resize_scratch_bytes", "nst_resize_u8",
+    "nst_resize_scratch_bytes", "nst_resize_u8", "nst_blend_mask8_u8",
 )
 NST_GRAM_CHW, NST_GRAM_HWC = 0, 1
 
@@ -148,6 +148,8 @@ def lib() -> ctypes.CDLL:
         L.nst_lab_destroy.restype = None
         L.nst_lab_ema_u8.argtypes = [vp, vp, vp, i, i, i, i, f, f, i, f, f, vp, i, vp]
         L.nst_blend_u8.argtypes = [vp, vp, vp, i, f, f, vp, i, i, i, vp]
+        L.nst_blend_mask8_u8.argtypes = [vp, vp, vp, i, f, f, vp, i, i, i, vp]
+        L.nst_blend_mask8_u8.restype = i
         L.nst_gram.argtypes = [vp, i, i, i, i, i, vp, vp, sz, vp]
         L.nst_gram_workspace_bytes.argtypes = [i, i, i, ctypes.POINTER(sz)]
         L.nst_gram_workspace_bytes.restype = i

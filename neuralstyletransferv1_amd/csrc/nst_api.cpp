@@ -1251,6 +1251,18 @@ int nst_blend_u8(const uint8_t* styled, const uint8_t* orig, const float* mask, 
   return NST_OK;
 }
 
+int nst_blend_mask8_u8(const uint8_t* styled, const uint8_t* orig, const uint8_t* mask, int composite_mode, float blend,
+                       float one_minus_blend, uint8_t* out, int n, int h, int w, void* stream) {
+  if (!styled || !orig || !mask || !out || n <= 0 || h <= 0 || w <= 0 || composite_mode < 0 || composite_mode > 1) {
+    set_error("nst_blend_mask8_u8: invalid arguments");
+    return NST_E_INVALID;
+  }
+  hipError_t e = launch_blend(styled, orig, nullptr, composite_mode, blend, one_minus_blend, out, n, h * w,
+                              (hipStream_t)stream, mask);
+  if (e != hipSuccess) { set_error(std::string("blend launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
 int nst_gram_workspace_bytes(int n, int c, int hw, size_t* out) {
   if (n <= 0 || c <= 0 || hw <= 0 || !out) { set_error("nst_gram_workspace_bytes: invalid arguments"); return NST_E_INVALID; }
   *out = gram_workspace_bytes(n, c, hw);

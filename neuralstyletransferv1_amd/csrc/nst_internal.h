@@ -148,7 +148,7 @@ hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigm
                                hipStream_t st);
 hipError_t launch_prepad_encode(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st);
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,
-                        float omb, uint8_t* out, int n, int hw, hipStream_t st);
+                        float omb, uint8_t* out, int n, int hw, hipStream_t st, const uint8_t* mask8 = nullptr);
 size_t gram_workspace_bytes(int n, int c, int hw);
 // relu: Gram of ReLU(F) (bf16 HWC only: the VGG program's stored pre-activations)
 hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, int hw, float* G, void* ws,

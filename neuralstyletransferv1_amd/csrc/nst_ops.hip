@@ -663,7 +663,8 @@ hipError_t launch_seg_gauss_u8(const uint8_t* m, int n, int h, int w, float sigm
 // Mask composite (pipeline.py:2040-2043) + uniform blend with the original (pipeline.py:2087-2092)
 // + ToPILImage truncation.  S = styled/255, O = original/255 (to_tensor).
 __global__ __launch_bounds__(256) void blend_kernel(const uint8_t* __restrict__ s, const uint8_t* __restrict__ o,
-                                                    const float* __restrict__ mask, int mode, float b, float omb,
+                                                    const float* __restrict__ mask,
+                                                    const uint8_t* __restrict__ mask8, int mode, float b, float omb,
                                                     uint8_t* out, size_t npix) {
   const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npix) return;
@@ -672,8 +673,8 @@ __global__ __launch_bounds__(256) void blend_kernel(const uint8_t* __restrict__ 
     const float S = (float)s[p * 3 + ch] / 255.0f;
     const float O = (float)o[p * 3 + ch] / 255.0f;
     float C = S;
-    if (mask) {
-      const float al = mask[p];
+    if (mask || mask8) {  // alpha = the fp32 mask, or an 8-bit mask read as m / 255 (pipeline.py:353)
+      const float al = mask ? mask[p] : (float)mask8[p] / 255.0f;
       const float oal = 1.0f - al;
       const float v = mode == 0 ? (al * S + oal * O) : (oal * S + al * O);
       C = fminf(fmaxf(v, 0.f), 1.f);
@@ -689,9 +690,9 @@ __global__ __launch_bounds__(256) void blend_kernel(const uint8_t* __restrict__ 
 }
 
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b, float omb,
-                        uint8_t* out, int n, int hw, hipStream_t st) {
+                        uint8_t* out, int n, int hw, hipStream_t st, const uint8_t* mask8) {
   const size_t npix = (size_t)n * hw;
-  hipLaunchKernelGGL(blend_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, s, o, mask, mode, b,
+  hipLaunchKernelGGL(blend_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, s, o, mask, mask8, mode, b,
                      omb, out, npix);
   return hipGetLastError();
 }

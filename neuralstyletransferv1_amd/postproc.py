@@ -108,7 +108,8 @@ class LabSmoother:
 
 def blend_frames(styled_u8: torch.Tensor, orig_u8: torch.Tensor, blend: float = 1.0,
                  mask: Optional[torch.Tensor] = None, composite_mode: str = "keep") -> torch.Tensor:
-    """[n,h,w,3] uint8 styled/original (+ optional [n,h,w] fp32 alpha) -> [n,h,w,3] uint8."""
+    """[n,h,w,3] uint8 styled/original (+ optional [n,h,w] fp32 alpha, or uint8 mask read as m / 255)
+    -> [n,h,w,3] uint8."""
     _lib.require_gpu_tensor(styled_u8, "styled")
     _lib.require_gpu_tensor(orig_u8, "orig")
     if styled_u8.shape != orig_u8.shape:
@@ -116,13 +117,22 @@ def blend_frames(styled_u8: torch.Tensor, orig_u8: torch.Tensor, blend: float = 
     styled_u8, orig_u8 = styled_u8.contiguous(), orig_u8.contiguous()
     n, h, w, _ = styled_u8.shape
     mptr = None
+    out = torch.empty_like(styled_u8)
+    mode = 0 if composite_mode == "keep" else 1
+    if mask is not None and mask.dtype == torch.uint8:  # 8-bit mask (DeepLab / PNG bytes): alpha = m / 255 fused
+        _lib.require_gpu_tensor(mask, "mask")
+        mask = mask.contiguous()
+        if mask.numel() != n * h * w:
+            raise _lib.NstError("mask must be [n,h,w]")
+        check(lib().nst_blend_mask8_u8(styled_u8.data_ptr(), orig_u8.data_ptr(), mask.data_ptr(), mode,
+                                       float(np.float32(blend)), float(np.float32(1.0 - blend)), out.data_ptr(), n, h, w,
+                                       _lib.stream_ptr(styled_u8.device)), "nst_blend_mask8_u8")
+        return out
     if mask is not None:
         mask = mask.to(styled_u8.device, torch.float32).contiguous()
         if mask.numel() != n * h * w:
             raise _lib.NstError("mask must be [n,h,w] alpha")
         mptr = mask.data_ptr()
-    out = torch.empty_like(styled_u8)
-    mode = 0 if composite_mode == "keep" else 1
     check(lib().nst_blend_u8(styled_u8.data_ptr(), orig_u8.data_ptr(), mptr, mode, float(np.float32(blend)),
                              float(np.float32(1.0 - blend)), out.data_ptr(), n, h, w,
                              _lib.stream_ptr(styled_u8.device)), "nst_blend_u8")

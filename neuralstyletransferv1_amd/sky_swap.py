@@ -1,0 +1,238 @@
+"""sky_swap.py drop-in: DeepLab v3+ masks for single images and frame directories (configs[4] mask producer).
+
+Same flags as the reference CLI (sky_swap.py:368-400); the network, the class selection, the morphology,
+the feather and both resamplers run on the MI355X through libnst_hip (deeplab.py).  Host-side work is the
+reference's file I/O (PIL decode / PNG encode), the optional debug images and the plate composite of the
+single-image mode.  `--device` is accepted for compatibility; the engine always runs on the GPU (there is no
+CPU path).  Usage as in the reference, e.g.
+
+    python -m neuralstyletransferv1_amd.sky_swap --batch_frames work/frames --weights deeplab-resnet.pth.tar \\
+        --target_labels person --mask_feather 3
+"""
+from __future__ import annotations
+
+import argparse
+import os
+from pathlib import Path
+
+import numpy as np
+import torch
+from PIL import Image, ImageOps
+
+from . import deeplab
+
+BATCH = 8
+
+_PALETTE = np.array([[0, 0, 0], [128, 64, 128], [244, 35, 232], [70, 70, 70], [102, 102, 156], [190, 153, 153],
+                     [153, 153, 153], [250, 170, 30], [220, 220, 0], [107, 142, 35], [152, 251, 152], [70, 130, 180],
+                     [220, 20, 60], [255, 0, 0], [0, 0, 142], [0, 0, 70], [0, 60, 100], [0, 80, 100], [0, 0, 230],
+                     [119, 11, 32], [255, 255, 255]], dtype=np.uint8)  # sky_swap.py:8-14
+
+
+def _colorize(pred: np.ndarray) -> Image.Image:
+    return Image.fromarray(_PALETTE[np.clip(pred, 0, len(_PALETTE) - 1)], mode="RGB")
+
+
+def _transpose(arr: np.ndarray, mode: str) -> np.ndarray:
+    """sky_swap.py:23-34."""
+    if mode == "rot90":
+        return np.rot90(arr, 1)
+    if mode == "rot270":
+        return np.rot90(arr, 3)
+    if mode == "flip_h":
+        return np.ascontiguousarray(np.flip(arr, axis=1))
+    if mode == "flip_v":
+        return np.ascontiguousarray(np.flip(arr, axis=0))
+    return arr
+
+
+def guess_sky_id(pred: np.ndarray, num_classes: int, top_frac: float = 0.4) -> int:
+    """sky_swap.py:221-239 on a class map: the class with the largest share of the top rows."""
+    h, w = pred.shape
+    top_h = max(1, int(h * float(top_frac)))
+    scores = []
+    for cid in range(int(num_classes)):
+        full = (pred == cid).sum() / float(h * w)
+        top = (pred[:top_h, :] == cid).sum() / float(top_h * w)
+        scores.append((top, full, cid))
+    scores.sort(reverse=True)
+    best_top, best_full, best_cid = scores[0]
+    print(f"[info] scan_sky: best_id={best_cid} top={best_top:.3f} full={best_full:.3f}")
+    return int(best_cid)
+
+
+def _fit_plate(plate: Image.Image, size, mode: str) -> Image.Image:
+    """sky_swap.py:242-259 _resize_plate_preserve_ar."""
+    W, H = size
+    if mode == "crop":
+        return ImageOps.fit(plate, (W, H), method=Image.LANCZOS, bleed=0.0, centering=(0.5, 0.5))
+    if mode == "pad":
+        contained = ImageOps.contain(plate, (W, H), method=Image.LANCZOS)
+        canvas = Image.new("RGB", (W, H))
+        canvas.paste(contained.getpixel((0, 0)), [0, 0, W, H])
+        canvas.paste(contained, ((W - contained.width) // 2, (H - contained.height) // 2))
+        return canvas
+    return plate.resize((W, H), Image.LANCZOS)
+
+
+def composite(base: Image.Image, plate: Image.Image, mask_u8: np.ndarray, fit_mode: str = "crop") -> Image.Image:
+    """sky_swap.py:261-267."""
+    b = np.array(base.convert("RGB"))
+    p = np.array(_fit_plate(plate.convert("RGB"), (b.shape[1], b.shape[0]), fit_mode))
+    alpha = (mask_u8.astype(np.float32) / 255.0)[..., None]
+    return Image.fromarray((alpha * p + (1.0 - alpha) * b).astype(np.uint8))
+
+
+def _select_ids(args, used_nc: int, sky_id: int):
+    ids = None
+    if args.target_labels:
+        ids = deeplab.lookup_label_ids([s for s in args.target_labels.split(",") if s.strip()], used_nc)
+    elif args.target_ids:
+        try:
+            ids = sorted(set(int(x) for x in args.target_ids.split(",") if x.strip()))
+        except Exception as e:  # noqa: BLE001
+            print(f"[warn] could not parse --target_ids: {e}")
+    return ids or [int(sky_id)]
+
+
+def _mask_kwargs(args):
+    return dict(expand_px=int(args.mask_expand or 0), contract_px=int(args.mask_contract or 0),
+                feather_px=int(args.mask_feather or 0), expand_pct=float(args.mask_expand_pct or 0.0),
+                contract_pct=float(args.mask_contract_pct or 0.0), feather_pct=float(args.mask_feather_pct or 0.0))
+
+
+def batch_masks(args, model, used_nc: int, dev: torch.device) -> None:
+    """sky_swap.py:271-366 batch_masks_from_frames, frames grouped into same-size batches of 8 on the GPU."""
+    fdir = Path(args.batch_frames)
+    odir = Path(args.batch_out_dir or str(fdir.parent / "masks"))
+    odir.mkdir(parents=True, exist_ok=True)
+    frames = sorted(list(fdir.glob("frame_*.png")) + list(fdir.glob("frame_*.jpg")) + list(fdir.glob("frame_*.jpeg")))
+    if not frames:
+        raise FileNotFoundError(f"[batch][error] No frames like frame_*.png/.jpg in {fdir}")
+    me = deeplab.MaskEngine(model, dev, resolution=int(args.resolution or 0))
+    sky_id = args.sky_id
+    if args.scan_sky:
+        probe = np.array(Image.open(frames[0]).convert("RGB"))
+        _, pred = me.masks(torch.from_numpy(probe[None]).to(dev), [0], return_pred=True)
+        sky_id = guess_sky_id(pred[0].cpu().numpy(), used_nc, args.scan_top_frac)
+    ids = _select_ids(args, used_nc, sky_id)
+    n_ok = 0
+    i = 0
+    while i < len(frames):
+        batch, imgs = [], []
+        while i < len(frames) and len(batch) < BATCH:
+            try:
+                im = np.array(Image.open(frames[i]).convert("RGB"))
+            except Exception as ex:  # noqa: BLE001
+                print(f"[batch][warn] failed {frames[i].name}: {ex}")
+                i += 1
+                continue
+            if imgs and im.shape != imgs[0].shape:
+                break
+            batch.append(frames[i])
+            imgs.append(im)
+            i += 1
+        if not batch:
+            continue
+        x = torch.from_numpy(np.stack(imgs)).to(dev)
+        masks, preds = me.masks(x, ids, close_ks=5, return_pred=True, **_mask_kwargs(args))
+        masks = masks.cpu().numpy()
+        preds = preds.cpu().numpy()
+        for fp, m, pred, im in zip(batch, masks, preds, imgs):
+            num = fp.stem.split("_")[-1]
+            m = _transpose(m, args.transpose)
+            if args.debug_pred:
+                _colorize(_transpose(pred, args.transpose)).resize((im.shape[1], im.shape[0]), Image.NEAREST).save(
+                    odir / f"pred_{num}.png")
+            if args.debug_overlay:
+                alpha = (m.astype(np.float32) / 255.0)[:, :, None]
+                red = np.zeros_like(im)
+                red[..., 0] = 255
+                if m.shape[:2] == im.shape[:2]:
+                    Image.fromarray((alpha * red + (1 - alpha) * im).astype(np.uint8)).save(odir / f"overlay_{num}.jpg",
+                                                                                             quality=92)
+            Image.fromarray(m).save(odir / f"mask_{num}.png")
+            n_ok += 1
+    print(f"[batch] wrote {n_ok}/{len(frames)} masks to {odir}")
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--image", required=False)
+    ap.add_argument("--weights", required=True)
+    ap.add_argument("--backbone", choices=["resnet", "drn"], default="resnet")
+    ap.add_argument("--sky_id", type=int, default=deeplab.CITYSCAPES_SKY_ID_DEFAULT)
+    ap.add_argument("--num_classes", type=int, default=None)
+    ap.add_argument("--scan_sky", action="store_true")
+    ap.add_argument("--scan_top_frac", type=float, default=0.4)
+    ap.add_argument("--plate")
+    ap.add_argument("--plate_fit", choices=["crop", "pad", "stretch"], default="crop")
+    ap.add_argument("--out_mask", default="sky_mask.png")
+    ap.add_argument("--out_image", default="sky_swapped.jpg")
+    ap.add_argument("--device", choices=["cpu", "cuda", "mps"], default="cpu")
+    ap.add_argument("--resolution", type=int, default=256)
+    ap.add_argument("--mask_expand", type=int, default=0)
+    ap.add_argument("--mask_contract", type=int, default=0)
+    ap.add_argument("--mask_feather", type=int, default=3)
+    ap.add_argument("--mask_expand_pct", type=float, default=0.0)
+    ap.add_argument("--mask_contract_pct", type=float, default=0.0)
+    ap.add_argument("--mask_feather_pct", type=float, default=0.0)
+    ap.add_argument("--batch_frames", type=str, default=None)
+    ap.add_argument("--batch_out_dir", type=str, default=None)
+    ap.add_argument("--target_labels", type=str, default=None)
+    ap.add_argument("--target_ids", type=str, default=None)
+    ap.add_argument("--debug_pred", action="store_true")
+    ap.add_argument("--debug_overlay", action="store_true")
+    ap.add_argument("--transpose", choices=["none", "rot90", "rot270", "flip_h", "flip_v"], default="none")
+    ap.add_argument("--morph_close_ks", type=int, default=5,
+                    help="accepted for compatibility: the reference never passes it on (infer_mask always closes 5x5)")
+    # build additions
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16", help="DeepLab compute dtype on the MI355X")
+    args = ap.parse_args(argv)
+    if not args.batch_frames and not args.image:
+        ap.error("either --image or --batch_frames must be provided")
+    if args.backbone != "resnet":
+        ap.error("libnst_hip builds the resnet backbone (the one sky_swap.py's configs use)")
+    for path, label in ((args.image, "input image"), (args.weights, "weights checkpoint"), (args.plate, "sky plate")):
+        if path and not os.path.exists(path):
+            raise FileNotFoundError(f"[error] {label} not found: {path}")
+    if args.device != "cuda":
+        print(f"[note] --device {args.device}: the mask network runs on the MI355X (libnst_hip has no CPU path)")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    model, used_nc = deeplab.load_deeplab(args.weights, args.num_classes, dev, args.dtype)
+    if args.batch_frames:
+        batch_masks(args, model, used_nc, dev)
+        return 0
+    src = np.array(Image.open(args.image).convert("RGB"))
+    me = deeplab.MaskEngine(model, dev, resolution=int(args.resolution or 0))
+    x = torch.from_numpy(src[None]).to(dev)
+    sky_id = args.sky_id
+    if args.scan_sky:
+        _, pred = me.masks(x, [0], return_pred=True)
+        sky_id = guess_sky_id(pred[0].cpu().numpy(), used_nc, args.scan_top_frac)
+    elif used_nc == 21 and args.sky_id == deeplab.CITYSCAPES_SKY_ID_DEFAULT:
+        print("[warn] Checkpoint looks VOC-like (21 classes). Default Cityscapes sky_id=10 may be incorrect. "
+              "Use --scan_sky or set --sky_id explicitly.")
+    ids = _select_ids(args, used_nc, sky_id)
+    # single-image mode works at the working size (sky_swap.py:505-563: the mask is not upscaled back)
+    ww, hh = deeplab.working_size(src.shape[1], src.shape[0], int(args.resolution or 0))
+    work = Image.fromarray(src).resize((ww, hh), Image.LANCZOS) if (ww, hh) != (src.shape[1], src.shape[0]) else \
+        Image.fromarray(src)
+    me_work = deeplab.MaskEngine(model, dev, resolution=0)
+    mask = me_work.masks(torch.from_numpy(np.array(work)[None]).to(dev), ids, close_ks=5,
+                         **_mask_kwargs(args))[0].cpu().numpy()
+    mask = _transpose(mask, args.transpose)
+    Image.fromarray(mask).save(args.out_mask)
+    print(f"[ok] wrote mask → {args.out_mask}")
+    if args.plate:
+        out = composite(work, Image.open(args.plate).convert("RGB"), mask, fit_mode=args.plate_fit)
+        out.save(args.out_image, quality=95)
+        print(f"[ok] wrote composite → {args.out_image}")
+    else:
+        print("[note] no --plate provided; skipping composite")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
