@@ -21,6 +21,8 @@
 //     sqrt(var + eps), beta = bias - mean * alpha), + residual, ReLU, NHWC store at a channel offset.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "nst_hip.h"
 #include "seg_internal.h"
 
@@ -69,17 +71,22 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
   const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
   const char* in_img = (const char*)p.in + (size_t)img * p.hi * p.wi * p.cs * ESZ + b_c0 * 16;
   const int nck = p.cin / (128 / ESZ);
-  const int nstage = p.kh * p.kw * nck;
+  const int nstage_all = p.kh * p.kw * nck;   // packed stages per 64-row block (every tap)
+  const int nstage = p.ntaps * nck;           // stages this launch runs (live taps only)
   const int ablk = (row0 + a_row) >> 6;
-  const char* wsrc = (const char*)p.wpk + ((size_t)ablk * nstage * 64 + (a_row & 63)) * 128 + a_c0 * 16;
+  const char* wsrc = (const char*)p.wpk + ((size_t)ablk * nstage_all * 64 + (a_row & 63)) * 128 + a_c0 * 16;
   const size_t wstage = 64 * 128;
+  // this workgroup's K slice (split-K: blockIdx.z of ksplit)
+  const int s_begin = (int)(((long)nstage * blockIdx.z) / p.ksplit);
+  const int s_end = (int)(((long)nstage * (blockIdx.z + 1)) / p.ksplit);
 
   u32x4_g ra[A_CPT], rb[B_CPT];
   auto load_stage = [&](int s) {
-    const char* wa = wsrc + (size_t)s * wstage;
+    const int ti = s / nck, cc = s - ti * nck;
+    const int tap = p.taps[ti];
+    const char* wa = wsrc + (size_t)(tap * nck + cc) * wstage;
 #pragma unroll
     for (int j = 0; j < A_CPT; ++j) ra[j] = *(const u32x4_g*)(wa + j * 16);
-    const int tap = s / nck, cc = s - tap * nck;
     const int ky = tap / p.kw, kx = tap - ky * p.kw;
     const int iy = iy0 + ky * p.dil, ix = ix0 + kx * p.dil;
     const bool ok = pvalid && (unsigned)iy < (unsigned)p.hi && (unsigned)ix < (unsigned)p.wi;
@@ -118,12 +125,12 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4_g{0.f, 0.f, 0.f, 0.f};
 
-  load_stage(0);
+  load_stage(s_begin);
   store_stage(0);
   __syncthreads();
-  for (int s = 0; s < nstage; ++s) {
-    const int cur = s & 1;
-    const bool more = s + 1 < nstage;
+  for (int s = s_begin; s < s_end; ++s) {
+    const int cur = (s - s_begin) & 1;
+    const bool more = s + 1 < s_end;
     if (more) load_stage(s + 1);
     const char* base = lds + cur * BUF;
 #pragma unroll
@@ -161,6 +168,10 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
     for (int i = 0; i < MI; ++i) {
       const int co = row0 + wm * (BM / 2) + i * 16 + 4 * g;
       if (co >= p.cout_store) continue;
+      if (p.ksplit > 1) {  // raw partial sums of this K slice; gemm_splitk_reduce applies the epilogue
+        *(f32x4_g*)(p.partial + ((size_t)blockIdx.z * p.npix + px) * p.cout_store + co) = acc[i][j];
+        continue;
+      }
       float v[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = acc[i][j][q] * p.scale[co + q] + p.shift[co + q];
@@ -191,29 +202,121 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
   }
 }
 
+// split-K epilogue: sum the K slices in slice order, then scale/shift, residual, ReLU, store (as the
+// single-pass epilogue does)
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmConvParams p, int f32) {
+  const int groups = p.cout_store >> 2;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)p.npix * groups) return;
+  const int px = (int)(e / groups), co = (int)(e % groups) * 4;
+  f32x4_g a = *(const f32x4_g*)(p.partial + (size_t)px * p.cout_store + co);
+  for (int z = 1; z < p.ksplit; ++z) a += *(const f32x4_g*)(p.partial + ((size_t)z * p.npix + px) * p.cout_store + co);
+  float v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = a[q] * p.scale[co + q] + p.shift[co + q];
+  if (p.res) {
+    if (f32) {
+      const float4 r = *(const float4*)((const float*)p.res + (size_t)px * p.res_cs + co);
+      v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+    } else {
+      const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
+      v[0] += bf_to_f((uint16_t)(r.x & 0xffff)); v[1] += bf_to_f((uint16_t)(r.x >> 16));
+      v[2] += bf_to_f((uint16_t)(r.y & 0xffff)); v[3] += bf_to_f((uint16_t)(r.y >> 16));
+    }
+  }
+  if (p.relu) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+  }
+  const size_t o = (size_t)px * p.out_cs + p.out_off + co;
+  if (f32 || p.out_f32) {
+    *(float4*)((float*)p.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    uint2 w;
+    w.x = (uint32_t)f_to_bf(v[0]) | ((uint32_t)f_to_bf(v[1]) << 16);
+    w.y = (uint32_t)f_to_bf(v[2]) | ((uint32_t)f_to_bf(v[3]) << 16);
+    *(uint2*)((uint16_t*)p.out + o) = w;
+  }
+}
+
 template <int BM, int BN, bool F32>
 void launch_tile(const GemmConvParams& p, hipStream_t st) {
-  const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM));
+  const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM), (unsigned)p.ksplit);
   hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, F32>), grid, dim3(256), 0, st, p);
+}
+
+// taps whose source row AND column land inside the image for at least one output pixel
+void live_taps(GemmConvParams& p) {
+  p.ntaps = 0;
+  for (int ky = 0; ky < p.kh; ++ky) {
+    bool row = false;
+    for (int oy = 0; oy < p.ho && !row; ++oy) {
+      const int iy = oy * p.stride - p.pad + ky * p.dil;
+      row = iy >= 0 && iy < p.hi;
+    }
+    if (!row) continue;
+    for (int kx = 0; kx < p.kw; ++kx) {
+      bool col = false;
+      for (int ox = 0; ox < p.wo && !col; ++ox) {
+        const int ix = ox * p.stride - p.pad + kx * p.dil;
+        col = ix >= 0 && ix < p.wi;
+      }
+      if (col) p.taps[p.ntaps++] = (unsigned char)(ky * p.kw + kx);
+    }
+  }
+}
+
+struct GemmShape {
+  bool big;
+  int ksplit;
+};
+GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
+  const int nstage = p.ntaps * (p.cin / gemm_stage_channels(dtype));
+  GemmShape g;
+  // 128x128 tiles when they alone give the chip a few waves of workgroups; 64x64 otherwise
+  g.big = (long)((p.npix + 127) / 128) * ((p.cout_store + 127) / 128) >= 512;
+  g.ksplit = 1;
+  if (!g.big) {  // fewer 64x64 tiles than a wave of the chip and a long K loop: split K (at most 8 slices)
+    const long tiles = (long)((p.npix + 63) / 64) * ((p.cout_store + 63) / 64);
+    if (tiles < 240 && nstage >= 16) {
+      long k = (480 + tiles - 1) / tiles;
+      k = std::min<long>(k, std::min<long>(8, nstage / 8));
+      g.ksplit = (int)std::max<long>(k, 1);
+    }
+  }
+  return g;
 }
 
 }  // namespace
 
-hipError_t launch_gemm_conv(int dtype, const GemmConvParams& p, hipStream_t st) {
+size_t gemm_partial_bytes(int dtype, const GemmConvParams& p0) {
+  GemmConvParams p = p0;
+  live_taps(p);
+  const GemmShape g = gemm_shape(dtype, p);
+  return g.ksplit > 1 ? (size_t)g.ksplit * p.npix * p.cout_store * 4 : 0;
+}
+
+hipError_t launch_gemm_conv(int dtype, GemmConvParams& p, hipStream_t st) {
   const int ck = gemm_stage_channels(dtype);
   if (p.npix <= 0 || p.cin <= 0 || p.cin % ck || p.cs % 8 || p.cout_store % 4 || p.out_off % 4 ||
-      p.out_cs % 4 || (p.res && p.res_cs % 4))
+      p.out_cs % 4 || (p.res && p.res_cs % 4) || p.kh * p.kw > 64)
     return hipErrorInvalidValue;
-  // 128x128 tiles when they alone give the chip a few waves of workgroups; 64x64 otherwise
-  const long big = (long)((p.npix + 127) / 128) * ((p.cout_store + 127) / 128);
+  live_taps(p);
+  if (p.ntaps == 0) return hipErrorInvalidValue;
+  const GemmShape g = gemm_shape(dtype, p);
+  p.ksplit = p.partial ? g.ksplit : 1;
   const bool f32 = dtype == NST_DT_F32;
-  if (big >= 512) {
+  if (g.big) {
     if (f32) launch_tile<128, 128, true>(p, st);
     else launch_tile<128, 128, false>(p, st);
   } else {
     if (f32) launch_tile<64, 64, true>(p, st);
     else launch_tile<64, 64, false>(p, st);
   }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || p.ksplit == 1) return e;
+  const size_t n = (size_t)p.npix * (p.cout_store / 4);
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, f32 ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -146,6 +146,8 @@ int out_extent(int in, int k, int s, int d, int p) { return (in + 2 * p - d * (k
 
 struct nst_seg {
   int device = 0, dtype = NST_DT_BF16, nc = 0, ncs = 0;
+  int cache_n = 0, cache_h = 0, cache_w = 0;  // geometry of the cached workspace plan
+  size_t cache_partial = 0;
   SegConv stem;
   std::vector<Bottleneck> blocks;  // layer1 (3), layer2 (4), layer3 (23), layer4 (3: multi-grid 1, 2, 4)
   int layer_last[4] = {0, 0, 0, 0};
@@ -157,7 +159,15 @@ namespace {
 struct SegPlan {
   int n = 0, h = 0, w = 0;
   int h2, w2, h4, w4, h8, w8, h16, w16;
-  size_t col, stem, pool, x0, x1, t1, t2, r, lowf, cat5, gapv, gapo, aspo, dcat, d1, d2, logits, end;
+  size_t col, stem, pool, x0, x1, t1, t2, r, lowf, cat5, gapv, gapo, aspo, dcat, d1, d2, logits, partial, end;
+};
+
+// launch context: a dry run walks the program only to size the split-K scratch
+struct SegRun {
+  bool dry = false;
+  size_t partial_need = 0;
+  float* partial = nullptr;
+  size_t partial_bytes = 0;
 };
 
 SegPlan seg_plan(const nst_seg* s, int n, int h, int w) {
@@ -192,14 +202,15 @@ SegPlan seg_plan(const nst_seg* s, int n, int h, int w) {
   P.d1 = take(p4 * 256 * e);
   P.d2 = take(p4 * 256 * e);
   P.logits = take(p4 * s->ncs * 4);
+  P.partial = o;
   P.end = o;
   return P;
 }
 
-// one conv_gemm launch
-hipError_t run(const nst_seg* s, const SegConv& L, const void* in, int n, int hi, int wi, int cs, void* out, int ho,
-               int wo, int out_cs, int out_off, const void* res, int res_cs, int relu, int out_f32, int cout_store,
-               hipStream_t st) {
+// one conv_gemm launch (or, in a dry run, its split-K scratch need)
+hipError_t run(const nst_seg* s, SegRun& R, const SegConv& L, const void* in, int n, int hi, int wi, int cs, void* out,
+               int ho, int wo, int out_cs, int out_off, const void* res, int res_cs, int relu, int out_f32,
+               int cout_store, hipStream_t st) {
   GemmConvParams p;
   std::memset(&p, 0, sizeof(p));
   p.in = in;
@@ -214,6 +225,13 @@ hipError_t run(const nst_seg* s, const SegConv& L, const void* in, int n, int hi
   p.out = out; p.out_cs = out_cs; p.out_off = out_off;
   p.cout_store = cout_store;
   p.out_f32 = out_f32;
+  p.ksplit = 1;
+  const size_t need = gemm_partial_bytes(s->dtype, p);
+  if (R.dry) {
+    R.partial_need = std::max(R.partial_need, need);
+    return hipSuccess;
+  }
+  p.partial = (need && need <= R.partial_bytes) ? R.partial : nullptr;
   return launch_gemm_conv(s->dtype, p, st);
 }
 
@@ -223,15 +241,15 @@ hipError_t run(const nst_seg* s, const SegConv& L, const void* in, int n, int hi
     if (_e != hipSuccess) { set_error(std::string(#expr) + ": " + hipGetErrorString(_e)); return NST_E_HIP; } \
   } while (0)
 
-int seg_forward_impl(nst_seg* s, const SegPlan& P, const void* x, int x_u8, float* logits_out, uint8_t* pred,
-                     char* ws, hipStream_t st) {
+int seg_forward_impl(nst_seg* s, const SegPlan& P, SegRun& R, const void* x, int x_u8, float* logits_out,
+                     uint8_t* pred, char* ws, hipStream_t st) {
   const int n = P.n;
   const size_t e = s->dtype == NST_DT_F32 ? 4 : 2;
   // stem
-  SEG_CHECK(launch_seg_stem_im2col(s->dtype, x, x_u8, n, P.h, P.w, P.h2, P.w2, s->stem.cinp, ws + P.col, st));
-  SEG_CHECK(run(s, s->stem, ws + P.col, n, P.h2, P.w2, s->stem.cinp, ws + P.stem, P.h2, P.w2, 64, 0, nullptr, 0, 1, 0,
+  if (!R.dry) SEG_CHECK(launch_seg_stem_im2col(s->dtype, x, x_u8, n, P.h, P.w, P.h2, P.w2, s->stem.cinp, ws + P.col, st));
+  SEG_CHECK(run(s, R, s->stem, ws + P.col, n, P.h2, P.w2, s->stem.cinp, ws + P.stem, P.h2, P.w2, 64, 0, nullptr, 0, 1, 0,
                 64, st));
-  SEG_CHECK(launch_seg_maxpool(s->dtype, ws + P.stem, n, P.h2, P.w2, 64, ws + P.pool, P.h4, P.w4, st));
+  if (!R.dry) SEG_CHECK(launch_seg_maxpool(s->dtype, ws + P.stem, n, P.h2, P.w2, 64, ws + P.pool, P.h4, P.w4, st));
   // residual layers
   const char* cur = ws + P.pool;
   int ch = 64, hh = P.h4, ww = P.w4;
@@ -241,15 +259,15 @@ int seg_forward_impl(nst_seg* s, const SegPlan& P, const void* x, int x_u8, floa
     const Bottleneck& B = s->blocks[b];
     const int planes = B.c1.cout, outc = B.c3.cout;
     const int ho = out_extent(hh, 3, B.c2.stride, B.c2.dil, B.c2.pad), wo = out_extent(ww, 3, B.c2.stride, B.c2.dil, B.c2.pad);
-    SEG_CHECK(run(s, B.c1, cur, n, hh, ww, ch, ws + P.t1, hh, ww, planes, 0, nullptr, 0, 1, 0, planes, st));
-    SEG_CHECK(run(s, B.c2, ws + P.t1, n, hh, ww, planes, ws + P.t2, ho, wo, planes, 0, nullptr, 0, 1, 0, planes, st));
+    SEG_CHECK(run(s, R, B.c1, cur, n, hh, ww, ch, ws + P.t1, hh, ww, planes, 0, nullptr, 0, 1, 0, planes, st));
+    SEG_CHECK(run(s, R, B.c2, ws + P.t1, n, hh, ww, planes, ws + P.t2, ho, wo, planes, 0, nullptr, 0, 1, 0, planes, st));
     const void* res = cur;
     if (B.has_ds) {
-      SEG_CHECK(run(s, B.ds, cur, n, hh, ww, ch, ws + P.r, ho, wo, outc, 0, nullptr, 0, 0, 0, outc, st));
+      SEG_CHECK(run(s, R, B.ds, cur, n, hh, ww, ch, ws + P.r, ho, wo, outc, 0, nullptr, 0, 0, 0, outc, st));
       res = ws + P.r;
     }
     char* dst = (b == (size_t)s->layer_last[0]) ? ws + P.lowf : xb[xi];
-    SEG_CHECK(run(s, B.c3, ws + P.t2, n, ho, wo, planes, dst, ho, wo, outc, 0, res, outc, 1, 0, outc, st));
+    SEG_CHECK(run(s, R, B.c3, ws + P.t2, n, ho, wo, planes, dst, ho, wo, outc, 0, res, outc, 1, 0, outc, st));
     if (dst == xb[xi]) xi ^= 1;
     cur = dst;
     ch = outc; hh = ho; ww = wo;
@@ -257,23 +275,41 @@ int seg_forward_impl(nst_seg* s, const SegPlan& P, const void* x, int x_u8, floa
   // ASPP (input: layer4 output, 2048 channels at /16)
   const int h16 = hh, w16 = ww;
   for (int i = 0; i < 4; ++i)
-    SEG_CHECK(run(s, s->aspp[i], cur, n, h16, w16, 2048, ws + P.cat5, h16, w16, 1280, 256 * i, nullptr, 0, 1, 0, 256, st));
-  SEG_CHECK(launch_seg_avgpool(s->dtype, cur, n, h16 * w16, 2048, 2048, ws + P.gapv, st));
-  SEG_CHECK(run(s, s->gap, ws + P.gapv, n, 1, 1, 2048, ws + P.gapo, 1, 1, 256, 0, nullptr, 0, 1, 0, 256, st));
-  SEG_CHECK(launch_seg_resize_ac(s->dtype, ws + P.gapo, n, 1, 1, 256, 256, ws + P.cat5, h16, w16, 1280, 1024, st));
-  SEG_CHECK(run(s, s->proj, ws + P.cat5, n, h16, w16, 1280, ws + P.aspo, h16, w16, 256, 0, nullptr, 0, 1, 0, 256, st));
+    SEG_CHECK(run(s, R, s->aspp[i], cur, n, h16, w16, 2048, ws + P.cat5, h16, w16, 1280, 256 * i, nullptr, 0, 1, 0, 256, st));
+  if (!R.dry) SEG_CHECK(launch_seg_avgpool(s->dtype, cur, n, h16 * w16, 2048, 2048, ws + P.gapv, st));
+  SEG_CHECK(run(s, R, s->gap, ws + P.gapv, n, 1, 1, 2048, ws + P.gapo, 1, 1, 256, 0, nullptr, 0, 1, 0, 256, st));
+  if (!R.dry) SEG_CHECK(launch_seg_resize_ac(s->dtype, ws + P.gapo, n, 1, 1, 256, 256, ws + P.cat5, h16, w16, 1280, 1024, st));
+  SEG_CHECK(run(s, R, s->proj, ws + P.cat5, n, h16, w16, 1280, ws + P.aspo, h16, w16, 256, 0, nullptr, 0, 1, 0, 256, st));
   // decoder
-  SEG_CHECK(run(s, s->low, ws + P.lowf, n, P.h4, P.w4, 256, ws + P.dcat, P.h4, P.w4, 320, 256, nullptr, 0, 1, 0, 64, st));
-  SEG_CHECK(launch_seg_resize_ac(s->dtype, ws + P.aspo, n, h16, w16, 256, 256, ws + P.dcat, P.h4, P.w4, 320, 0, st));
-  SEG_CHECK(run(s, s->dec1, ws + P.dcat, n, P.h4, P.w4, 320, ws + P.d1, P.h4, P.w4, 256, 0, nullptr, 0, 1, 0, 256, st));
-  SEG_CHECK(run(s, s->dec2, ws + P.d1, n, P.h4, P.w4, 256, ws + P.d2, P.h4, P.w4, 256, 0, nullptr, 0, 1, 0, 256, st));
-  SEG_CHECK(run(s, s->cls, ws + P.d2, n, P.h4, P.w4, 256, ws + P.logits, P.h4, P.w4, s->ncs, 0, nullptr, 0, 0, 1,
+  SEG_CHECK(run(s, R, s->low, ws + P.lowf, n, P.h4, P.w4, 256, ws + P.dcat, P.h4, P.w4, 320, 256, nullptr, 0, 1, 0, 64, st));
+  if (!R.dry) SEG_CHECK(launch_seg_resize_ac(s->dtype, ws + P.aspo, n, h16, w16, 256, 256, ws + P.dcat, P.h4, P.w4, 320, 0, st));
+  SEG_CHECK(run(s, R, s->dec1, ws + P.dcat, n, P.h4, P.w4, 320, ws + P.d1, P.h4, P.w4, 256, 0, nullptr, 0, 1, 0, 256, st));
+  SEG_CHECK(run(s, R, s->dec2, ws + P.d1, n, P.h4, P.w4, 256, ws + P.d2, P.h4, P.w4, 256, 0, nullptr, 0, 1, 0, 256, st));
+  SEG_CHECK(run(s, R, s->cls, ws + P.d2, n, P.h4, P.w4, 256, ws + P.logits, P.h4, P.w4, s->ncs, 0, nullptr, 0, 0, 1,
                 s->ncs, st));
   (void)e;
-  if (logits_out || pred)
+  if (!R.dry && (logits_out || pred))
     SEG_CHECK(launch_seg_upsample_argmax((const float*)(ws + P.logits), n, P.h4, P.w4, s->nc, s->ncs, P.h, P.w, pred,
                                          logits_out, st));
   return NST_OK;
+}
+
+// the full plan: the layout above plus the split-K scratch a dry run of the program asks for
+SegPlan seg_plan_full(nst_seg* s, int n, int h, int w) {
+  SegPlan P = seg_plan(s, n, h, w);
+  size_t partial = 0;
+  if (s->cache_n == n && s->cache_h == h && s->cache_w == w) {
+    partial = s->cache_partial;
+  } else {
+    SegRun R;
+    R.dry = true;
+    static char dummy[1];
+    (void)seg_forward_impl(s, P, R, dummy, 1, nullptr, nullptr, dummy, nullptr);
+    partial = R.partial_need;
+    s->cache_n = n; s->cache_h = h; s->cache_w = w; s->cache_partial = partial;
+  }
+  P.end = P.partial + al256(partial);
+  return P;
 }
 
 }  // namespace
@@ -472,7 +508,7 @@ int nst_seg_num_classes(const nst_seg* s) { return s ? s->nc : 0; }
 
 int nst_seg_workspace_bytes(const nst_seg* s, int n, int h, int w, size_t* out) {
   if (!s || !out || n <= 0 || h < 8 || w < 8) { set_error("nst_seg_workspace_bytes: invalid arguments"); return NST_E_INVALID; }
-  *out = seg_plan(s, n, h, w).end;
+  *out = seg_plan_full(const_cast<nst_seg*>(s), n, h, w).end;
   return NST_OK;
 }
 
@@ -483,9 +519,12 @@ int nst_seg_forward(nst_seg* s, const void* x, int x_fmt, int n, int h, int w, f
     return NST_E_INVALID;
   }
   if ((size_t)n * h * w > (size_t)1 << 31) { set_error("nst_seg_forward: batch too large"); return NST_E_SHAPE; }
-  const SegPlan P = seg_plan(s, n, h, w);
+  const SegPlan P = seg_plan_full(s, n, h, w);
   if (!workspace || workspace_bytes < P.end) { set_error("nst_seg_forward: workspace too small"); return NST_E_WORKSPACE; }
-  return seg_forward_impl(s, P, x, x_fmt == NST_IO_U8_NHWC, logits, pred, (char*)workspace, (hipStream_t)stream);
+  SegRun R;
+  R.partial = (float*)((char*)workspace + P.partial);
+  R.partial_bytes = P.end - P.partial;
+  return seg_forward_impl(s, P, R, x, x_fmt == NST_IO_U8_NHWC, logits, pred, (char*)workspace, (hipStream_t)stream);
 }
 
 int nst_seg_mask_scratch_bytes(int n, int h, int w, size_t* out) {

@@ -30,10 +30,22 @@ struct GemmConvParams {
   int out_cs, out_off;
   int cout_store;          // output channels written (multiple of 4; channels past the real count get 0)
   int out_f32;
+  // taps that touch the image for some output pixel (the others only read zero padding and add exact zeros:
+  // skipped — the ASPP's dilation-12/18 convs on a 9x16 map keep 3 and 1 of their 9 taps)
+  int ntaps;
+  unsigned char taps[64];  // ky * kw + kx
+  // split-K (small GEMMs): blockIdx.z = K slice; slices write fp32 partials [ksplit][npix][cout_store] to
+  // `partial` and gemm_splitk_reduce applies the epilogue, summing the slices in fixed order (deterministic)
+  int ksplit;
+  float* partial;
 };
 
-// dtype: NST_DT_F32 / NST_DT_BF16.  Picks the tile shape from the GEMM's size.
-hipError_t launch_gemm_conv(int dtype, const GemmConvParams& p, hipStream_t st);
+// dtype: NST_DT_F32 / NST_DT_BF16.  Picks the tile shape and the K split from the GEMM's size; p.taps /
+// p.ntaps are filled here (gemm_live_taps).  partial: scratch of gemm_partial_bytes(...) bytes or nullptr
+// (no split).
+hipError_t launch_gemm_conv(int dtype, GemmConvParams& p, hipStream_t st);
+// bytes of split-K scratch the launch of this conv would use (0: no split)
+size_t gemm_partial_bytes(int dtype, const GemmConvParams& p);
 // stage width in channels for a dtype (64 bf16, 32 fp32)
 inline int gemm_stage_channels(int dtype) { return dtype == 1 ? 64 : 32; }
 

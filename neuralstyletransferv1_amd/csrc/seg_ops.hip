@@ -33,29 +33,42 @@ inline unsigned blocks_for(size_t n, int per = 256) { return (unsigned)((n + per
 // array against the float64 tuples), then .float() -> float32 — reproduced operation for operation.
 __global__ __launch_bounds__(256) void stem_im2col_kernel(const void* __restrict__ x, int x_u8, int f32, int n, int h,
                                                           int w, int ho, int wo, int kp, void* __restrict__ col) {
+  // one thread = one output pixel x one kernel row ky: the 21 columns k = ky*21 .. ky*21+20 (kx-major, then
+  // channel) read 7 horizontally adjacent source pixels; ky == 7 writes the zero columns 147 .. kp-1
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total = (size_t)n * ho * wo * kp;
+  const size_t total = (size_t)n * ho * wo * 8;
   if (e >= total) return;
-  const int k = (int)(e % kp);
-  const size_t px = e / kp;
+  const int ky = (int)(e & 7);
+  const size_t px = e >> 3;
   const int ox = (int)(px % wo);
   const int oy = (int)((px / wo) % ho);
   const int img = (int)(px / ((size_t)wo * ho));
-  float v = 0.f;
-  if (k < 147) {
-    const int c = k % 3, tap = k / 3, ky = tap / 7, kx = tap % 7;
-    const int iy = oy * 2 - 3 + ky, ix = ox * 2 - 3 + kx;
-    if (iy >= 0 && iy < h && ix >= 0 && ix < w) {
-      if (x_u8) {
-        const double mean[3] = {0.485, 0.456, 0.406}, sd[3] = {0.229, 0.224, 0.225};
-        const float x01 = (float)((const uint8_t*)x)[(((size_t)img * h + iy) * w + ix) * 3 + c] / 255.0f;
-        v = (float)(((double)x01 - mean[c]) / sd[c]);
-      } else {
-        v = ((const float*)x)[(((size_t)img * 3 + c) * h + iy) * w + ix];
+  const size_t row = px * kp;
+  if (ky == 7) {
+    for (int k = 147; k < kp; ++k) st_act(col, row + k, 0.f, f32);
+    return;
+  }
+  const int iy = oy * 2 - 3 + ky;
+  const bool rv = iy >= 0 && iy < h;
+  const double mean[3] = {0.485, 0.456, 0.406}, sd[3] = {0.229, 0.224, 0.225};
+#pragma unroll
+  for (int kx = 0; kx < 7; ++kx) {
+    const int ix = ox * 2 - 3 + kx;
+    const bool ok = rv && ix >= 0 && ix < w;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float v = 0.f;
+      if (ok) {
+        if (x_u8) {
+          const float x01 = (float)((const uint8_t*)x)[(((size_t)img * h + iy) * w + ix) * 3 + c] / 255.0f;
+          v = (float)(((double)x01 - mean[c]) / sd[c]);
+        } else {
+          v = ((const float*)x)[(((size_t)img * 3 + c) * h + iy) * w + ix];
+        }
       }
+      st_act(col, row + ky * 21 + kx * 3 + c, v, f32);
     }
   }
-  st_act(col, e, v, f32);
 }
 
 // ---- MaxPool2d(3, stride 2, padding 1) (resnet.py:65), NHWC ----
@@ -83,15 +96,24 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const void* __restrict__ i
   st_act(out, e, m, f32);
 }
 
-// ---- AdaptiveAvgPool2d(1) (aspp.py:55): torch takes mean over (h, w); summed here in fp64 ----
+// ---- AdaptiveAvgPool2d(1) (aspp.py:55): torch takes the mean over (h, w).  Block = 64 channels x 4 pixel
+// lanes (coalesced 64-channel rows), fp64 sums combined in fixed lane order ----
 __global__ __launch_bounds__(256) void avgpool_kernel(const void* __restrict__ in, int f32, int hw, int c, int cs,
                                                       void* __restrict__ out) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x, img = blockIdx.y;
-  if (ch >= c) return;
+  __shared__ double part[4][64];
+  const int t = threadIdx.x, cl = t & 63, lane = t >> 6;
+  const int ch = blockIdx.x * 64 + cl, img = blockIdx.y;
   double s = 0.0;
-  const size_t base = (size_t)img * hw * cs + ch;
-  for (int i = 0; i < hw; ++i) s += (double)ld_act(in, base + (size_t)i * cs, f32);
-  st_act(out, (size_t)img * cs + ch, (float)(s / hw), f32);
+  if (ch < c) {
+    const size_t base = (size_t)img * hw * cs + ch;
+    for (int i = lane; i < hw; i += 4) s += (double)ld_act(in, base + (size_t)i * cs, f32);
+  }
+  part[lane][cl] = s;
+  __syncthreads();
+  if (lane == 0 && ch < c) {
+    const double tot = ((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl];
+    st_act(out, (size_t)img * cs + ch, (float)(tot / hw), f32);
+  }
 }
 
 // ---- bilinear, align_corners=True (deeplab.py:31, aspp.py:71, decoder.py:39): torch's CPU
@@ -117,21 +139,25 @@ __device__ __forceinline__ AcAxis ac_axis(int dst, int in, int out) {
 __global__ __launch_bounds__(256) void resize_ac_kernel(const void* __restrict__ in, int f32, int n, int h, int w,
                                                         int c, int cs_in, void* __restrict__ out, int oh, int ow,
                                                         int cs_out, int off) {
+  // one thread = one output pixel x 8 consecutive channels
+  const int groups = c >> 3;
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total = (size_t)n * oh * ow * c;
+  const size_t total = (size_t)n * oh * ow * groups;
   if (e >= total) return;
-  const int ch = (int)(e % c);
-  const size_t px = e / c;
+  const int ch = (int)(e % groups) * 8;
+  const size_t px = e / groups;
   const int ox = (int)(px % ow), oy = (int)((px / ow) % oh), img = (int)(px / ((size_t)ow * oh));
   const AcAxis ay = ac_axis(oy, h, oh), ax = ac_axis(ox, w, ow);
   const size_t b = (size_t)img * h * w;
-  const float v00 = ld_act(in, (b + (size_t)ay.i0 * w + ax.i0) * cs_in + ch, f32);
-  const float v01 = ld_act(in, (b + (size_t)ay.i0 * w + ax.i1) * cs_in + ch, f32);
-  const float v10 = ld_act(in, (b + (size_t)ay.i1 * w + ax.i0) * cs_in + ch, f32);
-  const float v11 = ld_act(in, (b + (size_t)ay.i1 * w + ax.i1) * cs_in + ch, f32);
-  const float t0 = v00 * ax.l0 + v01 * ax.l1;
-  const float t1 = v10 * ax.l0 + v11 * ax.l1;
-  st_act(out, px * cs_out + off + ch, t0 * ay.l0 + t1 * ay.l1, f32);
+  const size_t i00 = (b + (size_t)ay.i0 * w + ax.i0) * cs_in + ch, i01 = (b + (size_t)ay.i0 * w + ax.i1) * cs_in + ch;
+  const size_t i10 = (b + (size_t)ay.i1 * w + ax.i0) * cs_in + ch, i11 = (b + (size_t)ay.i1 * w + ax.i1) * cs_in + ch;
+  const size_t o = px * cs_out + off + ch;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float t0 = ld_act(in, i00 + q, f32) * ax.l0 + ld_act(in, i01 + q, f32) * ax.l1;
+    const float t1 = ld_act(in, i10 + q, f32) * ax.l0 + ld_act(in, i11 + q, f32) * ax.l1;
+    st_act(out, o + q, t0 * ay.l0 + t1 * ay.l1, f32);
+  }
 }
 
 // ---- final upsample (deeplab.py:31) + argmax over classes (sky_swap.py:193: first maximum wins) ----
@@ -271,7 +297,8 @@ __global__ __launch_bounds__(256) void pil_v_kernel(const uint8_t* __restrict__ 
 
 hipError_t launch_seg_stem_im2col(int dtype, const void* x, int x_u8, int n, int h, int w, int ho, int wo, int kp,
                                   void* col, hipStream_t st) {
-  const size_t total = (size_t)n * ho * wo * kp;
+  if (kp < 147) return hipErrorInvalidValue;
+  const size_t total = (size_t)n * ho * wo * 8;
   hipLaunchKernelGGL(stem_im2col_kernel, dim3(blocks_for(total)), dim3(256), 0, st, x, x_u8, dtype == NST_DT_F32 ? 1 : 0,
                      n, h, w, ho, wo, kp, col);
   return hipGetLastError();
@@ -286,14 +313,15 @@ hipError_t launch_seg_maxpool(int dtype, const void* in, int n, int h, int w, in
 }
 
 hipError_t launch_seg_avgpool(int dtype, const void* in, int n, int hw, int c, int cs, void* out, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_kernel, dim3(blocks_for((size_t)c), (unsigned)n), dim3(256), 0, st, in,
+  hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((c + 63) / 64), (unsigned)n), dim3(256), 0, st, in,
                      dtype == NST_DT_F32 ? 1 : 0, hw, c, cs, out);
   return hipGetLastError();
 }
 
 hipError_t launch_seg_resize_ac(int dtype, const void* in, int n, int h, int w, int c, int cs_in, void* out, int oh,
                                 int ow, int cs_out, int off, hipStream_t st) {
-  const size_t total = (size_t)n * oh * ow * c;
+  if (c % 8 || cs_in % 8 || cs_out % 8 || off % 8) return hipErrorInvalidValue;
+  const size_t total = (size_t)n * oh * ow * (c / 8);
   hipLaunchKernelGGL(resize_ac_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, dtype == NST_DT_F32 ? 1 : 0, n,
                      h, w, c, cs_in, out, oh, ow, cs_out, off);
   return hipGetLastError();
