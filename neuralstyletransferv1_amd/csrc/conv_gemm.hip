@@ -273,8 +273,8 @@ struct GemmShape {
 GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
   const int nstage = p.ntaps * (p.cin / gemm_stage_channels(dtype));
   GemmShape g;
-  // 128x128 tiles when they alone give the chip a few waves of workgroups; 64x64 otherwise
-  g.big = (long)((p.npix + 127) / 128) * ((p.cout_store + 127) / 128) >= 512;
+  // 128x128 tiles when they alone fill the chip's 256 CUs; 64x64 otherwise
+  g.big = (long)((p.npix + 127) / 128) * ((p.cout_store + 127) / 128) >= 256;
   g.ksplit = 1;
   if (!g.big) {  // fewer 64x64 tiles than a wave of the chip and a long K loop: split K (at most 8 slices)
     const long tiles = (long)((p.npix + 63) / 64) * ((p.cout_store + 63) / 64);

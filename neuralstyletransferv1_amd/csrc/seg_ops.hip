@@ -33,54 +33,67 @@ inline unsigned blocks_for(size_t n, int per = 256) { return (unsigned)((n + per
 // array against the float64 tuples), then .float() -> float32 — reproduced operation for operation.
 __global__ __launch_bounds__(256) void stem_im2col_kernel(const void* __restrict__ x, int x_u8, int f32, int n, int h,
                                                           int w, int ho, int wo, int kp, void* __restrict__ col) {
-  // one thread = one output pixel x one kernel row ky: the 21 columns k = ky*21 .. ky*21+20 (kx-major, then
-  // channel) read 7 horizontally adjacent source pixels; ky == 7 writes the zero columns 147 .. kp-1
+  // one thread = one output pixel x 8 consecutive columns (one 16-byte bf16 / two 16-byte fp32 stores;
+  // consecutive threads write consecutive chunks of a pixel's row).  u8 frames go through a per-block table
+  // of the 3 x 256 normalised values, each computed once with the reference's float32 / float64 steps.
+  __shared__ float lut[3][256];
+  if (x_u8) {
+    const double mean[3] = {0.485, 0.456, 0.406}, sd[3] = {0.229, 0.224, 0.225};
+    for (int i = threadIdx.x; i < 768; i += blockDim.x) {
+      const int c = i >> 8, v = i & 255;
+      lut[c][v] = (float)(((double)((float)v / 255.0f) - mean[c]) / sd[c]);
+    }
+    __syncthreads();
+  }
+  const int chunks = kp >> 3;
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total = (size_t)n * ho * wo * 8;
+  const size_t total = (size_t)n * ho * wo * chunks;
   if (e >= total) return;
-  const int ky = (int)(e & 7);
-  const size_t px = e >> 3;
+  const int k0 = (int)(e % chunks) * 8;
+  const size_t px = e / chunks;
   const int ox = (int)(px % wo);
   const int oy = (int)((px / wo) % ho);
   const int img = (int)(px / ((size_t)wo * ho));
-  const size_t row = px * kp;
-  if (ky == 7) {
-    for (int k = 147; k < kp; ++k) st_act(col, row + k, 0.f, f32);
-    return;
-  }
-  const int iy = oy * 2 - 3 + ky;
-  const bool rv = iy >= 0 && iy < h;
-  const double mean[3] = {0.485, 0.456, 0.406}, sd[3] = {0.229, 0.224, 0.225};
+  float v[8];
 #pragma unroll
-  for (int kx = 0; kx < 7; ++kx) {
-    const int ix = ox * 2 - 3 + kx;
-    const bool ok = rv && ix >= 0 && ix < w;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      float v = 0.f;
-      if (ok) {
-        if (x_u8) {
-          const float x01 = (float)((const uint8_t*)x)[(((size_t)img * h + iy) * w + ix) * 3 + c] / 255.0f;
-          v = (float)(((double)x01 - mean[c]) / sd[c]);
-        } else {
-          v = ((const float*)x)[(((size_t)img * 3 + c) * h + iy) * w + ix];
-        }
+  for (int q = 0; q < 8; ++q) {
+    const int k = k0 + q;
+    v[q] = 0.f;
+    if (k < 147) {
+      const int c = k % 3, tap = k / 3, ky = tap / 7, kx = tap - ky * 7;
+      const int iy = oy * 2 - 3 + ky, ix = ox * 2 - 3 + kx;
+      if (iy >= 0 && iy < h && ix >= 0 && ix < w) {
+        if (x_u8) v[q] = lut[c][((const uint8_t*)x)[(((size_t)img * h + iy) * w + ix) * 3 + c]];
+        else v[q] = ((const float*)x)[(((size_t)img * 3 + c) * h + iy) * w + ix];
       }
-      st_act(col, row + ky * 21 + kx * 3 + c, v, f32);
     }
+  }
+  const size_t o = px * kp + k0;
+  if (f32) {
+    *(float4*)((float*)col + o) = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)((float*)col + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    uint4 u;
+    u.x = (uint32_t)bf16_rne(v[0]) | ((uint32_t)bf16_rne(v[1]) << 16);
+    u.y = (uint32_t)bf16_rne(v[2]) | ((uint32_t)bf16_rne(v[3]) << 16);
+    u.z = (uint32_t)bf16_rne(v[4]) | ((uint32_t)bf16_rne(v[5]) << 16);
+    u.w = (uint32_t)bf16_rne(v[6]) | ((uint32_t)bf16_rne(v[7]) << 16);
+    *(uint4*)((uint16_t*)col + o) = u;
   }
 }
 
 // ---- MaxPool2d(3, stride 2, padding 1) (resnet.py:65), NHWC ----
 __global__ __launch_bounds__(256) void maxpool_kernel(const void* __restrict__ in, int f32, int n, int h, int w, int c,
                                                       void* __restrict__ out, int ho, int wo) {
+  // one thread = one output pixel x 8 consecutive channels
+  const int groups = c >> 3;
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total = (size_t)n * ho * wo * c;
+  const size_t total = (size_t)n * ho * wo * groups;
   if (e >= total) return;
-  const int ch = (int)(e % c);
-  const size_t px = e / c;
+  const int ch = (int)(e % groups) * 8;
+  const size_t px = e / groups;
   const int ox = (int)(px % wo), oy = (int)((px / wo) % ho), img = (int)(px / ((size_t)wo * ho));
-  float m = -FLT_MAX;
+  float m[8];
   bool any = false;
   for (int dy = 0; dy < 3; ++dy) {
     const int iy = oy * 2 - 1 + dy;
@@ -88,12 +101,17 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const void* __restrict__ i
     for (int dx = 0; dx < 3; ++dx) {
       const int ix = ox * 2 - 1 + dx;
       if (ix < 0 || ix >= w) continue;
-      const float v = ld_act(in, (((size_t)img * h + iy) * w + ix) * c + ch, f32);
-      m = any ? fmaxf(m, v) : v;
+      const size_t b = (((size_t)img * h + iy) * w + ix) * c + ch;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = ld_act(in, b + q, f32);
+        m[q] = any ? fmaxf(m[q], v) : v;
+      }
       any = true;
     }
   }
-  st_act(out, e, m, f32);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st_act(out, px * c + ch + q, m[q], f32);
 }
 
 // ---- AdaptiveAvgPool2d(1) (aspp.py:55): torch takes the mean over (h, w).  Block = 64 channels x 4 pixel
@@ -297,8 +315,8 @@ __global__ __launch_bounds__(256) void pil_v_kernel(const uint8_t* __restrict__ 
 
 hipError_t launch_seg_stem_im2col(int dtype, const void* x, int x_u8, int n, int h, int w, int ho, int wo, int kp,
                                   void* col, hipStream_t st) {
-  if (kp < 147) return hipErrorInvalidValue;
-  const size_t total = (size_t)n * ho * wo * 8;
+  if (kp < 147 || kp % 8) return hipErrorInvalidValue;
+  const size_t total = (size_t)n * ho * wo * (kp / 8);
   hipLaunchKernelGGL(stem_im2col_kernel, dim3(blocks_for(total)), dim3(256), 0, st, x, x_u8, dtype == NST_DT_F32 ? 1 : 0,
                      n, h, w, ho, wo, kp, col);
   return hipGetLastError();
@@ -306,7 +324,8 @@ hipError_t launch_seg_stem_im2col(int dtype, const void* x, int x_u8, int n, int
 
 hipError_t launch_seg_maxpool(int dtype, const void* in, int n, int h, int w, int c, void* out, int ho, int wo,
                               hipStream_t st) {
-  const size_t total = (size_t)n * ho * wo * c;
+  if (c % 8) return hipErrorInvalidValue;
+  const size_t total = (size_t)n * ho * wo * (c / 8);
   hipLaunchKernelGGL(maxpool_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, dtype == NST_DT_F32 ? 1 : 0, n, h,
                      w, c, out, ho, wo);
   return hipGetLastError();
