@@ -338,6 +338,70 @@ int nst_resize_scratch_bytes(const nst_resize* r, int n, size_t* out);
 int nst_resize_u8(const nst_resize* r, const uint8_t* in, int n, int c, uint8_t* out, void* scratch,
                   size_t scratch_bytes, void* stream);
 
+/* ---- Region-blend compositor (region_blend.py; pipeline.py:1120-1407 --region_optimize and :1720-1839
+ * --region_mode) ----
+ * The reference's control logic (random.Random draws, blend specs, animations) stays on the host
+ * (neuralstyletransferv1_amd/regions.py); these entry points render, feather, rotate and composite. */
+#define NST_REGION_MAX 32     /* regions per composite */
+#define NST_REGION_TERMS 9    /* models A..H + the original per region */
+#define NST_REGION_MAX_SRC 16 /* sources per composite */
+/* mask geometry kinds (generate_region_masks, region_blend.py:925-980) */
+#define NST_RG_RECTS 0      /* grid_masks / fractal_quad_masks :109-135, 307-364: region k = rects[k] {y1,y2,x1,x2} */
+#define NST_RG_DIAGONAL 1   /* diagonal_masks :138-171: ivals[0] = 1 for x+y, 0 for (W-1-x)+y; dvals[3] = its max */
+#define NST_RG_VORONOI 2    /* voronoi_masks :174-236: points[k] = (x, y); divisor[k] = sqrt(w_k)+1e-6 or 0 */
+#define NST_RG_RADIAL 3     /* radial_masks :367-401: ivals = cx, cy; dvals[0] = rotation; lo/hi = wedge bounds */
+#define NST_RG_WAVES 4      /* wave_masks :404-447: ivals[0] = 0 horizontal, 1 vertical, 2 diagonal;
+                               dvals = frequency, amplitude, phase */
+#define NST_RG_SPIRAL 5     /* spiral_masks :450-485: ivals = cx, cy; dvals = tightness, rotation, max(H, W) */
+#define NST_RG_CONCENTRIC 6 /* concentric_masks :488-516: ivals = cx, cy; dvals[3] = r.max() */
+/*
+ * Hard (unfeathered) region masks [count][h][w] f32 0/1.  n_gen regions were generated (masks k >= n_gen
+ * repeat region n_gen-1; n_gen = 0 gives all ones, :977-978).  Band kinds use lo[k] <= t < hi[k].  All
+ * double constants are rounded to fp32 as torch rounds a Python float against a float32 tensor.
+ * scratch (NST_RG_WAVES only): h*w + 2052 floats.
+ */
+int nst_region_masks(int kind, int count, int n_gen, const int* ivals, const double* dvals, const double* lo,
+                     const double* hi, const int* rects, const double* points, const double* divisor, int h, int w,
+                     float* masks, float* scratch, void* stream);
+/* feather_mask (:69-102) in place on k planes: F.pad(reflect, ks/2) + the separable Gaussian whose ks (odd,
+ * <= 511) host fp32 taps are the reference's normalised torch taps.  scratch: k*h*w floats. */
+int nst_region_feather(float* masks, int k, int h, int w, const float* taps, int ks, float* scratch, void* stream);
+/* rotate_all_masks (:25-66): cv2.warpAffine(INTER_LINEAR, BORDER_REPLICATE) of each plane about (W/2, H/2)
+ * (OpenCV's fixed-point warp restated: cv2 absent, parity unpinned), then each pixel divided by the sum of
+ * the rotated planes clamped to 1e-6.  in != out. */
+int nst_region_rotate(const float* in, int k, int h, int w, double angle_deg, float* out, void* stream);
+/* compute_mask_bbox (:1969-1994): bbox[4k..4k+3] = {x1, y1, x2, y2} (exclusive ends) of the values >
+ * threshold in plane k, device int buffer; an empty plane leaves {INT_MAX, INT_MAX, -1, -1}. */
+int nst_region_bbox(const float* masks, int k, int h, int w, float threshold, int* bbox, void* stream);
+/* scratch floats nst_region_composite_u8 needs (crops mode only) */
+int nst_region_scratch_floats(int n, int h, int w, int crops, int with_orig, size_t* out);
+/*
+ * Region composite of a batch of n frames, out u8 NHWC [n,h,w,3] (ToPILImage truncation) and/or out_f32
+ * NCHW [n,3,h,w] in [0,1].  Sources s < n_src: f32 NCHW [n,3,src_hw[2s],src_hw[2s+1]] decoded with
+ * src_preset[s] (NST_PRESET_NONE for already-decoded images) and bilinearly fitted; source -1 is the
+ * original frame orig u8 NHWC [n,h,w,3] (to_tensor).  Region k blends n_terms[k] (<= 9) terms
+ * term_src[9k+j] with weights term_w[9k+j] (region_blend = zeros; += w * src in order).
+ *   boxes == NULL: composite_regions(_advanced) (:1049-1108, 1589-1679) over full-frame masks [n_regions][h][w],
+ *                  sources fitted to (h, w).
+ *   boxes != NULL: composite_from_crops (:2186-2294): region k covers the padded bbox boxes[4k..4k+3] =
+ *                  {x1,y1,x2,y2}, its sources are fitted to that crop; then the < 0.1 coverage-gap fill
+ *                  (original frame, or max-pool dilation 5/11/21 without one); scratch per
+ *                  nst_region_scratch_floats.
+ */
+int nst_region_composite_u8(const float* const* src_y, const int* src_hw, const int* src_preset, int n_src,
+                            const int* n_terms, const int* term_src, const float* term_w, int n_regions,
+                            const int* boxes, const uint8_t* orig, const float* masks, int n, int h, int w,
+                            float* scratch, size_t scratch_floats, uint8_t* out, float* out_f32, void* stream);
+/* --region_optimize crop input (pipeline.py:1309-1332): to_tensor(frame)[:, y1:y2, x1:x2] resized bilinearly
+ * (align_corners=False) to out_h x out_w when they differ -> f32 NCHW [n,3,out_h,out_w] in [0,1], the
+ * nst_forward NST_IO_F32_NCHW input.  box = {x1, y1, x2, y2}. */
+int nst_region_crop_input(const uint8_t* frames, int n, int h, int w, const int* box, int out_h, int out_w, float* out,
+                          void* stream);
+/* the advanced path's low-resolution outputs (pipeline.py:1786-1796): raw output y [n,3,h,w] decoded with
+ * preset, fitted to fit_h x fit_w, then resized bilinearly to out_h x out_w -> decoded f32 NCHW */
+int nst_region_resize(const float* y, int n, int h, int w, int preset, int fit_h, int fit_w, int out_h, int out_w,
+                      float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,7 +40,12 @@ EXPORTED_SYMBOLS = (
     "nst_seg_create", "nst_seg_destroy", "nst_seg_num_classes", "nst_seg_workspace_bytes", "nst_seg_forward",
     "nst_seg_mask_scratch_bytes", "nst_seg_mask", "nst_resize_create", "nst_resize_destroy",
     "nst_resize_scratch_bytes", "nst_resize_u8", "nst_blend_mask8_u8",
+    "nst_region_masks", "nst_region_feather", "nst_region_rotate", "nst_region_bbox", "nst_region_scratch_floats",
+    "nst_region_composite_u8", "nst_region_crop_input", "nst_region_resize",
 )
+# region compositor limits / geometry kinds (include/nst_hip.h NST_REGION_*, NST_RG_*)
+NST_REGION_MAX, NST_REGION_TERMS, NST_REGION_MAX_SRC = 32, 9, 16
+RG_KINDS = {"rects": 0, "diagonal": 1, "voronoi": 2, "radial": 3, "waves": 4, "spiral": 5, "concentric": 6}
 NST_GRAM_CHW, NST_GRAM_HWC = 0, 1
 
 # nst_create_ex kernel-selection flags (include/nst_hip.h NST_KSEL_*)
@@ -139,6 +144,20 @@ def lib() -> ctypes.CDLL:
         L.nst_resize_destroy.restype = None
         L.nst_resize_scratch_bytes.argtypes = [vp, i, ctypes.POINTER(sz)]
         L.nst_resize_u8.argtypes = [vp, vp, i, i, vp, vp, sz, vp]
+        pi, pd, pf = ctypes.POINTER(i), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(f)
+        L.nst_region_masks.argtypes = [i, i, i, pi, pd, pd, pd, pi, pd, pd, i, i, vp, vp, vp]
+        L.nst_region_feather.argtypes = [vp, i, i, i, pf, i, vp, vp]
+        L.nst_region_rotate.argtypes = [vp, i, i, i, ctypes.c_double, vp, vp]
+        L.nst_region_bbox.argtypes = [vp, i, i, i, f, vp, vp]
+        L.nst_region_scratch_floats.argtypes = [i, i, i, i, i, ctypes.POINTER(sz)]
+        L.nst_region_composite_u8.argtypes = [ctypes.POINTER(vp), pi, pi, i, pi, pi, pf, i, pi, vp, vp, i, i, i, vp,
+                                              sz, vp, vp, vp]
+        L.nst_region_crop_input.argtypes = [vp, i, i, i, pi, i, i, vp, vp]
+        L.nst_region_resize.argtypes = [vp, i, i, i, i, i, i, i, i, vp, vp]
+        for name in ("nst_region_masks", "nst_region_feather", "nst_region_rotate", "nst_region_bbox",
+                     "nst_region_scratch_floats", "nst_region_composite_u8", "nst_region_crop_input",
+                     "nst_region_resize"):
+            getattr(L, name).restype = i
         L.nst_output_hw.argtypes = [vp, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
         L.nst_workspace_bytes.argtypes = [vp, i, i, i, ctypes.POINTER(sz)]
         L.nst_forward.argtypes = [vp, vp, i, i, i, i, i, vp, i, vp, sz, vp]

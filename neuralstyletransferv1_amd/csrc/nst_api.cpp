@@ -17,6 +17,7 @@
 
 #include "nst_hip.h"
 #include "nst_internal.h"
+#include "post_common.h"
 
 namespace nst {
 
@@ -635,6 +636,15 @@ int pack_upload_conv(const ConvKernelInfo& k, int cin, int cout, int ks, const f
   return upload(pk.data(), pk.size() * 4, dev);
 }
 int upload_floats(const float* host, size_t n, float** dev) { return upload(host, n * 4, (void**)dev); }
+// the output decode constants of an io_preset (the region compositor's sources, region_api.cpp)
+bool decode_consts_for_preset(int preset, DecodeConsts& d) {
+  PresetConsts pc;
+  if (!preset_consts(preset, pc)) return false;
+  for (int c = 0; c < 3; ++c) {
+    d.p[c] = pc.dp[c]; d.q[c] = pc.dq[c]; d.r[c] = pc.dr[c]; d.s[c] = pc.ds[c]; d.perm[c] = pc.dperm[c];
+  }
+  return true;
+}
 void tile_grid_of(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx, int* ty) {
   tile_grid(k, sh, sw, oh, ow, tx, ty);
 }

@@ -1,0 +1,176 @@
+"""Region-blend compositor on the GPU (libnst_hip region kernels) against the reference's own vectors
+(tests/golden/regions.npz from region_blend.py) and, at 1080p, against the CPU oracle (oracle/region_oracle.py).
+
+Bars: hard masks bit-exact where the pattern needs only +,-,*,/,sqrt (grid, fractal, diagonal, voronoi,
+concentric); the atan2/sin patterns (radial, spiral, waves) may flip a pixel sitting on a band edge (GPU libm
+vs torch's SLEEF, <= 0.05 % of pixels).  Feathered masks 2e-6 absolute (separable vs 2-D conv rounding).
+Composites 2e-6 absolute in fp32, uint8 within 1 LSB of the truncated fp32 reference.  Rotation is checked
+against the oracle's restatement of cv2.warpAffine only (cv2 absent: parity unpinned).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from neuralstyletransferv1_amd import regions as R
+from oracle import region_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+G = np.load(os.path.join(GOLD, "regions.npz"))
+with open(os.path.join(GOLD, "regions.json")) as f:
+    META = json.load(f)
+H, W = META["H"], META["W"]
+DEV = torch.device("cuda", 0)
+EXACT = {"grid", "fractal", "diagonal", "voronoi", "concentric"}
+
+
+def gpu_masks(mode, count, seed, feather, h=H, w=W, sizes=None):
+    g = R.draw_geometry(h, w, mode, count, seed, sizes)
+    m = R.render_masks(g, h, w, feather, DEV)
+    torch.cuda.synchronize()
+    return g, m.cpu()
+
+
+@pytest.mark.parametrize("mode", R.MODES)
+@pytest.mark.parametrize("count", [4, 5, 7])
+def test_hard_masks_vs_reference(mode, count):
+    g, m = gpu_masks(mode, count, 7, 0)
+    ref = G[f"masks_{mode}_{count}"]
+    diff = int((m.numpy().astype(np.uint8) != ref).sum())
+    if g.mode in EXACT:
+        assert diff == 0, (g.mode, diff)
+    else:
+        assert diff <= max(1, ref.size // 2000), (g.mode, diff)
+
+
+def test_weighted_voronoi_and_feathers_vs_reference():
+    _, m = gpu_masks("voronoi", 4, 11, 0, sizes=META["region_sizes"])
+    assert np.array_equal(m.numpy().astype(np.uint8), G["masks_voronoi_sized"])
+    for mode in ("voronoi", "fractal"):
+        _, m = gpu_masks(mode, 4, 3, 6)
+        assert np.abs(m.numpy() - G[f"fmasks_{mode}"]).max() <= 2e-6, mode
+    _, m = gpu_masks("grid", 4, 1, 20)
+    assert np.abs(m.numpy() - G["fmasks_grid_f20"]).max() <= 2e-6
+
+
+def _sources():
+    outs = torch.from_numpy(G["src_outputs"])  # [3 models, 3, H, W] in [0,1]
+    orig_u8 = torch.from_numpy(G["src_orig_u8"])  # [H, W, 3]
+    srcs = [R.Source(outs[i:i + 1].contiguous().to(DEV), "none") for i in range(3)]
+    return outs, orig_u8, srcs
+
+
+def _check(got_f32, got_u8, ref):
+    ref = np.asarray(ref, dtype=np.float32)
+    assert np.abs(got_f32 - ref).max() <= 2e-6
+    ref_u8 = (torch.from_numpy(ref) * 255).to(torch.uint8).permute(1, 2, 0).numpy().astype(np.int16)
+    assert np.abs(got_u8.astype(np.int16) - ref_u8).max() <= 1
+
+
+def _terms(cfgs):
+    return [[(mi, w) for mi, w in zip(c.model_indices, c.model_weights)] for c in cfgs]
+
+
+def test_full_frame_composites_vs_reference():
+    outs, orig_u8, srcs = _sources()
+    masks = torch.from_numpy(G["comp_masks"]).to(DEV)
+    o = orig_u8[None].contiguous().to(DEV)
+    single = [[(a, 1.0)] for a in META["comp_assign"]]
+    for terms, ref in ((single, G["comp_out"]), (_terms(R.RegionConfig(*c) for c in META["adv_configs"]), G["adv_out"])):
+        f = R.composite(srcs, terms, masks, o, out_f32=True)[0].cpu().numpy()
+        u = R.composite(srcs, terms, masks, o)[0].cpu().numpy()
+        _check(f, u, ref)
+
+
+def test_scaled_sources_vs_reference():
+    outs, orig_u8, srcs = _sources()
+    masks = torch.from_numpy(G["comp_masks"]).to(DEV)
+    half = [R.Source(R.resized_source(s.y, "none", (H, W), (H // 2, W // 2)), "none") for s in srcs]
+    ref_half = torch.nn.functional.interpolate(outs, size=(H // 2, W // 2), mode="bilinear", align_corners=False)
+    assert (torch.cat([h.y for h in half]).cpu() - ref_half).abs().max() <= 1e-6
+    cf = [R.RegionConfig(*c) for c in META["adv_scaled_configs"]]
+    terms = [[((mi if c.scale == 1.0 else 3 + mi), w) for mi, w in zip(c.model_indices, c.model_weights)] for c in cf]
+    f = R.composite(srcs + half, terms, masks, None, out_f32=True)[0].cpu().numpy()
+    u = R.composite(srcs + half, terms, masks, None)[0].cpu().numpy()
+    _check(f, u, G["adv_scaled_out"])
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_crops_composite_vs_reference(case):
+    outs, orig_u8, _ = _sources()
+    c = META["crops"][case]
+    _, m = gpu_masks(c["mode"], c["count"], c["seed"], c["feather"])
+    assert np.abs(m.numpy() - G[f"crops_{case}_masks"]).max() <= 2e-6
+    masks = m.to(DEV)
+    boxes = R.mask_bboxes(masks)
+    assert [list(b) for b in boxes] == c["bbox"]
+    padded = [tuple(b) for b in c["padded"]]
+    cf = [R.RegionConfig(*x) for x in c["configs"]]
+    anims = R.parse_region_blend_animations("30,triangle", len(cf))
+    srcs, terms = [], []
+    for k, ((x1, y1, x2, y2), cfg) in enumerate(zip(padded, cf)):
+        wts = R.compute_animated_weights(cfg.model_weights, 7, anims[k])
+        tl = []
+        for mi, w in zip(cfg.model_indices, wts):
+            if mi < 0:
+                tl.append((-1, w))
+                continue
+            crop = (outs[mi][:, y1:y2, x1:x2].clone() * 0.9)[None].contiguous()
+            srcs.append(R.Source(crop.to(DEV), "none"))
+            tl.append((len(srcs) - 1, w))
+        terms.append(tl)
+    o = orig_u8[None].contiguous().to(DEV) if c["with_orig"] else None
+    f = R.composite(srcs, terms, masks, o, boxes=padded, out_f32=True)[0].cpu().numpy()
+    u = R.composite(srcs, terms, masks, o, boxes=padded)[0].cpu().numpy()
+    _check(f, u, G[f"crops_{case}_out"])
+
+
+def test_crop_input_matches_interpolate():
+    gen = torch.Generator().manual_seed(3)
+    fr = torch.randint(0, 256, (2, 70, 90, 3), generator=gen, dtype=torch.uint8)
+    box = (7, 5, 71, 63)
+    x01 = fr.permute(0, 3, 1, 2).float().div(255)[:, :, 5:63, 7:71]
+    same = R.crop_input(fr.to(DEV), box, (58, 64)).cpu()
+    assert torch.equal(same, x01)
+    small = R.crop_input(fr.to(DEV), box, (29, 32)).cpu()
+    ref = torch.nn.functional.interpolate(x01, size=(29, 32), mode="bilinear", align_corners=False)
+    assert (small - ref).abs().max() <= 1e-6
+
+
+def test_rotation_vs_restatement():
+    _, m = gpu_masks("voronoi", 5, 3, 4)
+    for ang in (2.0, 33.5, -71.0):
+        got = R.rotate_planes(m.to(DEV), ang).cpu()
+        ref = O.rotate(m, ang)
+        assert (got - ref).abs().max() <= 2e-6, ang
+
+
+@pytest.mark.parametrize("mode", ["voronoi", "spiral", "fractal"])
+def test_1080p_chain_vs_oracle(mode):
+    """masks + feather 20 + 4-model composite with the original at 1080p, raw imagenet_255 outputs decoded
+    on the fly (the reference decodes y/255 then clamps, pipeline.py:1445-1486)."""
+    h, w = 1080, 1920
+    g = R.draw_geometry(h, w, mode, 6, 5)
+    masks = R.render_masks(g, h, w, 20, DEV)
+    ref_masks = O.feather(O.masks_from_geometry(g, h, w), 20)
+    dm = (masks.cpu() - ref_masks).abs()
+    if g.mode in EXACT:
+        assert dm.max() <= 2e-6
+    else:  # band-edge flips of atan2/sin spread by the feather: a thin set of pixels
+        assert float((dm > 2e-6).float().mean()) < 0.01
+    gen = torch.Generator().manual_seed(9)
+    raw = [torch.rand(1, 3, h, w, generator=gen) * 300 - 20 for _ in range(4)]
+    orig_u8 = torch.randint(0, 256, (1, h, w, 3), generator=gen, dtype=torch.uint8)
+    cf = R.parse_region_configs(6, 4, "random", "A+B|C|O+D|B:0.3+D:0.7", None, 5, 0.0)
+    srcs = [R.Source(r.to(DEV), "imagenet_255") for r in raw]
+    got = R.composite(srcs, _terms(cf), masks, orig_u8.to(DEV), out_f32=True)[0].cpu()
+    dec = [(r[0] / 255.0).clamp(0, 1) for r in raw]
+    ref = O.composite_adv({1.0: dec}, masks.cpu(), cf, orig_u8[0].permute(2, 0, 1).float().div(255), h, w)
+    assert (got - ref).abs().max() <= 2e-6
+    u8 = R.composite(srcs, _terms(cf), masks, orig_u8.to(DEV))[0].cpu()
+    ref_u8 = (ref * 255).to(torch.uint8).permute(1, 2, 0)
+    assert (u8.int() - ref_u8.int()).abs().max() <= 1
