@@ -370,6 +370,9 @@ __global__ __launch_bounds__(256) void region_composite_kernel(RegionSrcSet ss, 
   float res[3] = {0.f, 0.f, 0.f}, ws = 0.f;
   for (int k = 0; k < t.n_regions; ++k) {
     const float m = masks[(size_t)k * hw + p];
+    // a zero mask adds rb * 0 = +0 to non-negative sums: skipping it is exact and skips its source reads
+    // (the feathered masks are exactly 0 beyond the Gaussian's radius, so most pixels touch one region)
+    if (m == 0.f) continue;
     float rb[3];
     region_blend_at(ss, t, k, b, orig, i, y, x, h, w, rb);
 #pragma unroll
@@ -405,6 +408,7 @@ __global__ __launch_bounds__(256) void crops_accum_kernel(RegionSrcSet ss, Regio
     const int x1 = t.box[k][0], y1 = t.box[k][1], x2 = t.box[k][2], y2 = t.box[k][3];
     if (x < x1 || x >= x2 || y < y1 || y >= y2) continue;
     const float m = masks[(size_t)k * hw + p];
+    if (m == 0.f) continue;  // exact, as in the full-frame composite
     float rb[3];
     region_blend_at(ss, t, k, b, orig, i, y - y1, x - x1, y2 - y1, x2 - x1, rb);
 #pragma unroll

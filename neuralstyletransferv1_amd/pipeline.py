@@ -18,9 +18,12 @@ Also on the GPU: the LAB multi-model blend (--blend_models_lab, pipeline.py:1841
 Gaussian mask feather (--mask_feather / --mask_feather_pct, pipeline.py:349-351; cv2's blur
 restated, parity unpinned because cv2 is absent here).
 
-Not built (rejected with a clear message if requested): region blending
-(--region_*), optical-flow EMA / motion blend (--flow_ema, --motion_blend), Magenta (TF-Hub) and
-Torch7 (OpenCV DNN) backends.
+Region blending (--region_mode / --region_optimize and their spec, animation and rotation flags,
+pipeline.py:1120-1407, 1720-1839) runs on the GPU compositor of regions.py.
+
+Not built (rejected with a clear message if requested): --region_morph's organic
+warp, optical-flow EMA / motion blend (--flow_ema, --motion_blend), Magenta (TF-Hub) and Torch7 (OpenCV
+DNN) backends.
 """
 from __future__ import annotations
 
@@ -114,9 +117,13 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--blend_models_weights", type=str, default=None)
     ap.add_argument("--blend_models_lab", action="store_true")
     ap.add_argument("--blend_models_lab_weights", type=str, default=None)
-    for flag, kw in (("--region_mode", dict(type=str, default=None)), ("--region_count", dict(type=int, default=4)),
-                     ("--region_sizes", dict(type=str, default=None)), ("--region_seed", dict(type=int, default=None)),
-                     ("--region_feather", dict(type=int, default=20)), ("--region_assignment", dict(type=str, default="random")),
+    for flag, kw in (("--region_mode", dict(type=str, default=None, choices=["grid", "diagonal", "voronoi", "fractal",
+                                                                           "radial", "waves", "spiral", "concentric",
+                                                                           "random"])),
+                     ("--region_count", dict(type=int, default=None)),
+                     ("--region_sizes", dict(type=str, default=None)), ("--region_seed", dict(type=str, default=None)),
+                     ("--region_feather", dict(type=int, default=20)),
+                     ("--region_assignment", dict(type=str, default="random", choices=["sequential", "random", "weighted"])),
                      ("--region_original", dict(type=float, default=0.0)), ("--region_rotate", dict(type=float, default=0.0)),
                      ("--region_blend_spec", dict(type=str, default=None)), ("--region_scales", dict(type=str, default=None)),
                      ("--region_optimize", dict(action="store_true")), ("--region_padding", dict(type=int, default=64)),
@@ -157,8 +164,8 @@ def reject_out_of_scope(args) -> None:
                                              or str(getattr(args, f"model_{s}")).lower() in ("magenta",)
                                              or str(getattr(args, f"model_{s}")).endswith(".t7")):
             bad.append(f"--model_{s} (magenta/torch7)")
-    if args.region_mode or args.region_optimize:
-        bad.append("--region_mode/--region_optimize")
+    if args.region_morph and str(args.region_morph).lower() not in ("none", "off", "0", "static"):
+        bad.append("--region_morph (organic cv2.remap warp)")
     if args.flow_ema or args.motion_blend:
         bad.append("--flow_ema/--motion_blend")
     if args.device != "cuda":
@@ -408,13 +415,14 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     save_map = save_map or {}
 
     # ---- models: A + optional B..H (RGB blend, pipeline.py:1872-1879) ----
-    slots = []
+    slots, slot_letters = [], []
     model_a, arch_a = load_model(str(model_path), args.model_type, dev, args.dtype, "A")
     if arch_a == "nst" and io_preset in ("auto", "raw_255", "imagenet_255"):  # pipeline.py:610-614
         _log(f"[model] Auto-switching io_preset from '{io_preset}' to 'raw_01' for NST_Train model")
         io_preset = "raw_01"
     slots.append((model_a, io_preset))
-    for s in SLOTS:
+    slot_letters.append(0)
+    for li, s in enumerate(SLOTS, start=1):
         p = getattr(args, f"model_{s}", None)
         if not p:
             continue
@@ -422,14 +430,23 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         ip = getattr(args, f"io_preset_{s}", None) or io_preset
         m, _ = load_model(p, t, dev, args.dtype, s.upper(), auto_nst=False)
         slots.append((m, ip))
-    if len(slots) > 1 and getattr(args, "blend_models_lab", False):
+        slot_letters.append(li)
+    # pipeline.py:1519-1520: the standard path blends only when one of B, C, D is in use, and counts models as
+    # 1 + B + C + D (slots E..H join the outputs list but the weights cover the first num_models of it)
+    n_blend = 1 + sum(1 for s in SLOTS[:3] if getattr(args, f"model_{s}", None))
+    regions = None
+    if args.region_mode and (args.region_optimize or n_blend > 1):
+        from .regions import RegionCompositor
+        regions = RegionCompositor(args, dev)
+        _log(f"[region] mode={args.region_mode} optimize={regions.optimized} seed={regions.seed}")
+    if n_blend > 1 and getattr(args, "blend_models_lab", False):
         # LAB blend (pipeline.py:1841-1870): L from A, a/b from the weighted mix of the others
         lab_wl, lab_wab = parse_lab_weights(getattr(args, "blend_models_lab_weights", None))
-        lab_rest = lab_weights_rest(args.blend_models_weights, len(slots))
+        lab_rest = lab_weights_rest(args.blend_models_weights, n_blend)
         weights = [lab_wl, lab_wab] + lab_rest
         _log(f"[blend] LAB blend: L={lab_wl},ab={lab_wab},rest={lab_rest}")
     else:
-        weights = parse_blend_weights(args.blend_models_weights, len(slots)) if len(slots) > 1 else [1.0]
+        weights = parse_blend_weights(args.blend_models_weights, n_blend) if n_blend > 1 else [1.0]
     _log(f"[cfg] io_preset={io_preset} models={len(slots)} weights={weights} dtype={args.dtype} gpus={world} batch={args.batch}")
     _log(f">> smoothing: {smooth_lightness}  alpha={smooth_alpha}  |  blend={blend}")
 
@@ -482,14 +499,23 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         orig = torch.from_numpy(np.stack([a for a, _ in loaded])).to(dev, non_blocking=True)
         xin = orig if loaded[0][1] is loaded[0][0] else torch.from_numpy(np.stack([b for _, b in loaded])).to(dev)
         h0, w0 = orig.shape[1], orig.shape[2]
-        if len(slots) == 1 and xin.shape[1:3] == orig.shape[1:3]:
+        fids = [f + 1 for f in idx]  # the reference's 1-based frame index (animations, rotation)
+        if regions is not None and regions.optimized:  # crops of the full-resolution frame (pipeline.py:1309)
+            styled = regions.optimized_frames(dict(zip(slot_letters, slots)), orig, fids)
+        elif regions is not None:
+            from .regions import Source, forward_raw
+            raw = [Source(forward_raw(m, xin, pr), pr) for m, pr in slots]
+            styled = regions.standard(raw, orig, fids, n_blend, (h0, w0))
+        elif n_blend == 1 and xin.shape[1:3] == orig.shape[1:3]:
             styled = slots[0][0].stylize_frames(xin, slots[0][1])
-        elif len(slots) > 1 and getattr(args, "blend_models_lab", False):
+        elif n_blend == 1:
+            styled = _slot_u8(slots[0][0], slots[0][1], xin, h0, w0)
+        elif getattr(args, "blend_models_lab", False):
             from .postproc import blend_models_lab
-            outs = [_slot_u8(m, pr, xin, h0, w0) for m, pr in slots]
+            outs = [_slot_u8(m, pr, xin, h0, w0) for m, pr in slots[:n_blend]]
             styled = blend_models_lab(outs, lab_rest, lab_wl, lab_wab)
         else:
-            styled = _blend_slots(slots, weights, xin, h0, w0)
+            styled = _blend_slots(slots[:n_blend], weights, xin, h0, w0)
         return torch.cat([styled, orig], dim=3) if need_orig else styled
 
     lab = LabSmoother(dev, smooth_lightness, smooth_alpha, smooth_chroma, chroma_alpha)

@@ -610,3 +610,232 @@ def resized_source(y: torch.Tensor, preset: str, fit_hw: Tuple[int, int], out_hw
     check(lib().nst_region_resize(y.data_ptr(), n, h, w, _lib.PRESETS[preset], fit_hw[0], fit_hw[1], out_hw[0],
                                   out_hw[1], out.data_ptr(), _stream(y.device)), "nst_region_resize")
     return out
+
+
+# ============================================================================ the pipeline's two region paths
+def forward_raw(model, x: torch.Tensor, preset: str) -> torch.Tensor:
+    """One nst_forward of a module-like model: x u8 NHWC frames or f32 NCHW [0,1] images -> raw f32 NCHW."""
+    dev = x.device
+    eng = model.engine(dev)
+    if x.dtype == torch.uint8:
+        n, h, w, _ = x.shape
+        fmt = _lib.NST_IO_U8_NHWC
+    else:
+        n, _, h, w = x.shape
+        fmt = _lib.NST_IO_F32_NCHW
+    oh, ow = eng.output_hw(h, w)
+    y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=dev)
+    ws = eng.workspace(n, h, w)
+    check(lib().nst_forward(eng._h, x.data_ptr(), fmt, n, h, w, _lib.PRESETS[preset], y.data_ptr(),
+                            _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(), _stream(dev)), "nst_forward")
+    return y
+
+
+class RegionCompositor:
+    """State of pipeline.py's region blending across the frames of one run (mask / config caches, parsed
+    animations), for either path.  `args` is the pipeline's argparse namespace."""
+
+    def __init__(self, args, device):
+        self.a = args
+        self.dev = torch.device(device)
+        self.optimized = bool(getattr(args, "region_optimize", False))
+        self.mode = args.region_mode
+        self.feather = int(getattr(args, "region_feather", 20))
+        self.rotate = float(getattr(args, "region_rotate", 0.0) or 0.0)
+        morph_spec = getattr(args, "region_morph", None)
+        self.morph = parse_morph_animation(morph_spec) if morph_spec else MorphAnimation(enabled=False)
+        if self.morph.enabled:
+            raise NstError("--region_morph (organic cv2.remap warp, region_blend.py:670-810) is not built on the MI355X "
+                           "engine")
+        self.oc = float(getattr(args, "region_original", 0.0) or 0.0)
+        self.blend_spec = getattr(args, "region_blend_spec", None)
+        self.scale_spec = getattr(args, "region_scales", None)
+        self.seed = parse_region_seed(getattr(args, "region_seed", None), self.optimized, self.rotate != 0)
+        self.cache: Dict[tuple, tuple] = {}
+        self.blend_anims = None
+        self.scale_anims = None
+        self._anims_parsed = False
+
+    # ---- masks: rotation + re-feather (region_blend.py:1757-1762) ----
+    def _animate(self, masks, frame_idx):
+        if self.rotate != 0:
+            masks = feather_planes(rotate_planes(masks, frame_idx * self.rotate), self.feather // 2)
+        return masks
+
+    # ---- standard path: every model styled the whole frame (pipeline.py:1720-1839) ----
+    def standard(self, raw: List[Source], orig_u8: torch.Tensor, frame_ids: List[int], num_models_quirk: int,
+                 fit_hw: Tuple[int, int]) -> torch.Tensor:
+        """raw[i]: output i of the compressed outputs list (A, then B..H in order) for the batch; frame_ids are
+        the reference's 1-based frame indices.  -> u8 [n,H,W,3]."""
+        a = self.a
+        H, W = fit_hw
+        n_out = len(raw)
+        count = getattr(a, "region_count", None) or num_models_quirk
+        assignment = getattr(a, "region_assignment", "random")
+        animating = self.rotate != 0
+        weights = None
+        if assignment == "weighted":
+            try:
+                from .pipeline import parse_blend_weights
+                weights = parse_blend_weights(getattr(a, "blend_models_weights", None), num_models_quirk)
+            except Exception:
+                weights = None
+        advanced = bool(self.blend_spec or self.scale_spec)
+        with_orig = self.oc > 0 or (advanced and bool(self.blend_spec) and "O" in self.blend_spec.upper())
+        sources, scale_of = list(raw), {1.0: list(range(n_out))}
+        if advanced:
+            for s in get_required_scales(count, num_models_quirk, assignment, self.blend_spec, self.scale_spec,
+                                         self.seed, self.oc):
+                if s != 1.0:  # pipeline.py:1786-1796: the full outputs resized down, upsampled by the composite
+                    hw = (int(H * s), int(W * s))
+                    scale_of[s] = []
+                    for r in raw:
+                        sources.append(Source(resized_source(r.y, r.preset, (H, W), hw), "none"))
+                        scale_of[s].append(len(sources) - 1)
+            # dict order as the reference builds it (scale 1.0 entry is the first only if listed first)
+        out = torch.empty((orig_u8.shape[0], H, W, 3), dtype=torch.uint8, device=self.dev)
+
+        def configs_for(k_masks):
+            if advanced:
+                return parse_region_configs(k_masks, n_out, assignment, self.blend_spec, self.scale_spec, self.seed,
+                                            self.oc)
+            asg = assign_models_to_regions(k_masks, n_out, assignment, weights, self.seed, self.oc)
+            return [RegionConfig([m], [1.0], 1.0) for m in asg]
+
+        for j, fid in enumerate(frame_ids):
+            if animating:  # cached masks + configs, rotated per frame (region_blend.py:1737-1762)
+                key = (H, W, count, advanced)
+                if key not in self.cache:
+                    m = render_masks(draw_geometry(H, W, self.mode, count, self.seed), H, W, self.feather, self.dev)
+                    self.cache[key] = (m, configs_for(m.shape[0]))
+                base, cfgs = self.cache[key]
+                masks = self._animate(base, fid)
+            elif self.seed is not None:  # a fixed seed regenerates the same masks and configs every frame
+                key = ("std", H, W, count, advanced)
+                if key not in self.cache:
+                    m = render_masks(draw_geometry(H, W, self.mode, count, self.seed), H, W, self.feather, self.dev)
+                    self.cache[key] = (m, configs_for(m.shape[0]))
+                masks, cfgs = self.cache[key]
+            else:  # no seed: fresh random regions and assignments per frame
+                masks = render_masks(draw_geometry(H, W, self.mode, count, self.seed), H, W, self.feather, self.dev)
+                cfgs = configs_for(masks.shape[0])
+            terms = []
+            for c in cfgs:
+                sc = c.scale
+                if sc not in scale_of:
+                    sc = min(list(scale_of.keys()), key=lambda s: abs(s - c.scale))
+                tl = []
+                for mi, w in zip(c.model_indices, c.model_weights):
+                    if mi != -1 and not (0 <= mi < n_out):
+                        raise NstError(f"region config names model {mi} but only {n_out} outputs exist")
+                    if mi == -1 and not with_orig:
+                        raise NstError("Region config uses original (-1) but no original frame provided")
+                    tl.append((-1 if mi == -1 else scale_of[sc][mi], w))
+                terms.append(tl)
+            if fid <= 2 or fid % 50 == 0:
+                print(f"[region] mode={self.mode} regions={masks.shape[0]} models={n_out} assignment={assignment} "
+                      f"feather={self.feather}px seed={self.seed}", flush=True)
+            if not animating and self.seed is not None:  # masks and terms shared by the batch: one launch
+                return composite(sources, terms, masks, orig_u8 if with_orig else None)
+            srcs_j = [Source(s.y[j:j + 1], s.preset) for s in sources]
+            out[j:j + 1] = composite(srcs_j, terms, masks, orig_u8[j:j + 1] if with_orig else None)
+        return out
+
+    # ---- --region_optimize: crops styled per region (pipeline.py:1120-1407) ----
+    def optimized_frames(self, slot_models: Dict[int, tuple], orig_u8: torch.Tensor, frame_ids: List[int]) -> torch.Tensor:
+        """slot_models: letter index (A=0..H=7) -> (model, io_preset) of the loaded slots."""
+        a = self.a
+        n, H, W, _ = orig_u8.shape
+        count = getattr(a, "region_count", None) or 4
+        assignment = getattr(a, "region_assignment", "sequential")
+        pad = int(getattr(a, "region_padding", 64))
+        num_models = len(slot_models)
+        sizes_spec = getattr(a, "region_sizes", None)
+        key = ("opt", H, W, count)
+        if key not in self.cache:
+            sizes = parse_region_sizes(sizes_spec, count) if sizes_spec else None
+            g = draw_geometry(H, W, self.mode, count, self.seed, sizes)
+            masks = render_masks(g, H, W, self.feather, self.dev)
+            cfgs = parse_region_configs(masks.shape[0], num_models, assignment, self.blend_spec, self.scale_spec,
+                                        self.seed, self.oc)
+            self.cache[key] = (masks, cfgs)
+        base, cfgs = self.cache[key]
+        with_orig = self.oc > 0 or bool(self.blend_spec and "O" in self.blend_spec.upper())
+        if not self._anims_parsed:
+            k = base.shape[0]
+            bspec = getattr(a, "blend_animate_regions", None) or getattr(a, "blend_animate", None)
+            sspec = getattr(a, "scale_animate_regions", None) or getattr(a, "scale_animate", None)
+            self.blend_anims = parse_region_blend_animations(bspec, k) if bspec else None
+            self.scale_anims = parse_region_scale_animations(sspec, k) if sspec else None
+            self._anims_parsed = True
+        out = torch.empty((n, H, W, 3), dtype=torch.uint8, device=self.dev)
+        # frames sharing masks, boxes and scales run as one batch per (region, model)
+        plans, order = {}, []
+        static_masks = None
+        for j, fid in enumerate(frame_ids):
+            if self.rotate != 0:
+                masks = self._animate(base, fid)
+                boxes = [(max(0, x1 - pad), max(0, y1 - pad), min(W, x2 + pad), min(H, y2 + pad))
+                         for x1, y1, x2, y2 in mask_bboxes(masks)]
+                mkey = ("rot", j)
+            else:  # static masks: their padded boxes are computed once per run
+                if static_masks is None:
+                    bkey = ("opt-boxes", H, W, count, pad)
+                    if bkey not in self.cache:
+                        self.cache[bkey] = [(max(0, x1 - pad), max(0, y1 - pad), min(W, x2 + pad), min(H, y2 + pad))
+                                            for x1, y1, x2, y2 in mask_bboxes(base)]
+                    static_masks = (base, self.cache[bkey])
+                masks, boxes = static_masks
+                mkey = ("static",)
+            scales = []
+            for k, c in enumerate(cfgs):
+                s = c.scale
+                if self.scale_anims and k < len(self.scale_anims):
+                    s = compute_animated_scale(s, fid, self.scale_anims[k])
+                scales.append(s)
+            wts = []
+            for k, c in enumerate(cfgs):
+                if self.blend_anims and k < len(self.blend_anims):
+                    wts.append(compute_animated_weights(c.model_weights, fid, self.blend_anims[k]))
+                else:
+                    wts.append(c.model_weights)
+            pk = (mkey, tuple(scales), tuple(tuple(w) for w in wts))
+            if pk not in plans:
+                plans[pk] = (masks, boxes, scales, wts, [])
+                order.append(pk)
+            plans[pk][4].append(j)
+        for pk in order:
+            masks, boxes, scales, wts, js = plans[pk]
+            idx = torch.tensor(js, device=self.dev)
+            frames = orig_u8 if len(js) == n else orig_u8.index_select(0, idx).contiguous()
+            srcs, terms = [], []
+            for k, c in enumerate(cfgs):
+                x1, y1, x2, y2 = boxes[k]
+                ch, cw = y2 - y1, x2 - x1
+                s = scales[k]
+                ih, iw = (max(1, int(ch * s)), max(1, int(cw * s))) if s < 1.0 else (ch, cw)
+                tl = []
+                crop = None
+                for mi, w in zip(c.model_indices, wts[k]):
+                    if mi == -1:
+                        if not with_orig:
+                            raise NstError("Region uses original but no original provided")
+                        tl.append((-1, w))
+                        continue
+                    if mi not in slot_models:
+                        raise NstError(f"Model {mi} not in styled_crops (model {chr(ord('A') + mi)} is not loaded)")
+                    model, preset = slot_models[mi]
+                    # pipeline.py:1363-1375: the crop path knows imagenet_255 and imagenet_01; every other preset
+                    # runs as raw 0..255 in / y/255 out
+                    preset = preset if preset in ("imagenet_255", "imagenet_01") else "raw_255"
+                    if crop is None:
+                        crop = crop_input(frames, (x1, y1, x2, y2), (ih, iw))
+                    srcs.append(Source(forward_raw(model, crop, preset), preset))
+                    tl.append((len(srcs) - 1, w))
+                terms.append(tl)
+            res = composite(srcs, terms, masks, frames if with_orig else None, boxes=boxes)
+            if len(js) == n:
+                out = res
+            else:
+                out.index_copy_(0, idx, res)
+        return out

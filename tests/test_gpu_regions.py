@@ -174,3 +174,125 @@ def test_1080p_chain_vs_oracle(mode):
     u8 = R.composite(srcs, _terms(cf), masks, orig_u8.to(DEV))[0].cpu()
     ref_u8 = (ref * 255).to(torch.uint8).permute(1, 2, 0)
     assert (u8.int() - ref_u8.int()).abs().max() <= 1
+
+
+# ----------------------------------------------------------------------------- CLI (pipeline.main) vs oracle
+from PIL import Image  # noqa: E402
+
+from neuralstyletransferv1_amd import pipeline as P  # noqa: E402
+from neuralstyletransferv1_amd import synthetic  # noqa: E402
+from oracle import nst_oracle as NO  # noqa: E402
+
+
+def _ckpts(tmp_path, seeds):
+    out = []
+    for s in seeds:
+        sd = synthetic.make_state_dict("johnson", s)
+        p = tmp_path / f"j{s}.pth"
+        torch.save(sd, p)
+        out.append((str(p), sd))
+    return out
+
+
+def _run_dir(tmp_path, frames, argv):
+    d_in, d_out = tmp_path / "in", tmp_path / "out"
+    d_in.mkdir()
+    for i, f in enumerate(frames):
+        Image.fromarray(f).save(d_in / f"frame_{i + 1:04d}.png")
+    assert P.main(["--input_dir", str(d_in), "--output_dir", str(d_out), "--work_dir", str(tmp_path / "w")] + argv) == 0
+    return [np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png")) for i in range(len(frames))]
+
+
+def _decoded(sd, x01, preset):
+    with torch.no_grad():
+        return NO.decode(NO.FORWARDS["johnson"](sd, NO.encode(x01, preset)), preset)
+
+
+def _close(got, ref, frac=0.002):
+    d = np.abs(got.astype(int) - ref.astype(int))
+    assert (d > 1).mean() <= frac, f"{(d > 1).mean():.4%} of values differ by > 1 LSB (max {d.max()})"
+
+
+@pytest.mark.parametrize("variant", ["simple", "advanced", "rotate"])
+def test_cli_region_mode_vs_oracle(tmp_path, variant):
+    """pipeline.py:1720-1839 (fp32): 3 models styled full frame, composited through the region masks, then the
+    LAB EMA (default on) and the save."""
+    cks = _ckpts(tmp_path, [0, 5, 9])
+    h, w = 72, 96
+    frames = synthetic.make_frames(3, h, w, seed=40)
+    argv = ["--model", cks[0][0], "--model_b", cks[1][0], "--model_c", cks[2][0], "--io_preset", "imagenet_255",
+            "--batch", "2"]
+    if variant == "simple":
+        mode, count, seed, feather, oc = "voronoi", 5, 3, 6, 0.3
+        argv += ["--region_mode", mode, "--region_count", "5", "--region_seed", "3", "--region_feather", "6",
+                 "--region_original", "0.3"]
+    elif variant == "advanced":
+        mode, count, seed, feather, oc = "grid", 3, 8, 8, 0.0  # region_count defaults to 1+B+C+D = 3
+        argv += ["--region_mode", mode, "--region_seed", "8", "--region_feather", "8", "--region_blend_spec",
+                 "A+B|C|O|B:0.2+C", "--region_scales", "1.0,0.5", "--no-smooth_lightness"]
+    else:
+        mode, count, seed, feather, oc = "diagonal", 3, None, 10, 0.0
+        argv += ["--region_mode", mode, "--region_rotate", "7.5", "--region_feather", "10",
+                 "--region_assignment", "sequential"]
+        seed = 42  # rotating without a seed: fixed 42 (pipeline.py:1742-1743)
+    got = _run_dir(tmp_path, frames, argv)
+    base = O.feather(O.masks_from_geometry(R.draw_geometry(h, w, mode, count, seed), h, w), feather)
+    ema = NO.LabEMA(variant != "advanced", 0.7)
+    for i, fr in enumerate(frames):
+        x01 = NO.to_tensor01(fr[None])
+        outs = [_decoded(sd, x01, "imagenet_255")[0] for _, sd in cks]
+        orig = x01[0]
+        if variant == "advanced":
+            cf = R.parse_region_configs(count, 3, "random", "A+B|C|O|B:0.2+C", "1.0,0.5", seed, 0.0)
+            half = [torch.nn.functional.interpolate(o[None], size=(int(h * 0.5), int(w * 0.5)), mode="bilinear",
+                                                    align_corners=False)[0] for o in outs]
+            out01 = O.composite_adv({1.0: outs, 0.5: half}, base, cf, orig, h, w)
+        else:
+            masks = base
+            asn = R.assign_models_to_regions(count, 3, "sequential" if variant == "rotate" else "random", None, seed, oc)
+            if variant == "rotate":
+                masks = O.feather(O.rotate(base, (i + 1) * 7.5), feather // 2)
+            cf = [R.RegionConfig([a], [1.0], 1.0) for a in asn]
+            out01 = O.composite_adv({1.0: outs}, masks, cf, orig if oc > 0 else None, h, w)
+        ref = ema(NO.to_pil_u8(out01[None])[0])
+        _close(got[i], ref)
+
+
+def test_cli_region_optimize_vs_oracle(tmp_path):
+    """pipeline.py:1120-1407 (fp32): per-region crops (padding 8) styled by the models of each region's blend,
+    scales 1.0 / 0.5, blend animation, composite_from_crops with the original; then the LAB EMA."""
+    cks = _ckpts(tmp_path, [1, 6])
+    h, w = 80, 112
+    frames = synthetic.make_frames(3, h, w, seed=41)
+    spec, scales, anim = "A|B|A+B|O+A", "1.0,0.5", "30,triangle"
+    got = _run_dir(tmp_path, frames, ["--model", cks[0][0], "--model_b", cks[1][0], "--io_preset", "imagenet_255",
+                                      "--region_optimize", "--region_mode", "fractal", "--region_count", "4",
+                                      "--region_padding", "8", "--region_blend_spec", spec, "--region_scales", scales,
+                                      "--blend_animate", anim, "--region_feather", "6", "--batch", "3"])
+    masks = O.feather(O.masks_from_geometry(R.draw_geometry(h, w, "fractal", 4, 42), h, w), 6)
+    cf = R.parse_region_configs(masks.shape[0], 2, "random", spec, scales, 42, 0.0)
+    boxes = []
+    for k in range(masks.shape[0]):
+        x1, y1, x2, y2 = O.bbox(masks[k])
+        boxes.append((max(0, x1 - 8), max(0, y1 - 8), min(w, x2 + 8), min(h, y2 + 8)))
+    anims = R.parse_region_blend_animations(anim, len(cf))
+    ema = NO.LabEMA(True, 0.7)
+    for i, fr in enumerate(frames):
+        x01 = NO.to_tensor01(fr[None])
+        styled = {}
+        for k, ((x1, y1, x2, y2), c) in enumerate(zip(boxes, cf)):
+            crop = x01[:, :, y1:y2, x1:x2]
+            ch, cw = y2 - y1, x2 - x1
+            if c.scale < 1.0:
+                crop = torch.nn.functional.interpolate(crop, size=(max(1, int(ch * c.scale)), max(1, int(cw * c.scale))),
+                                                       mode="bilinear", align_corners=False)
+            for mi in c.model_indices:
+                if mi < 0:
+                    continue
+                o = _decoded(cks[mi][1], crop, "imagenet_255")
+                if c.scale < 1.0:
+                    o = torch.nn.functional.interpolate(o, size=(ch, cw), mode="bilinear", align_corners=False)
+                styled.setdefault(mi, {})[k] = o[0]
+        wts = [R.compute_animated_weights(c.model_weights, i + 1, anims[k]) for k, c in enumerate(cf)]
+        out01 = O.composite_crops(styled, boxes, cf, masks, x01[0], h, w, wts)
+        _close(got[i], ema(NO.to_pil_u8(out01[None])[0]))
