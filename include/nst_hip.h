@@ -370,6 +370,19 @@ int nst_region_feather(float* masks, int k, int h, int w, const float* taps, int
  * (OpenCV's fixed-point warp restated: cv2 absent, parity unpinned), then each pixel divided by the sum of
  * the rotated planes clamped to 1e-6.  in != out. */
 int nst_region_rotate(const float* in, int k, int h, int w, double angle_deg, float* out, void* stream);
+/*
+ * warp_all_masks_organic (:737-810, --region_morph) of k planes: each plane j warped by cv2.remap(INTER_LINEAR,
+ * BORDER_REFLECT; OpenCV's fixed-point remap restated, cv2 absent: parity unpinned) through
+ * x + flow_x * max_disp, y + flow_y * max_disp, flows per mode (0 blob, 1 tentacle, 2 wave, 3 pulse; :688-715;
+ * frequency is the noise frequency the mode uses, i.e. 2x for tentacle); blob/tentacle fields are
+ * _simplex_noise_2d (:604-652) with the numpy PCG64 draws * 1000 in offsets[((j*2 + field)*2 + octave)*2 + xy]
+ * (field 0 seeded morph.seed + 100 j, field 1 that + 1000); then the coverage-gap dilations (5/11/21/41 where
+ * the sum < 0.1) and the normalisation by the clamped sum.  in != out.
+ */
+int nst_region_morph_scratch_floats(int k, int h, int w, size_t* out);
+int nst_region_morph(const float* in, int k, int h, int w, int mode, double frequency, double time_offset,
+                     double max_disp, const double* offsets, float* out, float* scratch, size_t scratch_floats,
+                     void* stream);
 /* compute_mask_bbox (:1969-1994): bbox[4k..4k+3] = {x1, y1, x2, y2} (exclusive ends) of the values >
  * threshold in plane k, device int buffer; an empty plane leaves {INT_MAX, INT_MAX, -1, -1}. */
 int nst_region_bbox(const float* masks, int k, int h, int w, float threshold, int* bbox, void* stream);

@@ -41,7 +41,8 @@ EXPORTED_SYMBOLS = (
     "nst_seg_mask_scratch_bytes", "nst_seg_mask", "nst_resize_create", "nst_resize_destroy",
     "nst_resize_scratch_bytes", "nst_resize_u8", "nst_blend_mask8_u8",
     "nst_region_masks", "nst_region_feather", "nst_region_rotate", "nst_region_bbox", "nst_region_scratch_floats",
-    "nst_region_composite_u8", "nst_region_crop_input", "nst_region_resize",
+    "nst_region_composite_u8", "nst_region_crop_input", "nst_region_resize", "nst_region_morph",
+    "nst_region_morph_scratch_floats",
 )
 # region compositor limits / geometry kinds (include/nst_hip.h NST_REGION_*, NST_RG_*)
 NST_REGION_MAX, NST_REGION_TERMS, NST_REGION_MAX_SRC = 32, 9, 16
@@ -149,12 +150,16 @@ def lib() -> ctypes.CDLL:
         L.nst_region_feather.argtypes = [vp, i, i, i, pf, i, vp, vp]
         L.nst_region_rotate.argtypes = [vp, i, i, i, ctypes.c_double, vp, vp]
         L.nst_region_bbox.argtypes = [vp, i, i, i, f, vp, vp]
+        dbl = ctypes.c_double
+        L.nst_region_morph_scratch_floats.argtypes = [i, i, i, ctypes.POINTER(sz)]
+        L.nst_region_morph.argtypes = [vp, i, i, i, i, dbl, dbl, dbl, pd, vp, vp, sz, vp]
         L.nst_region_scratch_floats.argtypes = [i, i, i, i, i, ctypes.POINTER(sz)]
         L.nst_region_composite_u8.argtypes = [ctypes.POINTER(vp), pi, pi, i, pi, pi, pf, i, pi, vp, vp, i, i, i, vp,
                                               sz, vp, vp, vp]
         L.nst_region_crop_input.argtypes = [vp, i, i, i, pi, i, i, vp, vp]
         L.nst_region_resize.argtypes = [vp, i, i, i, i, i, i, i, i, vp, vp]
         for name in ("nst_region_masks", "nst_region_feather", "nst_region_rotate", "nst_region_bbox",
+                     "nst_region_morph", "nst_region_morph_scratch_floats",
                      "nst_region_scratch_floats", "nst_region_composite_u8", "nst_region_crop_input",
                      "nst_region_resize"):
             getattr(L, name).restype = i

@@ -810,14 +810,33 @@ __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int 
     }
 }
 
-// G = (sum over the K slices, in slice order) / (c*hw)
-__global__ void gram_reduce_kernel(const float* __restrict__ part, int slices, size_t slice_stride, float denom,
-                                   float* __restrict__ G) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= slice_stride) return;
-  float s = part[i];
-  for (int k = 1; k < slices; ++k) s += part[(size_t)k * slice_stride + i];
-  G[i] = s / denom;
+// G = (sum over the K slices) / (c*hw), in a fixed order (bit-identical across runs): a 1024-thread block owns 64
+// consecutive entries; its 16 lane groups each sum a contiguous 1/16 of the slices with four interleaved
+// accumulators (independent loads in flight: the slices are read at HBM rate instead of one dependent load at a
+// time), combined ((a0 + a1) + (a2 + a3)), then the 16 group sums are added in group order.
+__global__ __launch_bounds__(1024) void gram_reduce_kernel(const float* __restrict__ part, int slices,
+                                                           size_t slice_stride, float denom, float* __restrict__ G) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const size_t e = (size_t)blockIdx.x * 64 + lane;
+  const int per = (slices + 15) / 16;
+  const int s0 = grp * per, s1 = min(slices, s0 + per);
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (e < slice_stride) {
+    int sidx = s0;
+    for (; sidx + 4 <= s1; sidx += 4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += part[(size_t)(sidx + j) * slice_stride + e];
+    }
+    for (int j = 0; sidx < s1; ++sidx, ++j) a[j] += part[(size_t)sidx * slice_stride + e];
+  }
+  red[grp][lane] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (grp == 0 && e < slice_stride) {
+    float t = red[0][lane];
+    for (int g = 1; g < 16; ++g) t += red[g][lane];
+    G[e] = t / denom;
+  }
 }
 
 namespace {
@@ -831,7 +850,10 @@ GramPlan gram_plan(int n, int c, int hw) {
   g.tt = (c + g.ti - 1) / g.ti;
   const int blocks = g.tt * g.tt * n;
   const int fills = (hw + 63) / 64;
-  g.slices = std::max(1, std::min(fills, (512 + blocks - 1) / blocks));
+  // enough K slices to fill the chip (~512 workgroups), but their fp32 partials (c*c*4 B each) no more than
+  // twice the bytes of F itself: beyond that the split-K traffic costs more than the parallelism gains
+  const int cap = std::max(1, (int)(((size_t)2 * 2 * hw) / ((size_t)4 * c)));
+  g.slices = std::max(1, std::min(std::min(fills, cap), (512 + blocks - 1) / blocks));
   g.kslice = ((fills + g.slices - 1) / g.slices) * 64;
   g.slices = (hw + g.kslice - 1) / g.kslice;
   g.ws_bytes = g.slices > 1 ? (size_t)g.slices * n * c * c * sizeof(float) : 0;
@@ -876,7 +898,7 @@ hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, i
 #undef NST_GRAM_GO
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((slice + 255) / 256)), dim3(256), 0, st, dst, g.slices, slice,
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((slice + 63) / 64)), dim3(1024), 0, st, dst, g.slices, slice,
                      denom, G);
   return hipGetLastError();
 }

@@ -115,6 +115,34 @@ int nst_region_rotate(const float* in, int k, int h, int w, double angle_deg, fl
   return NST_OK;
 }
 
+int nst_region_morph_scratch_floats(int k, int h, int w, size_t* out) {
+  if (k <= 0 || k > RG_MAX || h <= 0 || w <= 0 || !out) {
+    set_error("nst_region_morph_scratch_floats: invalid arguments");
+    return NST_E_INVALID;
+  }
+  *out = 3 * (size_t)k * h * w + (size_t)4 * k * 1024 + 4 * (size_t)k + 16;
+  return NST_OK;
+}
+
+int nst_region_morph(const float* in, int k, int h, int w, int mode, double frequency, double time_offset,
+                     double max_disp, const double* offsets, float* out, float* scratch, size_t scratch_floats,
+                     void* stream) {
+  size_t need = 0;
+  if (!in || !out || in == out || !offsets || mode < 0 || mode > 3 || nst_region_morph_scratch_floats(k, h, w, &need) ||
+      !scratch || scratch_floats < need) {
+    set_error("nst_region_morph: invalid arguments (scratch: nst_region_morph_scratch_floats)");
+    return NST_E_INVALID;
+  }
+  MorphDevHost m = {};
+  m.mode = mode; m.k = k; m.freq = frequency; m.t = time_offset; m.max_disp = max_disp;
+  for (int j = 0; j < k; ++j)
+    for (int f = 0; f < 2; ++f)
+      for (int o = 0; o < 2; ++o)
+        for (int c = 0; c < 2; ++c) m.off[j][f][o][c] = offsets[((j * 2 + f) * 2 + o) * 2 + c];
+  RG_LAUNCH(launch_region_morph(m, in, h, w, out, scratch, (hipStream_t)stream), "region_morph");
+  return NST_OK;
+}
+
 int nst_region_bbox(const float* masks, int k, int h, int w, float threshold, int* bbox, void* stream) {
   if (!masks || !bbox || k <= 0 || k > 64 || h <= 0 || w <= 0) {
     set_error("nst_region_bbox: invalid arguments");

@@ -60,6 +60,13 @@ hipError_t launch_region_crops(const RegionSrcSet& ss, const RegionTermsDev& t, 
                                float* out_f32, hipStream_t st);
 hipError_t launch_region_crop_input(const uint8_t* frames, int n, int h, int w, int x1, int y1, int x2, int y2,
                                     int oh, int ow, float* out, hipStream_t st);
+struct MorphDevHost {
+  int mode, k;
+  double freq, t, max_disp;
+  double off[RG_MAX][2][2][2];
+};
+hipError_t launch_region_morph(const MorphDevHost& m, const float* in, int h, int w, float* out, float* scratch,
+                               hipStream_t st);
 hipError_t launch_region_resize_fit(const RegionSrcDev& s, int n, int fh, int fw, int oh, int ow, float* out,
                                     hipStream_t st);
 

@@ -583,3 +583,231 @@ hipError_t launch_region_resize_fit(const RegionSrcDev& s, int n, int fh, int fw
 }
 
 }  // namespace nst
+
+namespace nst {
+
+// ---------------------------------------------------------------------------------------
+// --region_morph (warp_all_masks_organic, region_blend.py:535-810).
+// Noise fields (_simplex_noise_2d, :604-652): per octave o (two per field) the float64 sum
+//   sin(xx*fm + ox) * cos(yy*fm + oy) + sin((xx+yy)*fm*0.7 + ox*0.8)*0.5 + cos((xx-yy)*fm*0.5 + oy*0.6)*0.3
+// added into a float32 accumulator (numpy's in-place float32 += float64), xx/yy = linspace(0, frequency, W/H),
+// the random offsets drawn on the host from numpy's PCG64 in the reference's order; then / total amplitude and
+// the min/max normalisation in float32.  Masks are then remapped (cv2.remap INTER_LINEAR, BORDER_REFLECT,
+// restated: 1/32-pixel fixed point from cvRound(map * 32), float weight table) by x + flow_x*max_disp.
+struct MorphDev {
+  int mode;  // 0 blob, 1 tentacle, 2 wave, 3 pulse
+  int k;
+  double freq, t, max_disp, step_x, step_y;  // linspace steps of the noise grid (frequency / (n - 1))
+  double off[RG_MAX][2][2][2];               // [mask][field x/y][octave][offset x/y]
+};
+
+__device__ __forceinline__ double lin(int i, int n, double step, double stop) {
+  return i == n - 1 ? stop : (double)i * step;  // numpy.linspace(0, stop, n)
+}
+
+__global__ __launch_bounds__(256) void morph_noise_kernel(MorphDev m, int h, int w, float* __restrict__ raw,
+                                                          float2* __restrict__ part) {
+  __shared__ float smin[256], smax[256];
+  const size_t hw = (size_t)h * w;
+  const int kf = blockIdx.y;  // mask k, field f
+  const int k = kf >> 1, f = kf & 1;
+  const double tf = f ? m.t * 1.3 : m.t;  // _generate_flow_field: the y field runs at time_offset * 1.3
+  float mn = INFINITY, mx = -INFINITY;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < hw; i += (size_t)gridDim.x * 256) {
+    const int x = (int)(i % w), y = (int)(i / w);
+    const double xx = lin(x, w, m.step_x, m.freq), yy = lin(y, h, m.step_y, m.freq);
+    float acc = 0.f;
+    double amp = 1.0, fm = 1.0;
+    for (int o = 0; o < 2; ++o) {
+      const double ox = tf * (0.5 + 0.3 * o) + m.off[k][f][o][0];
+      const double oy = tf * (0.3 + 0.2 * o) + m.off[k][f][o][1];
+      double nz = sin(xx * fm + ox) * cos(yy * fm + oy);
+      nz = nz + sin((xx + yy) * fm * 0.7 + ox * 0.8) * 0.5;
+      nz = nz + cos((xx - yy) * fm * 0.5 + oy * 0.6) * 0.3;
+      acc = (float)((double)acc + nz * amp);
+      amp *= 0.5;
+      fm *= 2.0;
+    }
+    acc = acc / 1.5f;  // total amplitude 1 + 0.5
+    raw[(size_t)kf * hw + i] = acc;
+    mn = fminf(mn, acc);
+    mx = fmaxf(mx, acc);
+  }
+  smin[threadIdx.x] = mn;
+  smax[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + s]);
+      smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[(size_t)kf * gridDim.x + blockIdx.x] = make_float2(smin[0], smax[0]);
+}
+
+__global__ __launch_bounds__(256) void morph_minmax_kernel(const float2* __restrict__ part, int nb,
+                                                           float2* __restrict__ mm) {
+  __shared__ float smin[256], smax[256];
+  const int kf = blockIdx.x;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    mn = fminf(mn, part[(size_t)kf * nb + i].x);
+    mx = fmaxf(mx, part[(size_t)kf * nb + i].y);
+  }
+  smin[threadIdx.x] = mn;
+  smax[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + s]);
+      smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) mm[kf] = make_float2(smin[0], smax[0]);
+}
+
+__device__ __forceinline__ int reflect_cv(int p, int n) {  // cv2 BORDER_REFLECT: fedcba|abcdefgh|hgfedcb
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) p = p < 0 ? -p - 1 : 2 * n - p - 1;
+  return p;
+}
+
+// cv2.remap(src, map_x, map_y, INTER_LINEAR, BORDER_REFLECT) at one pixel
+__device__ __forceinline__ float remap_reflect(const float* src, int h, int w, float mx, float my) {
+  const int X = (int)rintf(mx * 32.f), Y = (int)rintf(my * 32.f);
+  const int sx = X >> 5, sy = Y >> 5;
+  const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);
+  const float w00 = (1.f - fy) * (1.f - fx), w01 = (1.f - fy) * fx, w10 = fy * (1.f - fx), w11 = fy * fx;
+  const int x0 = reflect_cv(sx, w), x1 = reflect_cv(sx + 1, w), y0 = reflect_cv(sy, h), y1 = reflect_cv(sy + 1, h);
+  const float t0 = src[(size_t)y0 * w + x0] * w00 + src[(size_t)y0 * w + x1] * w01;
+  const float t1 = src[(size_t)y1 * w + x0] * w10 + src[(size_t)y1 * w + x1] * w11;
+  return t0 + t1;
+}
+
+__global__ __launch_bounds__(256) void morph_warp_kernel(MorphDev m, const float* __restrict__ in, int h, int w,
+                                                         const float* __restrict__ raw, const float2* __restrict__ mm,
+                                                         float* __restrict__ out) {
+  const size_t hw = (size_t)h * w;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= hw) return;
+  const int x = (int)(i % w), y = (int)(i / w);
+  for (int k = 0; k < m.k; ++k) {
+    float mapx, mapy;
+    if (m.mode <= 1) {  // blob / tentacle: float32 noise fields
+      float fl[2];
+      for (int f = 0; f < 2; ++f) {
+        const float2 r = mm[2 * k + f];
+        const float v = (raw[(size_t)(2 * k + f) * hw + i] - r.x) / ((r.y - r.x) + 1e-6f);
+        fl[f] = (v * 2.f) - 1.f;
+      }
+      if (m.mode == 1) {  // flow_y += sin(linspace(0, 1, H) * pi * 3 + t) * 0.5 (float64, stored float32)
+        const double yl = lin(y, h, h > 1 ? 1.0 / (double)(h - 1) : 0.0, 1.0);
+        fl[1] = (float)((double)fl[1] + sin(yl * M_PI * 3.0 + m.t) * 0.5);
+      }
+      const float md = (float)m.max_disp;
+      mapx = (float)x + fl[0] * md;
+      mapy = (float)y + fl[1] * md;
+    } else {  // wave / pulse: float64 fields
+      double fx, fy;
+      if (m.mode == 2) {
+        const double sy = h > 1 ? M_PI * m.freq / (double)(h - 1) : 0.0, sx = w > 1 ? M_PI * m.freq / (double)(w - 1) : 0.0;
+        fx = sin(lin(y, h, sy, M_PI * m.freq) + m.t * 2.0);
+        fy = cos(lin(x, w, sx, M_PI * m.freq) + m.t * 1.5);
+      } else {
+        const double yc = (double)(y - h / 2), xc = (double)(x - w / 2);
+        const double r = sqrt(xc * xc + yc * yc) + 1e-6, th = atan2(yc, xc);
+        const double pu = sin(r * 0.05 - m.t * 3.0) * 0.5 + 0.5;
+        fx = cos(th) * pu;
+        fy = sin(th) * pu;
+      }
+      mapx = (float)((double)(float)x + fx * m.max_disp);
+      mapy = (float)((double)(float)y + fy * m.max_disp);
+    }
+    out[(size_t)k * hw + i] = remap_reflect(in + (size_t)k * hw, h, w, mapx, mapy);
+  }
+}
+
+// gap fill + normalisation of the warped set (region_blend.py:768-810): four max-pool dilations (5, 11, 21,
+// 41) applied only where the fp32 sum of the planes is < 0.1 (a pass with no gap changes nothing, so all run),
+// then each plane / clamp(sum, 1e-6)
+__global__ __launch_bounds__(256) void planes_rowmax_kernel(const float* __restrict__ in, int h, int w, int r,
+                                                            float* __restrict__ out) {
+  const size_t plane = (size_t)blockIdx.z * h * w;
+  const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+  if (x >= w) return;
+  const float* row = in + plane + (size_t)y * w;
+  float m = -INFINITY;
+  for (int j = max(0, x - r); j <= min(w - 1, x + r); ++j) m = fmaxf(m, row[j]);
+  out[plane + (size_t)y * w + x] = m;
+}
+
+__global__ __launch_bounds__(256) void planes_fill_kernel(const float* __restrict__ cur, const float* __restrict__ rmax,
+                                                          int k, int h, int w, int r, float* __restrict__ nxt) {
+  const size_t hw = (size_t)h * w;
+  const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+  if (x >= w) return;
+  const size_t p = (size_t)y * w + x;
+  float s = 0.f;
+  for (int j = 0; j < k; ++j) s = s + cur[(size_t)j * hw + p];
+  const float gap = s < 0.1f ? 1.f : 0.f;
+  for (int j = 0; j < k; ++j) {
+    const float* col = rmax + (size_t)j * hw + x;
+    float m = -INFINITY;
+    for (int q = max(0, y - r); q <= min(h - 1, y + r); ++q) m = fmaxf(m, col[(size_t)q * w]);
+    const float v = cur[(size_t)j * hw + p];
+    nxt[(size_t)j * hw + p] = (v * (1.f - gap)) + (m * gap);
+  }
+}
+
+__global__ __launch_bounds__(256) void planes_normalize_kernel(float* __restrict__ m, int k, size_t hw) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= hw) return;
+  float s = 0.f;
+  for (int j = 0; j < k; ++j) s = s + m[(size_t)j * hw + i];
+  s = fmaxf(s, 1e-6f);
+  for (int j = 0; j < k; ++j) m[(size_t)j * hw + i] = m[(size_t)j * hw + i] / s;
+}
+
+// scratch: 2*k*hw floats (noise) + 2*k*1024 float2 + 2*k float2 + 2*k*hw floats (ping-pong planes)
+hipError_t launch_region_morph(const MorphDevHost& mh, const float* in, int h, int w, float* out, float* scratch,
+                               hipStream_t st) {
+  MorphDev m;
+  m.mode = mh.mode; m.k = mh.k; m.freq = mh.freq; m.t = mh.t; m.max_disp = mh.max_disp;
+  m.step_x = w > 1 ? mh.freq / (double)(w - 1) : 0.0;
+  m.step_y = h > 1 ? mh.freq / (double)(h - 1) : 0.0;
+  for (int j = 0; j < mh.k; ++j)
+    for (int f = 0; f < 2; ++f)
+      for (int o = 0; o < 2; ++o)
+        for (int c = 0; c < 2; ++c) m.off[j][f][o][c] = mh.off[j][f][o][c];
+  const size_t hw = (size_t)h * w;
+  const int k = mh.k;
+  float* raw = scratch;
+  float2* part = (float2*)(scratch + 2 * (size_t)k * hw);
+  float2* mm = part + (size_t)2 * k * 1024;
+  float* a = (float*)(mm + 2 * k);
+  const int nb = (int)std::min<size_t>(1024, (hw + 255) / 256);
+  if (m.mode <= 1) {
+    hipLaunchKernelGGL(morph_noise_kernel, dim3(nb, 2 * k), dim3(256), 0, st, m, h, w, raw, part);
+    hipLaunchKernelGGL(morph_minmax_kernel, dim3(2 * k), dim3(256), 0, st, part, nb, mm);
+  }
+  const dim3 g1((unsigned)((hw + 255) / 256));
+  hipLaunchKernelGGL(morph_warp_kernel, g1, dim3(256), 0, st, m, in, h, w, raw, mm, out);
+  // dilation passes: out -> (raw: row max) -> a -> ... ending in out
+  const int radii[4] = {2, 5, 10, 20};
+  float* bufs[2] = {a, out};
+  const float* cur = out;
+  for (int it = 0; it < 4; ++it) {
+    hipLaunchKernelGGL(planes_rowmax_kernel, dim3((unsigned)((w + 255) / 256), (unsigned)h, (unsigned)k), dim3(256), 0,
+                       st, cur, h, w, radii[it], raw);
+    float* nxt = bufs[it & 1];
+    hipLaunchKernelGGL(planes_fill_kernel, dim3((unsigned)((w + 255) / 256), (unsigned)h), dim3(256), 0, st, cur, raw,
+                       k, h, w, radii[it], nxt);
+    cur = nxt;
+  }
+  hipLaunchKernelGGL(planes_normalize_kernel, g1, dim3(256), 0, st, out, k, hw);
+  return hipGetLastError();
+}
+
+}  // namespace nst

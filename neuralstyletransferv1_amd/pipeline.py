@@ -21,8 +21,7 @@ restated, parity unpinned because cv2 is absent here).
 Region blending (--region_mode / --region_optimize and their spec, animation and rotation flags,
 pipeline.py:1120-1407, 1720-1839) runs on the GPU compositor of regions.py.
 
-Not built (rejected with a clear message if requested): --region_morph's organic
-warp, optical-flow EMA / motion blend (--flow_ema, --motion_blend), Magenta (TF-Hub) and Torch7 (OpenCV
+Not built (rejected with a clear message if requested): optical-flow EMA / motion blend (--flow_ema, --motion_blend), Magenta (TF-Hub) and Torch7 (OpenCV
 DNN) backends.
 """
 from __future__ import annotations
@@ -164,8 +163,6 @@ def reject_out_of_scope(args) -> None:
                                              or str(getattr(args, f"model_{s}")).lower() in ("magenta",)
                                              or str(getattr(args, f"model_{s}")).endswith(".t7")):
             bad.append(f"--model_{s} (magenta/torch7)")
-    if args.region_morph and str(args.region_morph).lower() not in ("none", "off", "0", "static"):
-        bad.append("--region_morph (organic cv2.remap warp)")
     if args.flow_ema or args.motion_blend:
         bad.append("--flow_ema/--motion_blend")
     if args.device != "cuda":

@@ -15,8 +15,9 @@ Split of the work:
       rotation, bounding boxes, crop inputs, low-resolution sources and both composites (ToPILImage
       truncation fused).  No CPU fallback.
 
-Not built: --region_morph's organic warp (cv2.remap of noise-displaced masks, region_blend.py:670-810) is
-rejected loudly; its morph-spec parsing is here so the flag is validated like the reference's.
+--region_morph's organic warp (region_blend.py:535-810) runs on the GPU too: the noise fields' numpy PCG64
+draws are made here in the reference's order, the fields, cv2.remap (restated: cv2 is absent, parity
+unpinned), the gap dilations and the renormalisation in region_ops.hip.
 """
 from __future__ import annotations
 
@@ -511,6 +512,42 @@ def feather_planes(masks: torch.Tensor, feather: int) -> torch.Tensor:
     return masks
 
 
+_MORPH_KIND = {"blob": 0, "tentacle": 1, "wave": 2, "pulse": 3}
+
+
+def morph_offsets(morph: MorphAnimation, k: int) -> np.ndarray:
+    """The random offsets of _simplex_noise_2d (region_blend.py:620-635) for warp_all_masks_organic's k planes:
+    plane j seeds morph.seed + 100 j (field x) and that + 1000 (field y); per octave rng.random() * 1000 for x
+    then y -> float64 [k][2][2][2]."""
+    off = np.zeros((k, 2, 2, 2), dtype=np.float64)
+    for j in range(k):
+        for f, sd in enumerate((morph.seed + j * 100, morph.seed + j * 100 + 1000)):
+            rng = np.random.default_rng(sd)
+            for o in range(2):
+                off[j, f, o, 0] = rng.random() * 1000
+                off[j, f, o, 1] = rng.random() * 1000
+    return off
+
+
+def morph_planes(masks: torch.Tensor, morph: MorphAnimation, frame_idx: int) -> torch.Tensor:
+    """warp_all_masks_organic (region_blend.py:737-810) -> new planes (the caller re-feathers them)."""
+    if not morph.enabled:
+        return masks
+    K, H, W = masks.shape
+    mode = _MORPH_KIND.get(morph.mode, 0)  # unknown modes take the blob branch (region_blend.py:714)
+    freq = morph.frequency * 2 if mode == 1 else morph.frequency
+    t = frame_idx * morph.speed * 0.02
+    off = morph_offsets(morph, K) if mode <= 1 else np.zeros((K, 2, 2, 2))
+    sz = ctypes.c_size_t()
+    check(lib().nst_region_morph_scratch_floats(K, H, W, ctypes.byref(sz)), "nst_region_morph_scratch_floats")
+    scratch = torch.empty((sz.value,), dtype=torch.float32, device=masks.device)
+    out = torch.empty_like(masks)
+    check(lib().nst_region_morph(masks.data_ptr(), K, H, W, mode, float(freq), float(t), float(max(H, W) * morph.amplitude),
+                                 off.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), out.data_ptr(),
+                                 scratch.data_ptr(), sz.value, _stream(masks.device)), "nst_region_morph")
+    return out
+
+
 def rotate_planes(masks: torch.Tensor, angle_deg: float) -> torch.Tensor:
     """rotate_all_masks (region_blend.py:49-66): warp + renormalise; the angle-0 call returns its input."""
     if angle_deg == 0:
@@ -644,13 +681,11 @@ class RegionCompositor:
         self.rotate = float(getattr(args, "region_rotate", 0.0) or 0.0)
         morph_spec = getattr(args, "region_morph", None)
         self.morph = parse_morph_animation(morph_spec) if morph_spec else MorphAnimation(enabled=False)
-        if self.morph.enabled:
-            raise NstError("--region_morph (organic cv2.remap warp, region_blend.py:670-810) is not built on the MI355X "
-                           "engine")
         self.oc = float(getattr(args, "region_original", 0.0) or 0.0)
         self.blend_spec = getattr(args, "region_blend_spec", None)
         self.scale_spec = getattr(args, "region_scales", None)
-        self.seed = parse_region_seed(getattr(args, "region_seed", None), self.optimized, self.rotate != 0)
+        self.animating = self.rotate != 0 or self.morph.enabled
+        self.seed = parse_region_seed(getattr(args, "region_seed", None), self.optimized, self.animating)
         self.cache: Dict[tuple, tuple] = {}
         self.blend_anims = None
         self.scale_anims = None
@@ -660,6 +695,8 @@ class RegionCompositor:
     def _animate(self, masks, frame_idx):
         if self.rotate != 0:
             masks = feather_planes(rotate_planes(masks, frame_idx * self.rotate), self.feather // 2)
+        if self.morph.enabled:  # region_blend.py:1765-1768
+            masks = feather_planes(morph_planes(masks, self.morph, frame_idx), max(5, self.feather // 4))
         return masks
 
     # ---- standard path: every model styled the whole frame (pipeline.py:1720-1839) ----
@@ -672,7 +709,7 @@ class RegionCompositor:
         n_out = len(raw)
         count = getattr(a, "region_count", None) or num_models_quirk
         assignment = getattr(a, "region_assignment", "random")
-        animating = self.rotate != 0
+        animating = self.animating
         weights = None
         if assignment == "weighted":
             try:
@@ -773,7 +810,7 @@ class RegionCompositor:
         plans, order = {}, []
         static_masks = None
         for j, fid in enumerate(frame_ids):
-            if self.rotate != 0:
+            if self.animating:
                 masks = self._animate(base, fid)
                 boxes = [(max(0, x1 - pad), max(0, y1 - pad), min(W, x2 + pad), min(H, y2 + pad))
                          for x1, y1, x2, y2 in mask_bboxes(masks)]

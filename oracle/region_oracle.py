@@ -215,3 +215,104 @@ def rotate(masks: torch.Tensor, angle_deg: float) -> torch.Tensor:
         s += r
     s = s.clamp(min=1e-6)
     return torch.stack([r / s for r in rot], 0)
+
+
+# ------------------------------------------------------------------ --region_morph (region_blend.py:535-810)
+def simplex_noise(H: int, W: int, frequency: float, octaves: int, seed: int, time_offset: float = 0.0) -> np.ndarray:
+    """_simplex_noise_2d (region_blend.py:604-652): float64 octave sums into a float32 accumulator,
+    normalised to [0, 1] in float32 (pinned by tests/golden/regions.npz flow_*)."""
+    rng = np.random.default_rng(seed)
+    xx, yy = np.meshgrid(np.linspace(0, frequency, W), np.linspace(0, frequency, H))
+    acc = np.zeros((H, W), dtype=np.float32)
+    amp, total, fm = 1.0, 0.0, 1.0
+    for o in range(octaves):
+        ox = time_offset * (0.5 + 0.3 * o) + rng.random() * 1000
+        oy = time_offset * (0.3 + 0.2 * o) + rng.random() * 1000
+        nz = np.sin(xx * fm + ox) * np.cos(yy * fm + oy)
+        nz += np.sin((xx + yy) * fm * 0.7 + ox * 0.8) * 0.5
+        nz += np.cos((xx - yy) * fm * 0.5 + oy * 0.6) * 0.3
+        acc += nz * amp
+        total += amp
+        amp *= 0.5
+        fm *= 2.0
+    acc = acc / total
+    return (acc - acc.min()) / (acc.max() - acc.min() + 1e-6)
+
+
+def flow_field(H: int, W: int, frequency: float, seed: int, t: float):
+    """_generate_flow_field (region_blend.py:655-667)."""
+    return (simplex_noise(H, W, frequency, 2, seed, t) * 2 - 1,
+            simplex_noise(H, W, frequency, 2, seed + 1000, t * 1.3) * 2 - 1)
+
+
+def _remap_reflect(src: np.ndarray, map_x: np.ndarray, map_y: np.ndarray) -> np.ndarray:
+    """cv2.remap(src f32, map_x, map_y, INTER_LINEAR, BORDER_REFLECT) after OpenCV: cvRound(map * 32) fixed point,
+    float weight table, each tap reflected (fedcba|abcdef) -- PARITY UNPINNED (cv2 absent)."""
+    H, W = src.shape
+    X = np.rint(map_x.astype(np.float32) * np.float32(32)).astype(np.int64)
+    Y = np.rint(map_y.astype(np.float32) * np.float32(32)).astype(np.int64)
+    sx, sy = X >> 5, Y >> 5
+    fx = (X & 31).astype(np.float32) * np.float32(1 / 32)
+    fy = (Y & 31).astype(np.float32) * np.float32(1 / 32)
+
+    def refl(p, n):
+        if n == 1:
+            return np.zeros_like(p)
+        p = p.copy()
+        for _ in range(4):
+            p = np.where(p < 0, -p - 1, p)
+            p = np.where(p >= n, 2 * n - p - 1, p)
+        return p
+    x0, x1, y0, y1 = refl(sx, W), refl(sx + 1, W), refl(sy, H), refl(sy + 1, H)
+    one = np.float32(1)
+    t0 = src[y0, x0] * ((one - fy) * (one - fx)) + src[y0, x1] * ((one - fy) * fx)
+    t1 = src[y1, x0] * (fy * (one - fx)) + src[y1, x1] * (fy * fx)
+    return (t0 + t1).astype(np.float32)
+
+
+def morph(masks: torch.Tensor, mode: str, speed: float, amplitude: float, frequency: float, seed: int,
+          frame_idx: int) -> torch.Tensor:
+    """warp_all_masks_organic (region_blend.py:737-810) with warp_mask_organic (:670-734) per plane."""
+    K, H, W = masks.shape
+    t = frame_idx * speed * 0.02
+    warped = []
+    for j in range(K):
+        sd = seed + j * 100
+        if mode == "tentacle":
+            fx, fy = flow_field(H, W, frequency * 2, sd, t)
+            fy += np.sin(np.linspace(0, 1, H)[:, None] * np.pi * 3 + t) * 0.5
+        elif mode == "wave":
+            fx = np.sin(np.linspace(0, np.pi * frequency, H)[:, None] + t * 2) * np.ones((H, W))
+            fy = np.cos(np.linspace(0, np.pi * frequency, W)[None, :] + t * 1.5) * np.ones((H, W))
+        elif mode == "pulse":
+            yc, xc = np.arange(H)[:, None] - H // 2, np.arange(W)[None, :] - W // 2
+            r = np.sqrt(xc ** 2 + yc ** 2) + 1e-6
+            th = np.arctan2(yc, xc)
+            pu = np.sin(r * 0.05 - t * 3) * 0.5 + 0.5
+            fx, fy = np.cos(th) * pu, np.sin(th) * pu
+        else:
+            fx, fy = flow_field(H, W, frequency, sd, t)
+        md = max(H, W) * amplitude
+        fx, fy = fx * md, fy * md
+        gy = np.arange(H, dtype=np.float32)[:, None].repeat(W, axis=1)
+        gx = np.arange(W, dtype=np.float32)[None, :].repeat(H, axis=0)
+        warped.append(torch.from_numpy(_remap_reflect(masks[j].numpy(), (gx + fx).astype(np.float32),
+                                                      (gy + fy).astype(np.float32))))
+    s = torch.zeros(H, W)
+    for m in warped:
+        s += m
+    gap = (s < 0.1).float()
+    if gap.sum() > 0:
+        filled = list(warped)
+        for ks in (5, 11, 21, 41):
+            nf = [m * (1 - gap) + F.max_pool2d(m[None, None], ks, 1, ks // 2)[0, 0] * gap for m in filled]
+            s = torch.zeros(H, W)
+            for m in nf:
+                s += m
+            gap = (s < 0.1).float()
+            filled = nf
+            if gap.sum() == 0:
+                break
+        warped = filled
+    s = s.clamp(min=1e-6)
+    return torch.stack([m / s for m in warped], 0)

@@ -296,3 +296,40 @@ def test_cli_region_optimize_vs_oracle(tmp_path):
         wts = [R.compute_animated_weights(c.model_weights, i + 1, anims[k]) for k, c in enumerate(cf)]
         out01 = O.composite_crops(styled, boxes, cf, masks, x01[0], h, w, wts)
         _close(got[i], ema(NO.to_pil_u8(out01[None])[0]))
+
+
+@pytest.mark.parametrize("mode", ["blob", "tentacle", "wave", "pulse"])
+@pytest.mark.parametrize("hw", [(45, 80), (270, 480)])
+def test_morph_vs_restatement(mode, hw):
+    """warp_all_masks_organic on the GPU vs the oracle (numpy noise pinned by the goldens; cv2.remap restated:
+    parity unpinned).  float64 libm differences can move a remap coordinate across a 1/32-pixel step: a few
+    pixels may differ beyond float rounding."""
+    h, w = hw
+    _, m = gpu_masks("voronoi", 4, 3, 4, h, w)
+    morph = R.MorphAnimation(enabled=True, mode=mode, speed=1.5, amplitude=0.12, frequency=3.0)
+    got = R.morph_planes(m.to(DEV), morph, 7).cpu()
+    ref = O.morph(m, mode, 1.5, 0.12, 3.0, 42, 7)
+    d = (got - ref).abs()
+    assert float((d > 2e-6).float().mean()) < 1e-3, (mode, float(d.max()))
+    assert torch.allclose(got.sum(0), torch.ones(h, w), atol=1e-5)
+
+
+def test_cli_region_morph_vs_oracle(tmp_path):
+    """--region_morph blob with --region_rotate (standard path): masks rotated then warped then re-feathered
+    per frame (region_blend.py:1757-1768)."""
+    cks = _ckpts(tmp_path, [2, 7])
+    h, w = 64, 96
+    frames = synthetic.make_frames(2, h, w, seed=43)
+    got = _run_dir(tmp_path, frames, ["--model", cks[0][0], "--model_b", cks[1][0], "--io_preset", "imagenet_255",
+                                      "--region_mode", "concentric", "--region_count", "3", "--region_feather", "12",
+                                      "--region_rotate", "3", "--region_morph", "1.5,0.1,2.0,blob",
+                                      "--region_assignment", "sequential", "--no-smooth_lightness"])
+    base = O.feather(O.masks_from_geometry(R.draw_geometry(h, w, "concentric", 3, 42), h, w), 12)
+    for i, fr in enumerate(frames):
+        x01 = NO.to_tensor01(fr[None])
+        outs = [_decoded(sd, x01, "imagenet_255")[0] for _, sd in cks]
+        masks = O.feather(O.rotate(base, (i + 1) * 3.0), 6)
+        masks = O.feather(O.morph(masks, "blob", 1.5, 0.1, 2.0, 42, i + 1), 5)
+        cf = [R.RegionConfig([a], [1.0], 1.0) for a in R.assign_models_to_regions(3, 2, "sequential", None, 42, 0.0)]
+        out01 = O.composite_adv({1.0: outs}, masks, cf, None, h, w)
+        _close(got[i], NO.to_pil_u8(out01[None])[0], frac=0.01)

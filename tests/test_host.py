@@ -27,7 +27,7 @@ def test_cli_defaults_match_reference():
         True, 0.7, 1.0, "auto", "png", 85, 4, "keep", "input", "transformer", 0.85)
 
 
-@pytest.mark.parametrize("extra", [["--region_mode", "grid", "--region_morph", "blob"], ["--flow_ema"], ["--model_type", "magenta"],
+@pytest.mark.parametrize("extra", [["--flow_ema"], ["--model_type", "magenta"],
                                    ["--device", "cpu"], ["--motion_blend"]])
 def test_out_of_scope_requests_fail_loudly(extra, tmp_path):
     args = P.build_parser().parse_args(["--model", "x.pth", "--synthetic", "64x48"] + extra)

@@ -160,3 +160,25 @@ def test_rotation_restatement_properties():
     assert torch.allclose(s, torch.ones_like(s), atol=1e-5)
     back = O.rotate(masks, 360.0)
     assert (back - masks / masks.sum(0).clamp(min=1e-6)).abs().max() < 1e-5
+
+
+def test_morph_noise_fields_bit_exact():
+    fx, fy = O.flow_field(H, W, 3.0, 42, 3 * 1.0 * 0.02)
+    assert np.array_equal(np.stack([fx, fy]).astype(np.float32), G["flow_blob"])
+    fx, fy = O.flow_field(H, W, 6.0, 142, 5 * 1.5 * 0.02)
+    assert np.array_equal(np.stack([fx, fy]).astype(np.float32), G["flow_tentacle_base"])
+
+
+def test_morph_offsets_follow_numpy_draw_order():
+    m = R.MorphAnimation(enabled=True, seed=42)
+    off = R.morph_offsets(m, 2)
+    rng = np.random.default_rng(142 + 1000)
+    assert off[1, 1, 0, 0] == rng.random() * 1000 and off[1, 1, 0, 1] == rng.random() * 1000
+    assert off[1, 1, 1, 0] == rng.random() * 1000
+
+
+def test_morph_restatement_partition_of_unity():
+    masks = O.feather(O.masks_from_geometry(R.draw_geometry(H, W, "voronoi", 4, 3), H, W), 4)
+    for mode in ("blob", "tentacle", "wave", "pulse"):
+        r = O.morph(masks, mode, 1.0, 0.15, 3.0, 42, 5)
+        assert torch.allclose(r.sum(0), torch.ones(H, W), atol=1e-5), mode
