@@ -846,13 +846,15 @@ struct GramPlan {
 };
 GramPlan gram_plan(int n, int c, int hw) {
   GramPlan g;
-  g.ti = c <= 64 ? 64 : (c <= 128 ? 128 : 256);
+  // 128-channel tiles above 64 channels: the 256 tile left a c = 512 Gram with 4 output tiles, so all of its
+  // parallelism had to come from split-K partials of 1 MiB each
+  g.ti = c <= 64 ? 64 : 128;
   g.tt = (c + g.ti - 1) / g.ti;
   const int blocks = g.tt * g.tt * n;
   const int fills = (hw + 63) / 64;
   // enough K slices to fill the chip (~512 workgroups), but their fp32 partials (c*c*4 B each) no more than
-  // twice the bytes of F itself: beyond that the split-K traffic costs more than the parallelism gains
-  const int cap = std::max(1, (int)(((size_t)2 * 2 * hw) / ((size_t)4 * c)));
+  // four times the bytes of F (bf16) itself: beyond that the split-K traffic costs more than it buys
+  const int cap = std::max(1, (int)(((size_t)4 * 2 * hw) / ((size_t)4 * c)));
   g.slices = std::max(1, std::min(std::min(fills, cap), (512 + blocks - 1) / blocks));
   g.kslice = ((fills + g.slices - 1) / g.slices) * 64;
   g.slices = (hw + g.kslice - 1) / g.kslice;
