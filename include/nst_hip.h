@@ -415,6 +415,28 @@ int nst_region_crop_input(const uint8_t* frames, int n, int h, int w, const int*
 int nst_region_resize(const float* y, int n, int h, int w, int preset, int fit_h, int fit_w, int out_h, int out_w,
                       float* out, void* stream);
 
+/* ---- Temporal stage (pipeline.py:1884-1940 --flow_ema, :2072-2086 --motion_blend) ---- */
+/* pil_rgb.convert("L") (pipeline.py:1100): Pillow's integer luma (r*19595 + g*38470 + b*7471 + 0x8000) >> 16 of
+ * frames [n,h,w,3] -> gray [n,h,w] */
+int nst_gray_u8(const uint8_t* rgb, int n, int h, int w, uint8_t* gray, void* stream);
+/* cv2.calcOpticalFlowFarneback(prev, next, None, pyr_scale, levels, winsize, iterations, poly_n, poly_sigma, 0)
+ * (pipeline.py:1896-1899 passes 0.5, 3, 15, 3, 5, 1.1): OpenCV's optflowgf.cpp restated (cv2 absent: parity
+ * unpinned).  prev/next u8 [h,w] device, flow f32 [h,w,2] = (dx, dy); scratch per nst_flow_scratch_floats. */
+int nst_flow_scratch_floats(int h, int w, size_t* out);
+int nst_flow_farneback(const uint8_t* prev, const uint8_t* next, int h, int w, double pyr_scale, int levels,
+                       int winsize, int iterations, int poly_n, double poly_sigma, float* flow, float* scratch,
+                       size_t scratch_floats, void* stream);
+/* flow EMA (pipeline.py:1926-1931 with _warp_with_flow :425-439): out = clip(alpha*curr + (1-alpha)*warp(prev)),
+ * warp = cv2.remap(prev, x + dx, y + dy, INTER_LINEAR, BORDER_REPLICATE) restated; curr/prev/out f32 planar
+ * [3,h,w] in [0,1], out != prev */
+int nst_flow_fuse(const float* curr, const float* prev, const float* flow, int h, int w, float alpha,
+                  float one_minus_alpha, float* out, void* stream);
+/* motion-adaptive blend alpha (pipeline.py:2073-2080): m = GaussianBlur(clip(|flow| / motion_norm, 0, 1), sigma),
+ * alpha = max_alpha - span * m (span = max_alpha - min_alpha as the fp32 the reference multiplies by);
+ * alpha/scratch f32 [h,w] */
+int nst_motion_alpha(const float* flow, int h, int w, float motion_norm, double sigma, float max_alpha, float span,
+                     float* alpha, float* scratch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,20 @@
+// flow_internal.h — launchers of the temporal-stage kernels (flow_ops.hip), called by flow_api.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace nst {
+
+hipError_t launch_gray(const uint8_t* rgb, size_t npix, uint8_t* gray, hipStream_t st);
+size_t farneback_scratch_floats(int h, int w);
+hipError_t launch_farneback(const uint8_t* prev, const uint8_t* next, int h, int w, double pyr_scale, int levels,
+                            int winsize, int iterations, int poly_n, double poly_sigma, float* flow, float* scratch,
+                            hipStream_t st);
+hipError_t launch_flow_fuse(const float* curr, const float* prev, const float* flow, int h, int w, float a, float oma,
+                            float* out, hipStream_t st);
+hipError_t launch_motion_alpha(const float* flow, int h, int w, float norm, double sigma, float max_alpha, float span,
+                               float* alpha, float* tmp, hipStream_t st);
+
+}  // namespace nst

@@ -21,7 +21,11 @@ restated, parity unpinned because cv2 is absent here).
 Region blending (--region_mode / --region_optimize and their spec, animation and rotation flags,
 pipeline.py:1120-1407, 1720-1839) runs on the GPU compositor of regions.py.
 
-Not built (rejected with a clear message if requested): optical-flow EMA / motion blend (--flow_ema, --motion_blend), Magenta (TF-Hub) and Torch7 (OpenCV
+The flow-guided EMA (--flow_ema --flow_method farneback, pipeline.py:1884-1940) and the motion-adaptive
+blend (--motion_blend, :2072-2086) run on the GPU (temporal.py).
+
+Not built (rejected with a clear message if requested): DIS optical flow (the reference's
+default --flow_method), --flow_downscale > 1 (--flow_ema, --motion_blend), Magenta (TF-Hub) and Torch7 (OpenCV
 DNN) backends.
 """
 from __future__ import annotations
@@ -163,8 +167,10 @@ def reject_out_of_scope(args) -> None:
                                              or str(getattr(args, f"model_{s}")).lower() in ("magenta",)
                                              or str(getattr(args, f"model_{s}")).endswith(".t7")):
             bad.append(f"--model_{s} (magenta/torch7)")
-    if args.flow_ema or args.motion_blend:
-        bad.append("--flow_ema/--motion_blend")
+    if args.flow_ema and args.flow_method != "farneback":
+        bad.append("--flow_ema with --flow_method dis (cv2.DISOpticalFlow is not built; --flow_method farneback is)")
+    if args.flow_ema and int(args.flow_downscale or 1) > 1:
+        bad.append("--flow_downscale > 1 (the INTER_AREA flow pyramid is not built)")
     if args.device != "cuda":
         bad.append(f"--device {args.device} (this engine runs on MI355X only; there is no CPU path)")
     if bad:
@@ -484,19 +490,26 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     pool = ThreadPoolExecutor(max_workers=max(1, threads))
     sizes = [src.size(i) for i in range(len(src))]
     groups = plan_groups(sizes, world, max(1, args.batch))
-    need_orig = blend < 1.0 or bool(args.mask or args.mask_dir)
+    flow_mode = bool(getattr(args, "flow_ema", False))
+    need_orig = blend < 1.0 or bool(args.mask or args.mask_dir) or (flow_mode and bool(getattr(args, "motion_blend", False)))
 
     # the reference fits model A's output to the content size; with --inference_res the model
     # input is smaller than the content
     def stylize(idx: List[int]):
         if not idx:
             h0, w0 = sizes[0]
+            if flow_mode:
+                return torch.empty((0, 15 * h0 * w0), dtype=torch.uint8, device=dev)
             return torch.empty((0, h0, w0, 6 if need_orig else 3), dtype=torch.uint8, device=dev)
         loaded = list(pool.map(src.load, idx))
         orig = torch.from_numpy(np.stack([a for a, _ in loaded])).to(dev, non_blocking=True)
         xin = orig if loaded[0][1] is loaded[0][0] else torch.from_numpy(np.stack([b for _, b in loaded])).to(dev)
         h0, w0 = orig.shape[1], orig.shape[2]
         fids = [f + 1 for f in idx]  # the reference's 1-based frame index (animations, rotation)
+        if flow_mode:  # the temporal stage needs out01 before the ToPILImage truncation (pipeline.py:1884-1943)
+            out01 = _out01_f32(xin, orig, fids, h0, w0)
+            n = out01.shape[0]
+            return torch.cat([out01.view(torch.uint8).reshape(n, -1), orig.reshape(n, -1)], dim=1)
         if regions is not None and regions.optimized:  # crops of the full-resolution frame (pipeline.py:1309)
             styled = regions.optimized_frames(dict(zip(slot_letters, slots)), orig, fids)
         elif regions is not None:
@@ -515,13 +528,53 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             styled = _blend_slots(slots[:n_blend], weights, xin, h0, w0)
         return torch.cat([styled, orig], dim=3) if need_orig else styled
 
+    def _out01_f32(xin, orig, fids, h0, w0):
+        """out01 [n,3,h0,w0] float32: the frame's styled result before ToPILImage (model A / RGB blend / LAB
+        blend / region composite), for the temporal stage."""
+        from .regions import Source, composite, crop_input, forward_raw
+        if regions is not None and regions.optimized:
+            return regions.optimized_frames(dict(zip(slot_letters, slots)), orig, fids, out_f32=True)
+        if regions is not None:
+            raw = [Source(forward_raw(m, xin, pr), pr) for m, pr in slots]
+            return regions.standard(raw, orig, fids, n_blend, (h0, w0), out_f32=True)
+        if n_blend > 1 and getattr(args, "blend_models_lab", False):  # to_tensor of the LAB-blended image
+            from .postproc import blend_models_lab
+            outs = [_slot_u8(m, pr, xin, h0, w0) for m, pr in slots[:n_blend]]
+            u8 = blend_models_lab(outs, lab_rest, lab_wl, lab_wab)
+            return crop_input(u8, (0, 0, w0, h0), (h0, w0))
+        # model A alone, or the RGB blend: zeros + w_i * out_i, clamp -- one all-ones region of the compositor
+        raw = [Source(forward_raw(m, xin, pr), pr) for m, pr in slots[:n_blend]]
+        ones = torch.ones((1, h0, w0), dtype=torch.float32, device=dev)
+        return composite(raw, [[(i, w) for i, w in enumerate(weights[:n_blend])]], ones, None, out_f32=True)
+
     lab = LabSmoother(dev, smooth_lightness, smooth_alpha, smooth_chroma, chroma_alpha)
+    flow = None
+    if flow_mode:
+        from .temporal import FlowSmoother
+        flow = FlowSmoother(True, float(args.flow_alpha))
     mask_cache = {}
     pending = []
     t_start = time.perf_counter()
     done = [0]
 
     def consume(g: List[int], full):
+        motion = None
+        if flow_mode:  # unpack [out01 f32 | orig u8] and run the temporal stage in frame order
+            from .temporal import motion_alpha, planar_to_u8
+            h0, w0 = sizes[g[0]]
+            nb = 3 * h0 * w0 * 4
+            out01 = full[:, :nb].contiguous().view(torch.float32).reshape(len(g), 3, h0, w0)
+            orig = full[:, nb:].contiguous().reshape(len(g), h0, w0, 3)
+            if lab.hw is not None and lab.hw != (h0, w0):
+                flow.reset()
+            fused, flows = [], []
+            for j in range(len(g)):
+                fused.append(flow(out01[j], orig[j]))
+                flows.append(flow.last_flow)  # None for the first frame of a run (no previous frame)
+            if getattr(args, "motion_blend", False):  # pipeline.py:2072-2080 alpha from this frame's flow
+                motion = [None if fl is None else motion_alpha(fl, blend) for fl in flows]
+            styled = planar_to_u8(torch.stack(fused))
+            full = torch.cat([styled, orig], dim=3) if need_orig else styled
         styled = full[..., :3].contiguous() if need_orig else full
         h0, w0 = styled.shape[1], styled.shape[2]
         if lab.hw is not None and lab.hw != (h0, w0):
@@ -531,7 +584,12 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         if need_orig:
             orig = full[..., 3:].contiguous()
             alpha = _masks_for(g, h0, w0)
+            styled_in = styled
             styled = blend_frames(styled, orig, blend, alpha, args.composite_mode)
+            if motion is not None:  # frames with a flow and no mask: the motion-adaptive blend replaces it
+                for j, f in enumerate(g):
+                    if motion[j] is not None and not _has_mask(f):
+                        styled[j:j + 1] = blend_frames(styled_in[j:j + 1], orig[j:j + 1], 1.0, motion[j][None], "keep")
         host = styled.cpu().numpy()
         if not args.no_save:
             for j, f in enumerate(g):
@@ -539,6 +597,13 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         done[0] += len(g)
         el = time.perf_counter() - t_start
         _log(f"[frame] {done[0]}/{len(src)} styled  ({done[0] / max(el, 1e-9):.2f} frames/s)")
+
+    def _has_mask(f):  # pipeline.py:1985-1993 mask_used: a --mask, or this frame's --mask_dir file exists
+        if getattr(args, "mask", None):
+            return True
+        if not getattr(args, "mask_dir", None) or args.synthetic:
+            return False
+        return (Path(args.mask_dir) / f"mask_{names[f].split('_')[-1]}.png").exists()
 
     def _masks_for(g, h0, w0):
         mfile_global = getattr(args, "mask", None)

@@ -701,7 +701,7 @@ class RegionCompositor:
 
     # ---- standard path: every model styled the whole frame (pipeline.py:1720-1839) ----
     def standard(self, raw: List[Source], orig_u8: torch.Tensor, frame_ids: List[int], num_models_quirk: int,
-                 fit_hw: Tuple[int, int]) -> torch.Tensor:
+                 fit_hw: Tuple[int, int], out_f32: bool = False) -> torch.Tensor:
         """raw[i]: output i of the compressed outputs list (A, then B..H in order) for the batch; frame_ids are
         the reference's 1-based frame indices.  -> u8 [n,H,W,3]."""
         a = self.a
@@ -730,7 +730,9 @@ class RegionCompositor:
                         sources.append(Source(resized_source(r.y, r.preset, (H, W), hw), "none"))
                         scale_of[s].append(len(sources) - 1)
             # dict order as the reference builds it (scale 1.0 entry is the first only if listed first)
-        out = torch.empty((orig_u8.shape[0], H, W, 3), dtype=torch.uint8, device=self.dev)
+        n_fr = orig_u8.shape[0]
+        out = torch.empty((n_fr, 3, H, W) if out_f32 else (n_fr, H, W, 3),
+                          dtype=torch.float32 if out_f32 else torch.uint8, device=self.dev)
 
         def configs_for(k_masks):
             if advanced:
@@ -773,13 +775,14 @@ class RegionCompositor:
                 print(f"[region] mode={self.mode} regions={masks.shape[0]} models={n_out} assignment={assignment} "
                       f"feather={self.feather}px seed={self.seed}", flush=True)
             if not animating and self.seed is not None:  # masks and terms shared by the batch: one launch
-                return composite(sources, terms, masks, orig_u8 if with_orig else None)
+                return composite(sources, terms, masks, orig_u8 if with_orig else None, out_f32=out_f32)
             srcs_j = [Source(s.y[j:j + 1], s.preset) for s in sources]
-            out[j:j + 1] = composite(srcs_j, terms, masks, orig_u8[j:j + 1] if with_orig else None)
+            out[j:j + 1] = composite(srcs_j, terms, masks, orig_u8[j:j + 1] if with_orig else None, out_f32=out_f32)
         return out
 
     # ---- --region_optimize: crops styled per region (pipeline.py:1120-1407) ----
-    def optimized_frames(self, slot_models: Dict[int, tuple], orig_u8: torch.Tensor, frame_ids: List[int]) -> torch.Tensor:
+    def optimized_frames(self, slot_models: Dict[int, tuple], orig_u8: torch.Tensor, frame_ids: List[int],
+                         out_f32: bool = False) -> torch.Tensor:
         """slot_models: letter index (A=0..H=7) -> (model, io_preset) of the loaded slots."""
         a = self.a
         n, H, W, _ = orig_u8.shape
@@ -805,7 +808,8 @@ class RegionCompositor:
             self.blend_anims = parse_region_blend_animations(bspec, k) if bspec else None
             self.scale_anims = parse_region_scale_animations(sspec, k) if sspec else None
             self._anims_parsed = True
-        out = torch.empty((n, H, W, 3), dtype=torch.uint8, device=self.dev)
+        out = torch.empty((n, 3, H, W) if out_f32 else (n, H, W, 3), dtype=torch.float32 if out_f32 else torch.uint8,
+                          device=self.dev)
         # frames sharing masks, boxes and scales run as one batch per (region, model)
         plans, order = {}, []
         static_masks = None
@@ -870,7 +874,7 @@ class RegionCompositor:
                     srcs.append(Source(forward_raw(model, crop, preset), preset))
                     tl.append((len(srcs) - 1, w))
                 terms.append(tl)
-            res = composite(srcs, terms, masks, frames if with_orig else None, boxes=boxes)
+            res = composite(srcs, terms, masks, frames if with_orig else None, boxes=boxes, out_f32=out_f32)
             if len(js) == n:
                 out = res
             else:
