@@ -284,33 +284,57 @@ __global__ __launch_bounds__(256) void update_matrices_kernel(const float* __res
 }
 
 // FarnebackUpdateFlow_Blur: block_size x block_size box sums of M (rows and columns clamped to the frame)
-// in double, then the 2x2 solve with the 1e-3 regulariser
+// in double, then the 2x2 solve with the 1e-3 regulariser.  As OpenCV sums them: a running vertical sum per
+// column (each step adds the float difference entering - leaving row), then the horizontal window over the
+// vertical sums.  Vertical: one thread per column walks a strip of BOX_ROWS rows; horizontal: a 256-pixel row
+// segment and its halo staged in LDS.
+constexpr int BOX_ROWS = 16;
+
 __global__ __launch_bounds__(256) void box_v_kernel(const float* __restrict__ M, int h, int w, int m,
                                                     double* __restrict__ vs) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (size_t)h * w) return;
-  const int x = (int)(i % w), y = (int)(i / w);
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= w) return;
+  const int y0 = blockIdx.y * BOX_ROWS, y1 = min(h, y0 + BOX_ROWS);
+  auto row = [&](int q) { return M + ((size_t)min(max(q, 0), h - 1) * w + x) * 5; };
   double s[5] = {0, 0, 0, 0, 0};
-  for (int q = y - m; q <= y + m; ++q) {
-    const float* p = M + ((size_t)min(max(q, 0), h - 1) * w + x) * 5;
+  for (int q = y0 - m; q <= y0 + m; ++q) {
+    const float* p = row(q);
 #pragma unroll
     for (int c = 0; c < 5; ++c) s[c] += p[c];
   }
+  for (int y = y0; y < y1; ++y) {
+    if (y > y0) {
+      const float* pa = row(y + m);
+      const float* pd = row(y - m - 1);
 #pragma unroll
-  for (int c = 0; c < 5; ++c) vs[i * 5 + c] = s[c];
+      for (int c = 0; c < 5; ++c) s[c] += pa[c] - pd[c];
+    }
+    double* o = vs + ((size_t)y * w + x) * 5;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) o[c] = s[c];
+  }
 }
 
 __global__ __launch_bounds__(256) void box_h_solve_kernel(const double* __restrict__ vs, int h, int w, int m,
                                                           double scale, float* __restrict__ flow) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (size_t)h * w) return;
-  const int x = (int)(i % w), y = (int)(i / w);
+  extern __shared__ double seg[];  // (256 + 2m) x 5
+  const int y = blockIdx.y, x0 = blockIdx.x * 256;
+  const int n = 256 + 2 * m;
+  for (int j = threadIdx.x; j < n * 5; j += 256) {
+    const int e = j / 5, c = j - e * 5;
+    const int xs = min(max(x0 - m + e, 0), w - 1);
+    seg[j] = vs[((size_t)y * w + xs) * 5 + c];
+  }
+  __syncthreads();
+  const int x = x0 + threadIdx.x;
+  if (x >= w) return;
   double s[5] = {0, 0, 0, 0, 0};
-  for (int q = x - m; q <= x + m; ++q) {
-    const double* p = vs + ((size_t)y * w + min(max(q, 0), w - 1)) * 5;
+  for (int q = 0; q <= 2 * m; ++q) {
+    const double* p = seg + (threadIdx.x + q) * 5;
 #pragma unroll
     for (int c = 0; c < 5; ++c) s[c] += p[c];
   }
+  const size_t i = (size_t)y * w + x;
   const double g11 = s[0] * scale, g12 = s[1] * scale, g22 = s[2] * scale, h1 = s[3] * scale, h2 = s[4] * scale;
   const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
   flow[2 * i] = (float)((g11 * h2 - g12 * h1) * idet);
@@ -381,9 +405,12 @@ hipError_t launch_farneback(const uint8_t* prev, const uint8_t* next, int h, int
     hipLaunchKernelGGL(polyexp_h_kernel, gl, dim3(256), 0, st, row3, lh, lw, pt, R);
     const dim3 g1((unsigned)((ln + 255) / 256));
     hipLaunchKernelGGL(update_matrices_kernel, g1, dim3(256), 0, st, R, R + 5 * ln, flow, lh, lw, M);
+    const dim3 gv((unsigned)((lw + 255) / 256), (unsigned)((lh + BOX_ROWS - 1) / BOX_ROWS));
+    const dim3 gh((unsigned)((lw + 255) / 256), (unsigned)lh);
+    const size_t hl = (size_t)(256 + 2 * m) * 5 * sizeof(double);
     for (int it = 0; it < iterations; ++it) {
-      hipLaunchKernelGGL(box_v_kernel, g1, dim3(256), 0, st, M, lh, lw, m, vs);
-      hipLaunchKernelGGL(box_h_solve_kernel, g1, dim3(256), 0, st, vs, lh, lw, m, bscale, flow);
+      hipLaunchKernelGGL(box_v_kernel, gv, dim3(256), 0, st, M, lh, lw, m, vs);
+      hipLaunchKernelGGL(box_h_solve_kernel, gh, dim3(256), hl, st, vs, lh, lw, m, bscale, flow);
       if (it < iterations - 1)
         hipLaunchKernelGGL(update_matrices_kernel, g1, dim3(256), 0, st, R, R + 5 * ln, flow, lh, lw, M);
     }

@@ -196,9 +196,17 @@ def blur_solve(M: np.ndarray, winsize: int) -> np.ndarray:
     h, w, _ = M.shape
     m = winsize // 2
     ys, xs = np.arange(h), np.arange(w)
+    # running vertical sums per strip of 16 rows as the engine (and OpenCV) keeps them: the first window summed,
+    # then + (entering - leaving) with the row difference in float
     vs = np.zeros((h, w, 5))
-    for q in range(-m, m + 1):
-        vs += M[np.clip(ys + q, 0, h - 1)].astype(np.float64)
+    for y0 in range(0, h, 16):
+        s = np.zeros((w, 5))
+        for q in range(y0 - m, y0 + m + 1):
+            s = s + M[min(max(q, 0), h - 1)].astype(np.float64)
+        for y in range(y0, min(h, y0 + 16)):
+            if y > y0:
+                s = s + (M[min(y + m, h - 1)] - M[max(y - m - 1, 0)]).astype(np.float64)
+            vs[y] = s
     s = np.zeros((h, w, 5))
     for q in range(-m, m + 1):
         s += vs[:, np.clip(xs + q, 0, w - 1)]
