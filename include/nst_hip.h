@@ -426,6 +426,10 @@ int nst_flow_scratch_floats(int h, int w, size_t* out);
 int nst_flow_farneback(const uint8_t* prev, const uint8_t* next, int h, int w, double pyr_scale, int levels,
                        int winsize, int iterations, int poly_n, double poly_sigma, float* flow, float* scratch,
                        size_t scratch_floats, void* stream);
+/* --flow_downscale ds (pipeline.py:1886-1892, 1920-1923): gray [h,w] -> [h/ds, w/ds] by cv2.resize INTER_AREA at an
+ * exact integer factor (restated), and the small flow [hs,ws,2] back to [h,w,2] by INTER_LINEAR times mul = ds */
+int nst_flow_downscale_gray(const uint8_t* gray, int h, int w, int ds, uint8_t* out, void* stream);
+int nst_flow_upscale(const float* flow_small, int hs, int ws, int h, int w, float mul, float* flow, void* stream);
 /* flow EMA (pipeline.py:1926-1931 with _warp_with_flow :425-439): out = clip(alpha*curr + (1-alpha)*warp(prev)),
  * warp = cv2.remap(prev, x + dx, y + dy, INTER_LINEAR, BORDER_REPLICATE) restated; curr/prev/out f32 planar
  * [3,h,w] in [0,1], out != prev */

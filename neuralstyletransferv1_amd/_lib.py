@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = (
     "nst_region_masks", "nst_region_feather", "nst_region_rotate", "nst_region_bbox", "nst_region_scratch_floats",
     "nst_region_composite_u8", "nst_region_crop_input", "nst_region_resize", "nst_region_morph",
     "nst_region_morph_scratch_floats", "nst_gray_u8", "nst_flow_scratch_floats", "nst_flow_farneback",
-    "nst_flow_fuse", "nst_motion_alpha",
+    "nst_flow_fuse", "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale",
 )
 # region compositor limits / geometry kinds (include/nst_hip.h NST_REGION_*, NST_RG_*)
 NST_REGION_MAX, NST_REGION_TERMS, NST_REGION_MAX_SRC = 32, 9, 16
@@ -164,8 +164,10 @@ def lib() -> ctypes.CDLL:
         L.nst_flow_farneback.argtypes = [vp, vp, i, i, dbl, i, i, i, i, dbl, vp, vp, sz, vp]
         L.nst_flow_fuse.argtypes = [vp, vp, vp, i, i, f, f, vp, vp]
         L.nst_motion_alpha.argtypes = [vp, i, i, f, dbl, f, f, vp, vp, vp]
+        L.nst_flow_downscale_gray.argtypes = [vp, i, i, i, vp, vp]
+        L.nst_flow_upscale.argtypes = [vp, i, i, i, i, f, vp, vp]
         for name in ("nst_gray_u8", "nst_flow_scratch_floats", "nst_flow_farneback", "nst_flow_fuse",
-                     "nst_motion_alpha"):
+                     "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale"):
             getattr(L, name).restype = i
         for name in ("nst_region_masks", "nst_region_feather", "nst_region_rotate", "nst_region_bbox",
                      "nst_region_morph", "nst_region_morph_scratch_floats",

@@ -44,6 +44,24 @@ int nst_flow_farneback(const uint8_t* prev, const uint8_t* next, int h, int w, d
   return NST_OK;
 }
 
+int nst_flow_downscale_gray(const uint8_t* gray, int h, int w, int ds, uint8_t* out, void* stream) {
+  if (!gray || !out || ds < 2 || h % ds != 0 || w % ds != 0 || h / ds < 2 || w / ds < 2) {
+    set_error("nst_flow_downscale_gray: the frame must be an exact multiple of the factor (ds >= 2)");
+    return NST_E_SHAPE;
+  }
+  FL_LAUNCH(launch_area_down(gray, h, w, ds, out, (hipStream_t)stream), "area_down");
+  return NST_OK;
+}
+
+int nst_flow_upscale(const float* flow_small, int hs, int ws, int h, int w, float mul, float* flow, void* stream) {
+  if (!flow_small || !flow || hs <= 0 || ws <= 0 || h <= 0 || w <= 0) {
+    set_error("nst_flow_upscale: invalid arguments");
+    return NST_E_INVALID;
+  }
+  FL_LAUNCH(launch_resize_lin(flow_small, 1, hs, ws, 2, h, w, mul, flow, (hipStream_t)stream), "flow_upscale");
+  return NST_OK;
+}
+
 int nst_flow_fuse(const float* curr, const float* prev, const float* flow, int h, int w, float alpha,
                   float one_minus_alpha, float* out, void* stream) {
   if (!curr || !prev || !flow || !out || out == prev || h <= 0 || w <= 0) {

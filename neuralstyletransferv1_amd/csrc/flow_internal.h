@@ -12,6 +12,9 @@ size_t farneback_scratch_floats(int h, int w);
 hipError_t launch_farneback(const uint8_t* prev, const uint8_t* next, int h, int w, double pyr_scale, int levels,
                             int winsize, int iterations, int poly_n, double poly_sigma, float* flow, float* scratch,
                             hipStream_t st);
+hipError_t launch_area_down(const uint8_t* in, int h, int w, int ds, uint8_t* out, hipStream_t st);
+hipError_t launch_resize_lin(const float* in, int k, int h, int w, int c, int oh, int ow, float mul, float* out,
+                             hipStream_t st);
 hipError_t launch_flow_fuse(const float* curr, const float* prev, const float* flow, int h, int w, float a, float oma,
                             float* out, hipStream_t st);
 hipError_t launch_motion_alpha(const float* flow, int h, int w, float norm, double sigma, float max_alpha, float span,

@@ -421,6 +421,27 @@ hipError_t launch_farneback(const uint8_t* prev, const uint8_t* next, int h, int
   return hipGetLastError();
 }
 
+// ---- --flow_downscale (pipeline.py:1886-1892, 1920-1923): cv2.resize(gray, (W/ds, H/ds), INTER_AREA) for an
+// exact integer factor (OpenCV's resizeAreaFast: ds = 2 takes its SIMD rounding (sum + 2) >> 2, other factors
+// saturate_cast(sum / area)), and the flow brought back with INTER_LINEAR and scaled by ds ----
+__global__ __launch_bounds__(256) void area_down_kernel(const uint8_t* __restrict__ in, int w, int ds, int oh, int ow,
+                                                        uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)oh * ow) return;
+  const int x = (int)(i % ow), y = (int)(i / ow);
+  int sum = 0;
+  for (int r = 0; r < ds; ++r)
+    for (int c = 0; c < ds; ++c) sum += in[(size_t)(y * ds + r) * w + x * ds + c];
+  out[i] = ds == 2 ? (uint8_t)((sum + 2) >> 2) : (uint8_t)min(255, (int)rintf((float)sum * (1.f / (float)(ds * ds))));
+}
+
+hipError_t launch_area_down(const uint8_t* in, int h, int w, int ds, uint8_t* out, hipStream_t st) {
+  const int oh = h / ds, ow = w / ds;
+  const size_t n = (size_t)oh * ow;
+  hipLaunchKernelGGL(area_down_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, w, ds, oh, ow, out);
+  return hipGetLastError();
+}
+
 // ---- flow EMA: fused = clip(a * curr + (1 - a) * remap(prev, grid + flow, BORDER_REPLICATE)) ----
 __global__ __launch_bounds__(256) void flow_fuse_kernel(const float* __restrict__ curr, const float* __restrict__ prev,
                                                         const float* __restrict__ flow, int h, int w, float a,

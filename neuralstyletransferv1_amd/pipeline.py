@@ -25,7 +25,7 @@ The flow-guided EMA (--flow_ema --flow_method farneback, pipeline.py:1884-1940) 
 blend (--motion_blend, :2072-2086) run on the GPU (temporal.py).
 
 Not built (rejected with a clear message if requested): DIS optical flow (the reference's
-default --flow_method), --flow_downscale > 1 (--flow_ema, --motion_blend), Magenta (TF-Hub) and Torch7 (OpenCV
+default --flow_method) (--flow_ema, --motion_blend), Magenta (TF-Hub) and Torch7 (OpenCV
 DNN) backends.
 """
 from __future__ import annotations
@@ -169,8 +169,6 @@ def reject_out_of_scope(args) -> None:
             bad.append(f"--model_{s} (magenta/torch7)")
     if args.flow_ema and args.flow_method != "farneback":
         bad.append("--flow_ema with --flow_method dis (cv2.DISOpticalFlow is not built; --flow_method farneback is)")
-    if args.flow_ema and int(args.flow_downscale or 1) > 1:
-        bad.append("--flow_downscale > 1 (the INTER_AREA flow pyramid is not built)")
     if args.device != "cuda":
         bad.append(f"--device {args.device} (this engine runs on MI355X only; there is no CPU path)")
     if bad:
@@ -551,7 +549,7 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     flow = None
     if flow_mode:
         from .temporal import FlowSmoother
-        flow = FlowSmoother(True, float(args.flow_alpha))
+        flow = FlowSmoother(True, float(args.flow_alpha), max(1, int(args.flow_downscale or 1)))
     mask_cache = {}
     pending = []
     t_start = time.perf_counter()

@@ -8,8 +8,9 @@ Per frame, in frame order (the EMA state is the previous fused frame):
   prev_gray, prev_styled01 = gray, out01
 and, when --motion_blend is on, the blend alpha from |flow| (nst_motion_alpha).
 
-The reference's default --flow_method is DIS (cv2.DISOpticalFlow, PRESET_FAST); only Farneback is built here,
-so a DIS request fails loudly (pipeline.reject_out_of_scope).  cv2 is not installed in this environment: the
+--flow_downscale ds computes the flow on INTER_AREA-reduced grays (an exact integer factor of the frame) and
+brings it back with INTER_LINEAR x ds.  The reference's default --flow_method is DIS (cv2.DISOpticalFlow,
+PRESET_FAST); only Farneback is built here, so a DIS request fails loudly (pipeline.reject_out_of_scope).  cv2 is not installed in this environment: the
 Farneback, remap and GaussianBlur restatements are parity unpinned.
 """
 from __future__ import annotations
@@ -86,6 +87,24 @@ def motion_alpha(flow: torch.Tensor, blend: float) -> torch.Tensor:
     return alpha
 
 
+def downscale_gray(gray: torch.Tensor, ds: int) -> torch.Tensor:
+    """cv2.resize(gray, (W // ds, H // ds), interpolation=cv2.INTER_AREA) at an exact integer factor."""
+    h, w = gray.shape
+    out = torch.empty((h // ds, w // ds), dtype=torch.uint8, device=gray.device)
+    check(lib().nst_flow_downscale_gray(gray.contiguous().data_ptr(), h, w, int(ds), out.data_ptr(),
+                                        _lib.stream_ptr(gray.device)), "nst_flow_downscale_gray")
+    return out
+
+
+def upscale_flow(flow_small: torch.Tensor, h: int, w: int, ds: int) -> torch.Tensor:
+    """cv2.resize(flow_small, (W, H), INTER_LINEAR) * ds (pipeline.py:1920-1922)."""
+    hs, ws, _ = flow_small.shape
+    out = torch.empty((h, w, 2), dtype=torch.float32, device=flow_small.device)
+    check(lib().nst_flow_upscale(flow_small.contiguous().data_ptr(), hs, ws, h, w, float(ds), out.data_ptr(),
+                                 _lib.stream_ptr(flow_small.device)), "nst_flow_upscale")
+    return out
+
+
 def planar_to_u8(out01: torch.Tensor) -> torch.Tensor:
     """ToPILImage of float planes [n,3,h,w] in [0,1]: pic.mul(255).byte() -> [n,h,w,3] uint8."""
     n, _, h, w = out01.shape
@@ -98,9 +117,10 @@ def planar_to_u8(out01: torch.Tensor) -> torch.Tensor:
 class FlowSmoother:
     """The reference's temporal caches (prev_gray, prev_styled01, last_flow; reset on a frame-size change)."""
 
-    def __init__(self, flow_ema: bool, flow_alpha: float):
+    def __init__(self, flow_ema: bool, flow_alpha: float, downscale: int = 1):
         self.enabled = flow_ema
         self.alpha = flow_alpha
+        self.ds = max(1, int(downscale))
         self.scratch = FlowScratch()
         self.reset()
 
@@ -115,7 +135,12 @@ class FlowSmoother:
         self.last_flow = None
         if self.enabled and self.prev_gray is not None and self.prev_styled is not None:
             if self.prev_gray.shape == gray.shape:
-                flow = farneback(self.prev_gray, gray, self.scratch)
+                if self.ds > 1:  # pipeline.py:1886-1892, 1920-1923
+                    h, w = gray.shape
+                    small = farneback(downscale_gray(self.prev_gray, self.ds), downscale_gray(gray, self.ds), self.scratch)
+                    flow = upscale_flow(small, h, w, self.ds)
+                else:
+                    flow = farneback(self.prev_gray, gray, self.scratch)
                 out01 = fuse(out01, self.prev_styled, flow, self.alpha)
                 self.last_flow = flow
         self.prev_gray = gray

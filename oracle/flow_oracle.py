@@ -279,3 +279,20 @@ def motion_alpha(flow: np.ndarray, blend: float) -> np.ndarray:
     m = np.clip(mag / f32(8.0), 0, 1)
     m = gauss_blur(m, int(np.rint(3.0 * 8 + 1)) | 1, 3.0)
     return (f32(blend) - f32(blend - 0.4) * m).astype(f32)
+
+
+def area_down(gray_u8: np.ndarray, ds: int) -> np.ndarray:
+    """cv2.resize(gray, (W // ds, H // ds), INTER_AREA) at an exact integer factor (resizeAreaFast restated:
+    ds = 2 rounds (sum + 2) >> 2 as its SIMD path, other factors saturate_cast(sum / area))."""
+    h, w = gray_u8.shape
+    s = gray_u8.reshape(h // ds, ds, w // ds, ds).astype(np.int64).sum(axis=(1, 3))
+    if ds == 2:
+        return ((s + 2) >> 2).astype(np.uint8)
+    return np.minimum(255, np.rint(s.astype(f32) * f32(1.0 / (ds * ds)))).astype(np.uint8)
+
+
+def farneback_downscaled(prev: np.ndarray, nxt: np.ndarray, ds: int) -> np.ndarray:
+    """pipeline.py:1886-1892, 1920-1923: flow on the INTER_AREA-reduced grays, INTER_LINEAR back, times ds."""
+    h, w = prev.shape
+    small = farneback(area_down(prev, ds), area_down(nxt, ds))
+    return resize_lin(small, h, w, float(ds))

@@ -106,3 +106,22 @@ def test_cli_flow_ema_motion_blend_vs_oracle(tmp_path):
         got = np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png"))
         dd = np.abs(got.astype(int) - ref.astype(int))
         assert (dd > 1).mean() <= 0.005, f"frame {i}: {(dd > 1).mean():.4%} > 1 LSB (max {dd.max()})"
+
+
+def test_flow_downscale_vs_restatement():
+    prev, nxt = _pair(144, 256, 4, 2, seed=7)
+    for ds in (2, 4):
+        g = T.downscale_gray(torch.from_numpy(prev).to(DEV), ds).cpu().numpy()
+        assert np.array_equal(g, FO.area_down(prev, ds))
+    fs = T.FlowSmoother(True, 0.8, 2)
+    a = torch.rand(3, 144, 256, device=DEV)
+    fr0 = np.repeat(prev[..., None], 3, axis=2)
+    fr1 = np.repeat(nxt[..., None], 3, axis=2)
+    fs(a, torch.from_numpy(fr0).to(DEV))
+    fs(a, torch.from_numpy(fr1).to(DEV))
+    got = fs.last_flow.cpu().numpy()
+    ref = FO.farneback_downscaled(FO.gray(fr0), FO.gray(fr1), 2)
+    d = np.abs(got - ref)
+    assert (d > 4e-3).mean() <= 1e-3, float(d.max())
+    c = got[24:-24, 24:-24]
+    assert abs(float(np.median(c[..., 0])) - 4) < 0.1 and abs(float(np.median(c[..., 1])) - 2) < 0.1

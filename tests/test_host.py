@@ -28,8 +28,7 @@ def test_cli_defaults_match_reference():
 
 
 @pytest.mark.parametrize("extra", [["--flow_ema"], ["--model_type", "magenta"],
-                                   ["--device", "cpu"],
-                                   ["--flow_ema", "--flow_method", "farneback", "--flow_downscale", "2"]])
+                                   ["--device", "cpu"], ["--flow_ema", "--flow_method", "dis"]])
 def test_out_of_scope_requests_fail_loudly(extra, tmp_path):
     args = P.build_parser().parse_args(["--model", "x.pth", "--synthetic", "64x48"] + extra)
     with pytest.raises(SystemExit) as e:
