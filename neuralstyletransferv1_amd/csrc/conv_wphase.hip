@@ -25,8 +25,8 @@ namespace nst {
 
 constexpr int WP_RING = 3;  // operand reads in flight ahead of the MFMAs
 
-template <int CINP, int COUT, int TH, int NF>
-struct WpCfg {
+template <int CINP, int COUT, int TH, int NF, int SW = 2>
+struct WpCfg {  // SW: staged tensors per unit (2: the residual join's y and r, 1: y)
   static constexpr int NW = 8, NT = 512;          // wave w: phase w & 3, channel half w >> 2
   static constexpr int TW = 16;                   // source columns per tile = MFMA column block
   static constexpr int NCH = CINP / 8;            // 16-B chunks per pixel
@@ -40,7 +40,7 @@ struct WpCfg {
   static constexpr int QENT = NENT / 4;           // entries per wave and unit (four waves per chunk)
   static constexpr int NFMAX = NF;                // frames per launch (IN tables resident in LDS)
   static constexpr int NSLOT = 4;
-  static constexpr int SLOTB = 2 * NW * 1024;     // [y | r] x wave x lane x 16 B
+  static constexpr int SLOTB = SW * NW * 1024;    // [y | r] x wave x lane x 16 B
   static constexpr int MAPB = ((LH + LW) * 4 + 15) / 16 * 16;
   static constexpr int MAP_OFF = NENT * EB;
   static constexpr int NORM_OFF = MAP_OFF + 2 * MAPB;        // [y | r][frame][chunk]{scale[8], shift[8]}
@@ -70,7 +70,7 @@ struct WpCfg {
 
 template <int CINP, int COUT, int TH, int NF, int FILL, bool ZPAD>
 __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
-  using C = WpCfg<CINP, COUT, TH, NF>;
+  using C = WpCfg<CINP, COUT, TH, NF, (FILL >= WF_RES) ? 2 : 1>;
   constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
   constexpr int U = C::NUNIT, NS = C::NSUBW;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
 
 template <int CINP, int COUT, int TH, int NF, bool RES>
 struct WphaseInst {
-  using C = WpCfg<CINP, COUT, TH, NF>;
+  using C = WpCfg<CINP, COUT, TH, NF, RES ? 2 : 1>;
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;
@@ -486,7 +486,7 @@ const ConvKernelInfo* conv_table_wphase(int* count) {
       //  CINP COUT TH NF RES
       E(128, 64, WP1_TH, WP1_NF, false),  // deconv1 / up1
       E(128, 64, WP1_TH, WP1_NF, true),   // deconv1 joining the last residual block (fused join)
-      E(64, 32, 8, 16, false),                    // deconv2 / up2
+      E(64, 32, 12, 8, false),                    // deconv2 / up2: 12 rows (540 = 45 tiles) fit with one-tensor slots
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;
