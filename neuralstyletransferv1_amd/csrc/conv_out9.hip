@@ -27,6 +27,7 @@
 namespace nst {
 
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) uint64_t lds_u64;  // volatile LDS loads: never merged
 
 template <int CINP, int G, int NW>
 struct Out9Cfg {
@@ -42,7 +43,10 @@ struct Out9Cfg {
   // weight table: [part p][block (kx, kc)][K half h][row i = 3*ky + c] x 8 bytes (4 bf16); a lane's
   // 16-B A fragment is two ds_read_b64 (parts 0 and 1, PART_BYTES apart).  The 32 lanes of one
   // half read 27 different rows (the rotation permutes them), i.e. 27 consecutive 8-B slots: no
-  // bank conflict for any rotation; the 5 unused rows re-read row 0's address (broadcast).
+  // bank conflict for any rotation (ds_read_b64 banks 32-lane groups mod 64 dwords); the 5 unused
+  // rows re-read row 0's address (broadcast).  The two reads stay separate instructions: hipcc
+  // would merge them into one ds_read2_b64, which banks 16-lane groups mod 32 dwords, where rows
+  // r and r + 16 collide.
   static constexpr int NBLK = 9 * KC;
   static constexpr int BLK_BYTES = 2 * 27 * 8;
   static constexpr int PART_BYTES = NBLK * BLK_BYTES;
@@ -51,6 +55,10 @@ struct Out9Cfg {
   static constexpr int LDS = W_OFF + W_BYTES;
   static constexpr int ITEMS = LWS * NCH;         // 16-B loads per strip row
   static constexpr int IPL = (ITEMS + 63) / 64;   // per lane
+  // fill item lane + 64 j = chunk lane / PPJ of column PPJ j + lane % PPJ: the 8 lanes of a
+  // ds_write_b128 group write one chunk of 8 consecutive columns, 8 distinct 16-B bank slots (EB is an
+  // odd number of them); a wave's load still covers PPJ whole pixels
+  static constexpr int PPJ = 64 / NCH;
   static_assert(64 % NCH == 0, "a lane keeps one channel chunk");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
@@ -58,7 +66,7 @@ struct Out9Cfg {
 template <int CINP, int G, int NW, int OUTK, bool TANH>
 __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   using C = Out9Cfg<CINP, G, NW>;
-  constexpr int KC = C::KC, NCH = C::NCH, EB = C::EB;
+  constexpr int KC = C::KC, EB = C::EB;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: work-item math in SGPRs
@@ -101,17 +109,16 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   // B operand (pixels): column rho of the 32-column group, K half h
   char* ring = smem + wave * C::WAVE_LDS;
   const int b_lane = rho * EB + 16 * h;
-  // fill: item i = lane + 64*j -> strip column i / NCH, chunk lane % NCH (fixed per lane)
-  const int chunk = lane % NCH;
+  // fill: item lane + 64*j -> strip column PPJ*j + lane % PPJ, chunk lane / PPJ (fixed per lane)
+  const int chunk = lane / C::PPJ;
   const int pix_bytes = p.cs * 2;
   const int row_bytes = p.ws * pix_bytes;
   int coloff[C::IPL];
 #pragma unroll
   for (int j = 0; j < C::IPL; ++j) {
-    const int i = lane + 64 * j;
-    const int col = i / NCH;
+    const int col = C::PPJ * j + lane % C::PPJ;
     const int sx = map_axis(x0 + p.crop_x - p.pad + col, p.ws, p.axis_mode, p.pre);
-    coloff[j] = (i < C::ITEMS && sx >= 0) ? sx * pix_bytes + chunk * 16 : -1;
+    coloff[j] = (col < C::LWS && sx >= 0) ? sx * pix_bytes + chunk * 16 : -1;
   }
   float2 nm[8];
 #pragma unroll
@@ -136,13 +143,13 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   };
   // zero padding stays zero (the pad applies after the producer's IN + ReLU)
   auto store_row = [&](int v, int ro) {
-    char* dst = ring + (v & 1) * C::ROWB + (lane / NCH) * EB + chunk * 16;
+    char* dst = ring + (v & 1) * C::ROWB + (lane % C::PPJ) * EB + chunk * 16;
 #pragma unroll
     for (int j = 0; j < C::IPL; ++j) {
-      if (lane + 64 * j < C::ITEMS) {
+      if (C::PPJ * j + lane % C::PPJ < C::LWS) {
         const bool ok = ro >= 0 && coloff[j] >= 0;
         const uint4 v4 = norm_chunk<__bf16>(raw[j], nm);
-        *(uint4*)(dst + j * (64 / NCH) * EB) = ok ? v4 : make_uint4(0u, 0u, 0u, 0u);
+        *(uint4*)(dst + j * C::PPJ * EB) = ok ? v4 : make_uint4(0u, 0u, 0u, 0u);
       }
     }
   };
@@ -209,9 +216,9 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
       auto ld = [&](int kx, uint4 (&a)[KC], uint4 (&b)[KC][G]) {
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
-          const uint2 a0 = *(const uint2*)(ab + (kx * KC + kc) * C::BLK_BYTES);
-          const uint2 a1 = *(const uint2*)(ab + (kx * KC + kc) * C::BLK_BYTES + C::PART_BYTES);
-          a[kc] = make_uint4(a0.x, a0.y, a1.x, a1.y);
+          const uint64_t a0 = *(const volatile lds_u64*)(ab + (kx * KC + kc) * C::BLK_BYTES);
+          const uint64_t a1 = *(const volatile lds_u64*)(ab + (kx * KC + kc) * C::BLK_BYTES + C::PART_BYTES);
+          a[kc] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
 #pragma unroll
           for (int gi = 0; gi < G; ++gi) b[kc][gi] = *(const uint4*)(rb + (gi * 32 + kx) * EB + kc * 32);
         }
