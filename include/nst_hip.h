@@ -38,6 +38,7 @@ extern "C" {
 #define NST_ARCH_JOHNSON 0 /* transformer_net.py:4-41 */
 #define NST_ARCH_NST 1     /* transformer_net_nst.py:62-127 */
 #define NST_ARCH_RECONET 2 /* model.py:107-116 (frn=False, as pipeline.py:602 builds it) */
+#define NST_ARCH_RECONET_FRN 3 /* model.py:107-116 with frn=True: FRN + TLU (frn.py:7-78) */
 
 /* ---- compute dtypes ---- */
 #define NST_DT_F32 0  /* fp32 "parity" mode: exact-f32 MFMA (v_mfma_f32_16x16x4_f32) */

@@ -78,6 +78,8 @@ struct Layer {
   float* bias_rev = nullptr;
   float* gamma = nullptr;
   float* beta = nullptr;
+  float eps = 1e-5f;  // InstanceNorm2d eps, or |FRN.eps|
+  int frn = 0;        // statistics: mean / variance (InstanceNorm) or mean square (FRN, frn.py:71)
   bool prepad = false;  // image layer reading the pre-padded encoded input (conv_prep.hip)
 };
 
@@ -94,6 +96,7 @@ struct Op {
 };
 
 static int round_up(int v, int a) { return (v + a - 1) / a * a; }
+static bool is_reconet(int arch) { return arch == NST_ARCH_RECONET || arch == NST_ARCH_RECONET_FRN; }
 
 // x0_export (with fuse_res): block 1's conv1 also writes x_0 = ReLU(IN_2(C)) from its fill (only the
 // weight-stationary trunk kernel does), so block 2's join reads a stored x_0 like every later join
@@ -140,7 +143,7 @@ static void build_program(int arch, bool fuse_res, bool x0_export, std::vector<L
     L.push_back({"up2.conv", "up2.norm", 64, 32, 3, 1, AX_ZINSERT, 1, 0, true});
     L.push_back({"final", "", 32, 3, 9, 1, AX_ZERO, 4, 0, false});
   } else {
-    // model.py:69-116, frn=False
+    // model.py:69-116 (FRN at the InstanceNorm's index, frn=True)
     L.push_back({"encoder.layers.0.layers.0.layers.1", "encoder.layers.0.layers.1", 3, 48, 9, 1, AX_REFLECT, 4, 0, false});
     L.push_back({"encoder.layers.1.layers.0.layers.1", "encoder.layers.1.layers.1", 48, 96, 3, 2, AX_REFLECT, 1, 0, false});
     L.push_back({"encoder.layers.2.layers.0.layers.1", "encoder.layers.2.layers.1", 96, 192, 3, 2, AX_REFLECT, 1, 0, false});
@@ -153,8 +156,8 @@ static void build_program(int arch, bool fuse_res, bool x0_export, std::vector<L
     L.push_back({"decoder.layers.3.layers.0.layers.1", "decoder.layers.3.layers.1", 96, 48, 3, 1, AX_REFLECT_UP2, 1, 0, false});
     L.push_back({"decoder.layers.4.layers.0.layers.1", "", 48, 3, 9, 1, AX_REFLECT, 4, 0, false});
   }
-  const int nres = arch == NST_ARCH_RECONET ? 4 : 5;
-  const int relu_out = arch == NST_ARCH_RECONET ? 1 : 0;  // ReCoNet ResLayer: ReLU after the add
+  const int nres = is_reconet(arch) ? 4 : 5;
+  const int relu_out = is_reconet(arch) ? 1 : 0;  // ReCoNet ResLayer: ReLU (TLU) after the add
   const int u1 = 3 + 2 * nres, u2 = u1 + 1, fin = u1 + 2;
   conv(0, B_IMG, B_A, -1);
   conv(1, B_A, B_B, 0);
@@ -648,6 +651,67 @@ bool decode_consts_for_preset(int preset, DecodeConsts& d) {
 void tile_grid_of(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx, int* ty) {
   tile_grid(k, sh, sw, oh, ow, tx, ty);
 }
+// ReCoNet(frn=True) (model.py:18-60 with frn.py:7-78): every FRN / TLU pair runs as the InstanceNorm
+// / ReLU machinery with shifted activations.  TLU max(v, tau) = ReLU(v - tau) + tau, so the engine keeps
+// z' = z - tau wherever the reference keeps a TLU output z:
+//   * a ConvNormLayer with TLU: FRN shift beta - tau (the fill's ReLU then yields z');
+//   * a ResLayer's join x' = ReLU(FRN(y) + x'_prev + tau_prev - tau_act): shift beta + tau_prev - tau_act
+//     on the branch's second (activation-free) FRN;
+//   * every conv reading a z' adds sum_{c,ky,kx} W[o][c][ky][kx] tau_c to its bias: with reflection
+//     padding and nearest x2 upsampling a per-channel constant image stays constant, so
+//     conv(z) = conv(z') + that sum everywhere.
+// Layer indices: 0-2 encoder ConvNormLayers, 3 + 2r / 4 + 2r the branch of ResLayer r, 11 / 12 the
+// decoder ConvNormLayers, 13 the ConvTanhLayer.
+template <typename Get>
+int frn_layer(Get& get, int li, const LayerDef& d, const float* W, const float* b, const float* bt,
+              std::vector<float>& b_fold, std::vector<float>& bt_fold, float& eps) {
+  auto act_tau = [](int l) -> std::string {  // TLU after layer l's FRN
+    if (l <= 2) return "encoder.layers." + std::to_string(l) + ".layers.2.tau";
+    if (l <= 10) return "encoder.layers." + std::to_string(3 + (l - 3) / 2) + ".branch.0.layers.2.tau";
+    return l == 11 ? "decoder.layers.1.layers.2.tau" : "decoder.layers.3.layers.2.tau";
+  };
+  auto block_tau = [](int r) { return "encoder.layers." + std::to_string(3 + r) + ".activation.tau"; };
+  auto stream_tau = [&](int r) { return r == 0 ? act_tau(2) : block_tau(r - 1); };  // the stream entering block r
+  std::string in_tau;  // the TLU whose output this conv reads
+  if (li == 1 || li == 2) in_tau = act_tau(li - 1);
+  else if (li >= 3 && li <= 10) in_tau = (li - 3) % 2 == 0 ? stream_tau((li - 3) / 2) : act_tau(li - 1);
+  else if (li == 11) in_tau = block_tau(3);
+  else if (li >= 12) in_tau = act_tau(li - 1);
+  const float* tin = nullptr;
+  int rc = NST_OK;
+  if (!in_tau.empty() && (rc = get(in_tau, d.cin, &tin)) != NST_OK) return rc;
+  b_fold.assign(b, b + d.cout);
+  if (tin) {
+    const int kk = d.ks * d.ks;
+    for (int o = 0; o < d.cout; ++o) {
+      double s = b[o];
+      for (int c = 0; c < d.cin; ++c) {
+        double wsum = 0.0;
+        for (int t = 0; t < kk; ++t) wsum += W[((size_t)o * d.cin + c) * kk + t];
+        s += wsum * (double)tin[c];
+      }
+      b_fold[o] = (float)s;
+    }
+  }
+  if (d.norm.empty()) return NST_OK;
+  const float* e = nullptr;
+  if ((rc = get(d.norm + ".eps", 1, &e)) != NST_OK) return rc;
+  eps = std::fabs(e[0]);  // nu2 + eps.abs() (frn.py:74)
+  bt_fold.assign(bt, bt + d.cout);
+  const bool join = li >= 3 && li <= 10 && (li - 3) % 2 == 1;
+  const float *t_own = nullptr, *t_prev = nullptr;
+  if (join) {
+    const int r = (li - 3) / 2;
+    if ((rc = get(block_tau(r), d.cout, &t_own)) != NST_OK) return rc;
+    if ((rc = get(stream_tau(r), d.cout, &t_prev)) != NST_OK) return rc;
+  } else if ((rc = get(act_tau(li), d.cout, &t_own)) != NST_OK) {
+    return rc;
+  }
+  for (int c = 0; c < d.cout; ++c)
+    bt_fold[c] = (float)((double)bt[c] - (double)t_own[c] + (t_prev ? (double)t_prev[c] : 0.0));
+  return NST_OK;
+}
+
 }  // namespace nst
 
 extern "C" {
@@ -662,7 +726,7 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
 
 int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                   unsigned flags, nst_handle** out) {
-  if (!out || arch < 0 || arch > 2 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16) ||
+  if (!out || arch < 0 || arch > 3 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16) ||
       (flags & ~(unsigned)NST_KSEL_ALL) != 0) {
     set_error("nst_create: invalid arguments");
     return NST_E_INVALID;
@@ -716,7 +780,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     std::vector<int> modes;
     // x2 up-convs: weight-stationary phase kernel (conv_wphase.hip) where compiled; its fused join
     // has no ReLU after the sum (ReCoNet's has), so ReCoNet's residual consumers skip it
-    if (up && !(res_layer[li] && arch == NST_ARCH_RECONET) && !(flags & NST_KSEL_NO_WPHASE))
+    if (up && !(res_layer[li] && is_reconet(arch)) && !(flags & NST_KSEL_NO_WPHASE))
       modes.push_back(MODE_WPHASE);
     if (up) modes.push_back(MODE_PHASE);
     if (final_layer && d.cout == 3) {
@@ -725,7 +789,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     }
     // residual-trunk convs (128 -> 128, 3x3): weight-stationary kernel (conv_wstat.hip); ReCoNet's
     // trunk is 192 channels and its join has a ReLU after the sum, so it never matches
-    if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 1 && arch != NST_ARCH_RECONET &&
+    if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 1 && !is_reconet(arch) &&
         !(flags & NST_KSEL_NO_WSTAT))
       modes.push_back(MODE_WSTAT);
     // stride-2 down-convs: weight-stationary kernel (conv_ws2.hip) where compiled
@@ -750,7 +814,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk, 0, no_pers);
       if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW, 0, no_pers);
       const bool tanh_ok = mode != MODE_KYROT || !Ly.k_main ||
-                           (Ly.k_main->tanh_out == (arch == NST_ARCH_RECONET ? 1 : 0) && Ly.k_alt &&
+                           (Ly.k_main->tanh_out == (is_reconet(arch) ? 1 : 0) && Ly.k_alt &&
                             Ly.k_alt->tanh_out == Ly.k_main->tanh_out);
       if (Ly.k_main && tanh_ok && (!(image_in || final_layer) || Ly.k_alt)) { Ly.mode = mode; break; }
       Ly.k_main = nullptr;
@@ -768,6 +832,13 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     if (!final_layer) {
       if ((rc = get(d.norm + ".weight", d.cout, &gm)) != NST_OK) break;
       if ((rc = get(d.norm + ".bias", d.cout, &bt)) != NST_OK) break;
+    }
+    std::vector<float> b_fold, bt_fold;
+    if (arch == NST_ARCH_RECONET_FRN) {
+      if ((rc = frn_layer(get, (int)li, d, W, b, bt, b_fold, bt_fold, Ly.eps)) != NST_OK) break;
+      b = b_fold.data();
+      if (!final_layer) bt = bt_fold.data();
+      Ly.frn = final_layer ? 0 : 1;
     }
     auto upload_packed = [&](const std::vector<float>& pk, void** dst) -> int {
       if (compute_dtype == NST_DT_BF16) {
@@ -965,7 +1036,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       p.pad = 0;
       p.pre = 0;
     }
-    p.dec_tanh = (h->arch == NST_ARCH_RECONET && final_out) ? 1 : 0;
+    p.dec_tanh = (is_reconet(h->arch) && final_out) ? 1 : 0;
     p.wpk = Ly.wpk;
     p.bias = Ly.bias;
     if (Ly.mode == MODE_XSHIFT && final_out && y_fmt == NST_IO_U8_NHWC && pc.dperm[0] == 2) {
@@ -1025,7 +1096,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     if (e != hipSuccess) { set_error("conv " + Ly.d.conv + " launch: " + hipGetErrorString(e)); return NST_E_HIP; }
     if (!final_out) {
       e = launch_in_finalize(partial, n, p.tiles_x * p.tiles_y * k->part_rows, Ly.coutp, (double)p.hconv * (double)p.wconv,
-                             Ly.gamma, Ly.beta, 1e-5f, stats[op.layer], ws + P.off_seg, st);
+                             Ly.gamma, Ly.beta, Ly.eps, Ly.frn, stats[op.layer], ws + P.off_seg, st);
       if (e != hipSuccess) { set_error(std::string("finalize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
     }
     if (cap && !final_out) {

@@ -125,7 +125,7 @@ constexpr int IN_MAX_SEGMENTS = 128;
 int in_finalize_segments(int tiles);
 // seg_ws: n * IN_MAX_SEGMENTS * cstride * 16 bytes of scratch
 hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
-                              const float* gamma, const float* beta, float eps, float2* out,
+                              const float* gamma, const float* beta, float eps, int frn, float2* out,
                               void* seg_ws, hipStream_t st);
 hipError_t launch_residual(int dtype, const void* y, const float2* ys, const void* r,
                            const float2* rs, int r_relu, int relu_out, void* out, int n, int hw,

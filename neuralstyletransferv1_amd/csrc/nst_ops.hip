@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void in_partial_reduce_kernel(const float* __r
 
 __global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restrict__ seg, int nseg, int cstride,
                                                           double count, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float eps,
+                                                          const float* __restrict__ beta, float eps, int frn,
                                                           float2* __restrict__ out) {
   // 64 channels x 4 segment phases per block (the segments' loads in flight together), then a
   // fixed-order LDS combine: deterministic
@@ -82,7 +82,8 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restr
   if (q != 0 || c >= cstride) return;
   s1 = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
   s2 = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
-  const double mean = s1 / count;
+  // FRN (frn.py:71-74): nu2 = mean(x^2), x * rsqrt(nu2 + |eps|), then weight * x + bias
+  const double mean = frn ? 0.0 : s1 / count;
   double var = s2 / count - mean * mean;
   var = var < 0.0 ? 0.0 : var;
   const double rstd = 1.0 / sqrt(var + (double)eps);
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restr
 int in_finalize_segments(int tiles) { return max(1, min(IN_MAX_SEGMENTS, tiles / 64)); }
 
 hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
-                              const float* gamma, const float* beta, float eps, float2* out,
+                              const float* gamma, const float* beta, float eps, int frn, float2* out,
                               void* seg_ws, hipStream_t st) {
   const int nseg = in_finalize_segments(tiles);
   const int per_seg = (tiles + nseg - 1) / nseg;
@@ -102,7 +103,7 @@ hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstrid
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(in_finalize_kernel, dim3(n, (cstride + 63) / 64), dim3(256), 0, st, (const double2*)seg_ws,
-                     nseg, cstride, count, gamma, beta, eps, out);
+                     nseg, cstride, count, gamma, beta, eps, frn, out);
   return hipGetLastError();
 }
 

@@ -6,6 +6,8 @@ reference's exact state_dict names/shapes, and are output-calibrated so the styl
 image spans the io_preset's range instead of collapsing to black:
   * every conv before an InstanceNorm: N(0, 2/fan_in); bias U(-0.05, 0.05)
   * InstanceNorm affine: gamma U(0.8, 1.2), beta U(-0.2, 0.2)
+  * reconet_frn (ReCoNet(frn=True)): FRN weight U(0.8, 1.2), bias U(-0.2, 0.2), eps 1e-6 (seed 0) or
+    -1e-3 (other seeds: |eps| is what FRN adds); TLU tau U(-0.3, 0.3)
   * the output conv: std chosen so the raw output has std ~TARGET_STD around TARGET_MEAN
     (Johnson raw/imagenet_255: 127.5 +- 60; NST raw_01: 0.5 +- 0.25; ReCoNet pre-tanh: 0 +- 1).
 Frames: smooth gradients + shapes + low-amplitude noise so InstanceNorm statistics are
@@ -18,8 +20,8 @@ from typing import Dict
 import numpy as np
 import torch
 
-ARCHS = ("johnson", "nst", "reconet")
-_OUTPUT_CAL = {"johnson": (127.5, 60.0), "nst": (0.5, 0.25), "reconet": (0.0, 1.0)}
+ARCHS = ("johnson", "nst", "reconet", "reconet_frn")
+_OUTPUT_CAL = {"johnson": (127.5, 60.0), "nst": (0.5, 0.25), "reconet": (0.0, 1.0), "reconet_frn": (0.0, 1.0)}
 
 
 def build_module(arch: str):
@@ -29,14 +31,15 @@ def build_module(arch: str):
     if arch == "nst":
         from .transformer_net_nst import TransformerNet
         return TransformerNet()
-    if arch == "reconet":
+    if arch in ("reconet", "reconet_frn"):
         from .model import ReCoNet
-        return ReCoNet()
+        return ReCoNet(frn=arch == "reconet_frn")
     raise ValueError(f"unknown arch {arch!r}")
 
 
 def _final_conv_name(arch: str) -> str:
-    return {"johnson": "deconv3.conv2d", "nst": "final", "reconet": "decoder.layers.4.layers.0.layers.1"}[arch]
+    return {"johnson": "deconv3.conv2d", "nst": "final", "reconet": "decoder.layers.4.layers.0.layers.1",
+            "reconet_frn": "decoder.layers.4.layers.0.layers.1"}[arch]
 
 
 def make_state_dict(arch: str, seed: int = 0) -> Dict[str, torch.Tensor]:
@@ -53,6 +56,14 @@ def make_state_dict(arch: str, seed: int = 0) -> Dict[str, torch.Tensor]:
             v = rng.standard_normal(shape) * (std / np.sqrt(fan_in * 0.5))
         elif name == final + ".bias":
             v = mean + rng.uniform(-0.02, 0.02, shape) * max(std, 1e-3)
+        elif name.endswith(".tau"):  # TLU threshold [1, C, 1, 1]
+            v = rng.uniform(-0.3, 0.3, shape)
+        elif name.endswith(".eps"):  # FRN eps buffer [1]
+            v = np.full(shape, 1e-6 if seed == 0 else -1e-3)
+        elif len(shape) == 4 and shape[0] == 1 and shape[2:] == (1, 1) and name.endswith(".weight"):  # FRN gamma
+            v = rng.uniform(0.8, 1.2, shape)
+        elif len(shape) == 4 and shape[0] == 1 and shape[2:] == (1, 1) and name.endswith(".bias"):  # FRN beta
+            v = rng.uniform(-0.2, 0.2, shape)
         elif len(shape) == 4:
             # Conv2d [out,in,k,k]; ConvTranspose2d [in,out,k,k] (fan_in = out*k*k seen per output)
             fan_in = shape[1] * shape[2] * shape[3]

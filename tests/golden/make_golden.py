@@ -1,7 +1,7 @@
 """Generate tests/golden/*.npz from the REFERENCE modules (run in the build container only;
 /root/reference does not exist on the GPU box and nothing at test time reads it).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [arch ...]   (only those model cases)
 
 For each architecture the reference class itself (transformer_net.py / transformer_net_nst.py /
 model.py, imported from /root/reference) is instantiated, loaded with the seeded synthetic
@@ -34,6 +34,8 @@ CASES = [
     ("nst", 1, 1, 72, 100, "raw_01"),
     ("reconet", 0, 1, 64, 64, "imagenet_01"),
     ("reconet", 1, 1, 48, 84, "tanh"),
+    ("reconet_frn", 0, 1, 64, 64, "imagenet_01"),   # ReCoNet(frn=True): FRN + TLU (frn.py)
+    ("reconet_frn", 1, 2, 48, 84, "tanh"),
 ]
 
 
@@ -55,7 +57,7 @@ def ref_module(arch):
             import transformer_net_nst as m
             return m.TransformerNet()
         import model as m
-        return m.ReCoNet()
+        return m.ReCoNet(frn=arch == "reconet_frn")
     finally:
         sys.path.remove(REF)
 
@@ -75,9 +77,11 @@ def encode_for(x01: torch.Tensor, preset: str) -> torch.Tensor:
     return x01 * 255.0
 
 
-def main():
+def main(only=()):
     torch.set_num_threads(8)
     for arch, seed, n, h, w, preset in CASES:
+        if only and arch not in only:
+            continue
         sd = synthetic.make_state_dict(arch, seed)
         net = ref_module(arch)
         missing, unexpected = net.load_state_dict(sd, strict=False)
@@ -92,6 +96,8 @@ def main():
         np.savez_compressed(path, x=x.numpy(), y=y.numpy(), frames=frames, seed=seed, preset=preset,
                             weights_sha=weights_sha(sd), torch_version=torch.__version__)
         print(f"{path}: x{tuple(x.shape)} -> y{tuple(y.shape)} range [{float(y.min()):.3f}, {float(y.max()):.3f}]")
+    if only:
+        return
 
     sys.path.insert(0, REF)
     import utils as ref_utils
@@ -118,4 +124,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -23,8 +23,8 @@ FP32_REL_TOL = 1e-4
 BF16_SSIM_MIN = 0.98
 
 
-def _arch(path):
-    return os.path.basename(path).split("_")[1]
+def _arch(path):  # model_<arch>_s<seed>_<h>x<w>.npz (arch may hold "_": reconet_frn)
+    return os.path.basename(path)[len("model_"):].rsplit("_s", 1)[0]
 
 
 def _net(arch, seed, dtype, ksel=()):
@@ -62,6 +62,26 @@ def test_frames_u8_vs_oracle(path):
     out16 = _net(arch, seed, "bf16").stylize_frames(f_dev, preset).cpu().numpy()
     for i in range(frames.shape[0]):
         assert O.ssim(out16[i], ref[i]) >= BF16_SSIM_MIN
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_reconet_frn_ragged_vs_oracle(seed):
+    """ReCoNet(frn=True) (model.py with frn.py): FRN's mean-square statistics and |eps|, and the TLU
+    thresholds the engine folds into shifted activations, join shifts and conv biases, at a ragged
+    size (61 x 90 -> 64 x 92 output) against the oracle (bit-exact to the reference module's
+    goldens).  fp32: 1e-4 of the output magnitude; bf16 (a sanity bar; the frames tests hold the
+    SSIM >= 0.98 bar): mean |d| < 2.5e-2 on the [-1, 1] tanh output (measured 1.2e-2)."""
+    sd = synthetic.make_state_dict("reconet_frn", seed)
+    x = O.encode(O.to_tensor01(synthetic.make_frames(2, 61, 90, seed=40 + seed)), "imagenet_01")
+    ref = O.forward("reconet_frn", sd, x).numpy()
+    y = _net("reconet_frn", seed, "fp32")(x.cuda()).cpu().numpy()
+    assert y.shape == ref.shape
+    assert np.abs(y - ref).max() <= FP32_REL_TOL * np.abs(ref).max()
+    y16 = _net("reconet_frn", seed, "bf16")(x.cuda()).cpu().numpy()
+    assert np.abs(y16 - ref).mean() < 2.5e-2
+    # the thresholds matter: the same net with tau = 0 is a different function
+    sd0 = {k: (torch.zeros_like(v) if k.endswith(".tau") else v) for k, v in sd.items()}
+    assert np.abs(O.forward("reconet_frn", sd0, x).numpy() - ref).max() > 1e-2
 
 
 def test_1080p_fp32_and_bf16_vs_oracle():
@@ -219,7 +239,7 @@ def test_bf16_output_conv_mappings_agree(arch, h, w, preset):
     assert np.abs(ya - yb).max() <= 1e-4 * np.abs(yb).max() + 1e-6
 
 
-@pytest.mark.parametrize("arch", ["johnson", "nst", "reconet"])
+@pytest.mark.parametrize("arch", ["johnson", "nst", "reconet", "reconet_frn"])
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 def test_fused_residual_join_bit_exact(arch, dtype):
     """The residual add fused into the next conv's fill (VAR_RES, x_{k+1} written by that conv for
@@ -236,7 +256,7 @@ def test_fused_residual_join_bit_exact(arch, dtype):
     assert torch.equal(ya, yb)
 
 
-@pytest.mark.parametrize("arch", ["johnson", "nst", "reconet"])
+@pytest.mark.parametrize("arch", ["johnson", "nst", "reconet", "reconet_frn"])
 def test_prepadded_image_layer_bit_exact(arch):
     """bf16 first layer over the pre-padded encoded input (conv_prep.hip) against the encode fused
     into the conv's fill: same per-element arithmetic and the same LDS image, so bit-identical

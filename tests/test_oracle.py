@@ -13,8 +13,8 @@ from oracle import nst_oracle as O
 MODEL_GOLDENS = sorted(glob.glob(os.path.join(GOLDEN, "model_*.npz")))
 
 
-def _arch(path):
-    return os.path.basename(path).split("_")[1]
+def _arch(path):  # model_<arch>_s<seed>_<h>x<w>.npz (arch may hold "_": reconet_frn)
+    return os.path.basename(path)[len("model_"):].rsplit("_s", 1)[0]
 
 
 @pytest.mark.parametrize("path", MODEL_GOLDENS, ids=os.path.basename)
