@@ -298,7 +298,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
             *(u32x2_t*)(smem + C::OUT_OFF + ((2 * r + (ph >> 1)) * 2 * C::TW + 2 * px + (ph & 1)) * C::PIXP +
                         (((c0 >> 2) ^ C::swz(2 * px + (ph & 1))) << 3)) = pk;
           } else {
-            __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, ST_AUX);
           }
           const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
           stat4(s1, s2, x);
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
             *(const u32x4_t*)(smem + C::OUT_OFF + (row * 2 * C::TW + pix) * C::PIXP + (((cb >> 3) ^ C::swz(pix)) << 3));
         const int oy = oyb + row, ox = ox0 + pix;
         const bool ok = oy < p.oh && ox < p.ow;
-        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, ST_AUX);
       }
     }
   };

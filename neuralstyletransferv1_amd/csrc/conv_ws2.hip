@@ -257,7 +257,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
       const int x = pp % C::TW, oy = wk.oy0 + pp / C::TW, ox = wk.ox0 + x;
       const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * C::PIXB + (((cb >> 3) ^ (2 * (x & 7))) << 3));
       const bool ok = oy < p.oh && ox < p.ow;
-      __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, ST_AUX);
     }
   };
 

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
     for (int k = 0; k < C::NST; ++k) {  // store k = tile row k
       const u32x4_t v = *(const u32x4_t*)(smem + srd + k * C::TW * C::PIXB);
       if (wk_.oy0 + k < p.oh)
-        __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + k) * p.ow * C::PIXB, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + k) * p.ow * C::PIXB, ST_AUX);
     }
   };
 

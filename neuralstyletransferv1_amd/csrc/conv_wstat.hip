@@ -248,7 +248,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     const u32x4_t v = *(const u32x4_t*)(smem + ((r + 1) * C::LW + x + 1) * C::EB + c * 16);
     const bool ok = oy < p.oh && ox < p.ow;
     __builtin_amdgcn_raw_buffer_store_b128(v, launch_rsrc(p.res_out, fb),
-                                           ok ? (uint32_t)wk.n * fb + (uint32_t)(((oy * p.ws + ox) * p.cs + c * 8) * 2) : OOB, 0, 0);
+                                           ok ? (uint32_t)wk.n * fb + (uint32_t)(((oy * p.ws + ox) * p.cs + c * 8) * 2) : OOB, 0, ST_AUX);
   };
   constexpr int DPU = RES ? 2 : 1;                // requests per unit
   constexpr int KIN = 3 * DPU + (SOUT ? 2 : 0);   // vmcnt before a unit whose wait spans no epilogue
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         if constexpr (C::OST) {
           *(u32x2_t*)(smem + obase + r * C::TW * 256) = pk;
         } else {
-          __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : OOB, 0, ST_AUX);
         }
         const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
         stat4(s1, s2, x);
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
         const int x = pp & (C::TW - 1), oy = wk.ty0 + pp / C::TW, ox = wk.tx0 + x;
         const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * 256 + (((cb >> 3) ^ (2 * (x & 7))) << 3));
         const bool ok = oy < p.oh && ox < p.ow;
-        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? fo + (uint32_t)((oy * p.ow + ox) * 256 + cb) : OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? fo + (uint32_t)((oy * p.ow + ox) * 256 + cb) : OOB, 0, ST_AUX);
       }
     }
   };
