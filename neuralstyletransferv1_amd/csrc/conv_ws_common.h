@@ -30,10 +30,7 @@ __device__ __forceinline__ void stat4(f32x4_t& s1, f32x4_t& s2, const f32x4_t& x
 // cache policy of the activation stores: nt (streaming).  A store holds vmcnt until the L2 has taken
 // it, and every later unit wait counts it (in-order), so the trunk's output and residual-stream
 // stores sit in front of the next tile's loads; streaming stores measured ~1 % faster per step.
-#ifndef NST_ST_AUX
-#define NST_ST_AUX 2
-#endif
-constexpr int ST_AUX = NST_ST_AUX;
+constexpr int ST_AUX = 2;
 
 // what the fill applies to a staged input chunk
 // (join of ReLU(IN(r)): r normalised as a WF_NORM fill stages it, bf16-rounded)
