@@ -29,7 +29,7 @@ __device__ __forceinline__ void stat4(f32x4_t& s1, f32x4_t& s2, const f32x4_t& x
 
 // cache policy of the activation stores: nt (streaming).  A store holds vmcnt until the L2 has taken
 // it, and every later unit wait counts it (in-order), so the trunk's output and residual-stream
-// stores sit in front of the next tile's loads; streaming stores measured ~2 % faster per step.
+// stores sit in front of the next tile's loads; streaming stores measured ~1 % faster per step.
 constexpr int ST_AUX = 2;
 
 // what the fill applies to a staged input chunk
