@@ -1,4 +1,4 @@
-"""Secondary timings: the three architectures at 1080p, batch 8, bf16 (frames/s per GPU, HBM-resident
+"""Secondary timings: the three architectures (and ReCoNet(frn=True)) at 1080p, batch 8, bf16 (frames/s per GPU, HBM-resident
 uint8 frames, same step as bench.py).  Not part of the bench contract; numbers quoted in DESIGN.md."""
 import os, sys, time
 import torch
@@ -7,7 +7,7 @@ from neuralstyletransferv1_amd import synthetic
 
 dev = torch.device("cuda", 0)
 frames = torch.from_numpy(synthetic.make_frames(8, 1080, 1920, seed=5)).to(dev)
-for arch, preset in (("johnson", "imagenet_255"), ("nst", "raw_01"), ("reconet", "tanh")):
+for arch, preset in (("johnson", "imagenet_255"), ("nst", "raw_01"), ("reconet", "tanh"), ("reconet_frn", "tanh")):
     m = synthetic.build_module(arch)
     m.load_state_dict(synthetic.make_state_dict(arch, 0))
     m = m.to(dev).eval()
