@@ -125,11 +125,13 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   if (tid < COUT) ((float*)(smem + C::BIAS_OFF))[tid] = p.bias[tid];
 
   // ---- halo staging (conv_wstat.hip) ----
-  const size_t frame_bytes = (size_t)p.hs * p.ws * p.cs * 2;
-  auto frame_rsrc = [&](const void* base, int n) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (size_t)n * frame_bytes), (short)0,
-                                             (int)frame_bytes, 0x00020000);
-  };
+  // one buffer resource per tensor for the whole launch (the launcher keeps a launch's frames below
+  // 2^31 bytes): a frame is a 32-bit offset, no 64-bit scalar math per request
+  const uint32_t fb = (uint32_t)p.hs * p.ws * p.cs * 2;
+  const uint32_t launch_bytes = fb * (uint32_t)(p.n_work / ntile);
+  const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc((void*)p.in, (short)0, (int)launch_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? p.res_r : p.in), (short)0, (int)launch_bytes, 0x00020000);
   auto build_maps = [&](const Work& wk, int slot) {
     int* rowmap = (int*)(smem + C::MAP_OFF + slot * C::MAPB);
     int* colmap = rowmap + C::LH;
@@ -163,11 +165,11 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   };
   const uint32_t stg = (uint32_t)(uintptr_t)(smem + C::STG_OFF) + wv * 1024;
   auto request = [&](int n, int u, const Item& it) {
-    const uint32_t voff = (it.valid && it.src >= 0) ? (uint32_t)it.src : 0x80000000u;
+    const uint32_t voff = (it.valid && it.src >= 0) ? (uint32_t)it.src + (uint32_t)n * fb : 0x80000000u;
     const int soff = (2 * u + team) * 16;
     const uint32_t lds = stg + (u % C::NSLOT) * C::SLOTB;
-    dma16(frame_rsrc(p.in, n), voff, lds, soff);
-    if constexpr (RES) dma16(frame_rsrc(p.res_r, n), voff, lds + C::NW * 1024, soff);
+    dma16(rs_in, voff, lds, soff);
+    if constexpr (RES) dma16(rs_r, voff, lds + C::NW * 1024, soff);
   };
   auto consume = [&](const Work& wk, int u, const Item& it) {
     const int ch = 2 * u + team;
@@ -436,8 +438,12 @@ struct WphaseInst {
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
     const int ntile = (int)grid.x, n = (int)grid.y;
     const size_t fin = (size_t)p0.hs * p0.ws * p0.cs * 2, fout = (size_t)p0.oh * p0.ow * p0.cout_stride * 2;
-    for (int f0 = 0; f0 < n; f0 += C::NFMAX) {
-      const int nf = std::min(C::NFMAX, n - f0);
+    // frames per launch: the LDS IN tables' capacity, and a launch's input below 2^31 bytes (32-bit
+    // request offsets; 0x80000000 is the out-of-range offset)
+    const int fmax = (int)std::min<size_t>(C::NFMAX, (size_t)0x7FFFFF00u / std::max<size_t>(fin, 1));
+    if (fmax < 1) return;  // nst_api validates sizes before launching
+    for (int f0 = 0; f0 < n; f0 += fmax) {
+      const int nf = std::min(fmax, n - f0);
       ConvParams p = p0;
       p.in = (const char*)p0.in + f0 * fin;
       p.out = (char*)p0.out + f0 * fout;
