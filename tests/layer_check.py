@@ -30,11 +30,63 @@ def _nchw(t: torch.Tensor, c: int) -> torch.Tensor:
     return t[..., :c].float().cpu().permute(0, 3, 1, 2).contiguous()
 
 
+def _frn_tau_names(li: int):
+    """ReCoNet(frn=True) (model.py with frn.py): the TLU threshold each layer's conv reads (its bias
+    absorbs sum W tau) and the ones its FRN shift absorbs, as nst_api.cpp frn_layer folds them."""
+    def act_tau(l):
+        if l <= 2:
+            return f"encoder.layers.{l}.layers.2.tau"
+        if l <= 10:
+            return f"encoder.layers.{3 + (l - 3) // 2}.branch.0.layers.2.tau"
+        return "decoder.layers.1.layers.2.tau" if l == 11 else "decoder.layers.3.layers.2.tau"
+
+    def block_tau(r):
+        return f"encoder.layers.{3 + r}.activation.tau"
+
+    def stream_tau(r):
+        return act_tau(2) if r == 0 else block_tau(r - 1)
+    in_tau = None
+    if li in (1, 2):
+        in_tau = act_tau(li - 1)
+    elif 3 <= li <= 10:
+        in_tau = stream_tau((li - 3) // 2) if (li - 3) % 2 == 0 else act_tau(li - 1)
+    elif li == 11:
+        in_tau = block_tau(3)
+    elif li >= 12:
+        in_tau = act_tau(li - 1)
+    join = 3 <= li <= 10 and (li - 3) % 2 == 1
+    own = block_tau((li - 3) // 2) if join else (act_tau(li) if li <= 12 else None)
+    prev = stream_tau((li - 3) // 2) if join else None
+    return in_tau, own, prev
+
+
+def _frn_bias(sd, li, W, b):
+    in_tau = _frn_tau_names(li)[0]
+    if in_tau is None:
+        return b
+    t = sd[in_tau].double().flatten()
+    return (b.double() + (W.double().sum(dim=(2, 3)) * t[None, :]).sum(dim=1)).float()
+
+
+def _frn_stats(sd, li, norm, z):
+    """{gamma * rsqrt(mean(z^2) + |eps|), beta - tau_own (+ tau_prev on a join)} (frn.py:71-78)."""
+    _, own, prev = _frn_tau_names(li)
+    zd = z.double()
+    nu2 = (zd * zd).mean(dim=(2, 3))
+    eps = abs(float(sd[norm + ".eps"][0]))
+    scale = sd[norm + ".weight"].double().flatten()[None, :] / torch.sqrt(nu2 + eps)
+    shift = sd[norm + ".bias"].double().flatten() - sd[own].double().flatten()
+    if prev is not None:
+        shift = shift + sd[prev].double().flatten()
+    return torch.stack([scale, shift[None, :].expand_as(scale)], dim=-1).float()
+
+
 def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequence[Tuple[float, int]]] = None,
                  acc: torch.dtype = torch.float32) -> List[Dict]:
     """-> one record per op.  bands: None = every output row; else [(fraction, rows)] row bands
     (start = fraction of the output height, rounded down to even) checked per op (4K frames)."""
-    arch = {0: "johnson", 1: "nst", 2: "reconet"}[net.ARCH]
+    arch = {0: "johnson", 1: "nst", 2: "reconet", 3: "reconet_frn"}[net.ARCH]
+    frn = arch == "reconet_frn"
     sd = {k: v.detach().float().cpu() for k, v in net.state_dict().items()}
     eng = net.engine()
     fr_dev = torch.from_numpy(frames_u8).to(eng.device)
@@ -47,7 +99,7 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
         y_u8, _, _ = eng.forward_capture(fr_dev, "u8", preset, "u8")
         y_u8 = y_u8.cpu().numpy()
     torch.cuda.synchronize()
-    layers = B.LAYERS[arch]
+    layers = B.LAYERS["reconet" if frn else arch]
     host = [{k: (v.cpu() if v is not None else None) for k, v in c.items()} for c in caps]
     writer: Dict[int, Tuple[int, str]] = {}   # buffer -> (op, "act" | "res")
     layer_op: Dict[int, int] = {}            # layer -> conv op that ran it (its stats capture)
@@ -95,10 +147,12 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
             (r0, min(ch, r0 + k)) for f, k in bands for r0 in [min(max(0, int(f * ch)) // 2 * 2, max(0, ch - k) // 2 * 2)]})
         rec = {"op": i, "layer": conv, "mode": d["kernel_mode"], "elements": 0}
         W, bias = sd[conv + ".weight"], sd[conv + ".bias"]
+        if frn:  # TLU outputs are stored shifted by -tau: the bias absorbs sum W tau
+            bias = _frn_bias(sd, d["layer"], W, bias)
         for (r0, r1) in row_sets:
             z = B.conv_layer(get_rows, Hs, n, cin, W, bias, ks, st, axis, pad, pre, True, (r0, r1), acc)
             if final:
-                if arch == "reconet":
+                if arch.startswith("reconet"):
                     z = torch.tanh(z)
                 cy, cx = (d["conv_h"] - d["out_h"]) // 2, (d["conv_w"] - d["out_w"]) // 2
                 lo, hi = max(r0, cy), min(r1, cy + d["out_h"])
@@ -135,7 +189,8 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
                                    f"{ULP_MAX} ulp / atol {atol:.2e}; first at {tuple(bad.nonzero()[0].tolist())}")
             assert rec["ulp1_frac"] <= ULP1_FRAC_MAX, (i, conv, rec["ulp1_frac"])
             if bands is None:  # statistics need the whole frame
-                s_ref = B.in_stats(z, sd[norm + ".weight"], sd[norm + ".bias"])
+                s_ref = (_frn_stats(sd, d["layer"], norm, z) if frn else
+                         B.in_stats(z, sd[norm + ".weight"], sd[norm + ".bias"]))
                 s_got = host[i]["stats"][:, :cout]
                 err = (s_got - s_ref).abs() / s_ref.abs().amax(dim=1, keepdim=True).clamp_min(1e-6)
                 rec["stats_rel"] = float(err.max())

@@ -4,7 +4,7 @@ Every op of the program is recomputed on the CPU from the engine's own stored in
 nst_forward_capture) with the bf16 mode's rounding points (oracle/bf16_layers.py), so each kernel
 is checked alone: conv_ws9 (first layer), conv_ws2 (down-convs), conv_wstat (residual trunk, plain
 and with the fused residual join), conv_wphase (x2 up-convs), conv_out9 (output conv + decode +
-truncation), and on ReCoNet the generic bf16 kernels.  Bars (tests/layer_check.py): stored bf16
+truncation), and on ReCoNet (InstanceNorm and FRN/TLU) the generic bf16 kernels.  Bars (tests/layer_check.py): stored bf16
 outputs within 1 bf16 ulp (or 4e-6 of the layer's max |value| where the sum cancels), <= 0.1 % of
 elements 1 ulp off (measured <= 0.03 %), IN statistics within 1e-5, joined residual streams bit-exact, raw fp32 output
 within 5e-6, u8 frames >= 99.99 % identical and never more than 1 LSB off.
@@ -38,12 +38,13 @@ def _report(recs):
     ("johnson", 1, 64, 96, "imagenet_255"),   # u8 output path (output size == input size)
     ("nst", 1, 72, 100, "raw_01"),            # zero padding, pre-reflect 40, ConvTranspose phases, crop
     ("reconet", 1, 61, 90, "tanh"),           # 48/96/192 channels: generic bf16 kernels + tanh output
+    ("reconet_frn", 1, 61, 90, "tanh"),       # FRN + TLU: mean-square statistics, tau folded into biases / shifts
 ])
 def test_bf16_layers_small(arch, n, h, w, preset):
     frames = synthetic.make_frames(n, h, w, seed=40 + h)
     recs = LC.check_layers(_net(arch, 11), frames, preset, acc=torch.float64)
     _report(recs)
-    assert len(recs) == (14 if arch == "reconet" else 16)
+    assert len(recs) == (14 if arch.startswith("reconet") else 16)
 
 
 def test_bf16_layers_1080p():
