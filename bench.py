@@ -42,6 +42,9 @@ BATCH = 8
 PRESET = "imagenet_255"
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md chip table)
 HBM_PEAK_GBS = 8000.0
+# measured ceilings beside the spec: back-to-back v_mfma_f32_16x16x32_bf16 on random operands
+# at the trunk kernel's occupancy (two waves per SIMD), and a streaming copy, tools/peak_bench.hip
+PEAKS_JSON = "profiles/r02_s7_peaks.json"
 # Algorithmic work: 307,584 FLOP and 822 B (bf16 activations) per output pixel.
 FLOP_PER_PIXEL = 307584
 BYTES_PER_PIXEL = 822
@@ -58,6 +61,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode timing (profiling runs)")
     ap.add_argument("--cpu-frames", type=int, default=3, help="timed 1080p frames per CPU configuration")
+    ap.add_argument("--no-fp16", action="store_true", help="skip the fp16-mode timing")
     return ap.parse_args()
 
 
@@ -84,15 +88,17 @@ def cpu_baseline(frames_u8: np.ndarray, sd, nframes: int):
     """the reference's per-frame path on this host's cores (the oracle = its
     PyTorch-CPU fp32 arithmetic): 1 warm-up frame, then >= 3 timed frames, forward alone (preset ->
     Johnson fwd -> decode/clamp/ToPILImage) and the full chain (+ LAB L-EMA via Pillow/LittleCMS,
-    + blend 0.9 with the original: run_videos.py defaults), at 4 threads (pipeline.py:2172 default)
-    and at this job's CPU share (OMP_NUM_THREADS: 16 cores per GPU on the pool; the host's other
-    cores belong to the other GPUs' jobs)."""
+    + blend 0.9 with the original: run_videos.py defaults), at all physical cores the process may run
+    on (`value`), at this job's CPU share (OMP_NUM_THREADS: 16 cores per GPU on the
+    pool) and at 4 threads (pipeline.py:2172 default)."""
     from oracle import nst_oracle as O
     share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    allc = max(1, min(_physical_cores(), aff))
     prev_threads = torch.get_num_threads()
     runs = {}
     outs = []
-    for threads in (share, 4):
+    for threads in dict.fromkeys((allc, share, 4)):
         torch.set_num_threads(threads)
         ema = O.LabEMA(True, 0.65)
         O.stylize_u8("johnson", sd, frames_u8[:1], PRESET)  # warm-up frame
@@ -107,22 +113,39 @@ def cpu_baseline(frames_u8: np.ndarray, sd, nframes: int):
             t2 = time.perf_counter()
             t_fwd += t1 - t0
             t_post += t2 - t1
-            if threads == share:
+            if threads == allc:
                 outs.append(u8)
         runs[threads] = {"fwd_s_per_frame": t_fwd / nframes, "chain_s_per_frame": (t_fwd + t_post) / nframes}
     torch.set_num_threads(prev_threads)
-    main = runs[share]
+    main = runs[allc]
     return {
-        "value": 1.0 / main["fwd_s_per_frame"], "unit": "frames/s", "cores": share, "kind": "port",
+        "value": 1.0 / main["fwd_s_per_frame"], "unit": "frames/s", "cores": allc, "kind": "port",
         "sample": f"{nframes} timed synthetic 1920x1080 frames after 1 warm-up per configuration; value = forward "
-                  f"alone (preset {PRESET} -> Johnson fwd fp32 -> decode/clamp/ToPILImage) at {share} threads",
+                  f"alone (preset {PRESET} -> Johnson fwd fp32 -> decode/clamp/ToPILImage) at {allc} threads "
+                  f"(all physical cores available to the process)",
         "full_chain_frames_per_s": 1.0 / main["chain_s_per_frame"],
+        "share_threads": share,
+        "share_frames_per_s": 1.0 / runs[share]["fwd_s_per_frame"],
+        "share_full_chain_frames_per_s": 1.0 / runs[share]["chain_s_per_frame"],
         "threads4_frames_per_s": 1.0 / runs[4]["fwd_s_per_frame"],
         "threads4_full_chain_frames_per_s": 1.0 / runs[4]["chain_s_per_frame"],
         "s_per_frame": {str(k): v for k, v in runs.items()},
         "host": {"os_cpu_count": os.cpu_count(), "physical_cores": _physical_cores(),
                  "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None},
     }, outs
+
+
+def _measured_peaks():
+    """The measured MFMA / HBM ceilings kept under profiles/ (mean over its runs), or None."""
+    try:
+        with open(os.path.join(REPO, PEAKS_JSON)) as f:
+            runs = json.load(f)["runs"]
+        mf = float(np.mean([r["mfma_bf16_16x16x32_tflops"]["random_2w"] for r in runs]))
+        hb = float(np.mean([r["hbm_copy_gbs"] for r in runs]))
+        return {"mfma_tflops": round(mf, 1), "hbm_copy_gbs": round(hb, 1), "source": PEAKS_JSON,
+                "what": "v_mfma_f32_16x16x32_bf16 back to back on random operands at two waves per SIMD; streaming copy"}
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def _kernel_sha() -> str:
@@ -192,8 +215,36 @@ def main():
     total_frames = BATCH * args.steps * world
     fps = total_frames / elapsed
 
+    def time_steps(fn, k):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / k
+
+    # the GPU side of the reference's default per-frame chain (run_videos.py defaults): forward +
+    # LAB lightness EMA (alpha 0.65, frames in order) + uniform blend 0.9 with the original frame
+    from neuralstyletransferv1_amd.postproc import blend_frames
+    chain_ema = LabSmoother(dev, True, 0.65)
+
+    def chain_step():
+        return blend_frames(chain_ema(eng.stylize_u8(frames, PRESET)), frames, 0.9)
+    chain_s = time_steps(chain_step, max(3, min(args.steps, 10)))
+
+    # fp16 mode (NST_DT_F16): the same kernels with fp16 operands, the mode that holds +-1 LSB
+    eng16 = None
+    fp16_s = None
+    if not args.no_fp16:
+        net.compute_dtype = "fp16"
+        eng16 = net.engine(dev)
+        net.compute_dtype = "bf16"
+        fp16_s = time_steps(lambda: eng16.stylize_u8(frames, PRESET), max(3, min(args.steps, 10)))
+
     # profiled pass: per-conv HIP events on the forward's stream
     kp = max(3, min(args.steps, 10))
+    measured = _measured_peaks()
     eng.profile_begin()
     torch.cuda.synchronize(dev)
     for _ in range(kp):
@@ -272,6 +323,18 @@ def main():
             "avg_launch_ms": round(res_avg_ms, 4),
             "flop_per_launch": res_flop,
             "algorithmic_bytes_per_launch": res_bytes,
+            "measured_peak": measured,
+            "frac_of_measured_peak": (round(achieved_tflops / measured["mfma_tflops"], 4)
+                                      if (achieved_tflops and measured) else None),
+            "joined": {
+                "kernel": "wstat_kernel<8, WF_RES> (the same conv with the residual join in its fill, 4 launches/step)",
+                "avg_launch_ms": round(joined_avg_ms, 4),
+                "achieved": round(res_flop / (joined_avg_ms * 1e-3) / 1e12, 2) if joined_avg_ms else None,
+                "frac": round(res_flop / (joined_avg_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4) if joined_avg_ms else None,
+                "frac_of_measured_peak": (round(res_flop / (joined_avg_ms * 1e-3) / 1e12 / measured["mfma_tflops"], 4)
+                                          if (joined_avg_ms and measured) else None),
+                "algorithmic_bytes_per_launch": 2 * res_bytes,
+            },
         },
         "whole_path": {
             "gflop_per_frame": FLOP_PER_PIXEL * H * W / 1e9,
@@ -286,7 +349,19 @@ def main():
             "megapixels_per_frame": mp,
         },
         "cpu_baseline": None,
+        "gpu_full_chain": {
+            "frames_per_s": round(BATCH * world / chain_s, 2),
+            "ms_per_step": round(chain_s * 1e3, 4),
+            "what": "forward (bf16) + LAB lightness EMA (alpha 0.65, frames in order) + blend 0.9 with the original "
+                    "(run_videos.py defaults), one GPU, frames in HBM",
+        },
     }
+    if fp16_s is not None:
+        result["fp16_mode"] = {
+            "frames_per_s": round(BATCH * world / fp16_s, 2),
+            "ms_per_step": round(fp16_s * 1e3, 4),
+            "what": "NST_DT_F16: the bench kernels with fp16 weights/activations (fp16 MFMA, fp32 accumulate)",
+        }
     if rank == 0 and world == 1 and not args.no_fp32:
         # the fp32 parity mode (exact-f32 MFMA), same frames
         net.compute_dtype = "fp32"
@@ -308,8 +383,18 @@ def main():
         diff = [np.abs(gpu[i].astype(int) - cpu_outs[i].astype(int)) for i in range(k)]
         result["ssim_vs_cpu"] = round(float(min(ss)), 5)
         result["max_abs_lsb_vs_cpu"] = int(max(d.max() for d in diff))
+        result["within_1lsb_vs_cpu"] = round(float(np.mean([(d <= 1).mean() for d in diff])), 6)
         result["within_2lsb_vs_cpu"] = round(float(np.mean([(d <= 2).mean() for d in diff])), 6)
         result["speedup_vs_cpu"] = round(fps / cb["value"], 1)
+        if eng16 is not None:
+            g16 = eng16.stylize_u8(frames, PRESET).cpu().numpy()
+            d16 = [np.abs(g16[i].astype(int) - cpu_outs[i].astype(int)) for i in range(k)]
+            result["fp16_mode"].update({
+                "ssim_vs_cpu": round(float(min(O.ssim(g16[i], cpu_outs[i]) for i in range(k))), 6),
+                "max_abs_lsb_vs_cpu": int(max(d.max() for d in d16)),
+                "within_1lsb_values": round(float(np.mean([(d <= 1).mean() for d in d16])), 6),
+                "within_1lsb_pixels": round(float(np.mean([(d.max(-1) <= 1).mean() for d in d16])), 6),
+            })
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

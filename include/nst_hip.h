@@ -43,6 +43,9 @@ extern "C" {
 /* ---- compute dtypes ---- */
 #define NST_DT_F32 0  /* fp32 "parity" mode: exact-f32 MFMA (v_mfma_f32_16x16x4_f32) */
 #define NST_DT_BF16 1 /* bf16 "throughput" mode: bf16 MFMA, fp32 accumulate/statistics */
+#define NST_DT_F16 2  /* fp16 mode: fp16 weights/activations, fp16 MFMA at the bf16 rate, fp32 accumulate/statistics;
+                         3 more mantissa bits than bf16 = the reference's +-1 LSB uint8 bar.  Stored conv outputs
+                         must stay inside the fp16 range (|v| <= 65504) */
 
 /* ---- I/O formats for nst_forward ---- */
 #define NST_IO_F32_NCHW 0 /* raw model tensor [n,3,h,w] fp32 (TransformerNet.forward(X) surface) */
@@ -427,9 +430,22 @@ int nst_flow_scratch_floats(int h, int w, size_t* out);
 int nst_flow_farneback(const uint8_t* prev, const uint8_t* next, int h, int w, double pyr_scale, int levels,
                        int winsize, int iterations, int poly_n, double poly_sigma, float* flow, float* scratch,
                        size_t scratch_floats, void* stream);
-/* --flow_downscale ds (pipeline.py:1886-1892, 1920-1923): gray [h,w] -> [h/ds, w/ds] by cv2.resize INTER_AREA at an
- * exact integer factor (restated), and the small flow [hs,ws,2] back to [h,w,2] by INTER_LINEAR times mul = ds */
+/* DIS optical flow, the reference's default --flow_method (pipeline.py:1904-1914:
+ * cv2.DISOpticalFlow_create(cv2.DISOPTICAL_FLOW_PRESET_FAST).calc(prev, next, None)) for n frame pairs: OpenCV's
+ * dis_flow.cpp + variational_refinement.cpp restated with PRESET_FAST's parameters (patch 8, stride 4, finest scale 2,
+ * 16 gradient-descent iterations, 5 variational refinement iterations; cv2 absent: parity unpinned).  prev/next u8
+ * [n,h,w] device, flow f32 [n,h,w,2] = (dx, dy); scratch per nst_flow_dis_scratch_bytes (NST_E_SHAPE for frames too
+ * small for the pyramid: min(round(log2(max(h,w)/32)), floor(log2(min(h,w)/8))) < 2). */
+int nst_flow_dis_scratch_bytes(int n, int h, int w, size_t* out);
+int nst_flow_dis(const uint8_t* prev, const uint8_t* next, int n, int h, int w, float* flow, void* scratch,
+                 size_t scratch_bytes, void* stream);
+/* --flow_downscale ds (pipeline.py:1886-1892, 1920-1923): gray [h,w] -> [h//ds, w//ds] (floored, as the reference's
+ * (W0 // ds, H0 // ds)) by cv2.resize INTER_AREA (restated: integer scales take resizeAreaFast, others the fractional
+ * cells of ResizeArea_Invoker), and the small flow [hs,ws,2] back to [h,w,2] by INTER_LINEAR times mul = ds */
 int nst_flow_downscale_gray(const uint8_t* gray, int h, int w, int ds, uint8_t* out, void* stream);
+/* cv2.resize(img, (out_w, out_h), interpolation=INTER_AREA) of n u8 images [n,h,w,c] (c <= 4), downscaling only
+ * (out <= in): the DIS pyramid (cv2.DISOpticalFlow prepareBuffers) and --flow_downscale */
+int nst_resize_area_u8(const uint8_t* in, int n, int h, int w, int c, uint8_t* out, int out_h, int out_w, void* stream);
 int nst_flow_upscale(const float* flow_small, int hs, int ws, int h, int w, float mul, float* flow, void* stream);
 /* flow EMA (pipeline.py:1926-1931 with _warp_with_flow :425-439): out = clip(alpha*curr + (1-alpha)*warp(prev)),
  * warp = cv2.remap(prev, x + dx, y + dy, INTER_LINEAR, BORDER_REPLICATE) restated; curr/prev/out f32 planar

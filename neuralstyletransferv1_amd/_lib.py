@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("NST_HIP_LIB", os.path.join(_HERE, "libnst_hip.so"))
 
 NST_OK = 0
 NST_ARCH_JOHNSON, NST_ARCH_NST, NST_ARCH_RECONET, NST_ARCH_RECONET_FRN = 0, 1, 2, 3
-NST_DT_F32, NST_DT_BF16 = 0, 1
+NST_DT_F32, NST_DT_BF16, NST_DT_F16 = 0, 1, 2
 NST_IO_F32_NCHW, NST_IO_U8_NHWC = 0, 1
 PRESETS = {
     "none": 0,
@@ -43,7 +43,8 @@ EXPORTED_SYMBOLS = (
     "nst_region_masks", "nst_region_feather", "nst_region_rotate", "nst_region_bbox", "nst_region_scratch_floats",
     "nst_region_composite_u8", "nst_region_crop_input", "nst_region_resize", "nst_region_morph",
     "nst_region_morph_scratch_floats", "nst_gray_u8", "nst_flow_scratch_floats", "nst_flow_farneback",
-    "nst_flow_fuse", "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale",
+    "nst_flow_fuse", "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale", "nst_resize_area_u8",
+    "nst_flow_dis_scratch_bytes", "nst_flow_dis",
 )
 # region compositor limits / geometry kinds (include/nst_hip.h NST_REGION_*, NST_RG_*)
 NST_REGION_MAX, NST_REGION_TERMS, NST_REGION_MAX_SRC = 32, 9, 16
@@ -166,8 +167,12 @@ def lib() -> ctypes.CDLL:
         L.nst_motion_alpha.argtypes = [vp, i, i, f, dbl, f, f, vp, vp, vp]
         L.nst_flow_downscale_gray.argtypes = [vp, i, i, i, vp, vp]
         L.nst_flow_upscale.argtypes = [vp, i, i, i, i, f, vp, vp]
+        L.nst_resize_area_u8.argtypes = [vp, i, i, i, i, vp, i, i, vp]
+        L.nst_flow_dis_scratch_bytes.argtypes = [i, i, i, ctypes.POINTER(sz)]
+        L.nst_flow_dis.argtypes = [vp, vp, i, i, i, vp, vp, sz, vp]
         for name in ("nst_gray_u8", "nst_flow_scratch_floats", "nst_flow_farneback", "nst_flow_fuse",
-                     "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale"):
+                     "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale", "nst_resize_area_u8",
+                     "nst_flow_dis_scratch_bytes", "nst_flow_dis"):
             getattr(L, name).restype = i
         for name in ("nst_region_masks", "nst_region_feather", "nst_region_rotate", "nst_region_bbox",
                      "nst_region_morph", "nst_region_morph_scratch_floats",

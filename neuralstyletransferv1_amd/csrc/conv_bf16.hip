@@ -1,48 +1,6 @@
-// conv_bf16.hip — bf16 (throughput mode) instantiations of conv_kernel.
-// Tile choices per layer shape: see DESIGN.md "Kernels".
-#include "conv_impl.h"
-
-// Tile shapes (TH, TW, WM, WN) of the Johnson/NST layers; overridable at build time for tile sweeps
-// tile shapes (TH, TW, WM, WN) of the generic instantiations
-#define NST_C1_TILE 8, 32, 4, 1
-#define NST_C2_TILE 4, 16, 2, 2
-#define NST_C3_TILE 4, 16, 2, 2
-#define NST_D1_TILE 4, 16, 1, 4
-#define NST_D2_TILE 4, 16, 1, 4
+// conv_bf16.hip — bf16 (throughput mode) instantiations of the generic conv_kernel (conv_tab16.h).
+#include "conv_tab16.h"
 
 namespace nst {
-typedef __bf16 B;
-#define E(...) ConvInst<__VA_ARGS__>::info()
-constexpr int SD = MODE_STD, PH = MODE_PHASE, XS = MODE_XSHIFT;
-const ConvKernelInfo* conv_table_bf16(int* count) {
-  static const ConvKernelInfo table[] = {
-      //  T  MODE KS S CINP BN TH TW WM WN  IN           OUT
-      E(B, SD, 9, 1, 4, 32, NST_C1_TILE, IN_ACT, OUT_ACT),        // Johnson/NST conv1 over the pre-padded encoded input (conv_prep.hip)
-      E(B, SD, 9, 1, 4, 32, NST_C1_TILE, IN_U8_NHWC, OUT_ACT),    // Johnson/NST conv1 (frames)
-      E(B, SD, 9, 1, 4, 32, NST_C1_TILE, IN_F32_NCHW, OUT_ACT),   // Johnson/NST conv1 (tensor API)
-      E(B, SD, 3, 2, 32, 64, NST_C2_TILE, IN_ACT, OUT_ACT),       // conv2 / down2
-      E(B, SD, 3, 2, 64, 128, NST_C3_TILE, IN_ACT, OUT_ACT),      // conv3 / down3 / ReCoNet enc1
-      E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // residual trunk (register-streamed; see conv_bf16_wl.hip)
-      E(B, PH, 3, 1, 128, 64, NST_D1_TILE, IN_ACT, OUT_ACT),      // deconv1 / up1 / ReCoNet dec2 (phases)
-      E(B, PH, 3, 1, 64, 32, NST_D2_TILE, IN_ACT, OUT_ACT),       // deconv2 / up2 (phases)
-      E(B, XS, 9, 1, 32, 16, 8, 80, 8, 1, IN_ACT, OUT_U8_NHWC),   // deconv3 / final (frames, x-shift, 8 waves)
-      E(B, XS, 9, 1, 32, 16, 8, 80, 8, 1, IN_ACT, OUT_F32_NCHW),  // deconv3 / final (tensor API)
-      // ReCoNet (48/96/192 channels, bf16 padded to 64/128/192)
-      E(B, SD, 9, 1, 4, 64, 8, 32, 4, 1, IN_ACT, OUT_ACT),
-      E(B, SD, 9, 1, 4, 64, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
-      E(B, SD, 9, 1, 4, 64, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),
-      E(B, SD, 3, 2, 128, 192, 4, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(B, SD, 3, 1, 192, 192, 8, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(B, PH, 3, 1, 192, 128, 2, 16, 1, 4, IN_ACT, OUT_ACT),
-      // consumers of the residual stream (residual join fused into the fill)
-      E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
-      E(B, PH, 3, 1, 128, 64, NST_D1_TILE, IN_ACT, OUT_ACT, VAR_RES),
-      E(B, SD, 3, 1, 192, 192, 8, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
-      E(B, PH, 3, 1, 192, 128, 2, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
-      E(B, SD, 9, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
-      E(B, SD, 9, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
-  };
-  *count = (int)(sizeof(table) / sizeof(table[0]));
-  return table;
-}
+const ConvKernelInfo* conv_table_bf16(int* count) { return conv_table_16<__bf16>(count); }
 }  // namespace nst

@@ -18,7 +18,7 @@
 //   * MFMA operands: A = packed weights (rows = output channels) streamed from L2 as one
 //     coalesced 1 KiB fragment per wave-instruction, prefetched one K-step ahead;
 //     B = input pixels from LDS (cols = 16 output pixels).
-//     bf16: v_mfma_f32_16x16x32_bf16 (fp32 accumulate).  fp32: v_mfma_f32_16x16x4_f32
+//     bf16 / fp16: v_mfma_f32_16x16x32_{bf16,f16} (fp32 accumulate).  fp32: v_mfma_f32_16x16x4_f32
 //     (exact fp32 FMA chain) — the parity mode.
 //   * output-channel permutation: C row q of n-subtile t is output channel
 //     4*NSUB*(q>>2) + 4*t + (q&3) of the wave's range, so each lane ends up owning
@@ -87,6 +87,58 @@ typedef float f32x2v_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
   const f32x2v_t v = {lo, hi};
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_t));
+}
+
+// The two 16-bit activation formats of the MFMA paths, T = __bf16 or _Float16 (same layouts,
+// same MFMA shapes and rates on gfx950):
+//   bf16 (NST_DT_BF16)  the throughput mode: 8 significant bits;
+//   fp16 (NST_DT_F16)   11 significant bits: the mode that holds the reference's +-1 LSB uint8 bar
+//                       (stored conv outputs must stay inside the fp16 range, |v| <= 65504).
+// lo16 / hi16 unpack one half of a packed pair exactly; pack16 rounds two floats to nearest even
+// (one v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32).
+template <typename T>
+constexpr bool IS_F16 = std::is_same<T, _Float16>::value;
+typedef _Float16 f16x2v_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ float lo16(uint32_t w) {
+  if constexpr (IS_F16<T>) return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu));
+  else return bf16_lo(w);
+}
+template <typename T>
+__device__ __forceinline__ float hi16(uint32_t w) {
+  if constexpr (IS_F16<T>) return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+  else return bf16_hi(w);
+}
+template <typename T>
+__device__ __forceinline__ uint32_t pack16(float lo, float hi) {
+  if constexpr (IS_F16<T>) {
+    const f32x2v_t v = {lo, hi};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v_t));
+  } else {
+    return pack_bf16(lo, hi);
+  }
+}
+// acc + A x B on v_mfma_f32_16x16x32_{bf16,f16} (builtin form: hipcc allocates the accumulator)
+template <typename T>
+__device__ __forceinline__ f32x4_t mfma16x16x32(const uint4& a, const uint4& b, const f32x4_t& c) {
+  if constexpr (IS_F16<T>)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+template <typename T>
+__device__ __forceinline__ f32x16_t mfma32x32x16(const uint4& a, const uint4& b, const f32x16_t& c) {
+  if constexpr (IS_F16<T>)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+template <typename T>
+constexpr int dtype_code() {
+  return std::is_same<T, float>::value ? NST_DT_F32 : (IS_F16<T> ? NST_DT_F16 : NST_DT_BF16);
 }
 
 template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW, int WM, int WN>
@@ -161,8 +213,9 @@ struct ConvCfg {
 
 // Producer InstanceNorm apply (+ReLU) on one 16-byte chunk: v = v*scale + shift.
 // bf16: per channel pair, unpack (2 ops), one packed fp32 FMA (v_pk_fma_f32), one RNE pack
-// (v_cvt_pk_bf16_f32) and the ReLU as a packed int16 max with 0 on the bf16 bit patterns
-// (sign bit = int16 sign; rounding is monotone, so ReLU-after-round == round-after-ReLU).
+// (v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32) and the ReLU as a packed int16 max with 0 on the 16-bit
+// patterns (sign-magnitude: sign bit = int16 sign; rounding is monotone, so ReLU-after-round ==
+// round-after-ReLU).
 // Every producer IN the prologue applies is followed by a ReLU (ConvLayer -> IN -> ReLU in all
 // three nets; the residual's second IN is applied by the residual add instead), so the ReLU is
 // unconditional here.
@@ -175,11 +228,11 @@ __device__ __forceinline__ uint4 norm_chunk(uint4 raw, const float2* nm) {
     uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const f32x2_t x = {bf16_lo(w[j]), bf16_hi(w[j])};
+      const f32x2_t x = {lo16<T>(w[j]), hi16<T>(w[j])};
       const f32x2_t sc = {nm[2 * j].x, nm[2 * j + 1].x};
       const f32x2_t sh = {nm[2 * j].y, nm[2 * j + 1].y};
       f32x2_t y; y.x = __builtin_fmaf(x.x, sc.x, sh.x); y.y = __builtin_fmaf(x.y, sc.y, sh.y);
-      const i16x2_t r = __builtin_bit_cast(i16x2_t, __builtin_convertvector(y, bf16x2_t));
+      const i16x2_t r = __builtin_bit_cast(i16x2_t, pack16<T>(y.x, y.y));
       w[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
@@ -205,8 +258,8 @@ __device__ __forceinline__ uint4 res_chunk(uint4 y, uint4 r, const float2* yn, c
   if constexpr (sizeof(T) == 2) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      fy[2 * j] = bf16_lo(wy[j]); fy[2 * j + 1] = bf16_hi(wy[j]);
-      fr[2 * j] = bf16_lo(wr[j]); fr[2 * j + 1] = bf16_hi(wr[j]);
+      fy[2 * j] = lo16<T>(wy[j]); fy[2 * j + 1] = hi16<T>(wy[j]);
+      fr[2 * j] = lo16<T>(wr[j]); fr[2 * j + 1] = hi16<T>(wr[j]);
     }
   } else {
 #pragma unroll
@@ -218,7 +271,7 @@ __device__ __forceinline__ uint4 res_chunk(uint4 y, uint4 r, const float2* yn, c
     if (has_rn) {
       // r' = ReLU(IN_r(r)) exactly as a normalising fill stages it (norm_chunk): bf16 of one fma
       if constexpr (sizeof(T) == 2)
-        rr = fmaxf(bf16_lo(pack_bf16(__builtin_fmaf(rr, rn[j].x, rn[j].y), 0.f)), 0.f);
+        rr = fmaxf(lo16<T>(pack16<T>(__builtin_fmaf(rr, rn[j].x, rn[j].y), 0.f)), 0.f);
       else
         rr = fmaxf(rr * rn[j].x + rn[j].y, 0.f);
     }
@@ -227,7 +280,7 @@ __device__ __forceinline__ uint4 res_chunk(uint4 y, uint4 r, const float2* yn, c
     o[j] = relu_out ? fmaxf(v, 0.f) : v;
   }
   if constexpr (sizeof(T) == 2) {
-    return make_uint4(pack_bf16(o[0], o[1]), pack_bf16(o[2], o[3]), pack_bf16(o[4], o[5]), pack_bf16(o[6], o[7]));
+    return make_uint4(pack16<T>(o[0], o[1]), pack16<T>(o[2], o[3]), pack16<T>(o[4], o[5]), pack16<T>(o[6], o[7]));
   } else {
     return make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
   }
@@ -257,8 +310,8 @@ __device__ __forceinline__ uint4 load_image_entry(const ConvParams& p, int n, in
     }
   }
   if constexpr (PAIR) {
-    return make_uint4(pack_bf16(vals[0][0], vals[0][1]), pack_bf16(vals[0][2], 0.f),
-                      pack_bf16(vals[1][0], vals[1][1]), pack_bf16(vals[1][2], 0.f));
+    return make_uint4(pack16<T>(vals[0][0], vals[0][1]), pack16<T>(vals[0][2], 0.f),
+                      pack16<T>(vals[1][0], vals[1][1]), pack16<T>(vals[1][2], 0.f));
   } else {
     return make_uint4(__float_as_uint(vals[0][0]), __float_as_uint(vals[0][1]), __float_as_uint(vals[0][2]), 0u);
   }
@@ -696,8 +749,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
 #pragma unroll
       for (int t = 0; t < NSUB; ++t) {
         if constexpr (sizeof(T) == 2) {
-          acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8_t, a[t]), __builtin_bit_cast(bf16x8_t, b[m]), acc[m][t], 0, 0, 0);
+          acc[m][t] = mfma16x16x32<T>(a[t], b[m], acc[m][t]);
         } else {
           acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[t].x), __uint_as_float(b[m].x), acc[m][t], 0, 0, 0);
           acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[t].y), __uint_as_float(b[m].y), acc[m][t], 0, 0, 0);
@@ -914,10 +966,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
 #pragma unroll
               for (int h = 0; h < NSUB; h += 2) {
                 if (h + 1 < NSUB) {
-                  *(uint4*)(dst + h * 8) = make_uint4(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]),
-                                                      pack_bf16(v[4 * h + 4], v[4 * h + 5]), pack_bf16(v[4 * h + 6], v[4 * h + 7]));
+                  *(uint4*)(dst + h * 8) = make_uint4(pack16<T>(v[4 * h], v[4 * h + 1]), pack16<T>(v[4 * h + 2], v[4 * h + 3]),
+                                                      pack16<T>(v[4 * h + 4], v[4 * h + 5]), pack16<T>(v[4 * h + 6], v[4 * h + 7]));
                 } else {
-                  *(uint2*)(dst + h * 8) = make_uint2(pack_bf16(v[4 * h], v[4 * h + 1]), pack_bf16(v[4 * h + 2], v[4 * h + 3]));
+                  *(uint2*)(dst + h * 8) = make_uint2(pack16<T>(v[4 * h], v[4 * h + 1]), pack16<T>(v[4 * h + 2], v[4 * h + 3]));
                 }
               }
             } else {
@@ -1220,7 +1272,7 @@ struct ConvInst {
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
-    k.dtype = sizeof(T) == 2 ? NST_DT_BF16 : NST_DT_F32;
+    k.dtype = dtype_code<T>();
     k.mode = MODE;
     k.ks = KS; k.stride = S; k.cinp = CINP; k.bn = BN; k.th = TH; k.tw = TW; k.wm = WM; k.wn = WN;
     k.in_kind = INK; k.out_kind = OUTK;

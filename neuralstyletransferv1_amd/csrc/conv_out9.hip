@@ -1,6 +1,6 @@
 // conv_out9.hip — the output conv of the Johnson / NST / ReCoNet nets (9x9, C -> 3 channels:
 // transformer_net.py:37-38 deconv3, transformer_net_nst.py:91 final, model.py:78 ConvTanhLayer)
-// as a row-streaming "ky-rotation" GEMM on v_mfma_f32_32x32x16_bf16.
+// as a row-streaming "ky-rotation" GEMM on v_mfma_f32_32x32x16_{bf16,f16}.
 //
 // Why a separate mapping: with N = 3 output channels a plain implicit GEMM wastes 13 of 16 MFMA
 // columns, and any 2-D halo tile re-reads 9 input rows per output row.  Here
@@ -26,7 +26,6 @@
 
 namespace nst {
 
-typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) uint64_t lds_u64;  // volatile LDS loads: never merged
 
 template <int CINP, int G, int NW>
@@ -40,7 +39,7 @@ struct Out9Cfg {
   static constexpr int LWS = SW + 8;              // input columns per strip row
   static constexpr int ROWB = LWS * EB;
   static constexpr int WAVE_LDS = 2 * ROWB;
-  // weight table: [part p][block (kx, kc)][K half h][row i = 3*ky + c] x 8 bytes (4 bf16); a lane's
+  // weight table: [part p][block (kx, kc)][K half h][row i = 3*ky + c] x 8 bytes (4 x 16 bit); a lane's
   // 16-B A fragment is two ds_read_b64 (parts 0 and 1, PART_BYTES apart).  The 32 lanes of one
   // half read 27 different rows (the rotation permutes them), i.e. 27 consecutive 8-B slots: no
   // bank conflict for any rotation (ds_read_b64 banks 32-lane groups mod 64 dwords); the 5 unused
@@ -63,7 +62,7 @@ struct Out9Cfg {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int CINP, int G, int NW, int OUTK, bool TANH>
+template <typename T, int CINP, int G, int NW, int OUTK, bool TANH>
 __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   using C = Out9Cfg<CINP, G, NW>;
   constexpr int KC = C::KC, EB = C::EB;
@@ -148,7 +147,7 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
     for (int j = 0; j < C::IPL; ++j) {
       if (C::PPJ * j + lane % C::PPJ < C::LWS) {
         const bool ok = ro >= 0 && coloff[j] >= 0;
-        const uint4 v4 = norm_chunk<__bf16>(raw[j], nm);
+        const uint4 v4 = norm_chunk<T>(raw[j], nm);
         *(uint4*)(dst + j * C::PPJ * EB) = ok ? v4 : make_uint4(0u, 0u, 0u, 0u);
       }
     }
@@ -231,9 +230,7 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
         for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
           for (int gi = 0; gi < G; ++gi)
-            acc[gi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, av[kx & 1][kc]),
-                                                              __builtin_bit_cast(bf16x8_t, bv[kx & 1][kc][gi]),
-                                                              acc[gi], 0, 0, 0);
+            acc[gi] = mfma32x32x16<T>(av[kx & 1][kc], bv[kx & 1][kc][gi], acc[gi]);
         __builtin_amdgcn_sched_barrier(0);
       }
       // slot (t+1) % 9 now holds output row v - 8: store it, then clear it for output row v + 1
@@ -251,10 +248,10 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   }
 }
 
-template <int CINP, int G, int NW, int OUTK, bool TANH>
+template <typename T, int CINP, int G, int NW, int OUTK, bool TANH>
 struct Out9Inst {
   using C = Out9Cfg<CINP, G, NW>;
-  static constexpr auto kernel = out9_kernel<CINP, G, NW, OUTK, TANH>;
+  static constexpr auto kernel = out9_kernel<T, CINP, G, NW, OUTK, TANH>;
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;
@@ -283,7 +280,7 @@ struct Out9Inst {
   static ConvKernelInfo info() {
     ConvKernelInfo k;
     std::memset(&k, 0, sizeof(k));
-    k.dtype = NST_DT_BF16;
+    k.dtype = dtype_code<T>();
     k.mode = MODE_KYROT;
     k.ks = 9; k.stride = 1; k.cinp = CINP; k.bn = 16; k.th = 1; k.tw = C::SW; k.wm = NW; k.wn = 1;
     k.in_kind = IN_ACT; k.out_kind = OUTK;
@@ -299,11 +296,15 @@ struct Out9Inst {
 #define E(...) Out9Inst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_out9(int* count) {
   static const ConvKernelInfo table[] = {
-      //  CINP G NW OUT          TANH
-      E(32, 3, 8, OUT_U8_NHWC, false),   // Johnson deconv3 / NST final (frames)
-      E(32, 3, 8, OUT_F32_NCHW, false),  // tensor API
-      E(64, 3, 4, OUT_U8_NHWC, true),    // ReCoNet (48 channels, bf16 padded to 64; tanh output)
-      E(64, 3, 4, OUT_F32_NCHW, true),
+      //  T     CINP G NW OUT          TANH
+      E(__bf16, 32, 3, 8, OUT_U8_NHWC, false),    // Johnson deconv3 / NST final (frames)
+      E(__bf16, 32, 3, 8, OUT_F32_NCHW, false),   // tensor API
+      E(__bf16, 64, 3, 4, OUT_U8_NHWC, true),     // ReCoNet (48 channels, bf16 padded to 64; tanh output)
+      E(__bf16, 64, 3, 4, OUT_F32_NCHW, true),
+      E(_Float16, 32, 3, 8, OUT_U8_NHWC, false),  // fp16 mode
+      E(_Float16, 32, 3, 8, OUT_F32_NCHW, false),
+      E(_Float16, 64, 3, 4, OUT_U8_NHWC, true),
+      E(_Float16, 64, 3, 4, OUT_F32_NCHW, true),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

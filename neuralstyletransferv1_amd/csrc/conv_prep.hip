@@ -1,19 +1,20 @@
-// conv_prep.hip — first-layer input staging for the bf16 path.
+// conv_prep.hip — first-layer input staging for the 16-bit (bf16 / fp16) paths.
 //
 // The 9x9 image conv (transformer_net.py:34 conv1 / transformer_net_nst.py:64 down1 / model.py:71)
 // consumes the io_preset-encoded frame (pipeline.py:1445-1486).  Encoding inside that conv's LDS
 // fill cost ~40 VALU per pixel (byte gathers, the reference's exact division, the padding map) and
 // made it VALU-bound; here one streaming pass writes the encoded input ONCE, already padded
-// (reflection / NST's pre-reflect + zero padding resolved), as bf16 [n][hp][wp][4] (channel 3 = 0):
+// (reflection / NST's pre-reflect + zero padding resolved), as bf16 or fp16 [n][hp][wp][4] (channel 3 = 0):
 // 8 bytes per pixel, so the conv fill is plain 16-byte loads (two pixels per LDS entry) with an
 // identity coordinate map.  Arithmetic per element is the reference's: x01 = byte / 255 (ToTensor),
-// ((x01 * a) - b) / d, one RNE rounding to bf16 — bit-identical to the fused encode it replaces
+// ((x01 * a) - b) / d, one RNE rounding to the 16-bit format — bit-identical to the fused encode it replaces
 // (for uint8 frames through a per-block table of the 3 x 256 possible values).
 #include "conv_impl.h"
 
 namespace nst {
 
 // f32 NCHW input (tensor API): one thread per pixel, the encode formula per element
+template <typename T>
 __global__ __launch_bounds__(256) void prepad_encode_f32_kernel(ConvParams p, int hp, int wp, uint2* __restrict__ out) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x;
   const int y = blockIdx.y, n = blockIdx.z;
@@ -28,7 +29,7 @@ __global__ __launch_bounds__(256) void prepad_encode_f32_kernel(ConvParams p, in
       v[ch] = ((x01 * p.enc_a[ch]) - p.enc_b[ch]) / p.enc_d[ch];
     }
   }
-  out[((size_t)n * hp + y) * wp + x] = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], 0.f));
+  out[((size_t)n * hp + y) * wp + x] = make_uint2(pack16<T>(v[0], v[1]), pack16<T>(v[2], 0.f));
 }
 
 // uint8 frames: the encoded bf16 value of a channel depends only on its byte, so each block first
@@ -37,13 +38,14 @@ __global__ __launch_bounds__(256) void prepad_encode_f32_kernel(ConvParams p, in
 // pixels) + 3 LDS lookups; 4 consecutive output pixels per thread (32-byte contiguous stores).
 constexpr int PREP_PX = 4;
 constexpr int PREP_ROWS = 8;  // padded rows per block: the 768-entry table is built once per 8 rows
+template <typename T>
 __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int hp, int wp, uint4* __restrict__ out) {
   __shared__ uint16_t lut[3][256];
   for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
     const int ch = i >> 8, b = i & 255;
     const float x01 = (float)b / 255.0f;  // ToTensor: .float().div(255)
     const float v = ((x01 * p.enc_a[ch]) - p.enc_b[ch]) / p.enc_d[ch];
-    lut[ch][b] = (uint16_t)(pack_bf16(v, 0.f) & 0xffffu);
+    lut[ch][b] = (uint16_t)(pack16<T>(v, 0.f) & 0xffffu);
   }
   __syncthreads();
   const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * PREP_PX;
@@ -67,7 +69,7 @@ __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int
 #pragma unroll
       for (int j = 0; j < PREP_PX; ++j) {
         w[2 * j] = (uint32_t)lut[0][byte(3 * j + pr0)] | ((uint32_t)lut[1][byte(3 * j + pr1)] << 16);
-        w[2 * j + 1] = (uint32_t)lut[2][byte(3 * j + pr2)] | ((uint32_t)pack_bf16(0.f, 0.f) & 0xffff0000u);
+        w[2 * j + 1] = (uint32_t)lut[2][byte(3 * j + pr2)] | ((uint32_t)pack16<T>(0.f, 0.f) & 0xffff0000u);
       }
     } else {
 #pragma unroll
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int
         if (sy >= 0 && sxs[j] >= 0) {
           const uint8_t* px = row + (size_t)sxs[j] * 3;
           lo = (uint32_t)lut[0][px[pr0]] | ((uint32_t)lut[1][px[pr1]] << 16);
-          hi = (uint32_t)lut[2][px[pr2]] | ((uint32_t)pack_bf16(0.f, 0.f) & 0xffff0000u);
+          hi = (uint32_t)lut[2][px[pr2]] | ((uint32_t)pack16<T>(0.f, 0.f) & 0xffff0000u);
         }
         w[2 * j] = lo;
         w[2 * j + 1] = hi;
@@ -94,16 +96,23 @@ __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int
   }
 }
 
-hipError_t launch_prepad_encode(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st) {
+template <typename T>
+hipError_t launch_prepad(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st) {
   if (in_kind == IN_U8_NHWC) {
     const dim3 grid((unsigned)((wp + 256 * PREP_PX - 1) / (256 * PREP_PX)), (unsigned)((hp + PREP_ROWS - 1) / PREP_ROWS),
                     (unsigned)n);
-    hipLaunchKernelGGL(prepad_encode_u8_kernel, grid, dim3(256), 0, st, p, hp, wp, (uint4*)out);
+    hipLaunchKernelGGL(prepad_encode_u8_kernel<T>, grid, dim3(256), 0, st, p, hp, wp, (uint4*)out);
   } else {
     const dim3 grid((unsigned)((wp + 255) / 256), (unsigned)hp, (unsigned)n);
-    hipLaunchKernelGGL(prepad_encode_f32_kernel, grid, dim3(256), 0, st, p, hp, wp, (uint2*)out);
+    hipLaunchKernelGGL(prepad_encode_f32_kernel<T>, grid, dim3(256), 0, st, p, hp, wp, (uint2*)out);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_prepad_encode(int dtype, const ConvParams& p, int in_kind, int n, int hp, int wp, void* out,
+                                hipStream_t st) {
+  if (dtype == NST_DT_F16) return launch_prepad<_Float16>(p, in_kind, n, hp, wp, out, st);
+  return launch_prepad<__bf16>(p, in_kind, n, hp, wp, out, st);
 }
 
 }  // namespace nst

@@ -68,7 +68,7 @@ struct WpCfg {  // SW: staged tensors per unit (2: the residual join's y and r, 
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int CINP, int COUT, int TH, int NF, int FILL, bool ZPAD>
+template <typename T, int CINP, int COUT, int TH, int NF, int FILL, bool ZPAD>
 __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   using C = WpCfg<CINP, COUT, TH, NF, (FILL >= WF_RES) ? 2 : 1>;
   constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
@@ -185,16 +185,16 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
       const uint32_t w2[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float r0 = bf16_lo(w2[j]), r1 = bf16_hi(w2[j]);
-        if (RN) {  // ReLU(IN_r(r)) as a normalising fill stages it: bf16 of one fma
-          const uint32_t rn = pack_bf16(__builtin_fmaf(r0, nr[2 * j], nr[8 + 2 * j]),
+        float r0 = lo16<T>(w2[j]), r1 = hi16<T>(w2[j]);
+        if (RN) {  // ReLU(IN_r(r)) as a normalising fill stages it: one fma, rounded to T
+          const uint32_t rn = pack16<T>(__builtin_fmaf(r0, nr[2 * j], nr[8 + 2 * j]),
                                         __builtin_fmaf(r1, nr[2 * j + 1], nr[8 + 2 * j + 1]));
-          r0 = fmaxf(bf16_lo(rn), 0.f);
-          r1 = fmaxf(bf16_hi(rn), 0.f);
+          r0 = fmaxf(lo16<T>(rn), 0.f);
+          r1 = fmaxf(hi16<T>(rn), 0.f);
         }
-        const float a = bf16_lo(w[j]) * ny[2 * j] + ny[8 + 2 * j];
-        const float bb = bf16_hi(w[j]) * ny[2 * j + 1] + ny[8 + 2 * j + 1];
-        o[j] = pack_bf16(r0 + a, r1 + bb);
+        const float a = lo16<T>(w[j]) * ny[2 * j] + ny[8 + 2 * j];
+        const float bb = hi16<T>(w[j]) * ny[2 * j + 1] + ny[8 + 2 * j + 1];
+        o[j] = pack16<T>(r0 + a, r1 + bb);
       }
     } else if constexpr (FILL == WF_RAW) {
 #pragma unroll
@@ -202,9 +202,9 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float a = __builtin_fmaf(bf16_lo(w[j]), ny[2 * j], ny[8 + 2 * j]);
-        const float bb = __builtin_fmaf(bf16_hi(w[j]), ny[2 * j + 1], ny[8 + 2 * j + 1]);
-        const i16x2_t r = __builtin_bit_cast(i16x2_t, pack_bf16(a, bb));
+        const float a = __builtin_fmaf(lo16<T>(w[j]), ny[2 * j], ny[8 + 2 * j]);
+        const float bb = __builtin_fmaf(hi16<T>(w[j]), ny[2 * j + 1], ny[8 + 2 * j + 1]);
+        const i16x2_t r = __builtin_bit_cast(i16x2_t, pack16<T>(a, bb));
         o[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
       }
     }
@@ -231,13 +231,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     const int tx = rem / NRD, y = rem % NRD;
     return *(const uint4*)(smem + lbase + (y * C::LW + tx) * C::EB + 64 * q);
   };
-  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
-    const u32x4_t av = __builtin_bit_cast(u32x4_t, a), bv = __builtin_bit_cast(u32x4_t, bop);
-    if (first)
-      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(av), "v"(bv));
-    else
-      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
-  };
+  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) { mfma_tied<T>(c, a, bop, first); };
   auto kloop = [&](Acc& acc, auto&& hook, auto&& bound) {
     constexpr int NI = C::NPART * PRD, D = WP_RING;
     uint4 ring[D];
@@ -271,7 +265,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     }
   };
 
-  // ---- epilogue: bias, bf16 NHWC stores of this phase's pixels, one partial row per phase ----
+  // ---- epilogue: bias, 16-bit NHWC stores of this phase's pixels, one partial row per phase ----
   auto epilogue = [&](const Work& wk, Acc& acc) {
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA results -> VALU reads
     const size_t obytes = (size_t)p.oh * p.ow * p.cout_stride * 2;
@@ -295,7 +289,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
         for (int r = 0; r < TH; ++r) {
           const bool valid = decltype(all_valid)::value || (oy0 + 2 * r < p.oh && ox < p.ow);
           const f32x4_t v = add4(acc[r][t], bias);
-          const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+          const u32x2_t pk = {pack16<T>(v[0], v[1]), pack16<T>(v[2], v[3])};
           if constexpr (C::OST) {  // into the LDS output tile: row 2r + a, pixel 2 px + b
             *(u32x2_t*)(smem + C::OUT_OFF + ((2 * r + (ph >> 1)) * 2 * C::TW + 2 * px + (ph & 1)) * C::PIXP +
                         (((c0 >> 2) ^ C::swz(2 * px + (ph & 1))) << 3)) = pk;
@@ -418,7 +412,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   vm_wait<0>();  // no LDS-DMA may land after the workgroup has released its LDS
 }
 
-template <int CINP, int COUT, int TH, int NF, bool RES>
+template <typename T, int CINP, int COUT, int TH, int NF, bool RES>
 struct WphaseInst {
   using C = WpCfg<CINP, COUT, TH, NF, RES ? 2 : 1>;
   static int cus() {
@@ -432,7 +426,7 @@ struct WphaseInst {
   }
   template <int FILL, bool ZPAD>
   static void go(const ConvParams& p, int nb, hipStream_t st) {
-    hipLaunchKernelGGL((wphase_kernel<CINP, COUT, TH, NF, FILL, ZPAD>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((wphase_kernel<T, CINP, COUT, TH, NF, FILL, ZPAD>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   // grid.x = source tiles per frame, grid.y = frames; chunks of <= NFMAX frames per launch
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
@@ -470,7 +464,7 @@ struct WphaseInst {
   static ConvKernelInfo info() {
     ConvKernelInfo k;
     std::memset(&k, 0, sizeof(k));
-    k.dtype = NST_DT_BF16;
+    k.dtype = dtype_code<T>();
     k.mode = MODE_WPHASE;
     k.ks = 3; k.stride = 1; k.cinp = CINP; k.bn = COUT; k.th = TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
     k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
@@ -489,10 +483,13 @@ constexpr int WP1_NF = 8;  // frames per launch (IN tables in LDS)
 #define E(...) WphaseInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wphase(int* count) {
   static const ConvKernelInfo table[] = {
-      //  CINP COUT TH NF RES
-      E(128, 64, WP1_TH, WP1_NF, false),  // deconv1 / up1
-      E(128, 64, WP1_TH, WP1_NF, true),   // deconv1 joining the last residual block (fused join)
-      E(64, 32, 12, 8, false),                    // deconv2 / up2: 12 rows (540 = 45 tiles) fit with one-tensor slots
+      //  T     CINP COUT TH NF RES
+      E(__bf16, 128, 64, WP1_TH, WP1_NF, false),    // deconv1 / up1
+      E(__bf16, 128, 64, WP1_TH, WP1_NF, true),     // deconv1 joining the last residual block (fused join)
+      E(__bf16, 64, 32, 12, 8, false),              // deconv2 / up2: 12 rows (540 = 45 tiles) fit with one-tensor slots
+      E(_Float16, 128, 64, WP1_TH, WP1_NF, false),  // fp16 mode
+      E(_Float16, 128, 64, WP1_TH, WP1_NF, true),
+      E(_Float16, 64, 32, 12, 8, false),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

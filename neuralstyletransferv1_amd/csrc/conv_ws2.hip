@@ -69,7 +69,7 @@ struct W2Cfg {
 
 // OCC = waves per SIMD the register allocation must allow: 4 = two workgroups per CU (conv2's
 // 8-row tiles fit 126 VGPRs and 72 KB of LDS), 2 = one
-template <int CINP, int COUT, int TH, bool ZPAD, int OCC>
+template <typename T, int CINP, int COUT, int TH, bool ZPAD, int OCC>
 __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
   using C = W2Cfg<CINP, COUT, TH>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
       if ((k + 1) * C::NT > C::NCHK && k * C::NT + tid >= C::NCHK) continue;
       int ly, lx;
       entry_of(k, ly, lx);
-      uint4 v = norm_chunk<__bf16>(pf[k], nm);  // IN + ReLU (as the generic kernel's fill)
+      uint4 v = norm_chunk<T>(pf[k], nm);  // IN + ReLU (as the generic kernel's fill)
       if (ZPAD && ((padm >> k) & 1u)) v = make_uint4(0u, 0u, 0u, 0u);  // zero padding stays zero after IN + ReLU
       *(uint4*)(smem + ly * C::RS + (lx & 1) * C::LWE * C::EB + (lx >> 1) * C::EB + fc * 16) = v;
     }
@@ -181,13 +181,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
     asm volatile("" : "+v"(base));
     return *(const uint4*)(smem + base + y * C::RS + (dx & 1) * C::LWE * C::EB + (dx >> 1) * C::EB + 64 * q);
   };
-  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
-    const u32x4_t av = __builtin_bit_cast(u32x4_t, a), bv = __builtin_bit_cast(u32x4_t, bop);
-    if (first)
-      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(av), "v"(bv));
-    else
-      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
-  };
+  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) { mfma_tied<T>(c, a, bop, first); };
   auto kloop = [&](Acc& acc) {
     constexpr int NI = C::NPART * PRD, D = W2_RING;
     uint4 ring[D];
@@ -211,7 +205,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
     }
   };
 
-  // ---- epilogue: bias, bf16 into the LDS output tile, IN partials from the fp32 values ----
+  // ---- epilogue: bias, 16-bit values into the LDS output tile, IN partials from the fp32 values ----
   auto epilogue = [&](const Work& wk, Acc& acc) {
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA results -> VALU reads
     const int c0 = 16 * cg + 4 * g;
@@ -225,7 +219,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
       const int row = r0 + r;
       const bool valid = full || (wk.oy0 + row < p.oh && wk.ox0 + px < p.ow);
       const f32x4_t v = add4(acc[r], bias);
-      const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+      const u32x2_t pk = {pack16<T>(v[0], v[1]), pack16<T>(v[2], v[3])};
       *(u32x2_t*)(smem + obase + row * C::TW * C::PIXB) = pk;
       const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
       stat4(s1, s2, x);
@@ -291,7 +285,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
   }
 }
 
-template <int CINP, int COUT, int TH, int OCC>
+template <typename T, int CINP, int COUT, int TH, int OCC>
 struct Ws2Inst {
   using C = W2Cfg<CINP, COUT, TH>;
   static int cus() {
@@ -309,14 +303,14 @@ struct Ws2Inst {
     p.n_work = (int)grid.x * (int)grid.y;
     const int nb = std::min(p.n_work, cus() * (OCC / 2));  // workgroups resident per CU
     if (p.axis_mode == AX_ZERO || p.axis_mode == AX_ZERO_PREREFLECT)
-      hipLaunchKernelGGL((ws2_kernel<CINP, COUT, TH, true, OCC>), dim3(nb), dim3(C::NT), 0, st, p);
+      hipLaunchKernelGGL((ws2_kernel<T, CINP, COUT, TH, true, OCC>), dim3(nb), dim3(C::NT), 0, st, p);
     else
-      hipLaunchKernelGGL((ws2_kernel<CINP, COUT, TH, false, OCC>), dim3(nb), dim3(C::NT), 0, st, p);
+      hipLaunchKernelGGL((ws2_kernel<T, CINP, COUT, TH, false, OCC>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
     std::memset(&k, 0, sizeof(k));
-    k.dtype = NST_DT_BF16;
+    k.dtype = dtype_code<T>();
     k.mode = MODE_WS2;
     k.ks = 3; k.stride = 2; k.cinp = CINP; k.bn = COUT; k.th = TH; k.tw = C::TW; k.wm = C::NRG; k.wn = C::NCG;
     k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
@@ -334,9 +328,11 @@ constexpr int W2_C3_TH = 8;
 #define E(...) Ws2Inst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_ws2(int* count) {
   static const ConvKernelInfo table[] = {
-      //  CINP COUT TH OCC
-      E(32, 64, W2_C2_TH, W2_C2_TH <= 8 ? 4 : 2),  // conv2 / down2
-      E(64, 128, W2_C3_TH, W2_C3_TH <= 4 ? 4 : 2),  // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
+      //  T     CINP COUT TH OCC
+      E(__bf16, 32, 64, W2_C2_TH, W2_C2_TH <= 8 ? 4 : 2),    // conv2 / down2
+      E(__bf16, 64, 128, W2_C3_TH, W2_C3_TH <= 4 ? 4 : 2),   // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
+      E(_Float16, 32, 64, W2_C2_TH, W2_C2_TH <= 8 ? 4 : 2),  // fp16 mode
+      E(_Float16, 64, 128, W2_C3_TH, W2_C3_TH <= 4 ? 4 : 2),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

@@ -70,7 +70,7 @@ struct W9Cfg {
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
-template <int NW>
+template <typename T, int NW>
 __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   using C = W9Cfg<NW>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
@@ -138,12 +138,14 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   typedef f32x4_t Acc[C::TH][2];
   auto mfma32 = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
     const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, bop),
-                                                first ? z : c, 0, 0, 0);
+    c = mfma16x16x32<T>(a, bop, first ? z : c);
   };
   auto mfma16 = [&](f32x4_t& c, const uint2& a, const uint2& bop) {
-    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4_t, a), __builtin_bit_cast(s16x4_t, bop), c,
-                                                  0, 0, 0);
+    if constexpr (IS_F16<T>)
+      c = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4_t, a), __builtin_bit_cast(f16x4_t, bop), c, 0, 0, 0);
+    else
+      c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4_t, a), __builtin_bit_cast(s16x4_t, bop), c,
+                                                    0, 0, 0);
   };
   // ---- K loop over the wave's 16 halo rows ----
   auto kloop = [&](Acc& acc, int buf) {
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
     }
   };
 
-  // ---- epilogue: bias, bf16 into the LDS output tile, IN partials from the fp32 values ----
+  // ---- epilogue: bias, 16-bit values into the LDS output tile, IN partials from the fp32 values ----
   auto epilogue = [&](const Work& wk_, Acc& acc) {
     const f32x4_t bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (4 * g) * 4);
     const f32x4_t bias1 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 + 4 * g) * 4);
@@ -206,8 +208,8 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
 #pragma unroll
       for (int y = 0; y < C::TH; ++y) {
         const f32x4_t va = add4(acc[y][0], bias0), vb = add4(acc[y][1], bias1);
-        const u32x2_t pa = {pack_bf16(va[0], va[1]), pack_bf16(va[2], va[3])};
-        const u32x2_t pb = {pack_bf16(vb[0], vb[1]), pack_bf16(vb[2], vb[3])};
+        const u32x2_t pa = {pack16<T>(va[0], va[1]), pack16<T>(va[2], va[3])};
+        const u32x2_t pb = {pack16<T>(vb[0], vb[1]), pack16<T>(vb[2], vb[3])};
         *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o0) = pa;
         *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o1) = pb;
         f32x4_t xa = va, xb = vb;
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   vm_wait<0>();
 }
 
-template <int NW>
+template <typename T, int NW>
 struct Ws9Inst {
   using C = W9Cfg<NW>;
   static int cus() {
@@ -310,12 +312,12 @@ struct Ws9Inst {
     ConvParams p = p0;
     p.n_work = (int)grid.x * (int)grid.y;
     const int nb = std::min(p.n_work, cus() * (8 / NW));  // 8 waves per CU (VGPRs)
-    hipLaunchKernelGGL(ws9_kernel<NW>, dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((ws9_kernel<T, NW>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
     std::memset(&k, 0, sizeof(k));
-    k.dtype = NST_DT_BF16;
+    k.dtype = dtype_code<T>();
     k.mode = MODE_WS9;
     k.ks = 9; k.stride = 1; k.cinp = 4; k.bn = C::COUT; k.th = C::TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
     k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
@@ -330,8 +332,8 @@ struct Ws9Inst {
 };
 
 const ConvKernelInfo* conv_table_ws9(int* count) {
-  static const ConvKernelInfo table[] = {Ws9Inst<WS9_NW>::info()};
-  *count = 1;
+  static const ConvKernelInfo table[] = {Ws9Inst<__bf16, WS9_NW>::info(), Ws9Inst<_Float16, WS9_NW>::info()};
+  *count = 2;
   return table;
 }
 

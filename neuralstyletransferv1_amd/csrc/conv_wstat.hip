@@ -5,7 +5,7 @@
 // producer's InstanceNorm apply + ReLU (or the residual join, RES) in the fill, this layer's
 // InstanceNorm partial sums in the epilogue.
 //
-// Why a separate kernel: 128 x 1152 bf16 weights are 144 VGPRs per wave when eight waves split the
+// Why a separate kernel: 128 x 1152 16-bit (bf16 / fp16) weights are 144 VGPRs per wave when eight waves split the
 // output channels 16 each — the whole weight tensor fits in one CU's register file.  So each wave
 // loads its 16 channels' weights ONCE per launch and keeps them in registers; the K loop reads only
 // pixel operands from LDS, has no weight stream, no weight ring and no per-stage barrier.  The
@@ -73,7 +73,7 @@ struct WsCfg {
 
 // XO: a WF_NORM fill also writes what it staged for the tile's own pixels (ReLU(IN(y)), the first
 // residual block's input x_0) to res_out, so the next join reads x_0 instead of re-normalising
-template <int TH, int FILL, bool ZPAD, bool XO>
+template <typename T, int TH, int FILL, bool ZPAD, bool XO>
 __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   using C = WsCfg<TH, FILL>;
   constexpr bool RES = C::RES;
@@ -211,11 +211,11 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
       const uint32_t w2[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float r0 = bf16_lo(w2[j]), r1 = bf16_hi(w2[j]);
+        float r0 = lo16<T>(w2[j]), r1 = hi16<T>(w2[j]);
         const float4 n = ny[j];
-        const float a = bf16_lo(w[j]) * n.x + n.z;
-        const float bb = bf16_hi(w[j]) * n.y + n.w;
-        o[j] = pack_bf16(r0 + a, r1 + bb);
+        const float a = lo16<T>(w[j]) * n.x + n.z;
+        const float bb = hi16<T>(w[j]) * n.y + n.w;
+        o[j] = pack16<T>(r0 + a, r1 + bb);
       }
     } else if constexpr (FILL == WF_RAW) {
 #pragma unroll
@@ -225,9 +225,9 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float4 n = ny[j];
-        const float a = __builtin_fmaf(bf16_lo(w[j]), n.x, n.z);
-        const float bb = __builtin_fmaf(bf16_hi(w[j]), n.y, n.w);
-        const i16x2_t r = __builtin_bit_cast(i16x2_t, pack_bf16(a, bb));
+        const float a = __builtin_fmaf(lo16<T>(w[j]), n.x, n.z);
+        const float bb = __builtin_fmaf(hi16<T>(w[j]), n.y, n.w);
+        const i16x2_t r = __builtin_bit_cast(i16x2_t, pack16<T>(a, bb));
         o[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
       }
     }
@@ -271,13 +271,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   // The hazards hipcc cannot see are covered by construction: each tile's first MFMA of a row
   // takes C = 0 (no VALU write feeds an MFMA), operands come from loads it waits for, an
   // accumulation chain needs no wait states, and mfma_drain() pads before the epilogue reads.
-  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
-    const u32x4_t av = __builtin_bit_cast(u32x4_t, a), bv = __builtin_bit_cast(u32x4_t, bop);
-    if (first)
-      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(av), "v"(bv));
-    else
-      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
-  };
+  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) { mfma_tied<T>(c, a, bop, first); };
   auto kloop = [&](Acc& acc, auto&& hook, auto&& bound) {
     constexpr int NI = 4 * PRD, D = WS_RING;
     uint4 ring[D];
@@ -329,7 +323,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
       for (int r = 0; r < TH; ++r) {
         const bool valid = decltype(all_valid)::value || (wk.ty0 + r < p.oh && ox < p.ow);
         const f32x4_t v = add4(acc[r], bias);
-        const u32x2_t pk = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+        const u32x2_t pk = {pack16<T>(v[0], v[1]), pack16<T>(v[2], v[3])};
         if constexpr (C::OST) {
           *(u32x2_t*)(smem + obase + r * C::TW * 256) = pk;
         } else {
@@ -473,7 +467,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   vm_wait<0>();  // no LDS-DMA may land after the workgroup has released its LDS
 }
 
-template <int TH, bool RES>
+template <typename T, int TH, bool RES>
 struct WstatInst {
   using C = WsCfg<TH, RES ? WF_RES : WF_NORM>;  // NFMAX, LDS and weight sizes shared by the FILL variants
   static int cus() {
@@ -487,7 +481,7 @@ struct WstatInst {
   }
   template <int FILL, bool ZPAD, bool XO = false>
   static void go(const ConvParams& p, int nb, hipStream_t st) {
-    hipLaunchKernelGGL((wstat_kernel<TH, FILL, ZPAD, XO>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((wstat_kernel<T, TH, FILL, ZPAD, XO>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   // grid.x = tiles per frame, grid.y = frames; launched in chunks of <= NFMAX frames (the IN tables
   // of a launch's frames live in LDS)
@@ -526,7 +520,7 @@ struct WstatInst {
   static ConvKernelInfo info() {
     ConvKernelInfo k;
     std::memset(&k, 0, sizeof(k));
-    k.dtype = NST_DT_BF16;
+    k.dtype = dtype_code<T>();
     k.mode = MODE_WSTAT;
     k.ks = 3; k.stride = 1; k.cinp = C::CINP; k.bn = 128; k.th = TH; k.tw = C::TW; k.wm = C::NW; k.wn = 1;
     k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
@@ -544,8 +538,10 @@ constexpr int WSTAT_TH = 8;  // tile rows
 #define E(...) WstatInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wstat(int* count) {
   static const ConvKernelInfo table[] = {
-      E(WSTAT_TH, false),  // residual trunk
-      E(WSTAT_TH, true),   // + residual join in the fill
+      E(__bf16, WSTAT_TH, false),    // residual trunk
+      E(__bf16, WSTAT_TH, true),     // + residual join in the fill
+      E(_Float16, WSTAT_TH, false),  // fp16 mode
+      E(_Float16, WSTAT_TH, true),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

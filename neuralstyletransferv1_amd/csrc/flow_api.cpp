@@ -45,11 +45,46 @@ int nst_flow_farneback(const uint8_t* prev, const uint8_t* next, int h, int w, d
 }
 
 int nst_flow_downscale_gray(const uint8_t* gray, int h, int w, int ds, uint8_t* out, void* stream) {
-  if (!gray || !out || ds < 2 || h % ds != 0 || w % ds != 0 || h / ds < 2 || w / ds < 2) {
-    set_error("nst_flow_downscale_gray: the frame must be an exact multiple of the factor (ds >= 2)");
+  if (!gray || !out || ds < 2) { set_error("nst_flow_downscale_gray: invalid arguments (ds >= 2)"); return NST_E_INVALID; }
+  if (h / ds < 2 || w / ds < 2) {
+    set_error("nst_flow_downscale_gray: frame " + std::to_string(w) + "x" + std::to_string(h) + " too small for factor " +
+              std::to_string(ds));
     return NST_E_SHAPE;
   }
-  FL_LAUNCH(launch_area_down(gray, h, w, ds, out, (hipStream_t)stream), "area_down");
+  FL_LAUNCH(launch_area_resize(gray, 1, h, w, 1, h / ds, w / ds, out, (hipStream_t)stream), "area_resize");
+  return NST_OK;
+}
+
+int nst_flow_dis_scratch_bytes(int n, int h, int w, size_t* out) {
+  if (n <= 0 || h <= 0 || w <= 0 || !out) { set_error("nst_flow_dis_scratch_bytes: invalid arguments"); return NST_E_INVALID; }
+  const int rc = dis_check_shape(h, w);
+  if (rc != 0) {
+    set_error(std::string("nst_flow_dis: frame ") + std::to_string(w) + "x" + std::to_string(h) +
+              (rc == -1 ? " is too small for DIS PRESET_FAST (its coarsest pyramid level would lie below the finest, 2)"
+                        : " is too wide for the inverse search's stripe buffer"));
+    return NST_E_SHAPE;
+  }
+  *out = dis_scratch_bytes(n, h, w);
+  return NST_OK;
+}
+
+int nst_flow_dis(const uint8_t* prev, const uint8_t* next, int n, int h, int w, float* flow, void* scratch,
+                 size_t scratch_bytes, void* stream) {
+  size_t need = 0;
+  if (!prev || !next || !flow || !scratch) { set_error("nst_flow_dis: invalid arguments"); return NST_E_INVALID; }
+  const int rc = nst_flow_dis_scratch_bytes(n, h, w, &need);
+  if (rc != NST_OK) return rc;
+  if (scratch_bytes < need) { set_error("nst_flow_dis: scratch too small"); return NST_E_WORKSPACE; }
+  FL_LAUNCH(launch_dis(prev, next, n, h, w, flow, scratch, (hipStream_t)stream), "dis");
+  return NST_OK;
+}
+
+int nst_resize_area_u8(const uint8_t* in, int n, int h, int w, int c, uint8_t* out, int out_h, int out_w, void* stream) {
+  if (!in || !out || n <= 0 || h <= 0 || w <= 0 || c <= 0 || c > 4 || out_h <= 0 || out_w <= 0 || out_h > h || out_w > w) {
+    set_error("nst_resize_area_u8: invalid arguments (downscaling only: 0 < out <= in, 1..4 channels)");
+    return NST_E_INVALID;
+  }
+  FL_LAUNCH(launch_area_resize(in, n, h, w, c, out_h, out_w, out, (hipStream_t)stream), "area_resize");
   return NST_OK;
 }
 

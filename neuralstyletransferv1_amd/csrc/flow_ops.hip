@@ -12,6 +12,7 @@
 //   * the motion-adaptive blend alpha: clip(|flow| / 8) blurred (cv2.GaussianBlur sigma 3), then
 //     max_alpha - (max_alpha - min_alpha) * m.
 // One thread per output element throughout; all planes fp32 in HBM (the box sums in fp64, as OpenCV).
+#include <cfloat>
 #include <math.h>
 
 #include <algorithm>
@@ -421,24 +422,93 @@ hipError_t launch_farneback(const uint8_t* prev, const uint8_t* next, int h, int
   return hipGetLastError();
 }
 
-// ---- --flow_downscale (pipeline.py:1886-1892, 1920-1923): cv2.resize(gray, (W/ds, H/ds), INTER_AREA) for an
-// exact integer factor (OpenCV's resizeAreaFast: ds = 2 takes its SIMD rounding (sum + 2) >> 2, other factors
-// saturate_cast(sum / area)), and the flow brought back with INTER_LINEAR and scaled by ds ----
-__global__ __launch_bounds__(256) void area_down_kernel(const uint8_t* __restrict__ in, int w, int ds, int oh, int ow,
-                                                        uint8_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (size_t)oh * ow) return;
-  const int x = (int)(i % ow), y = (int)(i / ow);
-  int sum = 0;
-  for (int r = 0; r < ds; ++r)
-    for (int c = 0; c < ds; ++c) sum += in[(size_t)(y * ds + r) * w + x * ds + c];
-  out[i] = ds == 2 ? (uint8_t)((sum + 2) >> 2) : (uint8_t)min(255, (int)rintf((float)sum * (1.f / (float)(ds * ds))));
+// ---- cv2.resize(src, (ow, oh), interpolation=INTER_AREA) of u8 images (--flow_downscale's grays,
+// pipeline.py:1886-1892, and the DIS pyramid) — OpenCV's resize.cpp restated (cv2 absent: parity unpinned):
+//   * integer scales in both axes (is_area_fast): resizeAreaFast_, the int sum of each iscale_x x iscale_y
+//     block times the fp32 1/area, rounded (cvRound); at scale 2 x 2 ResizeAreaFastVec's (sum + 2) >> 2;
+//   * otherwise (downscaling, scale >= 1) ResizeArea_Invoker with computeResizeAreaTab's fractional cells:
+//     per destination column the source columns sx with weight alpha (fp32 of a double ratio, the partial
+//     first / last cells only beyond 1e-3), per destination row the rows sy with beta; per row
+//     buf = sum(S[sy][sx] * alpha) over the column's cells in order, sum = beta * buf (first row) or
+//     sum += beta * buf, then cvRound + saturate.  The cell tables are recomputed per thread in double,
+//     exactly as the host would (no table upload per geometry). ----
+struct AreaCells {
+  int sx[3], n_mid;       // first partial cell (or -1), the full cells sx1 .. sx1 + n_mid - 1, last partial cell (or -1)
+  float a_first, a_mid, a_last;
+  int sx1;
+};
+__device__ __forceinline__ AreaCells area_cells(int d, int ssize, double scale) {
+  AreaCells c;
+  const double fs1 = d * scale, fs2 = fs1 + scale;
+  const double cell = fmin(scale, ssize - fs1);
+  int s1 = (int)ceil(fs1), s2 = (int)floor(fs2);
+  s2 = min(s2, ssize - 1);
+  s1 = min(s1, s2);
+  c.sx[0] = (s1 - fs1 > 1e-3) ? s1 - 1 : -1;
+  c.a_first = (float)((s1 - fs1) / cell);
+  c.sx1 = s1;
+  c.n_mid = s2 - s1;
+  c.a_mid = (float)(1.0 / cell);
+  c.sx[2] = (fs2 - s2 > 1e-3) ? s2 : -1;
+  c.a_last = (float)(fmin(fmin(fs2 - s2, 1.0), cell) / cell);
+  return c;
 }
 
-hipError_t launch_area_down(const uint8_t* in, int h, int w, int ds, uint8_t* out, hipStream_t st) {
-  const int oh = h / ds, ow = w / ds;
-  const size_t n = (size_t)oh * ow;
-  hipLaunchKernelGGL(area_down_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, w, ds, oh, ow, out);
+__global__ __launch_bounds__(256) void area_resize_kernel(const uint8_t* __restrict__ in, int n, int h, int w, int ch,
+                                                          int oh, int ow, double sx_scale, double sy_scale, int fast,
+                                                          int isx, int isy, uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)n * oh * ow * ch) return;
+  const int c = (int)(i % ch);
+  size_t r = i / ch;
+  const int dx = (int)(r % ow);
+  r /= ow;
+  const int dy = (int)(r % oh);
+  const int f = (int)(r / oh);
+  const uint8_t* S = in + (size_t)f * h * w * ch;
+  if (fast) {
+    int sum = 0;
+    for (int yy = 0; yy < isy; ++yy)
+      for (int xx = 0; xx < isx; ++xx) sum += S[((size_t)(dy * isy + yy) * w + dx * isx + xx) * ch + c];
+    if (isx == 2 && isy == 2) {  // ResizeAreaFastVec: (sum + 2) >> 2 (halves round up), SIMD and tail alike
+      out[i] = (uint8_t)((sum + 2) >> 2);
+      return;
+    }
+    const float scale = 1.f / (float)(isx * isy);
+    out[i] = (uint8_t)min(255, max(0, (int)rintf((float)sum * scale)));
+    return;
+  }
+  const AreaCells X = area_cells(dx, w, sx_scale), Y = area_cells(dy, h, sy_scale);
+  auto row_buf = [&](int sy) {
+    const uint8_t* R = S + (size_t)sy * w * ch + c;
+    float buf = 0.f;
+    if (X.sx[0] >= 0) buf = buf + (float)R[(size_t)X.sx[0] * ch] * X.a_first;
+    for (int k = 0; k < X.n_mid; ++k) buf = buf + (float)R[(size_t)(X.sx1 + k) * ch] * X.a_mid;
+    if (X.sx[2] >= 0) buf = buf + (float)R[(size_t)X.sx[2] * ch] * X.a_last;
+    return buf;
+  };
+  float sum = 0.f;
+  bool first = true;
+  auto add_row = [&](int sy, float beta) {
+    const float b = beta * row_buf(sy);
+    sum = first ? b : sum + b;
+    first = false;
+  };
+  if (Y.sx[0] >= 0) add_row(Y.sx[0], Y.a_first);
+  for (int k = 0; k < Y.n_mid; ++k) add_row(Y.sx1 + k, Y.a_mid);
+  if (Y.sx[2] >= 0) add_row(Y.sx[2], Y.a_last);
+  out[i] = (uint8_t)min(255, max(0, (int)rintf(sum)));
+}
+
+hipError_t launch_area_resize(const uint8_t* in, int n, int h, int w, int ch, int oh, int ow, uint8_t* out,
+                              hipStream_t st) {
+  // resize(): inv_scale = dsize / ssize, scale = 1 / inv_scale; is_area_fast when both are integers
+  const double sx = 1. / ((double)ow / w), sy = 1. / ((double)oh / h);
+  const int isx = (int)lrint(sx), isy = (int)lrint(sy);
+  const int fast = fabs(sx - isx) < DBL_EPSILON && fabs(sy - isy) < DBL_EPSILON;
+  const size_t total = (size_t)n * oh * ow * ch;
+  hipLaunchKernelGGL(area_resize_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, n, h, w, ch, oh, ow,
+                     sx, sy, fast, isx, isy, out);
   return hipGetLastError();
 }
 
@@ -450,7 +520,10 @@ __global__ __launch_bounds__(256) void flow_fuse_kernel(const float* __restrict_
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= hw) return;
   const int x = (int)(i % w), y = (int)(i / w);
-  const float mx = (float)x + flow[2 * i], my = (float)y + flow[2 * i + 1];
+  // cv2's saturate_cast<int>(map * 32) saturates (NaN -> INT_MIN); clamping the map far outside the frame first
+  // gives the same replicated-border sample and keeps the int conversion defined
+  const float mx = fminf(fmaxf((float)x + flow[2 * i], -2.f * w), 3.f * w);
+  const float my = fminf(fmaxf((float)y + flow[2 * i + 1], -2.f * h), 3.f * h);
   const int X = (int)rintf(mx * 32.f), Y = (int)rintf(my * 32.f);
   const int sx = X >> 5, sy = Y >> 5;
   const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);

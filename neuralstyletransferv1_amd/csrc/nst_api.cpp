@@ -25,6 +25,7 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 const ConvKernelInfo* conv_table_bf16(int* count);
+const ConvKernelInfo* conv_table_f16(int* count);
 const ConvKernelInfo* conv_table_bf16_wl(int* count);
 const ConvKernelInfo* conv_table_f32(int* count);
 const ConvKernelInfo* conv_table_out9(int* count);
@@ -37,17 +38,19 @@ const ConvKernelInfo* conv_table_ws9(int* count);
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
                                        int out_kind, int res, bool no_persistent) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
-  const TableFn tables_bf16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_ws9,
-                                 conv_table_out9, conv_table_bf16};
+  // 16-bit formats (bf16, fp16) share the specialised tables; an entry matches only its own dtype
+  const TableFn tables_16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_ws9,
+                               conv_table_out9, conv_table_bf16, conv_table_f16};
   const TableFn tables_f32[] = {conv_table_f32};
-  const TableFn* tables = dtype == NST_DT_BF16 ? tables_bf16 : tables_f32;
-  const int ntables = dtype == NST_DT_BF16 ? 7 : 1;
-  for (int ti = (dtype == NST_DT_BF16 && no_persistent) ? 1 : 0; ti < ntables; ++ti) {
+  const bool h16 = dtype != NST_DT_F32;
+  const TableFn* tables = h16 ? tables_16 : tables_f32;
+  const int ntables = h16 ? 8 : 1;
+  for (int ti = (h16 && no_persistent) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
     const ConvKernelInfo* t = tables[ti](&count);
     for (int i = 0; i < count; ++i) {
       const ConvKernelInfo& k = t[i];
-      if (k.mode == mode && k.ks == ks && k.stride == stride && k.cinp == cinp && k.bn == bn &&
+      if (k.dtype == dtype && k.mode == mode && k.ks == ks && k.stride == stride && k.cinp == cinp && k.bn == bn &&
           k.in_kind == in_kind && k.out_kind == out_kind && k.res == res)
         return &k;
     }
@@ -224,6 +227,26 @@ uint16_t f32_to_bf16_rne(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
+
+// IEEE binary16, round to nearest even (values >= 65520 -> inf, as the device's v_cvt_pk_f16_f32)
+uint16_t f32_to_f16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  const uint16_t sign = (uint16_t)((u >> 16) & 0x8000u);
+  uint32_t a = u & 0x7fffffffu;
+  if (a > 0x7f800000u) return sign | 0x7e00u;   // NaN
+  if (a >= 0x477ff000u) return sign | 0x7c00u;  // rounds past 65504
+  if (a >= 0x38800000u) {                       // normal: rebias the exponent, RNE on the 13 dropped bits
+    a -= 0x38000000u;
+    a += 0xfffu + ((a >> 13) & 1u);
+    return sign | (uint16_t)(a >> 13);
+  }
+  float af;  // subnormal or zero: units of 2^-24 (exact power-of-two scaling), nearbyint rounds to even
+  std::memcpy(&af, &a, 4);
+  return sign | (uint16_t)std::nearbyint(af * 16777216.0f);
+}
+// packed weights -> device, in the layer's compute dtype
+int upload_weights(int dtype, const std::vector<float>& pk, void** dst);
 
 // Sub-pixel phase weights of an x2 up-conv: output pixel (2y + a, 2x + b) is a 2x2 conv over the
 // source grid, window tap (ty, tx); its weight is the sum of the 3x3 taps landing on that source
@@ -450,6 +473,12 @@ int upload(const void* host, size_t bytes, void** dev) {
   NST_HIP_CHECK(hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice));
   return NST_OK;
 }
+int upload_weights(int dtype, const std::vector<float>& pk, void** dst) {
+  if (dtype == NST_DT_F32) return upload(pk.data(), pk.size() * 4, dst);
+  std::vector<uint16_t> pb(pk.size());
+  for (size_t i = 0; i < pk.size(); ++i) pb[i] = dtype == NST_DT_F16 ? f32_to_f16_rne(pk[i]) : f32_to_bf16_rne(pk[i]);
+  return upload(pb.data(), pb.size() * 2, dst);
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -511,7 +540,7 @@ void tile_grid(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx,
 
 Plan make_plan(const nst_handle* h, int n, int H, int W) {
   Plan P;
-  const size_t esz = h->dtype == NST_DT_BF16 ? 2 : 4;
+  const size_t esz = h->dtype == NST_DT_F32 ? 4 : 2;
   int bh[NBUF], bw[NBUF];
   const size_t nops = h->prog.size();
   P.ih.resize(nops); P.iw.resize(nops); P.oh.resize(nops); P.ow.resize(nops); P.ch.resize(nops); P.cw.resize(nops);
@@ -527,6 +556,16 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         return P;
       }
       const int ch = conv_out_dim(Ly.d, sh), cw = conv_out_dim(Ly.d, sw);
+      // the conv kernels address a frame (a launch's frames, for the weight-stationary ones) with
+      // 32-bit buffer offsets, 0x80000000 and up reserved as the out-of-range offset: one frame's
+      // activation must stay below 2^31 bytes (a 16-bit 128-channel map of 8.4 Gpx / 4)
+      const size_t fin = (size_t)sh * sw * (op.src == B_IMG ? 8 : Ly.cinp) * esz;
+      const size_t fout = (size_t)ch * cw * Ly.coutp * esz;
+      if (std::max(fin, fout) >= (size_t)0x7FFFFF00u) {
+        P.err = "input " + std::to_string(H) + "x" + std::to_string(W) + " too large: layer " + Ly.d.conv +
+                " needs " + std::to_string(std::max(fin, fout)) + " bytes per frame (limit 2^31)";
+        return P;
+      }
       if (op.src == B_IMG && Ly.prepad) {  // bf16 x4 per pixel over the conv's padded input extent
         // + tail slack: the 9x9 kernel's last tile row reads up to 16 halo rows (and a row of column
         // wrap) from its tile origin, which may lie past the last frame's padded extent
@@ -630,13 +669,7 @@ namespace nst {
 // upload it (bf16 or fp32 per the kernel); used by the VGG program (vgg_gatys.cpp)
 int pack_upload_conv(const ConvKernelInfo& k, int cin, int cout, int ks, const float* W, int coutp, void** dev) {
   LayerDef d{"", "", cin, cout, ks, 1, AX_ZERO, ks / 2, 0, false};
-  const std::vector<float> pk = pack_weights(k, d, W, coutp);
-  if (k.dtype == NST_DT_BF16) {
-    std::vector<uint16_t> pb(pk.size());
-    for (size_t i = 0; i < pk.size(); ++i) pb[i] = f32_to_bf16_rne(pk[i]);
-    return upload(pb.data(), pb.size() * 2, dev);
-  }
-  return upload(pk.data(), pk.size() * 4, dev);
+  return upload_weights(k.dtype, pack_weights(k, d, W, coutp), dev);
 }
 int upload_floats(const float* host, size_t n, float** dev) { return upload(host, n * 4, (void**)dev); }
 // the output decode constants of an io_preset (the region compositor's sources, region_api.cpp)
@@ -726,7 +759,7 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
 
 int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                   unsigned flags, nst_handle** out) {
-  if (!out || arch < 0 || arch > 3 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16) ||
+  if (!out || arch < 0 || arch > 3 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16 && compute_dtype != NST_DT_F16) ||
       (flags & ~(unsigned)NST_KSEL_ALL) != 0) {
     set_error("nst_create: invalid arguments");
     return NST_E_INVALID;
@@ -841,12 +874,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       Ly.frn = final_layer ? 0 : 1;
     }
     auto upload_packed = [&](const std::vector<float>& pk, void** dst) -> int {
-      if (compute_dtype == NST_DT_BF16) {
-        std::vector<uint16_t> pb(pk.size());
-        for (size_t i = 0; i < pk.size(); ++i) pb[i] = f32_to_bf16_rne(pk[i]);
-        return upload(pb.data(), pb.size() * 2, dst);
-      }
-      return upload(pk.data(), pk.size() * 4, dst);
+      return upload_weights(compute_dtype, pk, dst);
     };
     if (Ly.mode == MODE_KYROT) {
       if ((rc = upload_packed(pack_kyrot_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
@@ -959,7 +987,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
   }
   DeviceGuard guard(h->device);
   hipStream_t st = (hipStream_t)stream;
-  const size_t esz = h->dtype == NST_DT_BF16 ? 2 : 4;
+  const size_t esz = h->dtype == NST_DT_F32 ? 4 : 2;
   char* ws = (char*)workspace;
   void* bufs[NBUF];
   for (int b = 0; b < NBUF; ++b) bufs[b] = ws + P.off_buf[b];
@@ -1026,7 +1054,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       // identity coordinate map (pad 0, no reflection)
       const int hp = P.ch[i] + Ly.d.ks - 1, wp = P.cw[i] + Ly.d.ks - 1;
       void* pre = ws + P.off_pre;
-      hipError_t e = launch_prepad_encode(p, x_fmt == NST_IO_U8_NHWC ? IN_U8_NHWC : IN_F32_NCHW, n, hp, wp, pre, st);
+      hipError_t e = launch_prepad_encode(h->dtype, p, x_fmt == NST_IO_U8_NHWC ? IN_U8_NHWC : IN_F32_NCHW, n, hp, wp, pre, st);
       if (e != hipSuccess) { set_error(std::string("prepad launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
       p.in = pre;
       p.hs = hp;
@@ -1169,7 +1197,7 @@ int nst_op_describe(const nst_handle* h, int n, int in_h, int in_w, int op_index
   out->cin_stride = op.src == B_IMG ? 3 : Ly.cinp;
   out->cout_stride = Ly.coutp;
   out->kernel_mode = Ly.mode;
-  out->elem_bytes = h->dtype == NST_DT_BF16 ? 2 : 4;
+  out->elem_bytes = h->dtype == NST_DT_F32 ? 4 : 2;
   return NST_OK;
 }
 

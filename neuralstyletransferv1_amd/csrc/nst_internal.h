@@ -146,7 +146,8 @@ hipError_t launch_lab_blend(const uint32_t* rgb2lab, const uint32_t* lab2rgb, co
                             hipStream_t st);
 hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigma, float* tmp, float* alpha,
                                hipStream_t st);
-hipError_t launch_prepad_encode(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st);
+hipError_t launch_prepad_encode(int dtype, const ConvParams& p, int in_kind, int n, int hp, int wp, void* out,
+                                hipStream_t st);
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,
                         float omb, uint8_t* out, int n, int hw, hipStream_t st, const uint8_t* mask8 = nullptr);
 size_t gram_workspace_bytes(int n, int c, int hw);

@@ -8,6 +8,7 @@
 #include "seg_internal.h"
 #include "nst_hip.h"
 #include "post_common.h"
+#include "conv_impl.h"
 
 namespace nst {
 
@@ -154,10 +155,10 @@ __global__ __launch_bounds__(256) void residual_kernel(const T* __restrict__ y, 
       const uint32_t wa[4] = {va[u].x, va[u].y, va[u].z, va[u].w}, wb[4] = {vb[u].x, vb[u].y, vb[u].z, vb[u].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        vy[2 * j] = __uint_as_float(wa[j] << 16);
-        vy[2 * j + 1] = __uint_as_float(wa[j] & 0xffff0000u);
-        vr[2 * j] = __uint_as_float(wb[j] << 16);
-        vr[2 * j + 1] = __uint_as_float(wb[j] & 0xffff0000u);
+        vy[2 * j] = lo16<T>(wa[j]);
+        vy[2 * j + 1] = hi16<T>(wa[j]);
+        vr[2 * j] = lo16<T>(wb[j]);
+        vr[2 * j + 1] = hi16<T>(wb[j]);
       }
     } else {
       vy[0] = __uint_as_float(va[u].x); vy[1] = __uint_as_float(va[u].y);
@@ -170,9 +171,9 @@ __global__ __launch_bounds__(256) void residual_kernel(const T* __restrict__ y, 
     for (int j = 0; j < CPC; ++j) {
       float rr = vr[j];
       if (rs) {
-        // as a normalising fill stages it (conv_impl.h norm_chunk): bf16 of one fma
+        // as a normalising fill stages it (conv_impl.h norm_chunk): one fma, rounded to T
         if constexpr (sizeof(T) == 2)
-          rr = (float)(__bf16)__builtin_fmaf(rr, rsc[j], rsh[j]);
+          rr = lo16<T>(pack16<T>(__builtin_fmaf(rr, rsc[j], rsh[j]), 0.f));
         else
           rr = rr * rsc[j] + rsh[j];
         if (r_relu) rr = fmaxf(rr, 0.f);
@@ -186,10 +187,7 @@ __global__ __launch_bounds__(256) void residual_kernel(const T* __restrict__ y, 
     if constexpr (sizeof(T) == 2) {
       uint32_t w[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        __bf16 lo = (__bf16)o[2 * j], hi = (__bf16)o[2 * j + 1];
-        w[j] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
-      }
+      for (int j = 0; j < 4; ++j) w[j] = pack16<T>(o[2 * j], o[2 * j + 1]);
       *(uint4*)dst = make_uint4(w[0], w[1], w[2], w[3]);
     } else {
       *(float4*)dst = make_float4(o[0], o[1], o[2], o[3]);
@@ -199,7 +197,7 @@ __global__ __launch_bounds__(256) void residual_kernel(const T* __restrict__ y, 
 
 hipError_t launch_residual(int dtype, const void* y, const float2* ys, const void* r, const float2* rs,
                            int r_relu, int relu_out, void* out, int n, int hw, int c, hipStream_t st) {
-  const int cpc = dtype == NST_DT_BF16 ? 8 : 4;
+  const int cpc = dtype == NST_DT_F32 ? 4 : 8;
   const int cv_n = c / cpc;
   if (c % cpc != 0 || cv_n > 256) return hipErrorInvalidValue;
   const int tpp = 256 / cv_n;
@@ -208,6 +206,9 @@ hipError_t launch_residual(int dtype, const void* y, const float2* ys, const voi
   if (dtype == NST_DT_BF16)
     hipLaunchKernelGGL(residual_kernel<__bf16>, grid, block, 0, st, (const __bf16*)y, ys, (const __bf16*)r, rs,
                        r_relu, relu_out, (__bf16*)out, hw, c);
+  else if (dtype == NST_DT_F16)
+    hipLaunchKernelGGL(residual_kernel<_Float16>, grid, block, 0, st, (const _Float16*)y, ys, (const _Float16*)r, rs,
+                       r_relu, relu_out, (_Float16*)out, hw, c);
   else
     hipLaunchKernelGGL(residual_kernel<float>, grid, block, 0, st, (const float*)y, ys, (const float*)r, rs, r_relu,
                        relu_out, (float*)out, hw, c);

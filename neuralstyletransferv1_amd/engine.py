@@ -17,7 +17,8 @@ from torch import nn
 from . import _lib
 from ._lib import NstError, NstParam, check, lib
 
-_DTYPES = {"fp32": _lib.NST_DT_F32, "float32": _lib.NST_DT_F32, "bf16": _lib.NST_DT_BF16, "bfloat16": _lib.NST_DT_BF16}
+_DTYPES = {"fp32": _lib.NST_DT_F32, "float32": _lib.NST_DT_F32, "bf16": _lib.NST_DT_BF16, "bfloat16": _lib.NST_DT_BF16,
+           "fp16": _lib.NST_DT_F16, "float16": _lib.NST_DT_F16}
 
 
 class Engine:
@@ -117,7 +118,7 @@ class Engine:
             y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=self.device)
             yf = _lib.NST_IO_F32_NCHW
         ops = self.op_descs(n, h, w)
-        dt = torch.bfloat16 if self.dtype == _lib.NST_DT_BF16 else torch.float32
+        dt = {_lib.NST_DT_BF16: torch.bfloat16, _lib.NST_DT_F16: torch.float16}.get(self.dtype, torch.float32)
         caps = []
         k = len(ops)
         act, res, st = (ctypes.c_void_p * k)(), (ctypes.c_void_p * k)(), (ctypes.c_void_p * k)()
@@ -192,7 +193,8 @@ class StylizationNet(nn.Module):
 
     def __init__(self):
         super().__init__()
-        # "fp32": parity mode (exact-f32 MFMA); "bf16": throughput mode (bf16 MFMA, fp32 accumulate)
+        # "fp32": parity mode (exact-f32 MFMA); "bf16": throughput mode (bf16 MFMA, fp32 accumulate);
+        # "fp16": fp16 MFMA at the bf16 rate, within +-1 LSB of the reference's uint8 frames
         self.compute_dtype = "fp32"
         # kernel selection (names of _lib.KSEL): e.g. {"no_wstat"} runs the residual trunk on the
         # generic kernel instead of the weight-stationary one; empty = the fastest mapping
@@ -213,7 +215,7 @@ class StylizationNet(nn.Module):
             device = torch.device("cuda", torch.cuda.current_device())
         dtype = dtype or self.compute_dtype
         if dtype not in _DTYPES:
-            raise NstError(f"compute_dtype must be fp32 or bf16, got {dtype!r}")
+            raise NstError(f"compute_dtype must be fp32, bf16 or fp16, got {dtype!r}")
         flags = 0
         for name in self.kernel_select:
             if name not in _lib.KSEL:

@@ -10,8 +10,9 @@ per-frame loop (`style_frames`, pipeline.py:527-2122, standard path :1409-1519 +
     -> LAB EMA (LUT, frame order) -> mask composite -> uniform blend --D2H--> host: PIL encode.
 
 Additions: --gpus N (frames round-robin over N GPUs, ordered gather to rank 0 over RCCL),
---batch B (frames per GPU step), --dtype {fp32,bf16} (fp32 = parity with the reference's
-arithmetic, default; bf16 = throughput mode), --synthetic WxH / --synthetic_frames N (an
+--batch B (frames per GPU step), --dtype {fp32,bf16,fp16} (fp32 = parity with the reference's
+arithmetic, default; bf16 = throughput mode; fp16 = bf16's speed within +-1 LSB of the reference),
+--synthetic WxH / --synthetic_frames N (an
 in-memory synthetic frame stream instead of files; config 4 of BASELINE.json).
 
 Also on the GPU: the LAB multi-model blend (--blend_models_lab, pipeline.py:1841-1870) and the
@@ -21,12 +22,12 @@ restated, parity unpinned because cv2 is absent here).
 Region blending (--region_mode / --region_optimize and their spec, animation and rotation flags,
 pipeline.py:1120-1407, 1720-1839) runs on the GPU compositor of regions.py.
 
-The flow-guided EMA (--flow_ema --flow_method farneback, pipeline.py:1884-1940) and the motion-adaptive
-blend (--motion_blend, :2072-2086) run on the GPU (temporal.py).
+The flow-guided EMA (--flow_ema with --flow_method dis, the default, or farneback, pipeline.py:1884-1940; any
+--flow_downscale factor, floored like the reference's (W0 // ds, H0 // ds)) and the motion-adaptive blend
+(--motion_blend, :2072-2086) run on the GPU (temporal.py).
 
-Not built (rejected with a clear message if requested): DIS optical flow (the reference's
-default --flow_method) (--flow_ema, --motion_blend), Magenta (TF-Hub) and Torch7 (OpenCV
-DNN) backends.
+Not built (rejected with a clear message if requested): Magenta (TF-Hub) and Torch7
+(OpenCV DNN) backends.
 """
 from __future__ import annotations
 
@@ -150,8 +151,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="--gpus > 1 process group: nccl (RCCL over xGMI, one GPU per rank) or gloo (host-staged "
                          "exchange; ranks may share a GPU, used by the tests)")
     ap.add_argument("--dist_timeout", type=float, default=600.0, help="seconds before a blocked exchange aborts")
-    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
-                    help="fp32 = parity with the reference arithmetic; bf16 = throughput mode")
+    ap.add_argument("--dtype", choices=["fp32", "bf16", "fp16"], default="fp32",
+                    help="fp32 = parity with the reference arithmetic; bf16 = throughput mode; fp16 = the "
+                         "throughput mode's speed within +-1 LSB of the reference (activations < 65504)")
     ap.add_argument("--synthetic", type=str, default=None, help="WxH: stylize an in-memory synthetic frame stream")
     ap.add_argument("--synthetic_frames", type=int, default=16)
     ap.add_argument("--no_save", action="store_true", help="do not encode/write outputs (throughput runs)")
@@ -167,8 +169,6 @@ def reject_out_of_scope(args) -> None:
                                              or str(getattr(args, f"model_{s}")).lower() in ("magenta",)
                                              or str(getattr(args, f"model_{s}")).endswith(".t7")):
             bad.append(f"--model_{s} (magenta/torch7)")
-    if args.flow_ema and args.flow_method != "farneback":
-        bad.append("--flow_ema with --flow_method dis (cv2.DISOpticalFlow is not built; --flow_method farneback is)")
     if args.device != "cuda":
         bad.append(f"--device {args.device} (this engine runs on MI355X only; there is no CPU path)")
     if bad:
@@ -549,7 +549,7 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     flow = None
     if flow_mode:
         from .temporal import FlowSmoother
-        flow = FlowSmoother(True, float(args.flow_alpha), max(1, int(args.flow_downscale or 1)))
+        flow = FlowSmoother(True, float(args.flow_alpha), max(1, int(args.flow_downscale or 1)), args.flow_method)
     mask_cache = {}
     pending = []
     t_start = time.perf_counter()
@@ -565,10 +565,8 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             orig = full[:, nb:].contiguous().reshape(len(g), h0, w0, 3)
             if lab.hw is not None and lab.hw != (h0, w0):
                 flow.reset()
-            fused, flows = [], []
-            for j in range(len(g)):
-                fused.append(flow(out01[j], orig[j]))
-                flows.append(flow.last_flow)  # None for the first frame of a run (no previous frame)
+            # None for the first frame of a run (no previous frame); the batch's flows come in one call
+            fused, flows = flow.batch(out01, orig)
             if getattr(args, "motion_blend", False):  # pipeline.py:2072-2080 alpha from this frame's flow
                 motion = [None if fl is None else motion_alpha(fl, blend) for fl in flows]
             styled = planar_to_u8(torch.stack(fused))

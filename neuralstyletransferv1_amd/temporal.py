@@ -3,15 +3,18 @@
 
 Per frame, in frame order (the EMA state is the previous fused frame):
   gray = pil_rgb.convert("L")                                   nst_gray_u8 (Pillow's integer luma)
-  flow = cv2.calcOpticalFlowFarneback(prev_gray, gray, None, 0.5, 3, 15, 3, 5, 1.1, 0)   nst_flow_farneback
+  flow = cv2.DISOpticalFlow_create(PRESET_FAST).calc(prev_gray, gray, None)      nst_flow_dis (default, :1904-1914)
+       | cv2.calcOpticalFlowFarneback(prev_gray, gray, None, 0.5, 3, 15, 3, 5, 1.1, 0)   nst_flow_farneback
   out01 = clip(a * out01 + (1 - a) * warp(prev_styled01, flow))                         nst_flow_fuse
   prev_gray, prev_styled01 = gray, out01
-and, when --motion_blend is on, the blend alpha from |flow| (nst_motion_alpha).
+and, when --motion_blend is on, the blend alpha from |flow| (nst_motion_alpha).  The flows depend only on the
+original frames, so a batch's flows are computed together (DIS: one call for all its frame pairs) before the
+sequential fuse.
 
---flow_downscale ds computes the flow on INTER_AREA-reduced grays (an exact integer factor of the frame) and
-brings it back with INTER_LINEAR x ds.  The reference's default --flow_method is DIS (cv2.DISOpticalFlow,
-PRESET_FAST); only Farneback is built here, so a DIS request fails loudly (pipeline.reject_out_of_scope).  cv2 is not installed in this environment: the
-Farneback, remap and GaussianBlur restatements are parity unpinned.
+--flow_downscale ds computes the flow on INTER_AREA-reduced grays of (W // ds, H // ds) (any factor: cv2's
+fractional area cells when ds does not divide the frame) and brings it back with INTER_LINEAR x ds.  cv2 is not
+installed in this environment: the DIS, Farneback, INTER_AREA, remap and GaussianBlur restatements are parity
+unpinned.
 """
 from __future__ import annotations
 
@@ -65,6 +68,33 @@ def farneback(prev_gray: torch.Tensor, gray: torch.Tensor, scratch: Optional[Flo
     return flow
 
 
+class DisScratch:
+    def __init__(self):
+        self.buf = None
+
+    def get(self, n, h, w, device):
+        sz = ctypes.c_size_t()
+        check(lib().nst_flow_dis_scratch_bytes(n, h, w, ctypes.byref(sz)), "nst_flow_dis_scratch_bytes")
+        if self.buf is None or self.buf.numel() < sz.value or self.buf.device != device:
+            self.buf = torch.empty((max(sz.value, 256),), dtype=torch.uint8, device=device)
+        return self.buf
+
+
+def dis(prev_gray: torch.Tensor, gray: torch.Tensor, scratch: Optional[DisScratch] = None) -> torch.Tensor:
+    """cv2.DISOpticalFlow_create(PRESET_FAST).calc of frame pairs: [n,h,w] (or [h,w]) uint8 x 2 -> flow
+    [n,h,w,2] (or [h,w,2]) float32 (dx, dy)."""
+    single = gray.dim() == 2
+    p = prev_gray[None] if single else prev_gray
+    g = gray[None] if single else gray
+    n, h, w = g.shape
+    dev = g.device
+    sc = (scratch or DisScratch()).get(n, h, w, dev)
+    flow = torch.empty((n, h, w, 2), dtype=torch.float32, device=dev)
+    check(lib().nst_flow_dis(p.contiguous().data_ptr(), g.contiguous().data_ptr(), n, h, w, flow.data_ptr(),
+                             sc.data_ptr(), sc.numel(), _lib.stream_ptr(dev)), "nst_flow_dis")
+    return flow[0] if single else flow
+
+
 def fuse(curr01: torch.Tensor, prev01: torch.Tensor, flow: torch.Tensor, alpha: float) -> torch.Tensor:
     """[3,h,w] float32 planes -> clip(a*curr + (1-a)*warp(prev, flow))."""
     _, h, w = curr01.shape
@@ -88,7 +118,8 @@ def motion_alpha(flow: torch.Tensor, blend: float) -> torch.Tensor:
 
 
 def downscale_gray(gray: torch.Tensor, ds: int) -> torch.Tensor:
-    """cv2.resize(gray, (W // ds, H // ds), interpolation=cv2.INTER_AREA) at an exact integer factor."""
+    """cv2.resize(gray, (W // ds, H // ds), interpolation=cv2.INTER_AREA) (pipeline.py:1886-1889: floored sizes,
+    any factor)."""
     h, w = gray.shape
     out = torch.empty((h // ds, w // ds), dtype=torch.uint8, device=gray.device)
     check(lib().nst_flow_downscale_gray(gray.contiguous().data_ptr(), h, w, int(ds), out.data_ptr(),
@@ -117,12 +148,60 @@ def planar_to_u8(out01: torch.Tensor) -> torch.Tensor:
 class FlowSmoother:
     """The reference's temporal caches (prev_gray, prev_styled01, last_flow; reset on a frame-size change)."""
 
-    def __init__(self, flow_ema: bool, flow_alpha: float, downscale: int = 1):
+    def __init__(self, flow_ema: bool, flow_alpha: float, downscale: int = 1, method: str = "dis"):
+        if method not in ("dis", "farneback"):
+            raise _lib.NstError(f"flow method must be dis or farneback, got {method!r}")
         self.enabled = flow_ema
         self.alpha = flow_alpha
         self.ds = max(1, int(downscale))
+        self.method = method
         self.scratch = FlowScratch()
+        self.dis_scratch = DisScratch()
         self.reset()
+
+    def flows(self, prev_gray: torch.Tensor, grays: torch.Tensor) -> torch.Tensor:
+        """Flows of the pairs (prev, grays[0]), (grays[0], grays[1]), ... -> [n,h,w,2] (pipeline.py:1886-1923:
+        optional INTER_AREA reduction by ds, the flow, INTER_LINEAR back x ds)."""
+        prevs = torch.cat([prev_gray[None], grays[:-1]], dim=0)
+        n, h, w = grays.shape
+        if self.ds > 1:
+            prevs = torch.stack([downscale_gray(g, self.ds) for g in prevs])
+            cur = torch.stack([downscale_gray(g, self.ds) for g in grays])
+        else:
+            cur = grays
+        if self.method == "dis":
+            small = dis(prevs, cur, self.dis_scratch)
+        else:
+            small = torch.stack([farneback(prevs[k], cur[k], self.scratch) for k in range(n)])
+        if self.ds > 1:
+            return torch.stack([upscale_flow(small[k], h, w, self.ds) for k in range(n)])
+        return small
+
+    def batch(self, out01: torch.Tensor, orig_u8: torch.Tensor):
+        """A batch of frames in order: out01 [n,3,h,w], orig_u8 [n,h,w,3] -> (fused out01 list, flow list; None
+        where a frame has no predecessor of its size)."""
+        n, _, h, w = out01.shape
+        grays = gray_u8(orig_u8)
+        fl = None
+        if self.enabled and self.prev_gray is not None and self.prev_gray.shape == grays.shape[1:]:
+            fl = self.flows(self.prev_gray, grays)
+        elif self.enabled and n > 1:
+            fl = self.flows(grays[0], grays[1:])
+            fl = [None] + list(fl)
+        fused, flows = [], []
+        for k in range(n):
+            f = None if fl is None else fl[k]
+            o = out01[k]
+            if f is not None and self.prev_styled is not None and self.prev_styled.shape == o.shape:
+                o = fuse(o, self.prev_styled, f, self.alpha)
+            else:
+                f = None
+            fused.append(o)
+            flows.append(f)
+            self.prev_styled = o
+        self.prev_gray = grays[-1]
+        self.last_flow = flows[-1]
+        return fused, flows
 
     def reset(self):
         self.prev_gray = None
@@ -135,12 +214,7 @@ class FlowSmoother:
         self.last_flow = None
         if self.enabled and self.prev_gray is not None and self.prev_styled is not None:
             if self.prev_gray.shape == gray.shape:
-                if self.ds > 1:  # pipeline.py:1886-1892, 1920-1923
-                    h, w = gray.shape
-                    small = farneback(downscale_gray(self.prev_gray, self.ds), downscale_gray(gray, self.ds), self.scratch)
-                    flow = upscale_flow(small, h, w, self.ds)
-                else:
-                    flow = farneback(self.prev_gray, gray, self.scratch)
+                flow = self.flows(self.prev_gray, gray[None])[0]
                 out01 = fuse(out01, self.prev_styled, flow, self.alpha)
                 self.last_flow = flow
         self.prev_gray = gray

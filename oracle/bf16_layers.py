@@ -1,7 +1,8 @@
 """ORACLE — TEST INFRASTRUCTURE ONLY (imported by tests/ alone; never by the product path).
 
-Per-layer restatement of the reference's stylization nets with the bf16 throughput mode's rounding
-points written out, for teacher-forced parity of every conv kernel: each layer is recomputed on
+Per-layer restatement of the reference's stylization nets with the 16-bit modes' rounding points
+written out (fmt "bf16": the throughput mode, NST_DT_BF16; fmt "fp16": NST_DT_F16 — the same rounding
+points with IEEE binary16 round-to-nearest-even instead of bf16), for teacher-forced parity of every conv kernel: each layer is recomputed on
 the CPU from the engine's OWN stored input activation (captured through nst_forward_capture), so
 a layer's error is measured alone instead of accumulated over the 16 layers before it.
 
@@ -95,8 +96,17 @@ def bf16(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.bfloat16).to(torch.float32)
 
 
+TORCH16 = {"bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+def rnd16(t: torch.Tensor, fmt: str = "bf16") -> torch.Tensor:
+    """Round fp32 values to the 16-bit format fmt (round to nearest even) and back."""
+    return t.to(TORCH16[fmt]).to(torch.float32)
+
+
 def bf16_ulp_diff(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """|a - b| in bf16 ulps (both bf16 tensors; +0 == -0)."""
+    """|a - b| in ulps of their 16-bit format (both bf16 or both fp16 tensors; sign-magnitude
+    patterns mapped to ordered integers; +0 == -0)."""
     def ordered(t):
         i = t.contiguous().view(torch.int16).to(torch.int32)
         return torch.where(i < 0, -(i & 0x7FFF), i)
@@ -105,13 +115,14 @@ def bf16_ulp_diff(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------------- the consumer's fill
 def fill_operand(y: torch.Tensor, ys: Optional[torch.Tensor], in_relu: bool, r: Optional[torch.Tensor] = None,
-                 rs: Optional[torch.Tensor] = None, relu_out: bool = False, round_bf16: bool = True) -> torch.Tensor:
+                 rs: Optional[torch.Tensor] = None, relu_out: bool = False, round_bf16: bool = True,
+                 fmt: str = "bf16") -> torch.Tensor:
     """The conv input the engine stages: y [n,c,h,w] (stored values), ys [n,c,2] {scale, shift}.
     No residual: fma(y, scale, shift) rounded once to fp32 (then bf16), ReLU.  Residual join
     (ResidualBlock): r' + (y*scale + shift) in unfused fp32, r' = relu(r*scale_r + shift_r) if rs
     (bf16: r' = the normalised fill of r, rounded to bf16 — block 1's input x_0 as the trunk stores
     it, conv_wstat.hip XO)."""
-    rnd = bf16 if round_bf16 else (lambda t: t)
+    rnd = (lambda t: rnd16(t, fmt)) if round_bf16 else (lambda t: t)
     if r is None:
         if ys is None:
             return y
@@ -124,7 +135,7 @@ def fill_operand(y: torch.Tensor, ys: Optional[torch.Tensor], in_relu: bool, r: 
     rr = r
     if rs is not None:
         if round_bf16:  # r' exactly as a normalising fill stages it (the stored x_0 of the fused trunk)
-            rr = fill_operand(r, rs, True, round_bf16=True)
+            rr = fill_operand(r, rs, True, round_bf16=True, fmt=fmt)
         else:
             rr = (r * rs[..., 0][:, :, None, None] + rs[..., 1][:, :, None, None]).clamp_min(0.0)
     v = rr + (y * sc + sh)
@@ -133,10 +144,10 @@ def fill_operand(y: torch.Tensor, ys: Optional[torch.Tensor], in_relu: bool, r: 
     return rnd(v)
 
 
-def encode_operand(frames_u8: np.ndarray, preset: str, round_bf16: bool = True) -> torch.Tensor:
-    """First-layer operand: encode(ToTensor(frame)) in the preset's fp32 arithmetic (+ bf16)."""
+def encode_operand(frames_u8: np.ndarray, preset: str, round_bf16: bool = True, fmt: str = "bf16") -> torch.Tensor:
+    """First-layer operand: encode(ToTensor(frame)) in the preset's fp32 arithmetic (+ 16-bit rounding)."""
     v = O.encode(O.to_tensor01(frames_u8), preset).float()
-    return bf16(v) if round_bf16 else v
+    return rnd16(v, fmt) if round_bf16 else v
 
 
 # ------------------------------------------------------------------------- conv emulation
@@ -150,7 +161,7 @@ def _pad(x: torch.Tensor, axis: int, pad: int, pre: int) -> torch.Tensor:
     raise ValueError(axis)
 
 
-def phase_weights(W: torch.Tensor, convT: bool, round_bf16: bool) -> torch.Tensor:
+def phase_weights(W: torch.Tensor, convT: bool, round_bf16: bool, fmt: str = "bf16") -> torch.Tensor:
     """[2,2,cout,cin,2,2] sub-pixel phase weights of a x2 up-conv (fp64 sums of the taps landing on
     one source pixel, then fp32 (and bf16)): output (2y+a, 2x+b) = sum_t Wp[a,b,:,:,ty,tx] *
     S[y + off_a + ty, x + off_b + tx], off = a - 1 for nearest x2 (clamped source), 0 for
@@ -181,7 +192,7 @@ def phase_weights(W: torch.Tensor, convT: bool, round_bf16: bool) -> torch.Tenso
                             else:
                                 out[a, b, :, :, ty, tx] += Wd[:, :, ky, kx]
     out = out.float()
-    return bf16(out) if round_bf16 else out
+    return rnd16(out, fmt) if round_bf16 else out
 
 
 def _reflect_idx(v: np.ndarray, L: int) -> np.ndarray:
@@ -222,14 +233,15 @@ def _pad_cols(x: torch.Tensor, axis: int, pad: int, pre: int) -> torch.Tensor:
 
 
 def conv_layer(get_rows, H: int, n: int, c: int, W: torch.Tensor, b: torch.Tensor, ks: int, stride: int, axis: int,
-               pad: int, pre: int, round_bf16: bool, rows: Tuple[int, int], acc: torch.dtype = torch.float32) -> torch.Tensor:
+               pad: int, pre: int, round_bf16: bool, rows: Tuple[int, int], acc: torch.dtype = torch.float32,
+               fmt: str = "bf16") -> torch.Tensor:
     """Output rows rows[0]..rows[1]-1 of one conv of the net -> fp32 acc + bias [n,cout,k,ow] (before
     rounding).  get_rows(src_row_indices) returns the staged operand rows [n,c,k,w] (fill applied);
     H = source height.  Up-convs need even row bounds."""
     r0, r1 = rows
     if axis in (REFLECT_UP2, ZINSERT):
         convT = axis == ZINSERT
-        Wp = phase_weights(W, convT, round_bf16).to(acc)
+        Wp = phase_weights(W, convT, round_bf16, fmt).to(acc)
         y0, y1 = r0 // 2, r1 // 2
         u = np.arange(y0 - 1, y1 + 1)  # source rows y0-1 .. y1 (one row of halo each side)
         idx = np.where((u < 0) | (u >= H), -1, u) if convT else np.clip(u, 0, H - 1)
@@ -244,7 +256,7 @@ def conv_layer(get_rows, H: int, n: int, c: int, W: torch.Tensor, b: torch.Tenso
                 src = S[:, :, oa + 1:oa + 1 + (y1 - y0) + 1, ob + 1:ob + 1 + w + 1]
                 out[:, :, a::2, bb::2] = F.conv2d(src, Wp[a, bb])
         return out.float() + b.float()[None, :, None, None]
-    Wr = (bf16(W) if round_bf16 else W).to(acc)
+    Wr = (rnd16(W, fmt) if round_bf16 else W).to(acc)
     u = np.arange(r0 * stride, (r1 - 1) * stride + ks)
     P = _gather(get_rows, source_rows(axis, u, H, pad, pre), n, c)
     P = _pad_cols(P, axis, pad, pre).to(acc)
@@ -253,7 +265,7 @@ def conv_layer(get_rows, H: int, n: int, c: int, W: torch.Tensor, b: torch.Tenso
 
 
 def forward_layers(arch: str, sd: Dict[str, torch.Tensor], x: torch.Tensor, round_bf16: bool = False,
-                   acc: torch.dtype = torch.float32) -> torch.Tensor:
+                   acc: torch.dtype = torch.float32, fmt: str = "bf16") -> torch.Tensor:
     """The whole net through this module's per-layer functions (x = encoded input [n,3,h,w]):
     with round_bf16=False it restates the reference forward (checked against nst_oracle.forward);
     with True it is the bf16 mode's rounding model end to end (stats from the fp32 values)."""
@@ -265,9 +277,9 @@ def forward_layers(arch: str, sd: Dict[str, torch.Tensor], x: torch.Tensor, roun
         H = operand.shape[2]
         oh = {REFLECT_UP2: 2 * H, ZINSERT: 2 * H}.get(axis, (H + 2 * pre + 2 * pad - ks) // st + 1)
         return conv_layer(lambda idx: operand.index_select(2, idx), H, n, operand.shape[1], sd[conv + ".weight"],
-                          sd[conv + ".bias"], ks, st, axis, pad, pre, round_bf16, (0, oh), acc)
+                          sd[conv + ".bias"], ks, st, axis, pad, pre, round_bf16, (0, oh), acc, fmt)
 
-    rnd = bf16 if round_bf16 else (lambda t: t)
+    rnd = (lambda t: rnd16(t, fmt)) if round_bf16 else (lambda t: t)
 
     def stats(i, z):
         return in_stats(z, sd[Ls[i][1] + ".weight"], sd[Ls[i][1] + ".bias"])
@@ -276,25 +288,25 @@ def forward_layers(arch: str, sd: Dict[str, torch.Tensor], x: torch.Tensor, roun
     z = run(0, op)
     y, s = rnd(z), stats(0, z)
     for i in (1, 2):
-        z = run(i, fill_operand(y, s, True, round_bf16=round_bf16))
+        z = run(i, fill_operand(y, s, True, round_bf16=round_bf16, fmt=fmt))
         y, s = rnd(z), stats(i, z)
     nres = 4 if arch == "reconet" else 5
     relu_out = arch == "reconet"
     xs, xst = y, s  # the residual stream: block 1's input is relu(IN(conv3)), applied lazily
-    xv = fill_operand(xs, xst, True, round_bf16=round_bf16)
+    xv = fill_operand(xs, xst, True, round_bf16=round_bf16, fmt=fmt)
     for r in range(nres):
         l1, l2 = 3 + 2 * r, 4 + 2 * r
         z1 = run(l1, xv)
         y1, s1 = rnd(z1), stats(l1, z1)
-        z2 = run(l2, fill_operand(y1, s1, True, round_bf16=round_bf16))
+        z2 = run(l2, fill_operand(y1, s1, True, round_bf16=round_bf16, fmt=fmt))
         y2, s2 = rnd(z2), stats(l2, z2)
-        xv = fill_operand(y2, s2, False, r=xv, relu_out=relu_out, round_bf16=round_bf16)
+        xv = fill_operand(y2, s2, False, r=xv, relu_out=relu_out, round_bf16=round_bf16, fmt=fmt)
     u1 = 3 + 2 * nres
     z = run(u1, xv)
     y, s = rnd(z), stats(u1, z)
-    z = run(u1 + 1, fill_operand(y, s, True, round_bf16=round_bf16))
+    z = run(u1 + 1, fill_operand(y, s, True, round_bf16=round_bf16, fmt=fmt))
     y, s = rnd(z), stats(u1 + 1, z)
-    out = run(u1 + 2, fill_operand(y, s, True, round_bf16=round_bf16))
+    out = run(u1 + 2, fill_operand(y, s, True, round_bf16=round_bf16, fmt=fmt))
     if arch == "reconet":
         out = torch.tanh(out)
     if arch == "nst":

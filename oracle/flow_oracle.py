@@ -255,8 +255,8 @@ def fuse(curr01: np.ndarray, prev01: np.ndarray, flow: np.ndarray, a: float) -> 
     """[3,h,w] planes; remap BORDER_REPLICATE in OpenCV's 1/32-pixel fixed point."""
     _, h, w = curr01.shape
     ys, xs = np.mgrid[0:h, 0:w]
-    mx = xs.astype(f32) + flow[..., 0]
-    my = ys.astype(f32) + flow[..., 1]
+    mx = np.clip(np.nan_to_num(xs.astype(f32) + flow[..., 0], nan=-2.0 * w), -2.0 * w, 3.0 * w).astype(f32)
+    my = np.clip(np.nan_to_num(ys.astype(f32) + flow[..., 1], nan=-2.0 * h), -2.0 * h, 3.0 * h).astype(f32)
     X = np.rint(mx * f32(32)).astype(np.int64)
     Y = np.rint(my * f32(32)).astype(np.int64)
     sx, sy = X >> 5, Y >> 5
@@ -281,14 +281,65 @@ def motion_alpha(flow: np.ndarray, blend: float) -> np.ndarray:
     return (f32(blend) - f32(blend - 0.4) * m).astype(f32)
 
 
+def _area_cells(ssize: int, dsize: int, scale: float):
+    """computeResizeAreaTab (OpenCV resize.cpp) for one axis: per destination index the (source, weight) cells,
+    weights the fp32 of the double ratios; partial first / last cells only beyond 1e-3."""
+    cells = []
+    for d in range(dsize):
+        fs1 = d * scale
+        fs2 = fs1 + scale
+        cell = min(scale, ssize - fs1)
+        s1, s2 = math.ceil(fs1), math.floor(fs2)
+        s2 = min(s2, ssize - 1)
+        s1 = min(s1, s2)
+        row = []
+        if s1 - fs1 > 1e-3:
+            row.append((s1 - 1, f32((s1 - fs1) / cell)))
+        for sx in range(s1, s2):
+            row.append((sx, f32(1.0 / cell)))
+        if fs2 - s2 > 1e-3:
+            row.append((s2, f32(min(min(fs2 - s2, 1.0), cell) / cell)))
+        cells.append(row)
+    return cells
+
+
+def area_resize(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
+    """cv2.resize(img, (ow, oh), interpolation=INTER_AREA) of a u8 image [h,w] or [h,w,c], downscaling (OpenCV
+    resize.cpp restated: integer scales -> resizeAreaFast_ (int block sum * fp32 1/area, cvRound; scale 2 x 2
+    -> ResizeAreaFastVec's (sum + 2) >> 2, rounding halves up), else ResizeArea_Invoker over computeResizeAreaTab's cells: per
+    source row buf = sum(S * alpha) in cell order, sum = beta * buf, then += beta * buf; cvRound + saturate)."""
+    h, w = img.shape[:2]
+    sx, sy = 1.0 / (ow / w), 1.0 / (oh / h)
+    isx, isy = int(round(sx)), int(round(sy))
+    x = img.reshape(h, w, -1)
+    if abs(sx - isx) < np.finfo(np.float64).eps and abs(sy - isy) < np.finfo(np.float64).eps:
+        s = x[:oh * isy, :ow * isx].reshape(oh, isy, ow, isx, -1).astype(np.int64).sum(axis=(1, 3))
+        if isx == 2 and isy == 2:  # ResizeAreaFastVec (scale 2 x 2): (sum + 2) >> 2, SIMD and tail alike
+            return ((s + 2) >> 2).astype(np.uint8).reshape((oh, ow) + img.shape[2:])
+        out = np.clip(np.rint(s.astype(f32) * f32(1.0 / (isx * isy))), 0, 255)
+        return out.astype(np.uint8).reshape((oh, ow) + img.shape[2:])
+    xc, yc = _area_cells(w, ow, sx), _area_cells(h, oh, sy)
+    xf = x.astype(f32)
+    out = np.empty((oh, ow, x.shape[2]), np.float32)
+    for dy, rows in enumerate(yc):
+        acc = None
+        for (r, beta) in rows:
+            buf = np.zeros((ow, x.shape[2]), f32)
+            for dx, cols in enumerate(xc):
+                b = f32(0)
+                for (c, a) in cols:
+                    b = (b + xf[r, c] * a).astype(f32)
+                buf[dx] = b
+            t = (beta * buf).astype(f32)
+            acc = t if acc is None else (acc + t).astype(f32)
+        out[dy] = acc
+    return np.clip(np.rint(out), 0, 255).astype(np.uint8).reshape((oh, ow) + img.shape[2:])
+
+
 def area_down(gray_u8: np.ndarray, ds: int) -> np.ndarray:
-    """cv2.resize(gray, (W // ds, H // ds), INTER_AREA) at an exact integer factor (resizeAreaFast restated:
-    ds = 2 rounds (sum + 2) >> 2 as its SIMD path, other factors saturate_cast(sum / area))."""
+    """--flow_downscale (pipeline.py:1886-1889): cv2.resize(gray, (W // ds, H // ds), INTER_AREA)."""
     h, w = gray_u8.shape
-    s = gray_u8.reshape(h // ds, ds, w // ds, ds).astype(np.int64).sum(axis=(1, 3))
-    if ds == 2:
-        return ((s + 2) >> 2).astype(np.uint8)
-    return np.minimum(255, np.rint(s.astype(f32) * f32(1.0 / (ds * ds)))).astype(np.uint8)
+    return area_resize(gray_u8, h // ds, w // ds)
 
 
 def farneback_downscaled(prev: np.ndarray, nxt: np.ndarray, ds: int) -> np.ndarray:

@@ -1,8 +1,9 @@
-"""Teacher-forced per-layer parity of the bf16 engine (helper of tests/test_gpu_layers.py).
+"""Teacher-forced per-layer parity of the 16-bit engine modes, bf16 and fp16 (helper of
+tests/test_gpu_layers.py).
 
 Runs one batch through nst_forward_capture, then recomputes every op on the CPU from the engine's
 own stored inputs (oracle/bf16_layers.py) and compares:
-  * each conv's stored bf16 output element-wise, in bf16 ulps;
+  * each conv's stored 16-bit output element-wise, in ulps of its format;
   * each conv's InstanceNorm {scale, shift} (from the engine's fp32 values) against the statistics
     of the oracle's fp32 values;
   * each joined residual stream bit for bit;
@@ -21,6 +22,9 @@ from oracle import bf16_layers as B
 ULP_MAX = 1              # stored bf16 outputs: at most one bf16 ulp apart ...
 ATOL_REL = 4e-6          # ... or within this fraction of the layer's max |value| (sums that cancel to ~0)
 ULP1_FRAC_MAX = 1e-3     # at most 0.1 % of the elements one ulp apart (accumulation-order rounding flips)
+# fp16's ulp is 8x finer than bf16's, so the same fp32 accumulation-order differences flip its
+# rounding ~8x as often: at most 0.8 % of the elements one fp16 ulp apart
+ULP1_FRAC_MAX_F16 = 8e-3
 STATS_REL = 1e-5         # IN scale/shift vs the oracle's statistics of its fp32 values (measured <= 4e-7)
 RAW_REL = 5e-6           # output conv raw fp32, relative to max |y| (measured <= 1.1e-6)
 U8_EXACT_MIN = 0.9999    # decoded u8 frames: >= 99.99 % identical, the rest 1 LSB (truncation boundary)
@@ -86,6 +90,8 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
     """-> one record per op.  bands: None = every output row; else [(fraction, rows)] row bands
     (start = fraction of the output height, rounded down to even) checked per op (4K frames)."""
     arch = {0: "johnson", 1: "nst", 2: "reconet", 3: "reconet_frn"}[net.ARCH]
+    fmt = "fp16" if net.compute_dtype in ("fp16", "float16") else "bf16"
+    ulp1_max = ULP1_FRAC_MAX_F16 if fmt == "fp16" else ULP1_FRAC_MAX
     frn = arch == "reconet_frn"
     sd = {k: v.detach().float().cpu() for k, v in net.state_dict().items()}
     eng = net.engine()
@@ -119,7 +125,7 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
 
         if d["src"] == -1:
             if x_enc is None:
-                x_enc = B.encode_operand(frames_u8, preset)
+                x_enc = B.encode_operand(frames_u8, preset, fmt=fmt)
             src = x_enc
 
             def get_rows(idx, src=src):
@@ -135,7 +141,7 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
 
             def get_rows(idx, ysrc=ysrc, ys=ys, r=r, rs=rs, d=d):
                 return B.fill_operand(ysrc.index_select(2, idx), ys, bool(d["in_relu"]),
-                                      None if r is None else r.index_select(2, idx), rs, bool(d["relu_out"]))
+                                      None if r is None else r.index_select(2, idx), rs, bool(d["relu_out"]), fmt=fmt)
             Hs = ysrc.shape[2]
             if d["res_out"] >= 0:  # the joined stream the op wrote for its own pixels: bit-exact
                 joined = get_rows(torch.arange(Hs))
@@ -150,7 +156,7 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
         if frn:  # TLU outputs are stored shifted by -tau: the bias absorbs sum W tau
             bias = _frn_bias(sd, d["layer"], W, bias)
         for (r0, r1) in row_sets:
-            z = B.conv_layer(get_rows, Hs, n, cin, W, bias, ks, st, axis, pad, pre, True, (r0, r1), acc)
+            z = B.conv_layer(get_rows, Hs, n, cin, W, bias, ks, st, axis, pad, pre, True, (r0, r1), acc, fmt)
             if final:
                 if arch.startswith("reconet"):
                     z = torch.tanh(z)
@@ -173,10 +179,11 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
                 rec["elements"] += zc.numel()
                 continue
             got_full = host[i]["act"]
+            rec["absmax"] = max(rec.get("absmax", 0.0), float(got_full.float().abs().max()))
             got = got_full[:, r0:r1].permute(0, 3, 1, 2)[:, :cout].contiguous()
             pad_ch = got_full[:, r0:r1, :, cout:]
             assert (pad_ch.float() == 0).all(), f"op {i} ({conv}): padded channels not zero"
-            ref = z.to(torch.bfloat16)
+            ref = z.to(B.TORCH16[fmt])
             ulp = B.bf16_ulp_diff(got, ref)
             diff = (got.float() - ref.float()).abs()
             atol = ATOL_REL * float(ref.float().abs().max())
@@ -187,7 +194,7 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
             rec["bad"] = rec.get("bad", 0) + int(bad.sum())
             assert not bad.any(), (f"op {i} ({conv}) rows {r0}:{r1}: {int(bad.sum())} elements beyond "
                                    f"{ULP_MAX} ulp / atol {atol:.2e}; first at {tuple(bad.nonzero()[0].tolist())}")
-            assert rec["ulp1_frac"] <= ULP1_FRAC_MAX, (i, conv, rec["ulp1_frac"])
+            assert rec["ulp1_frac"] <= ulp1_max, (i, conv, rec["ulp1_frac"])
             if bands is None:  # statistics need the whole frame
                 s_ref = (_frn_stats(sd, d["layer"], norm, z) if frn else
                          B.in_stats(z, sd[norm + ".weight"], sd[norm + ".bias"]))

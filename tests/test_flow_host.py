@@ -40,3 +40,28 @@ def test_fuse_and_motion_alpha_properties():
     assert np.allclose(a, 0.9, atol=1e-6)
     big = np.full((20, 30, 2), 50.0, np.float32)
     assert np.allclose(FO.motion_alpha(big, 0.9), 0.4, atol=1e-5)
+
+
+def test_area_resize_properties():
+    """cv2.resize INTER_AREA restated: same size is the identity, 2x2 rounds halves up, fractional cells keep the mean."""
+    rng = np.random.default_rng(3)
+    g = rng.integers(0, 256, (60, 84), dtype=np.uint8)
+    assert np.array_equal(FO.area_resize(g, 60, 84), g)
+    s = g.reshape(30, 2, 42, 2).astype(int).sum(axis=(1, 3))
+    assert np.array_equal(FO.area_resize(g, 30, 42), ((s + 2) >> 2).astype(np.uint8))
+    const = np.full((61, 89), 77, np.uint8)
+    assert np.array_equal(FO.area_resize(const, 20, 29), np.full((20, 29), 77, np.uint8))
+    small = FO.area_resize(g, 60 // 7, 84 // 5)
+    assert abs(float(small.mean()) - float(g.mean())) < 2.0
+
+
+def test_dis_restatement_recovers_translation():
+    from oracle import dis_oracle as DO
+    h, w = 128, 160
+    base = _texture(h, w, seed=4)
+    prev = np.clip(base[20:20 + h, 20:20 + w], 0, 255).astype(np.uint8)
+    for dx, dy in ((3, -2), (-4, 1)):
+        nxt = np.clip(base[20 - dy:20 - dy + h, 20 - dx:20 - dx + w], 0, 255).astype(np.uint8)
+        fl = DO.dis_flow(prev, nxt)[16:-16, 16:-16]
+        assert abs(float(np.median(fl[..., 0])) - dx) < 0.2 and abs(float(np.median(fl[..., 1])) - dy) < 0.2
+    assert DO.coarsest_scale(1080, 1920) == 6 and DO.coarsest_scale(96, 128) == 2

@@ -2,7 +2,8 @@
 
 Tolerances (north_star): fp32 parity mode within 1e-4 of the reference (relative to the
 output's magnitude) and +-1 LSB on uint8 frames; bf16 throughput mode SSIM >= 0.98 vs the
-CPU reference.  Integer/byte stages (LAB LUT gathers, EMA truncation, blend truncation) are
+CPU reference; fp16 mode (the bf16 kernels with fp16 operands) +-1 LSB on >= 99.9 % of the uint8
+values, never more than 2 LSB.  Integer/byte stages (LAB LUT gathers, EMA truncation, blend truncation) are
 bit-exact.
 """
 import glob
@@ -21,6 +22,10 @@ pytestmark = pytest.mark.gpu
 MODEL_GOLDENS = sorted(glob.glob(os.path.join(GOLDEN, "model_*.npz")))
 FP32_REL_TOL = 1e-4
 BF16_SSIM_MIN = 0.98
+# fp16 mode vs the CPU reference's uint8 frames (bars from the oracle's fp16 rounding model,
+# oracle/bf16_layers.py fmt="fp16": at 1080p 99.981 % of values / 99.945 % of pixels within 1 LSB, max 2)
+F16_MAX_LSB = 2
+F16_WITHIN1_MIN = 0.999
 
 
 def _arch(path):  # model_<arch>_s<seed>_<h>x<w>.npz (arch may hold "_": reconet_frn)
@@ -62,6 +67,10 @@ def test_frames_u8_vs_oracle(path):
     out16 = _net(arch, seed, "bf16").stylize_frames(f_dev, preset).cpu().numpy()
     for i in range(frames.shape[0]):
         assert O.ssim(out16[i], ref[i]) >= BF16_SSIM_MIN
+    outh = _net(arch, seed, "fp16").stylize_frames(f_dev, preset).cpu().numpy()
+    dh = np.abs(outh.astype(int) - ref.astype(int))
+    print(f"{os.path.basename(path)} fp16: max {dh.max()} LSB, within 1 LSB {(dh <= 1).mean():.6f}")
+    assert dh.max() <= F16_MAX_LSB and (dh <= 1).mean() >= F16_WITHIN1_MIN
 
 
 @pytest.mark.parametrize("seed", [0, 1])
@@ -69,8 +78,12 @@ def test_reconet_frn_ragged_vs_oracle(seed):
     """ReCoNet(frn=True) (model.py with frn.py): FRN's mean-square statistics and |eps|, and the TLU
     thresholds the engine folds into shifted activations, join shifts and conv biases, at a ragged
     size (61 x 90 -> 64 x 92 output) against the oracle (bit-exact to the reference module's
-    goldens).  fp32: 1e-4 of the output magnitude; bf16 (a sanity bar; the frames tests hold the
-    SSIM >= 0.98 bar): mean |d| < 2.5e-2 on the [-1, 1] tanh output (measured 1.2e-2)."""
+    goldens).  fp32: 1e-4 of the output magnitude.  bf16: mean |d| < 2.5e-2 on the [-1, 1] tanh output
+    (measured 1.23e-2); every layer of this net is held separately to 1 bf16 ulp, FRN statistics to
+    1e-7 and the raw output conv to 1.1e-6 (tests/test_gpu_layers.py), so what this bar measures is 14
+    layers of bf16 storage rounding compounding through FRN's per-channel rescaling (which, unlike
+    InstanceNorm, does not subtract the mean: a rounding offset stays in the activation), not a kernel
+    error.  fp16 (3 more mantissa bits, the same kernels): the original 1e-2 bar, with margin."""
     sd = synthetic.make_state_dict("reconet_frn", seed)
     x = O.encode(O.to_tensor01(synthetic.make_frames(2, 61, 90, seed=40 + seed)), "imagenet_01")
     ref = O.forward("reconet_frn", sd, x).numpy()
@@ -79,6 +92,9 @@ def test_reconet_frn_ragged_vs_oracle(seed):
     assert np.abs(y - ref).max() <= FP32_REL_TOL * np.abs(ref).max()
     y16 = _net("reconet_frn", seed, "bf16")(x.cuda()).cpu().numpy()
     assert np.abs(y16 - ref).mean() < 2.5e-2
+    yh = _net("reconet_frn", seed, "fp16")(x.cuda()).cpu().numpy()
+    print(f"frn seed {seed}: mean |d| bf16 {np.abs(y16 - ref).mean():.3e}, fp16 {np.abs(yh - ref).mean():.3e}")
+    assert np.abs(yh - ref).mean() < 1e-2
     # the thresholds matter: the same net with tau = 0 is a different function
     sd0 = {k: (torch.zeros_like(v) if k.endswith(".tau") else v) for k, v in sd.items()}
     assert np.abs(O.forward("reconet_frn", sd0, x).numpy() - ref).max() > 1e-2
@@ -94,6 +110,20 @@ def test_1080p_fp32_and_bf16_vs_oracle():
     assert d.max() <= 1 and (d > 0).mean() < 0.01
     out16 = _net("johnson", 0, "bf16").stylize_frames(f_dev, "imagenet_255").cpu().numpy()
     assert O.ssim(out16[0], ref[0]) >= BF16_SSIM_MIN
+
+
+def test_1080p_fp16_vs_oracle():
+    """configs[1]'s frame, fp16 mode vs the CPU reference (pre-LAB uint8): within 1 LSB on >= 99.97 % of
+    values (oracle rounding model: 99.981 %), max 2 LSB; per pixel (any channel) reported."""
+    sd = synthetic.make_state_dict("johnson", 0)
+    frames = synthetic.make_frames(1, 1080, 1920, seed=1000)
+    ref = O.stylize_u8("johnson", sd, frames, "imagenet_255")
+    out = _net("johnson", 0, "fp16").stylize_frames(torch.from_numpy(frames).cuda(), "imagenet_255").cpu().numpy()
+    d = np.abs(out.astype(int) - ref.astype(int))
+    print(f"1080p fp16: max {d.max()} LSB, values within 1 LSB {(d <= 1).mean():.6f}, pixels "
+          f"{(d.max(-1) <= 1).mean():.6f}, exact {(d == 0).mean():.4f}, ssim {O.ssim(out[0], ref[0]):.6f}")
+    assert d.max() <= F16_MAX_LSB
+    assert (d <= 1).mean() >= 0.9997
 
 
 def test_batch_invariance_and_determinism_1080p_bf16():

@@ -43,11 +43,19 @@ def _oracle_chain(arch_sds, weights, frames, preset, smooth=True, alpha=0.7, ble
     return outs
 
 
-def _close(a, b, max_lsb=None, frac=0.005):
+# After the LAB round trip (Pillow/LittleCMS, pipeline.py:1942-1978) a 1-LSB RGB difference before it can
+# move an L / a / b byte across a quantisation step, which LAB -> RGB turns into a few LSB.  The engine's LAB
+# stage is bit-exact (tests/test_gpu_parity.py), and test_pre_lab_within_1lsb_and_lab_attribution shows
+# that every post-LAB difference is the round trip of a <= 1 LSB pre-LAB one; this bounds the result.
+LAB_MAX_LSB = 12
+
+
+def _close(a, b, max_lsb, frac=0.005):
+    """every value within max_lsb, and at most frac of them more than 2 LSB apart"""
     d = np.abs(a.astype(int) - b.astype(int))
+    print(f"max |d| {d.max()} LSB, > 1 LSB {(d > 1).mean():.4%}, > 2 LSB {(d > 2).mean():.4%}")
     assert (d > 2).mean() <= frac, f"{(d > 2).mean():.4%} of values differ by >2 LSB (max {d.max()})"
-    if max_lsb is not None:
-        assert d.max() <= max_lsb
+    assert d.max() <= max_lsb, f"max |d| {d.max()} > {max_lsb} LSB"
 
 
 def test_single_image_cli_fp32(tmp_path):
@@ -60,7 +68,38 @@ def test_single_image_cli_fp32(tmp_path):
     assert rc == 0
     got = np.array(Image.open(outp))
     ref = _oracle_chain([("johnson", sd)], [1.0], [fr], "raw_255")[0]
-    _close(got, ref)
+    _close(got, ref, LAB_MAX_LSB)
+
+
+@pytest.mark.parametrize("preset,seed", [("raw_255", 0), ("imagenet_255", 1)])
+def test_pre_lab_within_1lsb_and_lab_attribution(tmp_path, preset, seed):
+    """fp32 CLI: (1) with --no-smooth_lightness the output (the stylised frame before the LAB stage) is
+    within +-1 LSB of the oracle everywhere; (2) with LAB smoothing on, the output is exactly the
+    reference's LAB EMA (Pillow/LittleCMS, oracle) applied to that GPU pre-LAB frame — so any larger
+    difference from the oracle chain is the LAB round trip of a <= 1 LSB pre-LAB difference."""
+    ck, sd = _ckpt(tmp_path, "johnson", seed)
+    frames = synthetic.make_frames(2, 96, 128, seed=60 + seed)
+    d_in = tmp_path / "in"
+    d_in.mkdir()
+    for i, f in enumerate(frames):
+        Image.fromarray(f).save(d_in / f"frame_{i + 1:04d}.png")
+    outs = {}
+    for tag, extra in (("pre", ["--no-smooth_lightness"]), ("lab", ["--smooth_alpha", "0.65"])):
+        d_out = tmp_path / f"out_{tag}"
+        assert P.main(["--input_dir", str(d_in), "--output_dir", str(d_out), "--model", ck, "--io_preset", preset,
+                       "--batch", "2", "--work_dir", str(tmp_path / f"w_{tag}")] + extra) == 0
+        outs[tag] = [np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png")) for i in range(2)]
+    ref_pre = _oracle_chain([("johnson", sd)], [1.0], list(frames), preset, smooth=False)
+    ref_lab = _oracle_chain([("johnson", sd)], [1.0], list(frames), preset, alpha=0.65)
+    ema = O.LabEMA(True, 0.65)
+    for i in range(2):
+        d = np.abs(outs["pre"][i].astype(int) - ref_pre[i].astype(int))
+        assert d.max() <= 1, f"pre-LAB max |d| {d.max()}"
+        assert np.array_equal(outs["lab"][i], ema(outs["pre"][i])), "post-LAB output is not LAB(pre-LAB)"
+        dl = np.abs(outs["lab"][i].astype(int) - ref_lab[i].astype(int))
+        print(f"{preset} frame {i}: pre-LAB max {d.max()} ({(d > 0).mean():.4%} off), post-LAB max {dl.max()} "
+              f"({(dl > 1).mean():.4%} > 1 LSB)")
+        assert dl.max() <= LAB_MAX_LSB
 
 
 def test_batch_dir_mask_blend_multimodel_fp32(tmp_path):
@@ -81,7 +120,7 @@ def test_batch_dir_mask_blend_multimodel_fp32(tmp_path):
                         alpha=0.65, blend=0.9, masks=[alpha] * 3)
     for i in range(3):
         got = np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png"))
-        _close(got, ref[i])
+        _close(got, ref[i], LAB_MAX_LSB)
 
 
 def test_synthetic_stream_bf16_nst_and_reconet(tmp_path):
@@ -153,7 +192,7 @@ def test_cli_lab_blend_and_feathered_mask(tmp_path):
         lab = O.lab_blend_u8(per, [0.5, 0.5], 0.4, 0.6)
         ref = O.blend_u8(lab, fr, alpha[..., None], "keep", 1.0)
         got = np.array(Image.open(outs[i]))
-        _close(got, ref, frac=0.01)
+        _close(got, ref, LAB_MAX_LSB, frac=0.01)
 
 
 def _lsb_report(got, ref):
@@ -189,7 +228,7 @@ def test_1080p_mask_blend_cli_vs_oracle(tmp_path):
             d, within2, dmax = _lsb_report(got, ref[i])
             print(dtype, i, "within 2 LSB", within2, "max", dmax, "ssim", O.ssim(got, ref[i]))
             if dtype == "fp32":
-                assert within2 >= 0.9999, (within2, dmax)
+                assert within2 >= 0.9999 and dmax <= LAB_MAX_LSB, (within2, dmax)
             else:
                 assert O.ssim(got, ref[i]) >= 0.98
 

@@ -27,8 +27,7 @@ def test_cli_defaults_match_reference():
         True, 0.7, 1.0, "auto", "png", 85, 4, "keep", "input", "transformer", 0.85)
 
 
-@pytest.mark.parametrize("extra", [["--flow_ema"], ["--model_type", "magenta"],
-                                   ["--device", "cpu"], ["--flow_ema", "--flow_method", "dis"]])
+@pytest.mark.parametrize("extra", [["--model_type", "magenta"], ["--model_type", "torch7"], ["--device", "cpu"]])
 def test_out_of_scope_requests_fail_loudly(extra, tmp_path):
     args = P.build_parser().parse_args(["--model", "x.pth", "--synthetic", "64x48"] + extra)
     with pytest.raises(SystemExit) as e:
