@@ -113,16 +113,22 @@ def cpu_baseline(frames_u8: np.ndarray, sd, nframes: int):
             t2 = time.perf_counter()
             t_fwd += t1 - t0
             t_post += t2 - t1
-            if threads == allc:
+            if threads == share:
                 outs.append(u8)
         runs[threads] = {"fwd_s_per_frame": t_fwd / nframes, "chain_s_per_frame": (t_fwd + t_post) / nframes}
     torch.set_num_threads(prev_threads)
-    main = runs[allc]
+    # value = the fastest configuration (the strongest baseline): on a shared GPU host all physical cores can be
+    # slower than the job's share (measured r03: 4.98 s/frame at 128 threads vs 2.45 s at 16)
+    best = min(runs, key=lambda t: runs[t]["fwd_s_per_frame"])
+    main = runs[best]
     return {
-        "value": 1.0 / main["fwd_s_per_frame"], "unit": "frames/s", "cores": allc, "kind": "port",
+        "value": 1.0 / main["fwd_s_per_frame"], "unit": "frames/s", "cores": best, "kind": "port",
         "sample": f"{nframes} timed synthetic 1920x1080 frames after 1 warm-up per configuration; value = forward "
-                  f"alone (preset {PRESET} -> Johnson fwd fp32 -> decode/clamp/ToPILImage) at {allc} threads "
-                  f"(all physical cores available to the process)",
+                  f"alone (preset {PRESET} -> Johnson fwd fp32 -> decode/clamp/ToPILImage) at {best} threads, the "
+                  f"fastest of {sorted(runs)} ({allc} = all physical cores available to the process)",
+        "all_cores_threads": allc,
+        "all_cores_frames_per_s": 1.0 / runs[allc]["fwd_s_per_frame"],
+        "all_cores_full_chain_frames_per_s": 1.0 / runs[allc]["chain_s_per_frame"],
         "full_chain_frames_per_s": 1.0 / main["chain_s_per_frame"],
         "share_threads": share,
         "share_frames_per_s": 1.0 / runs[share]["fwd_s_per_frame"],
@@ -166,7 +172,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from neuralstyletransferv1_amd import synthetic
-    from neuralstyletransferv1_amd.frames import gather_ordered
+    from neuralstyletransferv1_amd.frames import gather_finish, gather_start, owners, rank0_share
     from neuralstyletransferv1_amd.postproc import LabSmoother
     from neuralstyletransferv1_amd.transformer_net import TransformerNet
 
@@ -177,18 +183,31 @@ def main():
     net.compute_dtype = "bf16"
     eng = net.engine(dev)
 
-    # round-robin shard: rank r owns frames r, r+N, ... (distinct seeded content per rank)
-    frames_np = synthetic.make_frames(BATCH, H, W, seed=1000 + rank)
+    # round-robin shard: rank r owns frames r, r+N, ... (distinct seeded content per rank).  With --gather rank 0,
+    # which also runs the ordered post chain, stylizes a lighter share (frames.rank0_share)
+    caps = [rank0_share(world, BATCH) if args.gather else BATCH] + [BATCH] * (world - 1)
+    nloc = caps[rank]
+    frames_np = synthetic.make_frames(nloc, H, W, seed=1000 + rank)
     frames = torch.from_numpy(frames_np).to(dev)
-    group = list(range(BATCH * world))
+    group = list(range(sum(caps)))
+    assert sum(1 for o in owners(len(group), world, caps) if o == rank) == nloc
     ema = LabSmoother(dev, True, 0.65) if args.gather else None
+    inflight = [None]
+
+    def drain():  # complete the previous step's exchange; rank 0 runs its LAB EMA in frame order
+        ex, inflight[0] = inflight[0], None
+        if ex is not None:
+            full = gather_finish(ex)
+            if full is not None:
+                return ema(full)
+        return None
 
     def step():
         out = eng.stylize_u8(frames, PRESET)
-        if args.gather:
-            full = gather_ordered(out, group, world, rank)
-            if full is not None:
-                out = ema(full)
+        if args.gather:  # the exchange of step k overlaps the forward of step k+1 (frames.run_sharded's schedule)
+            prev = drain()
+            inflight[0] = gather_start(out, group, world, rank, caps)
+            return prev
         return out
 
     def timed(k):
@@ -199,6 +218,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(k):
             out = step()
+        if args.gather:
+            out = drain()  # the last step's exchange and EMA belong to the timed work
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -211,8 +232,10 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if args.gather:
+        drain()
     elapsed, out = timed(args.steps)           # the headline: no instrumentation
-    total_frames = BATCH * args.steps * world
+    total_frames = sum(caps) * args.steps
     fps = total_frames / elapsed
 
     def time_steps(fn, k):
@@ -231,12 +254,12 @@ def main():
 
     def chain_step():
         return blend_frames(chain_ema(eng.stylize_u8(frames, PRESET)), frames, 0.9)
-    chain_s = time_steps(chain_step, max(3, min(args.steps, 10)))
+    chain_s = time_steps(chain_step, max(3, min(args.steps, 10))) if world == 1 else None
 
     # fp16 mode (NST_DT_F16): the same kernels with fp16 operands, the mode that holds +-1 LSB
     eng16 = None
     fp16_s = None
-    if not args.no_fp16:
+    if not args.no_fp16 and world == 1:
         net.compute_dtype = "fp16"
         eng16 = net.engine(dev)
         net.compute_dtype = "bf16"
@@ -259,8 +282,8 @@ def main():
         parts = n.split(".")
         return parts[0] == "res1" or parts[1] == "conv2"
     hq, wq = (H + 3) // 4, (W + 3) // 4
-    res_flop = 2 * 128 * 128 * 9 * hq * wq * BATCH
-    res_bytes = hq * wq * 128 * 2 * 2 * BATCH  # bf16 activation in + out
+    res_flop = 2 * 128 * 128 * 9 * hq * wq * nloc
+    res_bytes = hq * wq * 128 * 2 * 2 * nloc  # bf16 activation in + out
     plain = [(n, ms, c) for (n, ms, c) in prof if n.startswith("res") and _plain(n)]
     joined = [(n, ms, c) for (n, ms, c) in prof if n.startswith("res") and not _plain(n)]
     res_launches = sum(c for _, _, c in plain)
@@ -306,7 +329,7 @@ def main():
                          f"fp32 accumulate, io_preset {PRESET}, uint8 frames in/out resident in HBM"
                          + ("; + ordered gather to rank 0 and rank-0 LAB EMA (configs[3] exchange)" if args.gather
                             else "")),
-            "global_batch": BATCH * world,
+            "global_batch": sum(caps),
             "frame_hw": [H, W],
             "parallelism": f"frames round-robin over {world} GPU(s), " +
                            ("point-to-point gather to rank 0" if args.gather else "no data-path collective"),
@@ -349,16 +372,17 @@ def main():
             "megapixels_per_frame": mp,
         },
         "cpu_baseline": None,
-        "gpu_full_chain": {
-            "frames_per_s": round(BATCH * world / chain_s, 2),
+    }
+    if chain_s is not None:
+        result["gpu_full_chain"] = {
+            "frames_per_s": round(nloc / chain_s, 2),
             "ms_per_step": round(chain_s * 1e3, 4),
             "what": "forward (bf16) + LAB lightness EMA (alpha 0.65, frames in order) + blend 0.9 with the original "
                     "(run_videos.py defaults), one GPU, frames in HBM",
-        },
-    }
+        }
     if fp16_s is not None:
         result["fp16_mode"] = {
-            "frames_per_s": round(BATCH * world / fp16_s, 2),
+            "frames_per_s": round(nloc / fp16_s, 2),
             "ms_per_step": round(fp16_s * 1e3, 4),
             "what": "NST_DT_F16: the bench kernels with fp16 weights/activations (fp16 MFMA, fp32 accumulate)",
         }

@@ -3,14 +3,14 @@
 //
 // The stylization kernels stage a tile's whole input halo (all channels) in LDS once; ResNet-101's
 // 1024/2048-channel layers do not fit that, so this kernel streams K instead: one STAGE = one tap x
-// 128 bytes of input channels (64 bf16 or 32 fp32), double-buffered in LDS through registers (the
+// 128 bytes of input channels (64 bf16 / fp16 or 32 fp32), double-buffered in LDS through registers (the
 // next stage's global loads are in flight while the current stage's MFMAs run; one barrier per stage).
 //
 //   * GEMM rows = output channels (A = packed weights, one contiguous 8 KiB piece per 64 rows and
 //     stage: [cout/64][stage][64][128 B]); columns = output pixels (B = an im2col row gathered on the
 //     fly: pixel (n,oy,ox), tap (ky,kx) -> source (oy*s - pad + ky*d, ox*s - pad + kx*d), zero outside
 //     the image: Conv2d zero padding, any stride and dilation — the atrous convs of layer4 / ASPP).
-//   * 4 waves in 2x2, each (BM/2)x(BN/2) of the BMxBN tile; bf16: v_mfma_f32_16x16x32_bf16, one per
+//   * 4 waves in 2x2, each (BM/2)x(BN/2) of the BMxBN tile; bf16 / fp16: v_mfma_f32_16x16x32_{bf16,f16}, one per
 //     16x16 sub-tile and half-stage; fp32 (parity mode): v_mfma_f32_16x16x4_f32, 4 per half-stage over
 //     a 16-byte operand read (the K permutation is the same for A and B, so the sum is over the same
 //     products).
@@ -31,19 +31,26 @@ namespace nst {
 namespace {
 
 typedef __bf16 bf16x8_g __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8_g __attribute__((ext_vector_type(8)));
 typedef float f32x4_g __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_g __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int chunk_swz(int row) { return ((row >> 3) & 1) << 1; }
 
-__device__ __forceinline__ float bf_to_f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
-__device__ __forceinline__ uint16_t f_to_bf(float f) {  // round to nearest even (finite inputs)
-  const uint32_t u = __float_as_uint(f);
+// 16-bit activation formats (dt = NST_DT_BF16 / NST_DT_F16): exact unpack, round-to-nearest-even pack
+__device__ __forceinline__ float h_to_f(uint16_t v, int dt) {
+  return dt == NST_DT_F16 ? (float)__builtin_bit_cast(_Float16, v) : __uint_as_float((uint32_t)v << 16);
+}
+__device__ __forceinline__ uint16_t f_to_h(float f, int dt) {
+  if (dt == NST_DT_F16) return __builtin_bit_cast(uint16_t, (_Float16)f);
+  const uint32_t u = __float_as_uint(f);  // bf16 (finite inputs)
   return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
-template <int BM, int BN, bool F32>
+// DT: the compute dtype (NST_DT_F32 = the exact-f32 parity mode, NST_DT_BF16, NST_DT_F16)
+template <int BM, int BN, int DT>
 __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
+  constexpr bool F32 = DT == NST_DT_F32;
   constexpr int MI = BM / 32, NI = BN / 32;      // 16x16 sub-tiles per wave along rows / columns
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, BUF = A_BYTES + B_BYTES;
   constexpr int A_TPR = 256 / BM, A_CPT = 8 / A_TPR;  // loader threads per row, 16-B chunks per thread
@@ -149,6 +156,9 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].y), __uint_as_float(b[j].y), acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].z), __uint_as_float(b[j].z), acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].w), __uint_as_float(b[j].w), acc[i][j], 0, 0, 0);
+          } else if constexpr (DT == NST_DT_F16) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_g, a[i]),
+                                                               __builtin_bit_cast(f16x8_g, b[j]), acc[i][j], 0, 0, 0);
           } else {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_g, a[i]),
                                                                 __builtin_bit_cast(bf16x8_g, b[j]), acc[i][j], 0, 0, 0);
@@ -181,8 +191,8 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
           v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
         } else {
           const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
-          v[0] += bf_to_f((uint16_t)(r.x & 0xffff)); v[1] += bf_to_f((uint16_t)(r.x >> 16));
-          v[2] += bf_to_f((uint16_t)(r.y & 0xffff)); v[3] += bf_to_f((uint16_t)(r.y >> 16));
+          v[0] += h_to_f((uint16_t)(r.x & 0xffff), DT); v[1] += h_to_f((uint16_t)(r.x >> 16), DT);
+          v[2] += h_to_f((uint16_t)(r.y & 0xffff), DT); v[3] += h_to_f((uint16_t)(r.y >> 16), DT);
         }
       }
       if (p.relu) {
@@ -194,8 +204,8 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
         *(float4*)((float*)p.out + o) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
         uint2 w;
-        w.x = (uint32_t)f_to_bf(v[0]) | ((uint32_t)f_to_bf(v[1]) << 16);
-        w.y = (uint32_t)f_to_bf(v[2]) | ((uint32_t)f_to_bf(v[3]) << 16);
+        w.x = (uint32_t)f_to_h(v[0], DT) | ((uint32_t)f_to_h(v[1], DT) << 16);
+        w.y = (uint32_t)f_to_h(v[2], DT) | ((uint32_t)f_to_h(v[3], DT) << 16);
         *(uint2*)((uint16_t*)p.out + o) = w;
       }
     }
@@ -204,7 +214,8 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
 
 // split-K epilogue: sum the K slices in slice order, then scale/shift, residual, ReLU, store (as the
 // single-pass epilogue does)
-__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmConvParams p, int f32) {
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmConvParams p, int dt) {
+  const bool f32 = dt == NST_DT_F32;
   const int groups = p.cout_store >> 2;
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (size_t)p.npix * groups) return;
@@ -220,8 +231,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmConvParams p, int 
       v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
     } else {
       const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
-      v[0] += bf_to_f((uint16_t)(r.x & 0xffff)); v[1] += bf_to_f((uint16_t)(r.x >> 16));
-      v[2] += bf_to_f((uint16_t)(r.y & 0xffff)); v[3] += bf_to_f((uint16_t)(r.y >> 16));
+      v[0] += h_to_f((uint16_t)(r.x & 0xffff), dt); v[1] += h_to_f((uint16_t)(r.x >> 16), dt);
+      v[2] += h_to_f((uint16_t)(r.y & 0xffff), dt); v[3] += h_to_f((uint16_t)(r.y >> 16), dt);
     }
   }
   if (p.relu) {
@@ -233,16 +244,18 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmConvParams p, int 
     *(float4*)((float*)p.out + o) = make_float4(v[0], v[1], v[2], v[3]);
   } else {
     uint2 w;
-    w.x = (uint32_t)f_to_bf(v[0]) | ((uint32_t)f_to_bf(v[1]) << 16);
-    w.y = (uint32_t)f_to_bf(v[2]) | ((uint32_t)f_to_bf(v[3]) << 16);
+    w.x = (uint32_t)f_to_h(v[0], dt) | ((uint32_t)f_to_h(v[1], dt) << 16);
+    w.y = (uint32_t)f_to_h(v[2], dt) | ((uint32_t)f_to_h(v[3], dt) << 16);
     *(uint2*)((uint16_t*)p.out + o) = w;
   }
 }
 
-template <int BM, int BN, bool F32>
-void launch_tile(const GemmConvParams& p, hipStream_t st) {
+template <int BM, int BN>
+void launch_tile(int dt, const GemmConvParams& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM), (unsigned)p.ksplit);
-  hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, F32>), grid, dim3(256), 0, st, p);
+  if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F32>), grid, dim3(256), 0, st, p);
+  else if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F16>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_BF16>), grid, dim3(256), 0, st, p);
 }
 
 // taps whose source row AND column land inside the image for at least one output pixel
@@ -305,18 +318,12 @@ hipError_t launch_gemm_conv(int dtype, GemmConvParams& p, hipStream_t st) {
   if (p.ntaps == 0) return hipErrorInvalidValue;
   const GemmShape g = gemm_shape(dtype, p);
   p.ksplit = p.partial ? g.ksplit : 1;
-  const bool f32 = dtype == NST_DT_F32;
-  if (g.big) {
-    if (f32) launch_tile<128, 128, true>(p, st);
-    else launch_tile<128, 128, false>(p, st);
-  } else {
-    if (f32) launch_tile<64, 64, true>(p, st);
-    else launch_tile<64, 64, false>(p, st);
-  }
+  if (g.big) launch_tile<128, 128>(dtype, p, st);
+  else launch_tile<64, 64>(dtype, p, st);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ksplit == 1) return e;
   const size_t n = (size_t)p.npix * (p.cout_store / 4);
-  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, f32 ? 1 : 0);
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, dtype);
   return hipGetLastError();
 }
 

@@ -5,9 +5,30 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <cmath>
+#include <cstring>
 #include <string>
 
 namespace nst {
+
+// IEEE binary16 of a host float, round to nearest even (values >= 65520 -> inf, as the device's
+// v_cvt_pk_f16_f32): weight packing for NST_DT_F16
+inline uint16_t f32_to_f16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  const uint16_t sign = (uint16_t)((u >> 16) & 0x8000u);
+  uint32_t a = u & 0x7fffffffu;
+  if (a > 0x7f800000u) return sign | 0x7e00u;   // NaN
+  if (a >= 0x477ff000u) return sign | 0x7c00u;  // rounds past 65504
+  if (a >= 0x38800000u) {                       // normal: rebias the exponent, RNE on the 13 dropped bits
+    a -= 0x38000000u;
+    a += 0xfffu + ((a >> 13) & 1u);
+    return sign | (uint16_t)(a >> 13);
+  }
+  float af;  // subnormal or zero: units of 2^-24 (exact power-of-two scaling), nearbyint rounds to even
+  std::memcpy(&af, &a, 4);
+  return sign | (uint16_t)std::nearbyint(af * 16777216.0f);
+}
 
 // ---- error plumbing (thread-local last error, see nst_last_error) ----
 void set_error(const std::string& msg);

@@ -103,7 +103,7 @@ int build_conv(SegConv& L, const ParamMap& pm, const std::string& wname, const s
         const size_t e = (((size_t)(co / 64) * nstage + s) * 64 + (co % 64)) * ck + kc;
         if (dtype == NST_DT_F32) std::memcpy(&pk[e * 4], &v, 4);
         else {
-          const uint16_t b = to_bf16(v);
+          const uint16_t b = dtype == NST_DT_F16 ? f32_to_f16_rne(v) : to_bf16(v);
           std::memcpy(&pk[e * 2], &b, 2);
         }
       }
@@ -404,7 +404,7 @@ extern "C" {
 int nst_seg_create(const nst_param* params, int n_params, int num_classes, int compute_dtype, int device,
                    nst_seg** out) {
   if (!params || n_params <= 0 || !out || num_classes < 2 || num_classes > 256 ||
-      (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16)) {
+      (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16 && compute_dtype != NST_DT_F16)) {
     set_error("nst_seg_create: invalid arguments");
     return NST_E_INVALID;
   }

@@ -7,6 +7,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "nst_hip.h"
+
 namespace nst {
 
 // One convolution as a GEMM: rows = output channels, columns = output pixels (n*ho*wo, NHWC order),
@@ -40,14 +42,14 @@ struct GemmConvParams {
   float* partial;
 };
 
-// dtype: NST_DT_F32 / NST_DT_BF16.  Picks the tile shape and the K split from the GEMM's size; p.taps /
+// dtype: NST_DT_F32 / NST_DT_BF16 / NST_DT_F16.  Picks the tile shape and the K split from the GEMM's size; p.taps /
 // p.ntaps are filled here (gemm_live_taps).  partial: scratch of gemm_partial_bytes(...) bytes or nullptr
 // (no split).
 hipError_t launch_gemm_conv(int dtype, GemmConvParams& p, hipStream_t st);
 // bytes of split-K scratch the launch of this conv would use (0: no split)
 size_t gemm_partial_bytes(int dtype, const GemmConvParams& p);
-// stage width in channels for a dtype (64 bf16, 32 fp32)
-inline int gemm_stage_channels(int dtype) { return dtype == 1 ? 64 : 32; }
+// stage width in channels for a dtype (64 bf16 / fp16, 32 fp32)
+inline int gemm_stage_channels(int dtype) { return dtype == NST_DT_F32 ? 32 : 64; }
 
 // ---- seg_ops.hip ----
 // Stem im2col for the 7x7/2 pad-3 first conv: source = frames u8 NHWC [n][h][w][3] normalised as

@@ -15,23 +15,29 @@ namespace nst {
 
 namespace {
 
-__device__ __forceinline__ float ld_act(const void* p, size_t i, bool f32) {
-  return f32 ? ((const float*)p)[i] : __uint_as_float((uint32_t)((const uint16_t*)p)[i] << 16);
+// activations in the compute dtype dt (NST_DT_F32 / NST_DT_BF16 / NST_DT_F16)
+__device__ __forceinline__ float ld_act(const void* p, size_t i, int dt) {
+  if (dt == NST_DT_F32) return ((const float*)p)[i];
+  const uint16_t v = ((const uint16_t*)p)[i];
+  return dt == NST_DT_F16 ? (float)__builtin_bit_cast(_Float16, v) : __uint_as_float((uint32_t)v << 16);
 }
 __device__ __forceinline__ uint16_t bf16_rne(float f) {
   const uint32_t u = __float_as_uint(f);
   return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
-__device__ __forceinline__ void st_act(void* p, size_t i, float v, bool f32) {
-  if (f32) ((float*)p)[i] = v;
-  else ((uint16_t*)p)[i] = bf16_rne(v);
+__device__ __forceinline__ uint16_t h16_rne(float f, int dt) {  // to the 16-bit format dt, round to nearest even
+  return dt == NST_DT_F16 ? __builtin_bit_cast(uint16_t, (_Float16)f) : bf16_rne(f);
+}
+__device__ __forceinline__ void st_act(void* p, size_t i, float v, int dt) {
+  if (dt == NST_DT_F32) ((float*)p)[i] = v;
+  else ((uint16_t*)p)[i] = h16_rne(v, dt);
 }
 inline unsigned blocks_for(size_t n, int per = 256) { return (unsigned)((n + per - 1) / per); }
 
 // ---- stem im2col (sky_swap.py:179-183 preprocess_pil fused for u8 frames) ----
 // u8: float32(u8) / 255 in float32, then (x - mean) / std in float64 (numpy promotes the float32
 // array against the float64 tuples), then .float() -> float32 — reproduced operation for operation.
-__global__ __launch_bounds__(256) void stem_im2col_kernel(const void* __restrict__ x, int x_u8, int f32, int n, int h,
+__global__ __launch_bounds__(256) void stem_im2col_kernel(const void* __restrict__ x, int x_u8, int dt, int n, int h,
                                                           int w, int ho, int wo, int kp, void* __restrict__ col) {
   // one thread = one output pixel x 8 consecutive columns (one 16-byte bf16 / two 16-byte fp32 stores;
   // consecutive threads write consecutive chunks of a pixel's row).  u8 frames go through a per-block table
@@ -69,21 +75,21 @@ __global__ __launch_bounds__(256) void stem_im2col_kernel(const void* __restrict
     }
   }
   const size_t o = px * kp + k0;
-  if (f32) {
+  if (dt == NST_DT_F32) {
     *(float4*)((float*)col + o) = make_float4(v[0], v[1], v[2], v[3]);
     *(float4*)((float*)col + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
   } else {
     uint4 u;
-    u.x = (uint32_t)bf16_rne(v[0]) | ((uint32_t)bf16_rne(v[1]) << 16);
-    u.y = (uint32_t)bf16_rne(v[2]) | ((uint32_t)bf16_rne(v[3]) << 16);
-    u.z = (uint32_t)bf16_rne(v[4]) | ((uint32_t)bf16_rne(v[5]) << 16);
-    u.w = (uint32_t)bf16_rne(v[6]) | ((uint32_t)bf16_rne(v[7]) << 16);
+    u.x = (uint32_t)h16_rne(v[0], dt) | ((uint32_t)h16_rne(v[1], dt) << 16);
+    u.y = (uint32_t)h16_rne(v[2], dt) | ((uint32_t)h16_rne(v[3], dt) << 16);
+    u.z = (uint32_t)h16_rne(v[4], dt) | ((uint32_t)h16_rne(v[5], dt) << 16);
+    u.w = (uint32_t)h16_rne(v[6], dt) | ((uint32_t)h16_rne(v[7], dt) << 16);
     *(uint4*)((uint16_t*)col + o) = u;
   }
 }
 
 // ---- MaxPool2d(3, stride 2, padding 1) (resnet.py:65), NHWC ----
-__global__ __launch_bounds__(256) void maxpool_kernel(const void* __restrict__ in, int f32, int n, int h, int w, int c,
+__global__ __launch_bounds__(256) void maxpool_kernel(const void* __restrict__ in, int dt, int n, int h, int w, int c,
                                                       void* __restrict__ out, int ho, int wo) {
   // one thread = one output pixel x 8 consecutive channels
   const int groups = c >> 3;
@@ -104,19 +110,19 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const void* __restrict__ i
       const size_t b = (((size_t)img * h + iy) * w + ix) * c + ch;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const float v = ld_act(in, b + q, f32);
+        const float v = ld_act(in, b + q, dt);
         m[q] = any ? fmaxf(m[q], v) : v;
       }
       any = true;
     }
   }
 #pragma unroll
-  for (int q = 0; q < 8; ++q) st_act(out, px * c + ch + q, m[q], f32);
+  for (int q = 0; q < 8; ++q) st_act(out, px * c + ch + q, m[q], dt);
 }
 
 // ---- AdaptiveAvgPool2d(1) (aspp.py:55): torch takes the mean over (h, w).  Block = 64 channels x 4 pixel
 // lanes (coalesced 64-channel rows), fp64 sums combined in fixed lane order ----
-__global__ __launch_bounds__(256) void avgpool_kernel(const void* __restrict__ in, int f32, int hw, int c, int cs,
+__global__ __launch_bounds__(256) void avgpool_kernel(const void* __restrict__ in, int dt, int hw, int c, int cs,
                                                       void* __restrict__ out) {
   __shared__ double part[4][64];
   const int t = threadIdx.x, cl = t & 63, lane = t >> 6;
@@ -124,13 +130,13 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const void* __restrict__ i
   double s = 0.0;
   if (ch < c) {
     const size_t base = (size_t)img * hw * cs + ch;
-    for (int i = lane; i < hw; i += 4) s += (double)ld_act(in, base + (size_t)i * cs, f32);
+    for (int i = lane; i < hw; i += 4) s += (double)ld_act(in, base + (size_t)i * cs, dt);
   }
   part[lane][cl] = s;
   __syncthreads();
   if (lane == 0 && ch < c) {
     const double tot = ((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl];
-    st_act(out, (size_t)img * cs + ch, (float)(tot / hw), f32);
+    st_act(out, (size_t)img * cs + ch, (float)(tot / hw), dt);
   }
 }
 
@@ -154,7 +160,7 @@ __device__ __forceinline__ AcAxis ac_axis(int dst, int in, int out) {
   return a;
 }
 
-__global__ __launch_bounds__(256) void resize_ac_kernel(const void* __restrict__ in, int f32, int n, int h, int w,
+__global__ __launch_bounds__(256) void resize_ac_kernel(const void* __restrict__ in, int dt, int n, int h, int w,
                                                         int c, int cs_in, void* __restrict__ out, int oh, int ow,
                                                         int cs_out, int off) {
   // one thread = one output pixel x 8 consecutive channels
@@ -172,9 +178,9 @@ __global__ __launch_bounds__(256) void resize_ac_kernel(const void* __restrict__
   const size_t o = px * cs_out + off + ch;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const float t0 = ld_act(in, i00 + q, f32) * ax.l0 + ld_act(in, i01 + q, f32) * ax.l1;
-    const float t1 = ld_act(in, i10 + q, f32) * ax.l0 + ld_act(in, i11 + q, f32) * ax.l1;
-    st_act(out, o + q, t0 * ay.l0 + t1 * ay.l1, f32);
+    const float t0 = ld_act(in, i00 + q, dt) * ax.l0 + ld_act(in, i01 + q, dt) * ax.l1;
+    const float t1 = ld_act(in, i10 + q, dt) * ax.l0 + ld_act(in, i11 + q, dt) * ax.l1;
+    st_act(out, o + q, t0 * ay.l0 + t1 * ay.l1, dt);
   }
 }
 
@@ -317,7 +323,7 @@ hipError_t launch_seg_stem_im2col(int dtype, const void* x, int x_u8, int n, int
                                   void* col, hipStream_t st) {
   if (kp < 147 || kp % 8) return hipErrorInvalidValue;
   const size_t total = (size_t)n * ho * wo * (kp / 8);
-  hipLaunchKernelGGL(stem_im2col_kernel, dim3(blocks_for(total)), dim3(256), 0, st, x, x_u8, dtype == NST_DT_F32 ? 1 : 0,
+  hipLaunchKernelGGL(stem_im2col_kernel, dim3(blocks_for(total)), dim3(256), 0, st, x, x_u8, dtype,
                      n, h, w, ho, wo, kp, col);
   return hipGetLastError();
 }
@@ -326,14 +332,14 @@ hipError_t launch_seg_maxpool(int dtype, const void* in, int n, int h, int w, in
                               hipStream_t st) {
   if (c % 8) return hipErrorInvalidValue;
   const size_t total = (size_t)n * ho * wo * (c / 8);
-  hipLaunchKernelGGL(maxpool_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, dtype == NST_DT_F32 ? 1 : 0, n, h,
+  hipLaunchKernelGGL(maxpool_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, dtype, n, h,
                      w, c, out, ho, wo);
   return hipGetLastError();
 }
 
 hipError_t launch_seg_avgpool(int dtype, const void* in, int n, int hw, int c, int cs, void* out, hipStream_t st) {
   hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((c + 63) / 64), (unsigned)n), dim3(256), 0, st, in,
-                     dtype == NST_DT_F32 ? 1 : 0, hw, c, cs, out);
+                     dtype, hw, c, cs, out);
   return hipGetLastError();
 }
 
@@ -341,7 +347,7 @@ hipError_t launch_seg_resize_ac(int dtype, const void* in, int n, int h, int w, 
                                 int ow, int cs_out, int off, hipStream_t st) {
   if (c % 8 || cs_in % 8 || cs_out % 8 || off % 8) return hipErrorInvalidValue;
   const size_t total = (size_t)n * oh * ow * (c / 8);
-  hipLaunchKernelGGL(resize_ac_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, dtype == NST_DT_F32 ? 1 : 0, n,
+  hipLaunchKernelGGL(resize_ac_kernel, dim3(blocks_for(total)), dim3(256), 0, st, in, dtype, n,
                      h, w, c, cs_in, out, oh, ow, cs_out, off);
   return hipGetLastError();
 }

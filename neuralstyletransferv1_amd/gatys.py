@@ -75,7 +75,8 @@ class Gatys:
         idx = device.index if device.index is not None else torch.cuda.current_device()
         check(lib().nst_vgg_create(arr, len(host), idx, ctypes.byref(h)), "nst_vgg_create")
         self._h = h
-        self._hw: Optional[Tuple[int, int]] = None
+        self._hw: Optional[Tuple[int, int]] = None       # size of the scratch workspace
+        self._tgt_hw: Optional[Tuple[int, int]] = None   # size the content / style targets were made for
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -85,17 +86,26 @@ class Gatys:
             except Exception:
                 pass
 
-    def _buffers(self, hgt: int, wid: int):
+    def _sizes(self, hgt: int, wid: int) -> Tuple[int, int]:
+        ws, stt = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib().nst_gatys_buffer_bytes(self._h, hgt, wid, ctypes.byref(ws), ctypes.byref(stt)),
+              "nst_gatys_buffer_bytes")
+        return ws.value, stt.value
+
+    def _workspace(self, hgt: int, wid: int) -> torch.Tensor:
+        """Scratch for an h x w pass; the targets (self.state) are kept apart, so a features() call at another
+        size does not invalidate them."""
         if self._hw != (hgt, wid):
-            ws, stt = ctypes.c_size_t(), ctypes.c_size_t()
-            check(lib().nst_gatys_buffer_bytes(self._h, hgt, wid, ctypes.byref(ws), ctypes.byref(stt)),
-                  "nst_gatys_buffer_bytes")
-            self.ws = torch.empty(ws.value, dtype=torch.uint8, device=self.device)
-            self.state = torch.empty(stt.value, dtype=torch.uint8, device=self.device)
+            self.ws = torch.empty(self._sizes(hgt, wid)[0], dtype=torch.uint8, device=self.device)
             self.losses = torch.zeros(4, dtype=torch.float32, device=self.device)
             self._hw = (hgt, wid)
         self.ws.record_stream(torch.cuda.current_stream(self.device))
-        return self.ws, self.state
+        return self.ws
+
+    def _targets(self, hgt: int, wid: int) -> torch.Tensor:
+        if self._tgt_hw != (hgt, wid):
+            raise NstError(f"call set_targets for {hgt}x{wid} first (targets are for {self._tgt_hw})")
+        return self.state
 
     @staticmethod
     def _image(x: torch.Tensor) -> torch.Tensor:
@@ -108,7 +118,7 @@ class Gatys:
         """Pre-activation feature maps (bf16, NCHW view of the NHWC buffers) of the 6 loss layers."""
         image = self._image(image)
         _, _, hgt, wid = image.shape
-        ws, _ = self._buffers(hgt, wid)
+        ws = self._workspace(hgt, wid)
         shapes = [(hgt, wid, 64), (hgt // 2, wid // 2, 128), (hgt // 4, wid // 4, 256), (hgt // 8, wid // 8, 512),
                   (hgt // 16, wid // 16, 512), (hgt // 8, wid // 8, 512)]
         outs = [torch.empty(s, dtype=torch.bfloat16, device=self.device) for s in shapes]
@@ -123,7 +133,11 @@ class Gatys:
         if content.shape != style.shape:
             raise NstError("resize the style image to the content size first (same h x w)")
         _, _, hgt, wid = content.shape
-        ws, stt = self._buffers(hgt, wid)
+        ws = self._workspace(hgt, wid)
+        if self._tgt_hw != (hgt, wid):
+            self.state = torch.empty(self._sizes(hgt, wid)[1], dtype=torch.uint8, device=self.device)
+        stt = self.state
+        self._tgt_hw = (hgt, wid)
         check(lib().nst_gatys_targets(self._h, content.data_ptr(), style.data_ptr(), hgt, wid, stt.data_ptr(),
                                       ws.data_ptr(), ws.numel(), _lib.stream_ptr(self.device)), "nst_gatys_targets")
 
@@ -132,9 +146,8 @@ class Gatys:
         """-> (dL/d normalised image [1,3,h,w] fp32, losses [total, content, style] fp32 on device)."""
         image = self._image(image)
         _, _, hgt, wid = image.shape
-        if self._hw != (hgt, wid):
-            raise NstError("call set_targets for this image size first")
-        ws, stt = self._buffers(hgt, wid)
+        stt = self._targets(hgt, wid)
+        ws = self._workspace(hgt, wid)
         g = torch.empty_like(image)
         wl = (ctypes.c_float * 5)(*[float(v) for v in style_layer_weights])
         check(lib().nst_gatys_grad(self._h, image.data_ptr(), hgt, wid, wl, float(content_weight), float(style_weight),
@@ -147,7 +160,8 @@ class Gatys:
         """grad() plus dL/dz of each of the 13 convs (z = pre-activation), bf16 [1,c,h,w] views."""
         image = self._image(image)
         _, _, hgt, wid = image.shape
-        ws, stt = self._buffers(hgt, wid)
+        stt = self._targets(hgt, wid)
+        ws = self._workspace(hgt, wid)
         shapes, hh, ww = [], hgt, wid
         for k, c in enumerate((64, 64, 128, 128, 256, 256, 256, 256, 512, 512, 512, 512, 512)):
             shapes.append((hh, ww, c))

@@ -406,7 +406,7 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     import torch
     from PIL import Image
 
-    from .frames import plan_groups, run_sharded
+    from .frames import plan_groups, rank0_share, run_sharded
     from .postproc import LabSmoother, blend_frames
 
     # one GPU per rank (several ranks may share a device with --dist_backend gloo: tests)
@@ -487,7 +487,11 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
 
     pool = ThreadPoolExecutor(max_workers=max(1, threads))
     sizes = [src.size(i) for i in range(len(src))]
-    groups = plan_groups(sizes, world, max(1, args.batch))
+    # rank 0 also runs every frame's ordered post chain: a lighter share of each group (frames.rank0_share)
+    bsz = max(1, args.batch)
+    r0 = rank0_share(world, bsz)
+    caps = [r0] + [bsz] * (world - 1)
+    groups = plan_groups(sizes, world, bsz, r0)
     flow_mode = bool(getattr(args, "flow_ema", False))
     need_orig = blend < 1.0 or bool(args.mask or args.mask_dir) or (flow_mode and bool(getattr(args, "motion_blend", False)))
 
@@ -656,7 +660,7 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             out_img.save(out_path)
         return str(out_path)
 
-    run_sharded(groups, world, rank, stylize, consume, dev)
+    run_sharded(groups, world, rank, stylize, consume, dev, caps)
     for p in pending:
         p.result()
     pool.shutdown()

@@ -2,10 +2,11 @@
 oracle/dis_oracle.py; cv2 absent: parity unpinned except the luma, which is Pillow's) and end to end through the CLI.
 
 DIS (the reference's default --flow_method): the GPU runs the restatement's fp32 operations in the same order
-(its 64-pixel patch sums as the same halving tree), so flows agree bit for bit except where a branch of the
-search (candidate choice, early stop, the 8-px rejection) sits on a rounding tie; bars: >= 99.5 % of flow values
-identical, the rest within 0.05 px at the 99.9th percentile; translation recovered within 0.15 px (the
-restatement's own accuracy at finest scale 2 on these textures).
+(its 64-pixel patch sums as the same halving tree); measured, more than half of the flow values are identical and
+the rest differ by a few fp32 ulps (<= 3.2e-6 px: rounding differences between the device and numpy in the
+variational refinement), so the bars are 1e-4 px at the 99.9th percentile and 0.05 px at most (room for a search
+branch that sits on a rounding tie); translation recovered within 0.15 px (the restatement's own accuracy at
+finest scale 2 on these textures).
 
 Bars: luma bit-exact vs Pillow; Farneback flow within 2e-3 px of the restatement on >= 99.9 % of pixels (the
 same fp32/fp64 operation order; the host exp() of the taps and libm differences can move a fraction of an ulp
@@ -119,7 +120,7 @@ def test_flow_downscale_vs_restatement():
     for ds in (2, 4):
         g = T.downscale_gray(torch.from_numpy(prev).to(DEV), ds).cpu().numpy()
         assert np.array_equal(g, FO.area_down(prev, ds))
-    fs = T.FlowSmoother(True, 0.8, 2)
+    fs = T.FlowSmoother(True, 0.8, 2, "farneback")
     a = torch.rand(3, 144, 256, device=DEV)
     fr0 = np.repeat(prev[..., None], 3, axis=2)
     fr1 = np.repeat(nxt[..., None], 3, axis=2)
@@ -154,7 +155,7 @@ def test_dis_vs_restatement(hw):
         d = np.abs(got[k] - ref)
         same = float((d == 0).mean())
         print(hw, k, f"identical {same:.5f}, max |d| {d.max():.3e}, p99.9 {np.quantile(d, 0.999):.3e}")
-        assert same >= 0.995 and np.quantile(d, 0.999) <= 0.05, (same, float(d.max()))
+        assert np.quantile(d, 0.999) <= 1e-4 and d.max() <= 0.05, (same, float(d.max()))
         c = got[k][16:-16, 16:-16]
         dx, dy = moves[k]
         assert abs(float(np.median(c[..., 0])) - dx) < 0.15 and abs(float(np.median(c[..., 1])) - dy) < 0.15
@@ -247,6 +248,6 @@ def test_cli_flow_downscale_non_divisor(tmp_path):
     ref = FO.resize_lin(small, h, w, 3.0)
     d = np.abs(got - ref)
     print("ds3", (d == 0).mean(), d.max())
-    assert (d == 0).mean() >= 0.99
+    assert np.quantile(d, 0.999) <= 1e-4 and d.max() <= 0.05
     c = got[30:-30, 30:-30]
     assert abs(float(np.median(c[..., 0])) - 6) < 0.5 and abs(float(np.median(c[..., 1])) + 3) < 0.5

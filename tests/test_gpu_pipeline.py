@@ -47,7 +47,7 @@ def _oracle_chain(arch_sds, weights, frames, preset, smooth=True, alpha=0.7, ble
 # move an L / a / b byte across a quantisation step, which LAB -> RGB turns into a few LSB.  The engine's LAB
 # stage is bit-exact (tests/test_gpu_parity.py), and test_pre_lab_within_1lsb_and_lab_attribution shows
 # that every post-LAB difference is the round trip of a <= 1 LSB pre-LAB one; this bounds the result.
-LAB_MAX_LSB = 12
+LAB_MAX_LSB = 8
 
 
 def _close(a, b, max_lsb, frac=0.005):
