@@ -9,13 +9,13 @@ BUILD := build/obj
 SLP ?= -fno-slp-vectorize
 CXXFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off $(SLP) -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
-SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/conv_gemm.hip $(CSRC)/seg_ops.hip $(CSRC)/region_ops.hip $(CSRC)/flow_ops.hip $(CSRC)/dis_ops.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp $(CSRC)/seg_deeplab.cpp $(CSRC)/region_api.cpp $(CSRC)/flow_api.cpp
+SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_f32s.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/conv_gemm.hip $(CSRC)/seg_ops.hip $(CSRC)/region_ops.hip $(CSRC)/flow_ops.hip $(CSRC)/dis_ops.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp $(CSRC)/seg_deeplab.cpp $(CSRC)/region_api.cpp $(CSRC)/flow_api.cpp
 OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
 LIB := $(PKG)/libnst_hip.so
 
 all: $(LIB)
 
-$(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h $(CSRC)/conv_tab16.h $(CSRC)/nst_internal.h $(CSRC)/seg_internal.h $(CSRC)/post_common.h $(CSRC)/region_internal.h $(CSRC)/flow_internal.h include/nst_hip.h
+$(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h $(CSRC)/conv_tab16.h $(CSRC)/conv_tab32.h $(CSRC)/nst_internal.h $(CSRC)/seg_internal.h $(CSRC)/post_common.h $(CSRC)/region_internal.h $(CSRC)/flow_internal.h include/nst_hip.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 

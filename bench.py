@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode timing (profiling runs)")
     ap.add_argument("--cpu-frames", type=int, default=3, help="timed 1080p frames per CPU configuration")
     ap.add_argument("--no-fp16", action="store_true", help="skip the fp16-mode timing")
+    ap.add_argument("--no-fp32s", action="store_true", help="skip the split-fp16 (fp32s) mode timing")
     return ap.parse_args()
 
 
@@ -256,14 +257,23 @@ def main():
         return blend_frames(chain_ema(eng.stylize_u8(frames, PRESET)), frames, 0.9)
     chain_s = time_steps(chain_step, max(3, min(args.steps, 10))) if world == 1 else None
 
-    # fp16 mode (NST_DT_F16): the same kernels with fp16 operands, the mode that holds +-1 LSB
-    eng16 = None
-    fp16_s = None
-    if not args.no_fp16 and world == 1:
-        net.compute_dtype = "fp16"
-        eng16 = net.engine(dev)
+    # the other precision modes, same step: fp16 (NST_DT_F16: the bench kernels with fp16 operands) and
+    # split-fp16 (NST_DT_F32S: fp32 activations, fp16 hi/lo operand pairs -- the fp32 parity bars)
+    alt_modes = {}
+    for key, dt, skip, what in (
+            ("fp16_mode", "fp16", args.no_fp16,
+             "NST_DT_F16: the bench kernels with fp16 weights/activations (fp16 MFMA, fp32 accumulate)"),
+            ("fp32s_mode", "fp32s", args.no_fp32s,
+             "NST_DT_F32S: fp32 activations, every conv operand an fp16 hi/lo pair (two fp16 MFMAs per K step, "
+             "generic kernels): the fp32 parity mode's +-1 LSB bar")):
+        if skip or world != 1:
+            continue
+        net.compute_dtype = dt
+        e_alt = net.engine(dev)
         net.compute_dtype = "bf16"
-        fp16_s = time_steps(lambda: eng16.stylize_u8(frames, PRESET), max(3, min(args.steps, 10)))
+        t_alt = time_steps(lambda: e_alt.stylize_u8(frames, PRESET), max(3, min(args.steps, 10)))
+        alt_modes[key] = (e_alt, {"frames_per_s": round(nloc / t_alt, 2), "ms_per_step": round(t_alt * 1e3, 4),
+                                  "what": what})
 
     # profiled pass: per-conv HIP events on the forward's stream
     kp = max(3, min(args.steps, 10))
@@ -380,12 +390,8 @@ def main():
             "what": "forward (bf16) + LAB lightness EMA (alpha 0.65, frames in order) + blend 0.9 with the original "
                     "(run_videos.py defaults), one GPU, frames in HBM",
         }
-    if fp16_s is not None:
-        result["fp16_mode"] = {
-            "frames_per_s": round(nloc / fp16_s, 2),
-            "ms_per_step": round(fp16_s * 1e3, 4),
-            "what": "NST_DT_F16: the bench kernels with fp16 weights/activations (fp16 MFMA, fp32 accumulate)",
-        }
+    for key, (_, info) in alt_modes.items():
+        result[key] = info
     if rank == 0 and world == 1 and not args.no_fp32:
         # the fp32 parity mode (exact-f32 MFMA), same frames
         net.compute_dtype = "fp32"
@@ -410,14 +416,14 @@ def main():
         result["within_1lsb_vs_cpu"] = round(float(np.mean([(d <= 1).mean() for d in diff])), 6)
         result["within_2lsb_vs_cpu"] = round(float(np.mean([(d <= 2).mean() for d in diff])), 6)
         result["speedup_vs_cpu"] = round(fps / cb["value"], 1)
-        if eng16 is not None:
-            g16 = eng16.stylize_u8(frames, PRESET).cpu().numpy()
-            d16 = [np.abs(g16[i].astype(int) - cpu_outs[i].astype(int)) for i in range(k)]
-            result["fp16_mode"].update({
-                "ssim_vs_cpu": round(float(min(O.ssim(g16[i], cpu_outs[i]) for i in range(k))), 6),
-                "max_abs_lsb_vs_cpu": int(max(d.max() for d in d16)),
-                "within_1lsb_values": round(float(np.mean([(d <= 1).mean() for d in d16])), 6),
-                "within_1lsb_pixels": round(float(np.mean([(d.max(-1) <= 1).mean() for d in d16])), 6),
+        for key, (e_alt, info) in alt_modes.items():
+            ga = e_alt.stylize_u8(frames, PRESET).cpu().numpy()
+            da = [np.abs(ga[i].astype(int) - cpu_outs[i].astype(int)) for i in range(k)]
+            info.update({
+                "ssim_vs_cpu": round(float(min(O.ssim(ga[i], cpu_outs[i]) for i in range(k))), 6),
+                "max_abs_lsb_vs_cpu": int(max(d.max() for d in da)),
+                "within_1lsb_values": round(float(np.mean([(d <= 1).mean() for d in da])), 6),
+                "within_1lsb_pixels": round(float(np.mean([(d.max(-1) <= 1).mean() for d in da])), 6),
             })
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -46,6 +46,10 @@ extern "C" {
 #define NST_DT_F16 2  /* fp16 mode: fp16 weights/activations, fp16 MFMA at the bf16 rate, fp32 accumulate/statistics;
                          3 more mantissa bits than bf16 = the reference's +-1 LSB uint8 bar.  Stored conv outputs
                          must stay inside the fp16 range (|v| <= 65504) */
+#define NST_DT_F32S 3 /* split-fp16 mode: fp32 activations in HBM; each conv operand is split into an fp16 pair
+                         v = hi + lo in LDS (weights at pack time), and two v_mfma_f32_16x16x32_f16 per K step give
+                         Wh*(xh + xl) + Wl*xh: ~22 significant bits per product (the fp32 parity bar) at a quarter of
+                         the exact-f32 MFMA cycles.  Conv inputs must stay inside the fp16 range (|v| <= 65504) */
 
 /* ---- I/O formats for nst_forward ---- */
 #define NST_IO_F32_NCHW 0 /* raw model tensor [n,3,h,w] fp32 (TransformerNet.forward(X) surface) */

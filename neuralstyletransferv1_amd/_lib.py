@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("NST_HIP_LIB", os.path.join(_HERE, "libnst_hip.so"))
 
 NST_OK = 0
 NST_ARCH_JOHNSON, NST_ARCH_NST, NST_ARCH_RECONET, NST_ARCH_RECONET_FRN = 0, 1, 2, 3
-NST_DT_F32, NST_DT_BF16, NST_DT_F16 = 0, 1, 2
+NST_DT_F32, NST_DT_BF16, NST_DT_F16, NST_DT_F32S = 0, 1, 2, 3
 NST_IO_F32_NCHW, NST_IO_U8_NHWC = 0, 1
 PRESETS = {
     "none": 0,

@@ -1,40 +1,6 @@
-// conv_f32.hip — fp32 (parity mode, exact-f32 MFMA) instantiations of conv_kernel.
-// Smaller tiles than bf16: an fp32 LDS entry is twice as wide.
-#include "conv_impl.h"
+// conv_f32.hip — fp32 (parity mode, exact-f32 MFMA) instantiations of conv_kernel (conv_tab32.h).
+#include "conv_tab32.h"
 
 namespace nst {
-typedef float F;
-#define E(...) ConvInst<__VA_ARGS__>::info()
-constexpr int SD = MODE_STD, PH = MODE_PHASE;
-const ConvKernelInfo* conv_table_f32(int* count) {
-  static const ConvKernelInfo table[] = {
-      //  T  MODE KS S CINP BN TH TW WM WN  IN           OUT
-      E(F, SD, 9, 1, 4, 32, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
-      E(F, SD, 9, 1, 4, 32, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),
-      E(F, SD, 3, 2, 32, 64, 4, 16, 4, 1, IN_ACT, OUT_ACT),
-      E(F, SD, 3, 2, 64, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(F, SD, 3, 1, 128, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(F, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT),
-      E(F, PH, 3, 1, 64, 32, 4, 16, 1, 4, IN_ACT, OUT_ACT),
-      E(F, SD, 9, 1, 32, 16, 4, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
-      E(F, SD, 9, 1, 32, 16, 4, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
-      // ReCoNet (48/96/192 channels: multiples of 16, no padding in fp32)
-      E(F, SD, 9, 1, 4, 48, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
-      E(F, SD, 9, 1, 4, 48, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),
-      E(F, SD, 3, 2, 48, 96, 4, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(F, SD, 3, 2, 96, 192, 2, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(F, SD, 3, 1, 192, 192, 4, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(F, PH, 3, 1, 192, 96, 2, 16, 1, 4, IN_ACT, OUT_ACT),
-      E(F, PH, 3, 1, 96, 48, 4, 16, 1, 4, IN_ACT, OUT_ACT),
-      // consumers of the residual stream (residual join fused into the fill)
-      E(F, SD, 3, 1, 128, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
-      E(F, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
-      E(F, SD, 3, 1, 192, 192, 4, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
-      E(F, PH, 3, 1, 192, 96, 2, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
-      E(F, SD, 9, 1, 48, 16, 2, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
-      E(F, SD, 9, 1, 48, 16, 2, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
-  };
-  *count = (int)(sizeof(table) / sizeof(table[0]));
-  return table;
-}
+const ConvKernelInfo* conv_table_f32(int* count) { return conv_table_32<float>(count); }
 }  // namespace nst

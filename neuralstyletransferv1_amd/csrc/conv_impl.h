@@ -136,9 +136,43 @@ __device__ __forceinline__ f32x16_t mfma32x32x16(const uint4& a, const uint4& b,
   else
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
+// The split-fp16 mode's activation type (NST_DT_F32S): fp32 in HBM, so every sizeof(T) == 4 path
+// (fills, IN apply, joins, epilogue stores) is the fp32 one; only the LDS operand form and the
+// MFMA differ.  A 16-B LDS chunk holds 4 channels as [hi0..hi3, lo0..lo3] (fp16, hi = RNE(v),
+// lo = RNE(v - hi)); the packed weights carry two fragments per K step, [Wh0..3, Wh0..3] and
+// [Wl0..3, 0 x 4], so two v_mfma_f32_16x16x32_f16 give Wh*(xh + xl) + Wl*xh (the dropped Wl*xl is
+// ~2^-22 of the product).
+struct F32Split {
+  float v;
+};
+template <typename T>
+constexpr bool IS_SPLIT = std::is_same<T, F32Split>::value;
+
 template <typename T>
 constexpr int dtype_code() {
+  if constexpr (IS_SPLIT<T>) return NST_DT_F32S;
   return std::is_same<T, float>::value ? NST_DT_F32 : (IS_F16<T> ? NST_DT_F16 : NST_DT_BF16);
+}
+
+// 4 fp32 channels -> the split LDS chunk [hi0..hi3, lo0..lo3]
+__device__ __forceinline__ uint4 split_chunk(uint4 raw) {
+  const float v[4] = {__uint_as_float(raw.x), __uint_as_float(raw.y), __uint_as_float(raw.z), __uint_as_float(raw.w)};
+  _Float16 hi[4], lo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hi[j] = (_Float16)v[j];
+    lo[j] = (_Float16)(v[j] - (float)hi[j]);  // exact in fp32: v and hi share the exponent range
+  }
+  auto pk = [](_Float16 a, _Float16 b) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  };
+  return make_uint4(pk(hi[0], hi[1]), pk(hi[2], hi[3]), pk(lo[0], lo[1]), pk(lo[2], lo[3]));
+}
+// a staged chunk in the layer's LDS operand form
+template <typename T>
+__device__ __forceinline__ uint4 lds_form(uint4 v) {
+  if constexpr (IS_SPLIT<T>) return split_chunk(v);
+  else return v;
 }
 
 template <typename T, int MODE, int KS, int S, int CINP, int BN, int TH, int TW, int WM, int WN>
@@ -179,7 +213,8 @@ struct ConvCfg {
   // weight-fragment prefetch depth: enough K-steps in flight to cover ~512 cycles of L2 latency
   // with this tile's MFMA work per step (16 cycles per bf16 16x16x32, 4 x 32 per fp32 step);
   // in the rowed loop it must divide the steps per row so every ring slot index is static
-  static constexpr int CYC_STEP = MSUB * NSUB * (sizeof(T) == 2 ? 16 : 128);
+  static constexpr int CYC_STEP = MSUB * NSUB * (sizeof(T) == 2 ? 16 : (IS_SPLIT<T> ? 32 : 128));
+  static constexpr int AF = IS_SPLIT<T> ? 2 : 1;  // A fragments per (K step, n-subtile)
   static constexpr int PF_RAW0 = (512 + CYC_STEP - 1) / CYC_STEP;
   static constexpr int PF_RAW = PF_RAW0 < 2 ? 2 : (PF_RAW0 > 16 ? 16 : PF_RAW0);
   static constexpr int pf_div(int want, int n) {
@@ -393,6 +428,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
   static_assert(!PERS || (INK == IN_ACT && C::ROWED), "persistent form: activation-input rowed layers");
   static_assert(!WL || C::ROWED, "LDS weight ring: rowed K loop");
   static_assert(!PERS || WL, "the persistent form streams weights through the LDS ring");
+  constexpr int AF = C::AF;
+  static_assert(AF == 1 || !WL, "split-fp16 mode: register-streamed weights only");
   // weight ring geometry (WL)
   constexpr int SC = WL ? wl_stage_steps<C::NSTEP, NSUBT, C::NW>() : 1;  // K-steps per stage
   static_assert(!WL || SC >= 2, "weight-ring stage: >= 2 steps, split evenly over the waves");
@@ -449,13 +486,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
   // weights: fragment (step s, n-subtile t) of this wave lives at wp[(s*NSUBT + t)*64]; a ring of
   // PF steps is kept in flight (steps >= NSTEP are zero padding; PERS wraps to the next tile's step 0)
   constexpr int PF = C::PF;
-  const uint4* wp = (const uint4*)p.wpk + ((size_t)cur.cb * C::NSTEP_PACK * NSUBT + wn * NSUB) * 64 + lane;
-  uint4 a_ring[WL ? 1 : PF][NSUB];
+  // (split mode: AF = 2 fragments per (step, n-subtile), fragment j of (s, t) at wp[((s*NSUBT + t)*2 + j)*64])
+  const uint4* wp = (const uint4*)p.wpk + ((size_t)cur.cb * C::NSTEP_PACK * NSUBT + wn * NSUB) * AF * 64 + lane;
+  uint4 a_ring[WL ? 1 : PF][NSUB * AF];
+  auto a_load = [&](uint4 (&dst)[NSUB * AF], int s) {
+#pragma unroll
+    for (int f = 0; f < NSUB * AF; ++f) dst[f] = wp[(s * NSUBT * AF + f) * 64];
+  };
   if constexpr (!WL) {
 #pragma unroll
-    for (int d = 0; d < PF; ++d)
-#pragma unroll
-      for (int t = 0; t < NSUB; ++t) a_ring[d][t] = wp[(d * NSUBT + t) * 64];
+    for (int d = 0; d < PF; ++d) a_load(a_ring[d], d);
   }
   // WL: stage j's fragments are contiguous in the packed weights; this wave loads fragments
   // [wave*FPW, wave*FPW+FPW) of each stage and stores them to the same place in the LDS ring
@@ -627,7 +667,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
             v = norm_chunk<T>(v, nmv);
           }
         }
-        *(uint4*)(smem + e * EB + 16 * c) = v;
+        *(uint4*)(smem + e * EB + 16 * c) = lds_form<T>(v);
       }
     }
   };
@@ -707,7 +747,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
             v = p.in_norm != nullptr ? norm_chunk<T>(praw[k], nm) : praw[k];
           }
         }
-        *(uint4*)(smem + (it >> 2) * EB + (it & 3) * 16 + 64 * q) = v;
+        *(uint4*)(smem + (it >> 2) * EB + (it & 3) * 16 + 64 * q) = lds_form<T>(v);
       }
     }
   };
@@ -722,7 +762,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
         const int e = it / NCH;
         const int ly = e / LWP, lx = e - ly * LWP;
         const uint4 v = load_image_entry<T, INK, PAIR>(p, wk.n, vy0 + ly, vx0 + lx);
-        *(uint4*)(smem + e * EB) = v;
+        *(uint4*)(smem + e * EB) = lds_form<T>(v);
       }
     }
   };
@@ -743,12 +783,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
   }
   typedef f32x4_t AccT[MSUB][NSUB];
 
-  auto mfma_step = [&](AccT& acc, const uint4 (&a)[NSUB], const uint4 (&b)[MSUB]) {
+  auto mfma_step = [&](AccT& acc, const uint4 (&a)[NSUB * AF], const uint4 (&b)[MSUB]) {
 #pragma unroll
     for (int m = 0; m < MSUB; ++m) {
 #pragma unroll
       for (int t = 0; t < NSUB; ++t) {
-        if constexpr (sizeof(T) == 2) {
+        if constexpr (IS_SPLIT<T>) {
+          acc[m][t] = mfma16x16x32<_Float16>(a[2 * t], b[m], acc[m][t]);      // Wh * (xh + xl)
+          acc[m][t] = mfma16x16x32<_Float16>(a[2 * t + 1], b[m], acc[m][t]);  // Wl * xh
+        } else if constexpr (sizeof(T) == 2) {
           acc[m][t] = mfma16x16x32<T>(a[t], b[m], acc[m][t]);
         } else {
           acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[t].x), __uint_as_float(b[m].x), acc[m][t], 0, 0, 0);
@@ -866,9 +909,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
 #pragma unroll
             for (int m = 0; m < MSUB; ++m) b[m] = *(const uint4*)(rp[m] + xo * EB + 64 * cg);
             mfma_step(acc, a_ring[slot], b);
-            const int sn = row * RS + pos + PF;
-#pragma unroll
-            for (int t = 0; t < NSUB; ++t) a_ring[slot][t] = wp[(sn * NSUBT + t) * 64];
+            a_load(a_ring[slot], row * RS + pos + PF);
           }
         }
       }
@@ -893,8 +934,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
             b[m] = *(const uint4*)(smem + e * EB + 16 * (c ^ swz<NCH>(e)));
           }
           mfma_step(acc, a_ring[d], b);
-#pragma unroll
-          for (int t = 0; t < NSUB; ++t) a_ring[d][t] = wp[((s + PF) * NSUBT + t) * 64];
+          a_load(a_ring[d], s + PF);
         }
       }
     }

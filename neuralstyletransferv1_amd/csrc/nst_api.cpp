@@ -28,6 +28,7 @@ const ConvKernelInfo* conv_table_bf16(int* count);
 const ConvKernelInfo* conv_table_f16(int* count);
 const ConvKernelInfo* conv_table_bf16_wl(int* count);
 const ConvKernelInfo* conv_table_f32(int* count);
+const ConvKernelInfo* conv_table_f32s(int* count);
 const ConvKernelInfo* conv_table_out9(int* count);
 const ConvKernelInfo* conv_table_wstat(int* count);
 const ConvKernelInfo* conv_table_wphase(int* count);
@@ -41,10 +42,11 @@ const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, 
   // 16-bit formats (bf16, fp16) share the specialised tables; an entry matches only its own dtype
   const TableFn tables_16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_ws9,
                                conv_table_out9, conv_table_bf16, conv_table_f16};
-  const TableFn tables_f32[] = {conv_table_f32};
-  const bool h16 = dtype != NST_DT_F32;
+  // 4-byte activation formats (fp32, split-fp16): the generic kernels only
+  const TableFn tables_f32[] = {conv_table_f32, conv_table_f32s};
+  const bool h16 = !f32_storage(dtype);
   const TableFn* tables = h16 ? tables_16 : tables_f32;
-  const int ntables = h16 ? 8 : 1;
+  const int ntables = h16 ? 8 : 2;
   for (int ti = (h16 && no_persistent) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
     const ConvKernelInfo* t = tables[ti](&count);
@@ -458,6 +460,23 @@ int upload(const void* host, size_t bytes, void** dev) {
 }
 int upload_weights(int dtype, const std::vector<float>& pk, void** dst) {
   if (dtype == NST_DT_F32) return upload(pk.data(), pk.size() * 4, dst);
+  if (dtype == NST_DT_F32S) {
+    // generic fragments [frag][lane][4] fp32 -> [frag][2][lane][8] fp16: [Wh0..3, Wh0..3] and
+    // [Wl0..3, 0 x 4] with Wh = RNE(w), Wl = RNE(w - Wh) (conv_impl.h F32Split)
+    const size_t nfrag = pk.size() / 256;
+    std::vector<uint16_t> pb(nfrag * 2 * 64 * 8, 0);
+    for (size_t f = 0; f < nfrag; ++f)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 4; ++j) {
+          const float w = pk[(f * 64 + lane) * 4 + j];
+          const uint16_t hi = f32_to_f16_rne(w);
+          const uint16_t lo = f32_to_f16_rne(w - f16_to_f32(hi));
+          pb[((f * 2) * 64 + lane) * 8 + j] = hi;
+          pb[((f * 2) * 64 + lane) * 8 + 4 + j] = hi;
+          pb[((f * 2 + 1) * 64 + lane) * 8 + j] = lo;
+        }
+    return upload(pb.data(), pb.size() * 2, dst);
+  }
   std::vector<uint16_t> pb(pk.size());
   for (size_t i = 0; i < pk.size(); ++i) pb[i] = dtype == NST_DT_F16 ? f32_to_f16_rne(pk[i]) : f32_to_bf16_rne(pk[i]);
   return upload(pb.data(), pb.size() * 2, dst);
@@ -523,7 +542,7 @@ void tile_grid(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx,
 
 Plan make_plan(const nst_handle* h, int n, int H, int W) {
   Plan P;
-  const size_t esz = h->dtype == NST_DT_F32 ? 4 : 2;
+  const size_t esz = act_elem_bytes(h->dtype);
   int bh[NBUF], bw[NBUF];
   const size_t nops = h->prog.size();
   P.ih.resize(nops); P.iw.resize(nops); P.oh.resize(nops); P.ow.resize(nops); P.ch.resize(nops); P.cw.resize(nops);
@@ -742,7 +761,8 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
 
 int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                   unsigned flags, nst_handle** out) {
-  if (!out || arch < 0 || arch > 3 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16 && compute_dtype != NST_DT_F16) ||
+  if (!out || arch < 0 || arch > 3 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16 && compute_dtype != NST_DT_F16 &&
+                                           compute_dtype != NST_DT_F32S) ||
       (flags & ~(unsigned)NST_KSEL_ALL) != 0) {
     set_error("nst_create: invalid arguments");
     return NST_E_INVALID;
@@ -776,7 +796,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
   // activation channel padding: fp32 chunks hold 4 channels (K step 16); bf16 chunks 8 (K step 32),
   // and bf16 tiles above 32 channels come in multiples of 64 (48->64, 96->128)
   auto pad_ch = [&](int c) {
-    if (compute_dtype == NST_DT_F32) return round_up(c, 16);
+    if (f32_storage(compute_dtype)) return round_up(c, 16);
     return c <= 32 ? 32 : round_up(c, 64);
   };
   int rc = NST_OK;
@@ -970,7 +990,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
   }
   DeviceGuard guard(h->device);
   hipStream_t st = (hipStream_t)stream;
-  const size_t esz = h->dtype == NST_DT_F32 ? 4 : 2;
+  const size_t esz = act_elem_bytes(h->dtype);
   char* ws = (char*)workspace;
   void* bufs[NBUF];
   for (int b = 0; b < NBUF; ++b) bufs[b] = ws + P.off_buf[b];
@@ -1180,7 +1200,7 @@ int nst_op_describe(const nst_handle* h, int n, int in_h, int in_w, int op_index
   out->cin_stride = op.src == B_IMG ? 3 : Ly.cinp;
   out->cout_stride = Ly.coutp;
   out->kernel_mode = Ly.mode;
-  out->elem_bytes = h->dtype == NST_DT_F32 ? 4 : 2;
+  out->elem_bytes = act_elem_bytes(h->dtype);
   return NST_OK;
 }
 

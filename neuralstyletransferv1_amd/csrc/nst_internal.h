@@ -9,6 +9,8 @@
 #include <cstring>
 #include <string>
 
+#include "nst_hip.h"
+
 namespace nst {
 
 // IEEE binary16 of a host float, round to nearest even (values >= 65520 -> inf, as the device's
@@ -29,6 +31,15 @@ inline uint16_t f32_to_f16_rne(float f) {
   std::memcpy(&af, &a, 4);
   return sign | (uint16_t)std::nearbyint(af * 16777216.0f);
 }
+// fp16 bits -> the value (exact)
+inline float f16_to_f32(uint16_t h) {
+  const int e = (h >> 10) & 31, m = h & 1023;
+  float v = e == 0 ? std::ldexp((float)m, -24) : (e == 31 ? INFINITY : std::ldexp((float)(m | 1024), e - 25));
+  return (h & 0x8000u) ? -v : v;
+}
+// Dtype of the HBM activations: 4-byte for fp32 and the split-fp16 mode, 2-byte for bf16 / fp16
+inline bool f32_storage(int dtype) { return dtype == NST_DT_F32 || dtype == NST_DT_F32S; }
+inline size_t act_elem_bytes(int dtype) { return f32_storage(dtype) ? 4 : 2; }
 
 // ---- error plumbing (thread-local last error, see nst_last_error) ----
 void set_error(const std::string& msg);

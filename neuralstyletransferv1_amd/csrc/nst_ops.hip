@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void residual_kernel(const T* __restrict__ y, 
 
 hipError_t launch_residual(int dtype, const void* y, const float2* ys, const void* r, const float2* rs,
                            int r_relu, int relu_out, void* out, int n, int hw, int c, hipStream_t st) {
-  const int cpc = dtype == NST_DT_F32 ? 4 : 8;
+  const int cpc = f32_storage(dtype) ? 4 : 8;
   const int cv_n = c / cpc;
   if (c % cpc != 0 || cv_n > 256) return hipErrorInvalidValue;
   const int tpp = 256 / cv_n;

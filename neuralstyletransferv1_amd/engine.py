@@ -18,7 +18,7 @@ from . import _lib
 from ._lib import NstError, NstParam, check, lib
 
 _DTYPES = {"fp32": _lib.NST_DT_F32, "float32": _lib.NST_DT_F32, "bf16": _lib.NST_DT_BF16, "bfloat16": _lib.NST_DT_BF16,
-           "fp16": _lib.NST_DT_F16, "float16": _lib.NST_DT_F16}
+           "fp16": _lib.NST_DT_F16, "float16": _lib.NST_DT_F16, "fp32s": _lib.NST_DT_F32S}
 
 
 class Engine:
@@ -194,7 +194,9 @@ class StylizationNet(nn.Module):
     def __init__(self):
         super().__init__()
         # "fp32": parity mode (exact-f32 MFMA); "bf16": throughput mode (bf16 MFMA, fp32 accumulate);
-        # "fp16": fp16 MFMA at the bf16 rate, within +-1 LSB of the reference's uint8 frames
+        # "fp16": fp16 MFMA at the bf16 rate (11 significant bits); "fp32s": fp32 activations with
+        # every conv operand split into an fp16 hi/lo pair (two fp16 MFMAs per K step, ~22 bits): the
+        # parity mode's +-1 LSB at a quarter of its MFMA cycles
         self.compute_dtype = "fp32"
         # kernel selection (names of _lib.KSEL): e.g. {"no_wstat"} runs the residual trunk on the
         # generic kernel instead of the weight-stationary one; empty = the fastest mapping
@@ -215,7 +217,7 @@ class StylizationNet(nn.Module):
             device = torch.device("cuda", torch.cuda.current_device())
         dtype = dtype or self.compute_dtype
         if dtype not in _DTYPES:
-            raise NstError(f"compute_dtype must be fp32, bf16 or fp16, got {dtype!r}")
+            raise NstError(f"compute_dtype must be fp32, fp32s, bf16 or fp16, got {dtype!r}")
         flags = 0
         for name in self.kernel_select:
             if name not in _lib.KSEL:

@@ -10,8 +10,9 @@ per-frame loop (`style_frames`, pipeline.py:527-2122, standard path :1409-1519 +
     -> LAB EMA (LUT, frame order) -> mask composite -> uniform blend --D2H--> host: PIL encode.
 
 Additions: --gpus N (frames round-robin over N GPUs, ordered gather to rank 0 over RCCL),
---batch B (frames per GPU step), --dtype {fp32,bf16,fp16} (fp32 = parity with the reference's
-arithmetic, default; bf16 = throughput mode; fp16 = bf16's speed within +-1 LSB of the reference),
+--batch B (frames per GPU step), --dtype {fp32,fp32s,bf16,fp16} (fp32 = parity with the reference's
+arithmetic, default; fp32s = fp32 activations on split-fp16 MFMAs, the parity bar at several times
+fp32's speed; bf16 = throughput mode; fp16 = near bf16's speed with 3 more mantissa bits),
 --synthetic WxH / --synthetic_frames N (an
 in-memory synthetic frame stream instead of files; config 4 of BASELINE.json).
 
@@ -151,9 +152,10 @@ def build_parser() -> argparse.ArgumentParser:
                     help="--gpus > 1 process group: nccl (RCCL over xGMI, one GPU per rank) or gloo (host-staged "
                          "exchange; ranks may share a GPU, used by the tests)")
     ap.add_argument("--dist_timeout", type=float, default=600.0, help="seconds before a blocked exchange aborts")
-    ap.add_argument("--dtype", choices=["fp32", "bf16", "fp16"], default="fp32",
-                    help="fp32 = parity with the reference arithmetic; bf16 = throughput mode; fp16 = the "
-                         "throughput mode's speed within +-1 LSB of the reference (activations < 65504)")
+    ap.add_argument("--dtype", choices=["fp32", "fp32s", "bf16", "fp16"], default="fp32",
+                    help="fp32 = parity with the reference arithmetic; fp32s = fp32 activations on split-fp16 "
+                         "MFMAs (the same +-1 LSB parity, faster; conv inputs < 65504); bf16 = throughput mode; "
+                         "fp16 = near the throughput mode's speed with 3 more mantissa bits (activations < 65504)")
     ap.add_argument("--synthetic", type=str, default=None, help="WxH: stylize an in-memory synthetic frame stream")
     ap.add_argument("--synthetic_frames", type=int, default=16)
     ap.add_argument("--no_save", action="store_true", help="do not encode/write outputs (throughput runs)")

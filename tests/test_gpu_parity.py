@@ -3,7 +3,7 @@
 Tolerances (north_star): fp32 parity mode within 1e-4 of the reference (relative to the
 output's magnitude) and +-1 LSB on uint8 frames; bf16 throughput mode SSIM >= 0.98 vs the
 CPU reference; fp16 mode (the bf16 kernels with fp16 operands) +-1 LSB on >= 99.9 % of the uint8
-values, never more than 2 LSB.  Integer/byte stages (LAB LUT gathers, EMA truncation, blend truncation) are
+values, never more than 2 LSB; split-fp16 mode (fp32 activations, fp16 hi/lo operand pairs) the fp32 bars.  Integer/byte stages (LAB LUT gathers, EMA truncation, blend truncation) are
 bit-exact.
 """
 import glob
@@ -96,6 +96,8 @@ def test_reconet_frn_ragged_vs_oracle(seed):
     yh = _net("reconet_frn", seed, "fp16")(x.cuda()).cpu().numpy()
     print(f"frn seed {seed}: mean |d| bf16 {np.abs(y16 - ref).mean():.3e}, fp16 {np.abs(yh - ref).mean():.3e}")
     assert np.abs(yh - ref).mean() < 1e-2
+    ys = _net("reconet_frn", seed, "fp32s")(x.cuda()).cpu().numpy()
+    assert np.abs(ys - ref).max() <= FP32_REL_TOL * np.abs(ref).max()
     # the thresholds matter: the same net with tau = 0 is a different function
     sd0 = {k: (torch.zeros_like(v) if k.endswith(".tau") else v) for k, v in sd.items()}
     assert np.abs(O.forward("reconet_frn", sd0, x).numpy() - ref).max() > 1e-2
@@ -111,6 +113,38 @@ def test_1080p_fp32_and_bf16_vs_oracle():
     assert d.max() <= 1 and (d > 0).mean() < 0.01
     out16 = _net("johnson", 0, "bf16").stylize_frames(f_dev, "imagenet_255").cpu().numpy()
     assert O.ssim(out16[0], ref[0]) >= BF16_SSIM_MIN
+
+
+@pytest.mark.parametrize("path", MODEL_GOLDENS, ids=os.path.basename)
+def test_fp32s_vs_reference_golden_and_oracle(path):
+    """Split-fp16 mode (NST_DT_F32S: fp32 activations, every conv operand an fp16 hi/lo pair, two fp16
+    MFMAs per K step) is held to the fp32 parity bars: raw output within 1e-4 of the reference
+    module's golden (relative to its magnitude) and uint8 frames within +-1 LSB of the oracle on
+    < 1 % of values."""
+    z = np.load(path)
+    arch, seed, preset = _arch(path), int(z["seed"]), str(z["preset"])
+    net = _net(arch, seed, "fp32s")
+    y = net(torch.from_numpy(z["x"]).cuda()).cpu().numpy()
+    rel = np.abs(y - z["y"]).max() / np.abs(z["y"]).max()
+    ref = O.stylize_u8(arch, synthetic.make_state_dict(arch, seed), z["frames"], preset)
+    out = net.stylize_frames(torch.from_numpy(z["frames"]).cuda(), preset).cpu().numpy()
+    d = np.abs(out.astype(int) - ref.astype(int))
+    print(f"{os.path.basename(path)} fp32s: raw rel {rel:.3e}, frames max {d.max()} LSB, differ {(d > 0).mean():.5f}")
+    assert rel <= FP32_REL_TOL
+    assert d.max() <= 1 and (d > 0).mean() < 0.01
+
+
+def test_1080p_fp32s_vs_oracle():
+    """configs[1]'s frame in the split-fp16 mode vs the CPU reference (pre-LAB uint8): every value within
+    +-1 LSB (the north_star bar), < 1 % of values off by one -- the fp32 parity mode's bars."""
+    sd = synthetic.make_state_dict("johnson", 0)
+    frames = synthetic.make_frames(1, 1080, 1920, seed=1000)
+    ref = O.stylize_u8("johnson", sd, frames, "imagenet_255")
+    out = _net("johnson", 0, "fp32s").stylize_frames(torch.from_numpy(frames).cuda(), "imagenet_255").cpu().numpy()
+    d = np.abs(out.astype(int) - ref.astype(int))
+    print(f"1080p fp32s: max {d.max()} LSB, values off by one {(d > 0).mean():.6f}, pixels within 1 LSB "
+          f"{(d.max(-1) <= 1).mean():.6f}")
+    assert d.max() <= 1 and (d > 0).mean() < 0.01
 
 
 def test_1080p_fp16_vs_oracle():
