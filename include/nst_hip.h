@@ -44,8 +44,8 @@ extern "C" {
 #define NST_DT_F32 0  /* fp32 "parity" mode: exact-f32 MFMA (v_mfma_f32_16x16x4_f32) */
 #define NST_DT_BF16 1 /* bf16 "throughput" mode: bf16 MFMA, fp32 accumulate/statistics */
 #define NST_DT_F16 2  /* fp16 mode: fp16 weights/activations, fp16 MFMA at the bf16 rate, fp32 accumulate/statistics;
-                         3 more mantissa bits than bf16 = the reference's +-1 LSB uint8 bar.  Stored conv outputs
-                         must stay inside the fp16 range (|v| <= 65504) */
+                         3 more mantissa bits than bf16 (1080p: ~99.95 % of pixels within +-1 LSB of the reference).
+                         Stored conv outputs must stay inside the fp16 range (|v| <= 65504) */
 #define NST_DT_F32S 3 /* split-fp16 mode: fp32 activations in HBM; each conv operand is split into an fp16 pair
                          v = hi + lo in LDS (weights at pack time), and two v_mfma_f32_16x16x32_f16 per K step give
                          Wh*(xh + xl) + Wl*xh: ~22 significant bits per product (the fp32 parity bar) at a quarter of
@@ -270,10 +270,14 @@ int nst_gram(const void* F, int dtype, int layout, int n, int c, int hw, float* 
  * with fp32 accumulation. */
 typedef struct nst_vgg nst_vgg;
 int nst_vgg_create(const nst_param* params, int n_params, int device, nst_vgg** out);
+/* flags: NST_VGG_GENERIC_ONLY runs every conv on the generic implicit-GEMM kernel (conv_vgg.hip) instead of
+ * conv2_1 onward on the K-streaming GEMM conv (conv_gemm.hip) — the same arithmetic in another order */
+#define NST_VGG_GENERIC_ONLY 0x1
+int nst_vgg_create_ex(const nst_param* params, int n_params, int device, unsigned flags, nst_vgg** out);
 void nst_vgg_destroy(nst_vgg* v);
 /* caller-owned device buffers: workspace (activations, gradients, Grams) and state (targets) */
 int nst_gatys_buffer_bytes(const nst_vgg* v, int h, int w, size_t* workspace, size_t* state);
-/* forward only: the pre-activations of relu1_1, relu2_1, relu3_1, relu4_1, relu5_1, relu4_2 (bf16
+/* forward only: the rectified feature maps relu1_1, relu2_1, relu3_1, relu4_1, relu5_1, relu4_2 (bf16
  * NHWC [h_l][w_l][c_l]) into feats[0..5] (NULL entries skipped) */
 int nst_vgg_features(nst_vgg* v, const float* image, int h, int w, void* const* feats, void* workspace,
                      size_t workspace_bytes, void* stream);

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("NST_HIP_LIB", os.path.join(_HERE, "libnst_hip.so"))
 NST_OK = 0
 NST_ARCH_JOHNSON, NST_ARCH_NST, NST_ARCH_RECONET, NST_ARCH_RECONET_FRN = 0, 1, 2, 3
 NST_DT_F32, NST_DT_BF16, NST_DT_F16, NST_DT_F32S = 0, 1, 2, 3
+NST_VGG_GENERIC_ONLY = 0x1
 NST_IO_F32_NCHW, NST_IO_U8_NHWC = 0, 1
 PRESETS = {
     "none": 0,
@@ -35,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "nst_lab_destroy", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
     "nst_profile_end", "nst_num_layers", "nst_layer_name", "nst_blend_models_u8", "nst_blend_models_lab_u8",
     "nst_mask_feather", "nst_create_ex", "nst_num_ops", "nst_op_describe", "nst_forward_capture",
-    "nst_gram_workspace_bytes", "nst_vgg_create", "nst_vgg_destroy", "nst_gatys_buffer_bytes", "nst_vgg_features",
+    "nst_gram_workspace_bytes", "nst_vgg_create", "nst_vgg_create_ex", "nst_vgg_destroy", "nst_gatys_buffer_bytes", "nst_vgg_features",
     "nst_gatys_targets", "nst_gatys_grad", "nst_adam_step", "nst_gatys_grad_capture",
     "nst_seg_create", "nst_seg_destroy", "nst_seg_num_classes", "nst_seg_workspace_bytes", "nst_seg_forward",
     "nst_seg_mask_scratch_bytes", "nst_seg_mask", "nst_resize_create", "nst_resize_destroy",
@@ -122,6 +123,7 @@ def lib() -> ctypes.CDLL:
         L.nst_forward_capture.argtypes = [vp, vp, i, i, i, i, i, vp, i, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(vp),
                                           ctypes.POINTER(vp), vp]
         L.nst_vgg_create.argtypes = [ctypes.POINTER(NstParam), i, i, ctypes.POINTER(vp)]
+        L.nst_vgg_create_ex.argtypes = [ctypes.POINTER(NstParam), i, i, ctypes.c_uint, ctypes.POINTER(vp)]
         L.nst_vgg_destroy.argtypes = [vp]
         L.nst_vgg_destroy.restype = None
         L.nst_gatys_buffer_bytes.argtypes = [vp, i, i, ctypes.POINTER(sz), ctypes.POINTER(sz)]
@@ -206,7 +208,7 @@ def lib() -> ctypes.CDLL:
         L.nst_layer_name.restype = ctypes.c_char_p
         for name in ("nst_seg_create", "nst_seg_num_classes", "nst_seg_workspace_bytes", "nst_seg_forward",
                      "nst_seg_mask_scratch_bytes", "nst_seg_mask", "nst_resize_create", "nst_resize_scratch_bytes",
-                     "nst_resize_u8", "nst_vgg_create", "nst_gatys_buffer_bytes", "nst_vgg_features", "nst_gatys_targets",
+                     "nst_resize_u8", "nst_vgg_create", "nst_vgg_create_ex", "nst_gatys_buffer_bytes", "nst_vgg_features", "nst_gatys_targets",
                      "nst_gatys_grad", "nst_adam_step", "nst_create", "nst_create_ex", "nst_op_describe", "nst_forward_capture", "nst_output_hw", "nst_workspace_bytes", "nst_forward", "nst_decode_resize_u8",
                      "nst_lab_create", "nst_lab_ema_u8", "nst_blend_u8", "nst_gram", "nst_profile_begin",
                      "nst_profile_end"):

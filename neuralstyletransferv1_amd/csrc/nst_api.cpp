@@ -222,13 +222,6 @@ struct nst_lab {
 
 namespace {
 
-uint16_t f32_to_bf16_rne(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
 
 // packed weights -> device, in the layer's compute dtype
 int upload_weights(int dtype, const std::vector<float>& pk, void** dst);

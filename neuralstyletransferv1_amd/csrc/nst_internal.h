@@ -31,6 +31,14 @@ inline uint16_t f32_to_f16_rne(float f) {
   std::memcpy(&af, &a, 4);
   return sign | (uint16_t)std::nearbyint(af * 16777216.0f);
 }
+// bfloat16 of a host float, round to nearest even (NaN stays NaN): weight packing for NST_DT_BF16
+inline uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
 // fp16 bits -> the value (exact)
 inline float f16_to_f32(uint16_t h) {
   const int e = (h >> 10) & 31, m = h & 1023;

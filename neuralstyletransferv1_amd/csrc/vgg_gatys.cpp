@@ -9,9 +9,15 @@
 // restatement (oracle/gatys_oracle.py), not the reference ("parity unpinned").
 //
 // Program (per image, h and w multiples of 16; bf16 activations, fp32 accumulation):
-//   forward: conv1_1 (image -> normalised in the fill) .. conv5_1, the 13 convs the loss needs; each
-//            stores its pre-activation z, the consumer applies the ReLU in its fill (unit IN table)
-//            or reads the 2x2 max-pool of ReLU(z);
+//   forward: conv1_1 (image -> normalised in the fill) .. conv5_1, the 13 convs the loss needs.
+//            Block 1 (512x512-scale maps, 64 channels: thousands of tiles) runs on the generic
+//            implicit-GEMM kernel, which stores the pre-activation z and lets the consumer apply the
+//            ReLU in its fill (unit IN table); conv2_1 .. conv5_1 (128-512 channels on 256^2 .. 32^2
+//            maps: a few hundred tiles, 4.6K-long K) run on the K-streaming GEMM conv of the DeepLab
+//            program (conv_gemm.hip: small LDS stages, 8 waves per CU, split-K below a wave of the chip)
+//            with the ReLU in its epilogue, so they store r = ReLU(z).  Every consumer of a stored map
+//            rectifies it or masks with it (ReLU(r) = r, r > 0 <=> z > 0), so both forms serve the
+//            pools, Grams, content term and backward masks unchanged;
 //   losses:  Grams of ReLU(z) at the 5 style layers (nst_gram, NHWC) vs the style targets, MSE of
 //            ReLU(z4_2) vs the content target;
 //   backward: the same generic conv kernel over the masked output gradient with flipped,
@@ -27,6 +33,7 @@
 
 #include "nst_hip.h"
 #include "nst_internal.h"
+#include "seg_internal.h"
 
 using namespace nst;
 
@@ -51,10 +58,32 @@ const float kMean[3] = {0.485f, 0.456f, 0.406f}, kStd[3] = {0.229f, 0.224f, 0.22
 struct VggConv {
   VggConvDef d;
   int cinp, coutp;
-  const ConvKernelInfo *kf = nullptr, *kb = nullptr;  // forward / input-gradient kernels
+  const ConvKernelInfo *kf = nullptr, *kb = nullptr;  // forward / input-gradient kernels (generic)
   void *wf = nullptr, *wb = nullptr;
   float *bf = nullptr, *bb = nullptr;
+  // conv_gemm.hip path: forward (conv2_1 onward) and input gradient (conv2_1 onward)
+  bool gemm_f = false, gemm_b = false;
+  void *gwf = nullptr, *gwb = nullptr;
+  float *gscale = nullptr, *gshift = nullptr, *gzero = nullptr;
 };
+// the layers on the GEMM conv: every conv whose input has >= 64 channels and whose map is at most a
+// quarter of the image (conv2_1 onward); input gradients of the same layers
+bool vgg_gemm_layer(int i) { return i >= 2; }
+
+// W[cout][cin][3][3] fp32 -> the GEMM conv's bf16 fragments [coutp/64][stage = tap*nck + cc][64 rows][64]
+// (seg_internal.h GemmConvParams::wpk)
+std::vector<uint16_t> pack_gemm(const float* W, int cout, int cin, int coutp) {
+  const int ck = gemm_stage_channels(NST_DT_BF16), nck = cin / ck, nstage = 9 * nck;
+  std::vector<uint16_t> pk((size_t)(coutp / 64) * nstage * 64 * ck, 0);
+  for (int co = 0; co < cout; ++co)
+    for (int ci = 0; ci < cin; ++ci)
+      for (int t = 0; t < 9; ++t) {
+        const int s = t * nck + ci / ck;
+        pk[(((size_t)(co / 64) * nstage + s) * 64 + (co % 64)) * ck + ci % ck] =
+            f32_to_bf16_rne(W[((size_t)co * cin + ci) * 9 + t]);
+      }
+  return pk;
+}
 
 const ConvKernelInfo* find_vgg(int cinp, int bn, int in_kind, int out_kind) {
   int count = 0;
@@ -65,6 +94,12 @@ const ConvKernelInfo* find_vgg(int cinp, int bn, int in_kind, int out_kind) {
 }
 
 size_t al(size_t v) { return (v + 255) / 256 * 256; }
+
+int upload_u16(const std::vector<uint16_t>& h, void** dev) {
+  NST_HIP_CHECK(hipMalloc(dev, h.size() * 2));
+  NST_HIP_CHECK(hipMemcpy(*dev, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  return NST_OK;
+}
 
 }  // namespace
 
@@ -81,9 +116,22 @@ namespace {
 struct VggPlan {
   int h = 0, w = 0;
   int ch[13], cw[13];  // conv output extents
-  size_t z[13], pool[4], ga, gb, gimg, gram[5], M[5], gram_ws, part, raw, losses, end;  // workspace offsets
+  size_t z[13], pool[4], ga, gb, gimg, gram[5], M[5], gram_ws, part, raw, losses, gpart, end;  // workspace offsets
+  size_t gpart_bytes;
   size_t sP, sA[5], send;                                                              // state offsets
 };
+
+// geometry of one 3x3 / pad 1 conv on the GEMM conv (pointers set by the caller)
+GemmConvParams gemm_geom(int cin, int cout, int h, int w) {
+  GemmConvParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.hi = h; p.wi = w; p.cs = cin; p.cin = cin;
+  p.kh = p.kw = 3; p.stride = 1; p.dil = 1; p.pad = 1;
+  p.ho = h; p.wo = w; p.npix = h * w;
+  p.out_cs = cout; p.out_off = 0; p.cout_store = cout;
+  p.ksplit = 1;
+  return p;
+}
 
 VggPlan vgg_plan(int h, int w) {
   VggPlan P;
@@ -115,6 +163,16 @@ VggPlan vgg_plan(int h, int w) {
   P.part = off; off += al(512 * 4);
   P.raw = off; off += al(8 * 4);
   P.losses = off; off += al(4 * 4);
+  // split-K scratch of the GEMM-conv layers (forward and input gradient), the largest one
+  size_t gp = 0;
+  for (int i = 0; i < 13; ++i) {
+    if (!vgg_gemm_layer(i)) continue;
+    GemmConvParams f = gemm_geom(kConvs[i].cin, kConvs[i].cout, P.ch[i], P.cw[i]);
+    GemmConvParams b = gemm_geom(kConvs[i].cout, kConvs[i].cin, P.ch[i], P.cw[i]);
+    gp = std::max(gp, std::max(gemm_partial_bytes(NST_DT_BF16, f), gemm_partial_bytes(NST_DT_BF16, b)));
+  }
+  P.gpart = off; off += al(std::max<size_t>(gp, 256));
+  P.gpart_bytes = gp;
   P.end = off;
   size_t so = 0;
   P.sP = so; so += al((size_t)P.ch[kContent] * P.cw[kContent] * 512 * 2);
@@ -174,7 +232,14 @@ int vgg_forward(nst_vgg* v, const VggPlan& P, const float* image, char* ws, hipS
   const float2* norm = nullptr;
   for (int i = 0; i < 13; ++i) {
     const VggConv& L = v->conv[i];
-    VGG_CHECK(run_conv(L.kf, src, src_kind, P.ch[i], P.cw[i], cs, norm, L.wf, L.bf, L.d.cout, L.coutp, ws + P.z[i], st));
+    if (L.gemm_f) {  // stores r = ReLU(z) (the epilogue's ReLU); the input is a stored r or a pooled map
+      GemmConvParams p = gemm_geom(L.d.cin, L.d.cout, P.ch[i], P.cw[i]);
+      p.in = src; p.wpk = L.gwf; p.scale = L.gscale; p.shift = L.gshift; p.relu = 1; p.out = ws + P.z[i];
+      p.partial = P.gpart_bytes ? (float*)(ws + P.gpart) : nullptr;
+      VGG_CHECK(launch_gemm_conv(NST_DT_BF16, p, st));
+    } else {
+      VGG_CHECK(run_conv(L.kf, src, src_kind, P.ch[i], P.cw[i], cs, norm, L.wf, L.bf, L.d.cout, L.coutp, ws + P.z[i], st));
+    }
     if (L.d.pool_after) {
       VGG_CHECK(launch_vgg_pool(ws + P.z[i], P.ch[i], P.cw[i], L.d.cout, ws + P.pool[pi], st));
       src = ws + P.pool[pi++];
@@ -194,7 +259,15 @@ int vgg_forward(nst_vgg* v, const VggPlan& P, const float* image, char* ws, hipS
 extern "C" {
 
 int nst_vgg_create(const nst_param* params, int n_params, int device, nst_vgg** out) {
-  if (!params || n_params <= 0 || !out) { set_error("nst_vgg_create: invalid arguments"); return NST_E_INVALID; }
+  return nst_vgg_create_ex(params, n_params, device, 0u, out);
+}
+
+int nst_vgg_create_ex(const nst_param* params, int n_params, int device, unsigned flags, nst_vgg** out) {
+  if (!params || n_params <= 0 || !out || (flags & ~(unsigned)NST_VGG_GENERIC_ONLY) != 0) {
+    set_error("nst_vgg_create: invalid arguments");
+    return NST_E_INVALID;
+  }
+  const bool gemm_ok = (flags & NST_VGG_GENERIC_ONLY) == 0;
   *out = nullptr;
   std::map<std::string, const nst_param*> byname;
   for (int i = 0; i < n_params; ++i)
@@ -231,6 +304,18 @@ int nst_vgg_create(const nst_param* params, int n_params, int device, nst_vgg** 
     if ((rc = pack_upload_conv(*L.kf, L.d.cin, L.d.cout, 3, W, L.coutp, &L.wf)) != NST_OK) break;
     if ((rc = pack_upload_conv(*L.kb, L.d.cout, L.d.cin, 3, Wt.data(), bcoutp, &L.wb)) != NST_OK) break;
     if ((rc = upload_floats(itb->second->data, L.d.cout, &L.bf)) != NST_OK) break;
+    if (gemm_ok && vgg_gemm_layer(i)) {
+      L.gemm_f = L.gemm_b = true;
+      const int cpb = (L.d.cin + 127) / 128 * 128;  // input-gradient outputs, padded to the 128-row tile
+      std::vector<uint16_t> pf = pack_gemm(W, L.d.cout, L.d.cin, L.d.cout), pb = pack_gemm(Wt.data(), L.d.cin, L.d.cout, cpb);
+      std::vector<float> one(512, 1.f), zero(512, 0.f), bias(512, 0.f);
+      std::memcpy(bias.data(), itb->second->data, (size_t)L.d.cout * 4);
+      if ((rc = upload_u16(pf, &L.gwf)) != NST_OK) break;
+      if ((rc = upload_u16(pb, &L.gwb)) != NST_OK) break;
+      if ((rc = upload_floats(one.data(), 512, &L.gscale)) != NST_OK) break;
+      if ((rc = upload_floats(bias.data(), 512, &L.gshift)) != NST_OK) break;
+      if ((rc = upload_floats(zero.data(), 512, &L.gzero)) != NST_OK) break;
+    }
   }
   if (rc == NST_OK) {
     std::vector<float> unit(2 * 512), zero(512, 0.f);
@@ -250,6 +335,8 @@ void nst_vgg_destroy(nst_vgg* v) {
     if (L.wf) (void)hipFree(L.wf);
     if (L.wb) (void)hipFree(L.wb);
     if (L.bf) (void)hipFree(L.bf);
+    for (void* q : {L.gwf, L.gwb, (void*)L.gscale, (void*)L.gshift, (void*)L.gzero})
+      if (q) (void)hipFree(q);
   }
   if (v->unit) (void)hipFree(v->unit);
   if (v->zero_bias) (void)hipFree(v->zero_bias);
@@ -280,8 +367,9 @@ int nst_vgg_features(nst_vgg* v, const float* image, int h, int w, void* const* 
   for (int k = 0; k < 6; ++k) {
     if (!feats[k]) continue;
     const int i = which[k];
-    const size_t bytes = (size_t)P.ch[i] * P.cw[i] * kConvs[i].cout * 2;
-    VGG_CHECK(hipMemcpyAsync(feats[k], ws + P.z[i], bytes, hipMemcpyDeviceToDevice, st));
+    // rectified: (z > 0) * z of the stored map (a stored z, or an r = ReLU(z) the GEMM conv wrote)
+    const size_t n = (size_t)P.ch[i] * P.cw[i] * kConvs[i].cout;
+    VGG_CHECK(launch_vgg_relu_bwd(ws + P.z[i], ws + P.z[i], nullptr, 0.f, n, feats[k], st));
   }
   return NST_OK;
 }
@@ -373,8 +461,15 @@ int gatys_grad_impl(nst_vgg* v, const float* image, int h, int w, const float* s
       VGG_CHECK(run_conv(L.kb, gbuf[cur], IN_ACT, P.ch[0], P.cw[0], c, nullptr, L.wb, v->zero_bias, 3, 16, grad, st));
       break;
     }
-    VGG_CHECK(run_conv(L.kb, gbuf[cur], IN_ACT, P.ch[i], P.cw[i], c, nullptr, L.wb, v->zero_bias, L.d.cin, L.d.cin,
-                       gbuf[cur ^ 1], st));
+    if (L.gemm_b) {
+      GemmConvParams p = gemm_geom(L.d.cout, L.d.cin, P.ch[i], P.cw[i]);
+      p.in = gbuf[cur]; p.wpk = L.gwb; p.scale = L.gscale; p.shift = L.gzero; p.relu = 0; p.out = gbuf[cur ^ 1];
+      p.partial = P.gpart_bytes ? (float*)(ws + P.gpart) : nullptr;
+      VGG_CHECK(launch_gemm_conv(NST_DT_BF16, p, st));
+    } else {
+      VGG_CHECK(run_conv(L.kb, gbuf[cur], IN_ACT, P.ch[i], P.cw[i], c, nullptr, L.wb, v->zero_bias, L.d.cin, L.d.cin,
+                         gbuf[cur ^ 1], st));
+    }
     cur ^= 1;
     const VggConv& Lp = v->conv[i - 1];
     ready = Lp.d.pool_after;

@@ -57,7 +57,9 @@ class VGG19Features(nn.Module):
 class Gatys:
     """One VGG-19 handle on one device plus the buffers of an h x w optimisation."""
 
-    def __init__(self, state: Dict[str, torch.Tensor], device: torch.device):
+    def __init__(self, state: Dict[str, torch.Tensor], device: torch.device, generic_only: bool = False):
+        """generic_only: every conv on the generic implicit-GEMM kernel (NST_VGG_GENERIC_ONLY) instead of
+        conv2_1 onward on the K-streaming GEMM conv; the same arithmetic summed in another order."""
         device = torch.device(device)
         if device.type != "cuda":
             raise NstError("the Gatys loop runs on MI355X (cuda) devices only; there is no CPU path")
@@ -73,7 +75,8 @@ class Gatys:
             arr[i].numel = v.numel()
         h = ctypes.c_void_p()
         idx = device.index if device.index is not None else torch.cuda.current_device()
-        check(lib().nst_vgg_create(arr, len(host), idx, ctypes.byref(h)), "nst_vgg_create")
+        flags = _lib.NST_VGG_GENERIC_ONLY if generic_only else 0
+        check(lib().nst_vgg_create_ex(arr, len(host), idx, flags, ctypes.byref(h)), "nst_vgg_create")
         self._h = h
         self._hw: Optional[Tuple[int, int]] = None       # size of the scratch workspace
         self._tgt_hw: Optional[Tuple[int, int]] = None   # size the content / style targets were made for
@@ -115,7 +118,7 @@ class Gatys:
         return x.to(torch.float32).contiguous()
 
     def features(self, image: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """Pre-activation feature maps (bf16, NCHW view of the NHWC buffers) of the 6 loss layers."""
+        """Rectified feature maps relu1_1 .. relu5_1, relu4_2 (bf16, NCHW view of the NHWC buffers)."""
         image = self._image(image)
         _, _, hgt, wid = image.shape
         ws = self._workspace(hgt, wid)
