@@ -60,6 +60,10 @@ def timed(fn, steps):
     return (time.perf_counter() - t0) / steps * 1e3
 
 
+# the mask program's dtype in the configs[4] step: sky_swap.py's default
+MASK_DT = "fp16"
+
+
 def main():
     model = deeplab.DeepLab(num_classes=19)
     model.load_state_dict(deeplab.make_state_dict(19, 0))
@@ -74,17 +78,18 @@ def main():
     out = {"workload": "configs[4]: DeepLab v3+ mask (256-px working size) + Johnson stylization + mask composite, "
                        "1920x1080 batch 8, bf16", "frames_per_step": N}
     res = {}
-    for dtype in ("bf16", "fp32"):
+    for dtype in ("bf16", "fp16", "fp32"):
         me = deeplab.MaskEngine(model, dev, resolution=256, dtype=dtype)
         res[dtype] = timed(lambda: me.masks(frames, ids, feather_px=3), STEPS)
-    me = deeplab.MaskEngine(model, dev, resolution=256, dtype="bf16")
+    me = deeplab.MaskEngine(model, dev, resolution=256, dtype=MASK_DT)
     hw = deeplab.working_size(W, H, 256)
     work = me._resampler("lanczos", H, W, hw[1], hw[0])(frames)
-    seg = model.engine(dev, "bf16")
+    seg = model.engine(dev, MASK_DT)
     fwd_ms = timed(lambda: seg.run(work, logits=False, pred=True), STEPS)
     lanczos_ms = timed(lambda: me._resampler("lanczos", H, W, hw[1], hw[0])(frames), STEPS)
     g_work = deeplab_gflop(hw[1], hw[0]) * N
-    out.update({"mask_ms_bf16": round(res["bf16"], 3), "mask_ms_fp32": round(res["fp32"], 3),
+    out.update({"mask_dtype": MASK_DT, "mask_ms_bf16": round(res["bf16"], 3), "mask_ms_fp16": round(res["fp16"], 3),
+                "mask_ms_fp32": round(res["fp32"], 3),
                 "lanczos_ms": round(lanczos_ms, 3), "deeplab_fwd_ms": round(fwd_ms, 3),
                 "deeplab_gflop_per_batch": round(g_work, 2),
                 "deeplab_tflops_working_size": round(g_work / fwd_ms, 1)})
@@ -102,7 +107,7 @@ def main():
     ms = timed(step, STEPS)
     styl_ms = timed(lambda: eng.stylize_u8(frames, "imagenet_255"), STEPS)
     out.update({"step_ms": round(ms, 3), "frames_per_s": round(N / ms * 1e3, 1), "stylize_ms": round(styl_ms, 3),
-                "mask_share": round(res["bf16"] / ms, 3)})
+                "mask_share": round(res[MASK_DT] / ms, 3)})
     print(json.dumps(out), flush=True)
 
 
