@@ -4,6 +4,29 @@
 #pragma once
 #include "conv_impl.h"
 
+// Tile shapes (TH, TW, WM, WN) of the Johnson/NST layers; overridable at build time for tile sweeps
+#ifndef NST_T32_C1
+#define NST_T32_C1 8, 32, 4, 1
+#endif
+#ifndef NST_T32_C2
+#define NST_T32_C2 4, 16, 4, 1
+#endif
+#ifndef NST_T32_C3
+#define NST_T32_C3 4, 16, 2, 2
+#endif
+#ifndef NST_T32_RES
+#define NST_T32_RES 4, 16, 2, 2
+#endif
+#ifndef NST_T32_D1
+#define NST_T32_D1 4, 16, 1, 4
+#endif
+#ifndef NST_T32_D2
+#define NST_T32_D2 4, 16, 1, 4
+#endif
+#ifndef NST_T32_OUT
+#define NST_T32_OUT 4, 32, 4, 1
+#endif
+
 namespace nst {
 template <typename F>
 const ConvKernelInfo* conv_table_32(int* count) {
@@ -11,15 +34,15 @@ const ConvKernelInfo* conv_table_32(int* count) {
   constexpr int SD = MODE_STD, PH = MODE_PHASE;
   static const ConvKernelInfo table[] = {
       //  T  MODE KS S CINP BN TH TW WM WN  IN           OUT
-      E(F, SD, 9, 1, 4, 32, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
-      E(F, SD, 9, 1, 4, 32, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),
-      E(F, SD, 3, 2, 32, 64, 4, 16, 4, 1, IN_ACT, OUT_ACT),
-      E(F, SD, 3, 2, 64, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(F, SD, 3, 1, 128, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),
-      E(F, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT),
-      E(F, PH, 3, 1, 64, 32, 4, 16, 1, 4, IN_ACT, OUT_ACT),
-      E(F, SD, 9, 1, 32, 16, 4, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
-      E(F, SD, 9, 1, 32, 16, 4, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
+      E(F, SD, 9, 1, 4, 32, NST_T32_C1, IN_U8_NHWC, OUT_ACT),
+      E(F, SD, 9, 1, 4, 32, NST_T32_C1, IN_F32_NCHW, OUT_ACT),
+      E(F, SD, 3, 2, 32, 64, NST_T32_C2, IN_ACT, OUT_ACT),
+      E(F, SD, 3, 2, 64, 128, NST_T32_C3, IN_ACT, OUT_ACT),
+      E(F, SD, 3, 1, 128, 128, NST_T32_RES, IN_ACT, OUT_ACT),
+      E(F, PH, 3, 1, 128, 64, NST_T32_D1, IN_ACT, OUT_ACT),
+      E(F, PH, 3, 1, 64, 32, NST_T32_D2, IN_ACT, OUT_ACT),
+      E(F, SD, 9, 1, 32, 16, NST_T32_OUT, IN_ACT, OUT_U8_NHWC),
+      E(F, SD, 9, 1, 32, 16, NST_T32_OUT, IN_ACT, OUT_F32_NCHW),
       // ReCoNet (48/96/192 channels: multiples of 16, no padding in fp32)
       E(F, SD, 9, 1, 4, 48, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
       E(F, SD, 9, 1, 4, 48, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),
@@ -29,8 +52,8 @@ const ConvKernelInfo* conv_table_32(int* count) {
       E(F, PH, 3, 1, 192, 96, 2, 16, 1, 4, IN_ACT, OUT_ACT),
       E(F, PH, 3, 1, 96, 48, 4, 16, 1, 4, IN_ACT, OUT_ACT),
       // consumers of the residual stream (residual join fused into the fill)
-      E(F, SD, 3, 1, 128, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
-      E(F, PH, 3, 1, 128, 64, 4, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
+      E(F, SD, 3, 1, 128, 128, NST_T32_RES, IN_ACT, OUT_ACT, VAR_RES),
+      E(F, PH, 3, 1, 128, 64, NST_T32_D1, IN_ACT, OUT_ACT, VAR_RES),
       E(F, SD, 3, 1, 192, 192, 4, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
       E(F, PH, 3, 1, 192, 96, 2, 16, 1, 4, IN_ACT, OUT_ACT, VAR_RES),
       E(F, SD, 9, 1, 48, 16, 2, 32, 4, 1, IN_ACT, OUT_U8_NHWC),

@@ -146,7 +146,17 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
             if d["res_out"] >= 0:  # the joined stream the op wrote for its own pixels: bit-exact
                 joined = get_rows(torch.arange(Hs))
                 got = _nchw(host[i]["res"], cin)
-                assert torch.equal(got, joined), f"op {i} ({conv}): joined residual stream differs"
+                if not torch.equal(got, joined):
+                    bad = (got != joined).nonzero()
+                    ex = []
+                    for q in bad[:6].tolist():
+                        b_, c_, y_, x_ = q
+                        ex.append({"at": q, "got": float(got[b_, c_, y_, x_]), "want": float(joined[b_, c_, y_, x_]),
+                                   "y": float(ysrc[b_, c_, y_, x_]), "r": float(r[b_, c_, y_, x_]),
+                                   "ys": ys[b_, c_].tolist(), "rs": None if rs is None else rs[b_, c_].tolist()})
+                    raise AssertionError(f"op {i} ({conv}): joined residual stream differs at {bad.shape[0]} of "
+                                         f"{got.numel()} values (nan got {int(got.isnan().sum())} want "
+                                         f"{int(joined.isnan().sum())}); {ex}")
         final = d["dst"] == -2
         ch = d["conv_h"]
         row_sets = [(0, ch)] if bands is None else sorted({
