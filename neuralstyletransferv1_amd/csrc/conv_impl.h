@@ -120,6 +120,18 @@ __device__ __forceinline__ uint32_t pack16(float lo, float hi) {
     return pack_bf16(lo, hi);
   }
 }
+// pack16 of fp32 values rounded as they are (the generic kernel's fills and epilogue): without the opaque
+// copies hipcc folds a producing fma / add into v_fma_mixlo_f16, which rounds the exact result to fp16 once,
+// so a value whose fp32 rounding lands on an fp16 tie comes out one ulp off the documented
+// fp32-then-fp16 arithmetic (and off the unfused residual kernel)
+template <typename T>
+__device__ __forceinline__ uint32_t pack16p(float lo, float hi) {
+  if constexpr (IS_F16<T>) {
+    asm("" : "+v"(lo));
+    asm("" : "+v"(hi));
+  }
+  return pack16<T>(lo, hi);
+}
 // acc + A x B on v_mfma_f32_16x16x32_{bf16,f16} (builtin form: hipcc allocates the accumulator)
 template <typename T>
 __device__ __forceinline__ f32x4_t mfma16x16x32(const uint4& a, const uint4& b, const f32x4_t& c) {
@@ -156,8 +168,10 @@ constexpr int dtype_code() {
 
 // 4 fp32 channels -> the split LDS chunk [hi0..hi3, lo0..lo3]
 __device__ __forceinline__ uint4 split_chunk(uint4 raw) {
-  const float v[4] = {__uint_as_float(raw.x), __uint_as_float(raw.y), __uint_as_float(raw.z), __uint_as_float(raw.w)};
+  float v[4] = {__uint_as_float(raw.x), __uint_as_float(raw.y), __uint_as_float(raw.z), __uint_as_float(raw.w)};
   _Float16 hi[4], lo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) asm("" : "+v"(v[j]));  // split the fp32 value itself (no v_fma_mixlo_f16 fold)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     hi[j] = (_Float16)v[j];
@@ -184,7 +198,14 @@ struct ConvCfg {
   // of 2*odd chunks puts the 16 lanes of every ds_read_b128 lane group ({0-3,12-15,20-27}, ...:
   // 8 pixels of lane group g and 8 of g^1) on 16 distinct bank slots with no XOR swizzle (pixel
   // parity alternates with g's chunk parity), so operand addresses are lane base + immediates.
-  static constexpr int EB = ((NCH % 4) == 0 ? NCH + 2 : NCH) * 16;               // bytes per LDS entry
+  static constexpr int NXS_ = 5;
+  // (a 4-byte x-shift halo that does not fit with 2 pad chunks takes one: NCH + 1 is odd, 2-way at worst)
+  static constexpr int EB0 = ((NCH % 4) == 0 ? NCH + 2 : NCH) * 16;
+  static constexpr int NENT0 = (MODE == MODE_PHASE ? TH + 2 : (TH - 1) * S + KS) *
+                               (MODE == MODE_XSHIFT ? NXS_ * ((((TW - 1) * S + KS) + NXS_ - 1) / NXS_)
+                                                    : ((S == 2) ? 2 * ((((TW - 1) * S + KS) + 1) / 2)
+                                                                : (MODE == MODE_PHASE ? TW + 2 : (TW - 1) * S + KS)));
+  static constexpr int EB = (NENT0 * EB0 > 150 * 1024 && (NCH % 4) == 0) ? (NCH + 1) * 16 : EB0;  // bytes per LDS entry
   static constexpr int NXS = 5;                                                   // x-shifts (XSHIFT)
   static constexpr int KP = PAIR ? (KS + 1) / 2 : (MODE == MODE_XSHIFT ? KS + NXS - 1 : KS);  // x-taps per row
   static constexpr int NTAP = MODE == MODE_PHASE ? 4 : KS * KP;
@@ -267,7 +288,7 @@ __device__ __forceinline__ uint4 norm_chunk(uint4 raw, const float2* nm) {
       const f32x2_t sc = {nm[2 * j].x, nm[2 * j + 1].x};
       const f32x2_t sh = {nm[2 * j].y, nm[2 * j + 1].y};
       f32x2_t y; y.x = __builtin_fmaf(x.x, sc.x, sh.x); y.y = __builtin_fmaf(x.y, sc.y, sh.y);
-      const i16x2_t r = __builtin_bit_cast(i16x2_t, pack16<T>(y.x, y.y));
+      const i16x2_t r = __builtin_bit_cast(i16x2_t, pack16p<T>(y.x, y.y));
       w[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
@@ -306,7 +327,7 @@ __device__ __forceinline__ uint4 res_chunk(uint4 y, uint4 r, const float2* yn, c
     if (has_rn) {
       // r' = ReLU(IN_r(r)) exactly as a normalising fill stages it (norm_chunk): bf16 of one fma
       if constexpr (sizeof(T) == 2)
-        rr = fmaxf(lo16<T>(pack16<T>(__builtin_fmaf(rr, rn[j].x, rn[j].y), 0.f)), 0.f);
+        rr = fmaxf(lo16<T>(pack16p<T>(__builtin_fmaf(rr, rn[j].x, rn[j].y), 0.f)), 0.f);
       else
         rr = fmaxf(rr * rn[j].x + rn[j].y, 0.f);
     }
@@ -315,7 +336,7 @@ __device__ __forceinline__ uint4 res_chunk(uint4 y, uint4 r, const float2* yn, c
     o[j] = relu_out ? fmaxf(v, 0.f) : v;
   }
   if constexpr (sizeof(T) == 2) {
-    return make_uint4(pack16<T>(o[0], o[1]), pack16<T>(o[2], o[3]), pack16<T>(o[4], o[5]), pack16<T>(o[6], o[7]));
+    return make_uint4(pack16p<T>(o[0], o[1]), pack16p<T>(o[2], o[3]), pack16p<T>(o[4], o[5]), pack16p<T>(o[6], o[7]));
   } else {
     return make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
   }
@@ -1006,10 +1027,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
 #pragma unroll
               for (int h = 0; h < NSUB; h += 2) {
                 if (h + 1 < NSUB) {
-                  *(uint4*)(dst + h * 8) = make_uint4(pack16<T>(v[4 * h], v[4 * h + 1]), pack16<T>(v[4 * h + 2], v[4 * h + 3]),
-                                                      pack16<T>(v[4 * h + 4], v[4 * h + 5]), pack16<T>(v[4 * h + 6], v[4 * h + 7]));
+                  *(uint4*)(dst + h * 8) = make_uint4(pack16p<T>(v[4 * h], v[4 * h + 1]), pack16p<T>(v[4 * h + 2], v[4 * h + 3]),
+                                                      pack16p<T>(v[4 * h + 4], v[4 * h + 5]), pack16p<T>(v[4 * h + 6], v[4 * h + 7]));
                 } else {
-                  *(uint2*)(dst + h * 8) = make_uint2(pack16<T>(v[4 * h], v[4 * h + 1]), pack16<T>(v[4 * h + 2], v[4 * h + 3]));
+                  *(uint2*)(dst + h * 8) = make_uint2(pack16p<T>(v[4 * h], v[4 * h + 1]), pack16p<T>(v[4 * h + 2], v[4 * h + 3]));
                 }
               }
             } else {

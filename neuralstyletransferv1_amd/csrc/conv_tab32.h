@@ -4,7 +4,9 @@
 #pragma once
 #include "conv_impl.h"
 
-// Tile shapes (TH, TW, WM, WN) of the Johnson/NST layers; overridable at build time for tile sweeps
+// Tile shapes (TH, TW, WM, WN) of the Johnson/NST layers; overridable at build time for tile sweeps.
+// Trunk 8x16 tiles on 8 waves (2x4) and 8-row up-conv / output tiles: r03 sweep of the split-fp16 mode
+// (tools/mode_profile.py), 221 -> 297 frames/s over the 4x16-tile shapes the fp32 mode started with
 #ifndef NST_T32_C1
 #define NST_T32_C1 8, 32, 4, 1
 #endif
@@ -15,23 +17,24 @@
 #define NST_T32_C3 4, 16, 2, 2
 #endif
 #ifndef NST_T32_RES
-#define NST_T32_RES 4, 16, 2, 2
+#define NST_T32_RES 8, 16, 2, 4
 #endif
 #ifndef NST_T32_D1
-#define NST_T32_D1 4, 16, 1, 4
+#define NST_T32_D1 8, 16, 1, 4
 #endif
 #ifndef NST_T32_D2
-#define NST_T32_D2 4, 16, 1, 4
+#define NST_T32_D2 8, 16, 1, 4
 #endif
 #ifndef NST_T32_OUT
-#define NST_T32_OUT 4, 32, 4, 1
+#define NST_T32_OUT 8, 32, 4, 1
 #endif
 
 namespace nst {
 template <typename F>
 const ConvKernelInfo* conv_table_32(int* count) {
 #define E(...) ConvInst<__VA_ARGS__>::info()
-  constexpr int SD = MODE_STD, PH = MODE_PHASE;
+  constexpr int SD = MODE_STD, PH = MODE_PHASE, XS = MODE_XSHIFT;
+  (void)XS;
   static const ConvKernelInfo table[] = {
       //  T  MODE KS S CINP BN TH TW WM WN  IN           OUT
       E(F, SD, 9, 1, 4, 32, NST_T32_C1, IN_U8_NHWC, OUT_ACT),
@@ -43,6 +46,10 @@ const ConvKernelInfo* conv_table_32(int* count) {
       E(F, PH, 3, 1, 64, 32, NST_T32_D2, IN_ACT, OUT_ACT),
       E(F, SD, 9, 1, 32, 16, NST_T32_OUT, IN_ACT, OUT_U8_NHWC),
       E(F, SD, 9, 1, 32, 16, NST_T32_OUT, IN_ACT, OUT_F32_NCHW),
+#ifdef NST_T32_XS
+      E(F, XS, 9, 1, 32, 16, NST_T32_XS, IN_ACT, OUT_U8_NHWC),   // output conv, 5 x-shifts x 3 channels per MFMA row block
+      E(F, XS, 9, 1, 32, 16, NST_T32_XS, IN_ACT, OUT_F32_NCHW),
+#endif
       // ReCoNet (48/96/192 channels: multiples of 16, no padding in fp32)
       E(F, SD, 9, 1, 4, 48, 8, 32, 4, 1, IN_U8_NHWC, OUT_ACT),
       E(F, SD, 9, 1, 4, 48, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),

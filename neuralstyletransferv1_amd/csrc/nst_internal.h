@@ -150,10 +150,12 @@ hipError_t launch_vgg_pool(const void* z, int h, int w, int c, void* out, hipStr
 hipError_t launch_vgg_pool_bwd(const void* z, const void* gp, int h, int w, int c, void* gz, hipStream_t st);
 hipError_t launch_vgg_relu_bwd(const void* z, const void* ga, const void* P, float cw, size_t elems, void* gz,
                                hipStream_t st);
-hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, float cw, const float* M, int hw, int c,
+hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, float cw, const void* Mb, int hw, int c,
                                void* gz, hipStream_t st);
-hipError_t launch_vgg_style_delta(const float* G, const float* A, int c, float k, float* M, float* loss_out,
-                                  hipStream_t st);
+// Mb: bf16 [c][c] = k (G - A); loss_out = sum (G - A)^2; parts: VGG_STYLE_PARTS floats of scratch
+constexpr int VGG_STYLE_PARTS = 256;
+hipError_t launch_vgg_style_delta(const float* G, const float* A, int c, float k, void* Mb, float* loss_out,
+                                  float* parts, hipStream_t st);
 int vgg_content_parts(size_t elems);
 hipError_t launch_vgg_losses(const void* z, const void* P, size_t elems, float* part, const float* style_raw,
                              float cscale, const float* sscale, float* losses, hipStream_t st);

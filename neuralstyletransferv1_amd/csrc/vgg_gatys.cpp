@@ -423,7 +423,7 @@ int gatys_grad_impl(nst_vgg* v, const float* image, int h, int w, const float* s
     VGG_CHECK(launch_gram(ws + P.z[i], NST_DT_BF16, 1, 1, c, hw, (float*)(ws + P.gram[l]), ws + P.gram_ws, st, 1));
     const double k = 4.0 * style_weight * wl / ((double)c * c * c * hw);
     VGG_CHECK(launch_vgg_style_delta((const float*)(ws + P.gram[l]), (const float*)(sp + P.sA[l]), c, (float)k,
-                                     (float*)(ws + P.M[l]), (float*)(ws + P.raw) + l, st));
+                                     ws + P.M[l], (float*)(ws + P.raw) + l, (float*)(ws + P.part), st));
     sscale[l] = (float)(style_weight * wl / ((double)c * c));
   }
   const size_t nc = (size_t)P.ch[kContent] * P.cw[kContent] * 512;
@@ -447,7 +447,7 @@ int gatys_grad_impl(nst_vgg* v, const float* image, int h, int w, const float* s
       const void* gin = cur >= 0 ? gbuf[cur] : nullptr;
       const int nxt = cur < 0 ? 0 : cur ^ 1;
       if (si >= 0) {
-        VGG_CHECK(launch_vgg_gram_bwd(ws + P.z[i], gin, Pc, cw, (const float*)(ws + P.M[si]), hw, c, gbuf[nxt], st));
+        VGG_CHECK(launch_vgg_gram_bwd(ws + P.z[i], gin, Pc, cw, ws + P.M[si], hw, c, gbuf[nxt], st));
       } else if (gin || Pc) {
         VGG_CHECK(launch_vgg_relu_bwd(ws + P.z[i], gin, Pc, cw, (size_t)hw * c, gbuf[nxt], st));
       } else {

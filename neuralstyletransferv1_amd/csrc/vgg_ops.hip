@@ -111,11 +111,12 @@ __global__ __launch_bounds__(256) void vgg_relu_bwd_kernel(const uint4* __restri
 // ---- Gram (style) gradient, fused with the ReLU backward and the other gradient terms:
 //   gz[p][i] = z[p][i] > 0 ? ga[p][i] + sum_j ReLU(z[p][j]) M[j][i] + cw * (ReLU(z[p][i]) - P[p][i]) : 0
 // M = 4 beta w_l (G - A) / (c^3 hw), symmetric (so row i of M is column i).  MFMA 16x16x32 bf16:
-// A = 16 pixels x 32 channels of ReLU(z), B = 32 x 16 of M (fp32 rounded to bf16).  Workgroup = 4
+// A = 16 pixels x 32 channels of ReLU(z), B = 32 x 16 of M (bf16, rounded once by vgg_style_delta_kernel).  Workgroup = 4
 // waves = 64 pixels x 64 channels, each wave 16 pixels x 64 channels.
+template <int C>
 __global__ __launch_bounds__(256) void vgg_gram_bwd_kernel(const __bf16* __restrict__ z, const __bf16* __restrict__ ga,
                                                            const __bf16* __restrict__ P, float cw,
-                                                           const float* __restrict__ M, int hw, int c,
+                                                           const __bf16* __restrict__ Mb, int hw,
                                                            __bf16* __restrict__ gz) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int row = lane & 15, g = lane >> 4;
@@ -125,17 +126,18 @@ __global__ __launch_bounds__(256) void vgg_gram_bwd_kernel(const __bf16* __restr
   f32x4_t acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < c; k += 32) {
+  // the whole K loop unrolled (C / 32 steps): every step's loads are independent of the MFMAs, so they
+  // issue ahead of them instead of one load latency per step
+#pragma unroll
+  for (int k = 0; k < C; k += 32) {
     float f[8];
-    unpack8(*(const uint4*)(z + (size_t)pa * c + k + 8 * g), f);
+    unpack8(*(const uint4*)(z + (size_t)pa * C + k + 8 * g), f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
     const uint4 a = pack8(f);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float* mr = M + (size_t)(i0 + 16 * t + row) * c + k + 8 * g;
-      const float4 m0 = *(const float4*)mr, m1 = *(const float4*)(mr + 4);
-      const uint4 b = make_uint4(bf_pack(m0.x, m0.y), bf_pack(m0.z, m0.w), bf_pack(m1.x, m1.y), bf_pack(m1.z, m1.w));
+      const uint4 b = *(const uint4*)(Mb + (size_t)(i0 + 16 * t + row) * C + k + 8 * g);
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
                                                        acc[t], 0, 0, 0);
     }
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(256) void vgg_gram_bwd_kernel(const __bf16* __restr
     for (int r = 0; r < 4; ++r) {
       const int p = p0 + 4 * g + r;
       if (p >= hw) continue;
-      const size_t o = (size_t)p * c + ch;
+      const size_t o = (size_t)p * C + ch;
       const float zv = (float)z[o];
       float v = acc[t][r];
       if (ga) v = v + (float)ga[o];
@@ -158,24 +160,39 @@ __global__ __launch_bounds__(256) void vgg_gram_bwd_kernel(const __bf16* __restr
   }
 }
 
-// ---- style delta + loss: M = k (G - A), loss_out = sum (G - A)^2 (one workgroup, fixed order) ----
-__global__ __launch_bounds__(1024) void vgg_style_delta_kernel(const float* __restrict__ G, const float* __restrict__ A,
-                                                               int cc, float k, float* __restrict__ M,
-                                                               float* __restrict__ loss_out) {
-  __shared__ float red[1024];
+// ---- style delta + loss: Mb = bf16(k (G - A)) (the gram-gradient GEMM's operand), per-block partial sums of
+// (G - A)^2, then one block adds the partials in block order (fixed order: deterministic) ----
+__global__ __launch_bounds__(256) void vgg_style_delta_kernel(const float* __restrict__ G, const float* __restrict__ A,
+                                                               int cc, float k, __bf16* __restrict__ Mb,
+                                                               float* __restrict__ part) {
+  __shared__ float red[256];
   float s = 0.f;
-  for (int i = threadIdx.x; i < cc; i += 1024) {
-    const float d = G[i] - A[i];
-    M[i] = k * d;
-    s = s + d * d;
+  for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < cc; i += gridDim.x * 256 * 4) {
+    const float4 gv = *(const float4*)(G + i), av = *(const float4*)(A + i);
+    const float d[4] = {gv.x - av.x, gv.y - av.y, gv.z - av.z, gv.w - av.w};
+    *(uint2*)(Mb + i) = make_uint2(bf_pack(k * d[0], k * d[1]), bf_pack(k * d[2], k * d[3]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s = s + d[j] * d[j];
   }
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int w = 512; w > 0; w >>= 1) {
+  for (int w = 128; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *loss_out = red[0];
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ __launch_bounds__(256) void vgg_sum_parts_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s = s + part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0];
 }
 
 // ---- content loss: partial sums of (ReLU(z) - P)^2 per block, then one block sums them ----
@@ -268,15 +285,28 @@ hipError_t launch_vgg_relu_bwd(const void* z, const void* ga, const void* P, flo
                      (const uint4*)ga, (const uint4*)P, cw, n, (uint4*)gz);
   return hipGetLastError();
 }
-hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, float cw, const float* M, int hw, int c,
+hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, float cw, const void* Mb, int hw, int c,
                                void* gz, hipStream_t st) {
-  hipLaunchKernelGGL(vgg_gram_bwd_kernel, dim3((unsigned)((hw + 63) / 64), (unsigned)(c / 64)), dim3(256), 0, st,
-                     (const __bf16*)z, (const __bf16*)ga, (const __bf16*)P, cw, M, hw, c, (__bf16*)gz);
+  const dim3 grid((unsigned)((hw + 63) / 64), (unsigned)(c / 64));
+  const __bf16 *zz = (const __bf16*)z, *gg = (const __bf16*)ga, *pp = (const __bf16*)P, *mm = (const __bf16*)Mb;
+  __bf16* out = (__bf16*)gz;
+  switch (c) {
+    case 64: hipLaunchKernelGGL(vgg_gram_bwd_kernel<64>, grid, dim3(256), 0, st, zz, gg, pp, cw, mm, hw, out); break;
+    case 128: hipLaunchKernelGGL(vgg_gram_bwd_kernel<128>, grid, dim3(256), 0, st, zz, gg, pp, cw, mm, hw, out); break;
+    case 256: hipLaunchKernelGGL(vgg_gram_bwd_kernel<256>, grid, dim3(256), 0, st, zz, gg, pp, cw, mm, hw, out); break;
+    case 512: hipLaunchKernelGGL(vgg_gram_bwd_kernel<512>, grid, dim3(256), 0, st, zz, gg, pp, cw, mm, hw, out); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
-hipError_t launch_vgg_style_delta(const float* G, const float* A, int c, float k, float* M, float* loss_out,
-                                  hipStream_t st) {
-  hipLaunchKernelGGL(vgg_style_delta_kernel, dim3(1), dim3(1024), 0, st, G, A, c * c, k, M, loss_out);
+// parts: scratch of VGG_STYLE_PARTS floats
+hipError_t launch_vgg_style_delta(const float* G, const float* A, int c, float k, void* Mb, float* loss_out,
+                                  float* parts, hipStream_t st) {
+  const int cc = c * c;
+  if (cc % 4 != 0) return hipErrorInvalidValue;
+  const int nb = std::min(VGG_STYLE_PARTS, (cc / 4 + 255) / 256);
+  hipLaunchKernelGGL(vgg_style_delta_kernel, dim3((unsigned)nb), dim3(256), 0, st, G, A, cc, k, (__bf16*)Mb, parts);
+  hipLaunchKernelGGL(vgg_sum_parts_kernel, dim3(1), dim3(256), 0, st, parts, nb, loss_out);
   return hipGetLastError();
 }
 int vgg_content_parts(size_t elems) { return (int)std::min<size_t>(512, (elems / 8 + 255) / 256); }

@@ -71,6 +71,26 @@ def test_fuse_and_motion_alpha_vs_restatement():
     assert np.abs(a - FO.motion_alpha(flow, 0.9)).max() <= 2e-6
 
 
+def test_fuse_non_finite_and_huge_flow():
+    """A degenerate flow (NaN, +-inf, 1e30) must not index outside the previous frame: the remap coordinates
+    are clamped to [-2w, 3w] x [-2h, 3h] before the 1/32-pixel fixed point (cv2's saturate_cast), NaN taken
+    to the low end; the output stays finite and equals the restatement."""
+    rng = np.random.default_rng(6)
+    h, w = 40, 56
+    cur = rng.random((3, h, w)).astype(np.float32)
+    prev = rng.random((3, h, w)).astype(np.float32)
+    flow = (rng.random((h, w, 2)).astype(np.float32) - 0.5) * 6
+    flow[3, 5] = np.nan
+    flow[7, 9, 0] = np.inf
+    flow[8, 10, 1] = -np.inf
+    flow[11, 12] = 1e30
+    flow[13, 14] = -1e30
+    got = T.fuse(torch.from_numpy(cur).to(DEV), torch.from_numpy(prev).to(DEV), torch.from_numpy(flow).to(DEV), 0.7)
+    got = got.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert np.abs(got - FO.fuse(cur, prev, flow, 0.7)).max() <= 2e-6
+
+
 def test_cli_flow_ema_motion_blend_vs_oracle(tmp_path):
     """pipeline.py:1884-2094 per frame: model -> out01 -> flow EMA (Farneback on Pillow luma) -> ToPILImage ->
     LAB EMA -> motion-adaptive blend with the original (--blend 0.9), fp32."""

@@ -449,3 +449,17 @@ def test_weight_stationary_image_conv_vs_generic(arch, h, w):
     d = np.abs(a.astype(int) - b.astype(int))
     assert d.mean() < 0.5 and (d > 2).mean() < 0.01, (d.mean(), (d > 2).mean(), d.max())
     assert np.abs(ya - yb).max() <= 3e-2 * np.abs(yb).max(), np.abs(ya - yb).max() / np.abs(yb).max()
+
+
+def test_frame_beyond_32bit_offsets_rejected_before_launch():
+    """The buffer-resource kernels address one frame with 32-bit offsets: nst_workspace_bytes (make_plan)
+    rejects a frame whose activation exceeds that budget with NST_E_SHAPE instead of launching a layer that
+    would silently skip its work; 1080p and 4K plan normally."""
+    import ctypes
+    from neuralstyletransferv1_amd._lib import lib
+    eng = _net("johnson", 0, "bf16").engine()
+    need = ctypes.c_size_t()
+    assert lib().nst_workspace_bytes(eng._h, 8, 2160, 3840, ctypes.byref(need)) == 0 and need.value > 0
+    rc = lib().nst_workspace_bytes(eng._h, 1, 8192, 16384, ctypes.byref(need))
+    assert rc == -3, rc  # NST_E_SHAPE
+    assert b"too large" in lib().nst_last_error()
