@@ -15,7 +15,28 @@ import re
 import sys
 
 
+_TARG = {"DF16b": "bf16", "DF16_": "fp16", "f": "float"}
+
+
+def pretty(k):
+    """hipcc leaves the _Float16/__bf16 template kernels mangled in the trace: _ZN3nst12wstat_kernelIDF16bLi8ELi0ELb0ELb0EE...
+    -> 'nst::wstat_kernel<bf16, 8, 0, false, false>'"""
+    m = re.match(r"_ZN3nst(\d+)(\w+?)I((?:DF16b|DF16_|f|Li-?\d+E|Lb[01]E)+)EEvNS_10ConvParamsE", k)
+    if not m or len(m.group(2)) != int(m.group(1)):
+        return k
+    args = []
+    for a in re.findall(r"DF16b|DF16_|f(?!\w)|Li-?\d+E|Lb[01]E|f", m.group(3)):
+        if a in _TARG:
+            args.append(_TARG[a])
+        elif a.startswith("Li"):
+            args.append(a[2:-1])
+        else:
+            args.append("true" if a[2] == "1" else "false")
+    return f"nst::{m.group(2)}<{', '.join(args)}>"
+
+
 def short(k):
+    k = pretty(k)
     m = re.search(r"conv_kernelI(DF16b|f)Li(\d)ELi(\d)ELi(\d)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)E", k)
     if m:
         t, mode, ks, s, ci, bn, th, tw, wm, wn, ink, outk, var = m.groups()
@@ -30,11 +51,11 @@ def load(d):
     dur = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "stats", "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            dur[pretty(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     ctr = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            ctr[r["Kernel_Name"]][r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+            ctr[pretty(r["Kernel_Name"])][r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
     return dur, ctr
 
 
@@ -65,7 +86,7 @@ def main():
     if "--res-json" in sys.argv:  # the dominant kernel's summary bench.py reads (keyed by the library build)
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from neuralstyletransferv1_amd._lib import trunk_kernel_sha
-        key = next(k for k in out if "wstat_kernel<8, 0," in k)
+        key = next(k for k in out if "wstat_kernel<bf16, 8, 0, false, false>" in k or "wstat_kernel<8, 0," in k)
         r = out[key]
         res = {
             "source": f"tools/prof_pass.sh {os.path.basename(d.rstrip('/'))} (rocprofv3 --kernel-trace --stats, then "
