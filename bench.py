@@ -306,7 +306,7 @@ def main():
     # HBM traffic of the dominant kernel from the rocprofv3 PMC pass of this same kernel build
     # (tools/prof_pass.sh + tools/pmc_summary.py write it keyed by the hash of the kernel's sources and
     # build flags, _lib.TRUNK_KERNEL_SOURCES); a summary of another version of the kernel is not used
-    traffic, traffic_note = None, "no PMC summary for this kernel build"
+    traffic, traffic_note, prof_us, prof_joined_us = None, "no PMC summary for this kernel build", None, None
     pmc_path = os.path.join(REPO, "profiles", "pmc_res_conv.json")
     if os.path.exists(pmc_path) and (H, W) == (1080, 1920):
         try:
@@ -314,6 +314,8 @@ def main():
                 pm = json.load(f)
             if pm.get("kernel_src_sha16") == _kernel_sha():
                 traffic, traffic_note = pm.get("hbm_bytes_per_launch"), pm.get("source")
+                prof_us = pm.get("avg_us_profiled")
+                prof_joined_us = (pm.get("joined") or {}).get("avg_us_profiled")
             else:
                 traffic_note = f"PMC summary is of kernel sources {pm.get('kernel_src_sha16')}, not this build"
         except Exception as e:  # noqa: BLE001
@@ -359,7 +361,14 @@ def main():
             "measured_peak": measured,
             "frac_of_measured_peak": (round(achieved_tflops / measured["mfma_tflops"], 4)
                                       if (achieved_tflops and measured) else None),
+            # the same kernel build's rocprofv3 --kernel-trace average (profiles/pmc_res_conv.json; profiled runs
+            # clock a few % lower than this un-profiled pass), so the fraction reproduces from the kept summary
+            "rocprof_avg_launch_ms": round(prof_us / 1e3, 4) if prof_us else None,
+            "rocprof_frac": round(res_flop / (prof_us * 1e-6) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4) if prof_us else None,
             "joined": {
+                "rocprof_avg_launch_ms": round(prof_joined_us / 1e3, 4) if prof_joined_us else None,
+                "rocprof_frac": (round(res_flop / (prof_joined_us * 1e-6) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4)
+                                 if prof_joined_us else None),
                 "kernel": "wstat_kernel<8, WF_RES> (the same conv with the residual join in its fill, 4 launches/step)",
                 "avg_launch_ms": round(joined_avg_ms, 4),
                 "achieved": round(res_flop / (joined_avg_ms * 1e-3) / 1e12, 2) if joined_avg_ms else None,

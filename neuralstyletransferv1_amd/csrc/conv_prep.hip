@@ -9,6 +9,8 @@
 // identity coordinate map.  Arithmetic per element is the reference's: x01 = byte / 255 (ToTensor),
 // ((x01 * a) - b) / d, one RNE rounding to the 16-bit format — bit-identical to the fused encode it replaces
 // (for uint8 frames through a per-block table of the 3 x 256 possible values).
+#include <algorithm>
+
 #include "conv_impl.h"
 
 namespace nst {
@@ -19,6 +21,11 @@ __global__ __launch_bounds__(256) void prepad_encode_f32_kernel(ConvParams p, in
   const int x = blockIdx.x * blockDim.x + threadIdx.x;
   const int y = blockIdx.y, n = blockIdx.z;
   if (x >= wp) return;
+  if (n == (int)gridDim.z - 1) {  // the slice after the last frame: zeroed slack (prepad_slack_rows)
+    if (y < prepad_slack_rows(wp)) out[((size_t)n * hp + y) * wp + x] = make_uint2(0u, 0u);
+    return;
+  }
+  if (y >= hp) return;
   const int sy = map_axis(y - p.pad, p.hs, p.axis_mode, p.pre);
   const int sx = map_axis(x - p.pad, p.ws, p.axis_mode, p.pre);
   float v[3] = {0.f, 0.f, 0.f};
@@ -51,6 +58,12 @@ __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int
   const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * PREP_PX;
   const int n = blockIdx.z;
   if (x0 >= wp) return;
+  if (n == (int)gridDim.z - 1) {  // the slice after the last frame: zeroed slack (prepad_slack_rows)
+    const int ye = min(prepad_slack_rows(wp), (int)(blockIdx.y + 1) * PREP_ROWS);
+    for (int y = blockIdx.y * PREP_ROWS; y < ye; ++y)
+      for (int j = 0; j < PREP_PX && x0 + j < wp; ++j) ((uint2*)out)[((size_t)n * hp + y) * wp + x0 + j] = make_uint2(0u, 0u);
+    return;
+  }
   // the 4 source columns of this thread (same for every row): consecutive and dword-aligned in the
   // interior, so the 12 bytes come as 3 dword loads; reflected / padded edges take byte loads
   int sxs[PREP_PX];
@@ -99,11 +112,13 @@ __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int
 template <typename T>
 hipError_t launch_prepad(const ConvParams& p, int in_kind, int n, int hp, int wp, void* out, hipStream_t st) {
   if (in_kind == IN_U8_NHWC) {
-    const dim3 grid((unsigned)((wp + 256 * PREP_PX - 1) / (256 * PREP_PX)), (unsigned)((hp + PREP_ROWS - 1) / PREP_ROWS),
-                    (unsigned)n);
+    // z = n: the zeroed slack after the last frame
+    const int rows = std::max(hp, prepad_slack_rows(wp));
+    const dim3 grid((unsigned)((wp + 256 * PREP_PX - 1) / (256 * PREP_PX)), (unsigned)((rows + PREP_ROWS - 1) / PREP_ROWS),
+                    (unsigned)n + 1);
     hipLaunchKernelGGL(prepad_encode_u8_kernel<T>, grid, dim3(256), 0, st, p, hp, wp, (uint4*)out);
   } else {
-    const dim3 grid((unsigned)((wp + 255) / 256), (unsigned)hp, (unsigned)n);
+    const dim3 grid((unsigned)((wp + 255) / 256), (unsigned)std::max(hp, prepad_slack_rows(wp)), (unsigned)n + 1);
     hipLaunchKernelGGL(prepad_encode_f32_kernel<T>, grid, dim3(256), 0, st, p, hp, wp, (uint2*)out);
   }
   return hipGetLastError();

@@ -562,10 +562,10 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         return P;
       }
       if (op.src == B_IMG && Ly.prepad) {  // bf16 x4 per pixel over the conv's padded input extent
-        // + tail slack: the 9x9 kernel's last tile row reads up to 16 halo rows (and a row of column
-        // wrap) from its tile origin, which may lie past the last frame's padded extent
+        // + zeroed tail slack (prepad_slack_rows): the 9x9 kernel's last tile row reads up to 16 halo rows
+        // (and a pixel of column wrap) from its tile origin, which may lie past the last frame's padded extent
         const int wpad = cw + Ly.d.ks - 1;
-        const size_t pb = (size_t)n * (ch + Ly.d.ks - 1) * wpad * 8 + (size_t)18 * wpad * 8 + 8192;
+        const size_t pb = ((size_t)n * (ch + Ly.d.ks - 1) + prepad_slack_rows(wpad)) * wpad * 8;
         if (pb > P.pre_bytes) P.pre_bytes = pb;
       }
       if (op.res_out >= 0) {  // the joined residual stream: same geometry as the conv input
@@ -996,18 +996,23 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       off += align256((size_t)n * h->layers[li].coutp * 8);
     }
   }
-  for (size_t i = 0; i < h->prog.size(); ++i) {
+  // run op i over frames f0 .. f0 + n - 1 (every activation buffer holds its frames contiguously at the
+  // op's shape, every IN table is [frame][channel])
+  auto run_op = [&](size_t i, int f0, int n) -> int {
     const Op& op = h->prog[i];
     const Layer& Ly = h->layers[op.layer];
+    const size_t in_fb = (size_t)P.ih[i] * P.iw[i] * Ly.cinp * esz, out_fb = (size_t)P.oh[i] * P.ow[i] * Ly.coutp * esz;
+    auto buf_in = [&](int b) { return (void*)((char*)bufs[b] + f0 * in_fb); };
+    auto buf_out = [&](int b) { return (void*)((char*)bufs[b] + f0 * out_fb); };
+    auto tab = [&](int layer) { return layer >= 0 ? stats[layer] + (size_t)f0 * h->layers[layer].coutp : nullptr; };
     if (op.kind == OP_RESADD) {
       const int hw = P.oh[i] * P.ow[i];
-      hipError_t e = launch_residual(h->dtype, bufs[op.src], stats[op.layer], bufs[op.r_buf],
-                                     op.r_norm >= 0 ? stats[op.r_norm] : nullptr, op.r_relu, op.relu_out,
-                                     bufs[op.dst], n, hw, Ly.coutp, st);
+      hipError_t e = launch_residual(h->dtype, buf_out(op.src), tab(op.layer), buf_out(op.r_buf), tab(op.r_norm), op.r_relu,
+                                     op.relu_out, buf_out(op.dst), n, hw, Ly.coutp, st);
       if (e != hipSuccess) { set_error(std::string("residual launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
       if (cap && cap->act && cap->act[i])
         NST_HIP_CHECK(hipMemcpyAsync(cap->act[i], bufs[op.dst], (size_t)n * hw * Ly.coutp * esz, hipMemcpyDeviceToDevice, st));
-      continue;
+      return NST_OK;
     }
     const bool image_in = op.src == B_IMG, final_out = op.dst == B_OUT;
     const ConvKernelInfo* k = Ly.k_main;
@@ -1015,7 +1020,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     if (final_out && y_fmt == NST_IO_F32_NCHW) k = Ly.k_alt;
     ConvParams p;
     std::memset(&p, 0, sizeof(p));
-    p.in = image_in ? x : bufs[op.src];
+    p.in = image_in ? x : buf_in(op.src);
     p.hs = P.ih[i];
     p.ws = P.iw[i];
     p.cs = image_in ? 3 : Ly.cinp;
@@ -1030,14 +1035,14 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       p.ph_off[1] = 1;
     }
     p.pre = Ly.d.pre;
-    p.in_norm = op.in_norm >= 0 ? stats[op.in_norm] : nullptr;
+    p.in_norm = tab(op.in_norm);
     p.in_relu = op.in_norm >= 0 && op.res_buf < 0 ? 1 : 0;
     if (op.res_buf >= 0) {
-      p.res_r = bufs[op.res_buf];
-      p.res_rnorm = op.r_norm >= 0 ? stats[op.r_norm] : nullptr;
+      p.res_r = buf_in(op.res_buf);
+      p.res_rnorm = tab(op.r_norm);
       p.res_relu = op.relu_out;
     }
-    p.res_out = op.res_out >= 0 ? bufs[op.res_out] : nullptr;
+    p.res_out = op.res_out >= 0 ? buf_in(op.res_out) : nullptr;
     for (int c = 0; c < 3; ++c) {
       p.enc_a[c] = pc.ea[c]; p.enc_b[c] = pc.eb[c]; p.enc_d[c] = pc.ed[c]; p.enc_perm[c] = pc.eperm[c];
       p.dec_p[c] = pc.dp[c]; p.dec_q[c] = pc.dq[c]; p.dec_r[c] = pc.dr[c]; p.dec_s[c] = pc.ds[c]; p.dec_perm[c] = pc.dperm[c];
@@ -1073,7 +1078,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     p.ow = P.ow[i];
     p.crop_y = (P.ch[i] - P.oh[i]) / 2;
     p.crop_x = (P.cw[i] - P.ow[i]) / 2;
-    p.out = final_out ? y : bufs[op.dst];
+    p.out = final_out ? y : buf_out(op.dst);
     p.cout_real = Ly.d.cout;
     p.cout_stride = Ly.coutp;
     tile_grid(*k, p.hs, p.ws, p.oh, p.ow, &p.tiles_x, &p.tiles_y);
@@ -1120,7 +1125,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     if (e != hipSuccess) { set_error("conv " + Ly.d.conv + " launch: " + hipGetErrorString(e)); return NST_E_HIP; }
     if (!final_out) {
       e = launch_in_finalize(partial, n, p.tiles_x * p.tiles_y * k->part_rows, Ly.coutp, (double)p.hconv * (double)p.wconv,
-                             Ly.gamma, Ly.beta, Ly.eps, Ly.frn, stats[op.layer], ws + P.off_seg, st);
+                             Ly.gamma, Ly.beta, Ly.eps, Ly.frn, tab(op.layer), ws + P.off_seg, st);
       if (e != hipSuccess) { set_error(std::string("finalize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
     }
     if (cap && !final_out) {
@@ -1133,6 +1138,11 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       if (cap->stats && cap->stats[i])
         NST_HIP_CHECK(hipMemcpyAsync(cap->stats[i], stats[op.layer], (size_t)n * Ly.coutp * 8, hipMemcpyDeviceToDevice, st));
     }
+    return NST_OK;
+  };
+  for (size_t i = 0; i < h->prog.size(); ++i) {
+    const int rc = run_op(i, 0, n);
+    if (rc != NST_OK) return rc;
   }
   return NST_OK;
 }

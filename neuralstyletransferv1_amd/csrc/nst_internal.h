@@ -188,6 +188,11 @@ hipError_t launch_lab_blend(const uint32_t* rgb2lab, const uint32_t* lab2rgb, co
                             hipStream_t st);
 hipError_t launch_mask_feather(const uint8_t* m, int n, int h, int w, float sigma, float* tmp, float* alpha,
                                hipStream_t st);
+// rows of zeroed slack after the last frame of the pre-padded input: the 9x9 kernels' last tile rows read up
+// to 16 halo rows past a frame's padded extent and a pair-chunk read wraps one pixel into the next row, so
+// every byte such a read can reach after the last frame is written (zero) by the prepad launch — a stale
+// NaN there would otherwise reach the MFMA through a zero weight (0 * NaN = NaN)
+__host__ __device__ inline int prepad_slack_rows(int wp) { return 18 + (1024 + wp - 1) / wp; }
 hipError_t launch_prepad_encode(int dtype, const ConvParams& p, int in_kind, int n, int hp, int wp, void* out,
                                 hipStream_t st);
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,

@@ -92,11 +92,65 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restr
   out[(size_t)n * cstride + c] = make_float2((float)scale, (float)((double)beta[c] - mean * scale));
 }
 
+// One-launch form for layers with few tiles per frame (the 270x480 trunk: ~1k): grid (n, cstride/16), block
+// 1024 = 16 channels x 64 tile phases, each thread sums tiles phase, phase + 64, ... in fp64 (<= 32 loads,
+// all in flight), then a fixed-order LDS tree over the 64 phases and the finalize.  Deterministic; half
+// the launches of the two-stage form, whose second launch is pure latency at this size.
+constexpr int IN_ONE_PH = 64, IN_ONE_CH = 16, IN_ONE_MAX_TILES = 2048;
+__global__ __launch_bounds__(1024) void in_stats_kernel(const float* __restrict__ partial, int tiles, int cstride,
+                                                        double count, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps, int frn,
+                                                        float2* __restrict__ out) {
+  __shared__ double red[IN_ONE_PH][IN_ONE_CH][2];
+  const int n = blockIdx.x;
+  const int cl = threadIdx.x & (IN_ONE_CH - 1), q = threadIdx.x / IN_ONE_CH;
+  const int c = blockIdx.y * IN_ONE_CH + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < cstride) {
+    const float2* p = (const float2*)partial + (size_t)n * tiles * cstride + c;
+    float2 v[IN_ONE_MAX_TILES / IN_ONE_PH];
+#pragma unroll
+    for (int k = 0; k < IN_ONE_MAX_TILES / IN_ONE_PH; ++k) {
+      const int t = q + k * IN_ONE_PH;
+      v[k] = t < tiles ? p[(size_t)t * cstride] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < IN_ONE_MAX_TILES / IN_ONE_PH; ++k) {
+      s1 += (double)v[k].x;
+      s2 += (double)v[k].y;
+    }
+  }
+  red[q][cl][0] = s1;
+  red[q][cl][1] = s2;
+  __syncthreads();
+  for (int h = IN_ONE_PH / 2; h >= 1; h >>= 1) {
+    if (q < h) {
+      red[q][cl][0] += red[q + h][cl][0];
+      red[q][cl][1] += red[q + h][cl][1];
+    }
+    __syncthreads();
+  }
+  if (q != 0 || c >= cstride) return;
+  s1 = red[0][cl][0];
+  s2 = red[0][cl][1];
+  const double mean = frn ? 0.0 : s1 / count;  // FRN: mean(x^2) only (frn.py:71-74)
+  double var = s2 / count - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  const double rstd = 1.0 / sqrt(var + (double)eps);
+  const double scale = (double)gamma[c] * rstd;
+  out[(size_t)n * cstride + c] = make_float2((float)scale, (float)((double)beta[c] - mean * scale));
+}
+
 int in_finalize_segments(int tiles) { return max(1, min(IN_MAX_SEGMENTS, tiles / 64)); }
 
 hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
                               const float* gamma, const float* beta, float eps, int frn, float2* out,
                               void* seg_ws, hipStream_t st) {
+  if (tiles <= IN_ONE_MAX_TILES) {
+    hipLaunchKernelGGL(in_stats_kernel, dim3(n, (cstride + IN_ONE_CH - 1) / IN_ONE_CH), dim3(1024), 0, st, partial,
+                       tiles, cstride, count, gamma, beta, eps, frn, out);
+    return hipGetLastError();
+  }
   const int nseg = in_finalize_segments(tiles);
   const int per_seg = (tiles + nseg - 1) / nseg;
   hipLaunchKernelGGL(in_partial_reduce_kernel, dim3(n, (cstride + 63) / 64, nseg), dim3(256), 0, st, partial,

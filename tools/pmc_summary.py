@@ -103,6 +103,11 @@ def main():
             "mfma_insts_per_launch": r.get("SQ_INSTS_MFMA"),
             "algorithmic_bytes_per_launch": 530841600,
         }
+        jk = next((k for k in out if "wstat_kernel<bf16, 8, 2, false, false>" in k), None)
+        if jk is not None:  # the joined variant (residual join in the fill), same PMC passes
+            j = out[jk]
+            res["joined"] = {"kernel": jk, "avg_us_profiled": j.get("avg_us"), "hbm_bytes_per_launch": j.get("hbm_bytes"),
+                             "eff_clock_ghz": j.get("eff_clock_ghz"), "algorithmic_bytes_per_launch": 2 * 530841600}
         with open(sys.argv[sys.argv.index("--res-json") + 1], "w") as f:
             json.dump(res, f, indent=1)
 
