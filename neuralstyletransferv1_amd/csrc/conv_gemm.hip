@@ -23,6 +23,7 @@
 
 #include <algorithm>
 
+#include "conv_ws_common.h"
 #include "nst_hip.h"
 #include "seg_internal.h"
 
@@ -212,6 +213,168 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
   }
 }
 
+// ---- LDS-DMA form (bf16 / fp16): 128 x BN tiles, 8 waves, one workgroup per CU ----
+// The register-staged kernel above keeps one stage in flight and spends VGPRs and ds_writes on the staging; here
+// every stage lands in LDS by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPR destination, zero for any offset past
+// the buffer = the im2col's zero padding) into a 3-slot ring, two stages ahead of the MFMAs, with counted vmcnt
+// waits and one raw barrier per stage (MI355X_MICROARCH / cdna_hip_programming 'glds ... 3 LDS buffers').
+//   * LDS image of a stage: rows (A: 128 output channels, B: BN pixels) x 128 B, lane-linear per DMA
+//     instruction (8 rows x 8 16-B slots); slot s of row r holds K chunk s ^ ((r >> 1) & 7), so the four 16-lane
+//     groups of every fragment ds_read_b128 (16 consecutive rows, chunk 4h + g) hit 16 distinct bank slots.
+//   * waves 2 (M) x 4 (N): 64 channels x BN/4 pixels each, v_mfma_f32_16x16x32_{bf16,f16}; the same epilogue
+//     (and split-K partials) as the register-staged kernel.
+constexpr uint32_t GL_OOB = 0xFFFFFF00u;
+template <int BN, int DT>
+__global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32_t w_bytes, uint32_t in_bytes) {
+  constexpr int BM = 128, NW = 8;
+  constexpr int MI = 4, NI = BN / 64;                  // 16x16 sub-tiles per wave
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, BUF = A_BYTES + B_BYTES;
+  constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;  // DMA instructions per wave and stage
+  constexpr int NINS = A_INS + B_INS;
+  constexpr int ESZ = 2;
+  __shared__ __attribute__((aligned(16))) char lds[3 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int pix0 = blockIdx.x * BN, row0 = blockIdx.y * BM;
+  const int nck = p.cin / 64;
+  const int nstage_all = p.kh * p.kw * nck;
+  const int nstage = p.ntaps * nck;
+  const int s_begin = (int)(((long)nstage * blockIdx.z) / p.ksplit);
+  const int s_end = (int)(((long)nstage * (blockIdx.z + 1)) / p.ksplit);
+
+  const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)p.wpk, (short)0, (int)w_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc((void*)p.in, (short)0, (int)in_bytes, 0x00020000);
+  // this lane's rows: DMA instruction j of this wave covers image rows 8 * (j * NW + wave) + lane / 8, slot lane % 8
+  const int slot = lane & 7;
+  uint32_t a_off[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int r = 8 * (j * NW + wave) + (lane >> 3);
+    const int co = row0 + r;
+    const int c = slot ^ ((r >> 1) & 7);
+    a_off[j] = ((uint32_t)((co >> 6) * nstage_all) * 64u + (uint32_t)(co & 63)) * 128u + (uint32_t)c * 16u;
+  }
+  uint32_t b_off[B_INS];
+  int b_iy[B_INS], b_ix[B_INS];
+  const int hw = p.ho * p.wo;
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int r = 8 * (j * NW + wave) + (lane >> 3);
+    const int gp = pix0 + r;
+    const int c = slot ^ ((r >> 1) & 7);
+    if (gp < p.npix) {
+      const int img = gp / hw, rr = gp - img * hw;
+      const int oy = rr / p.wo, ox = rr - oy * p.wo;
+      b_iy[j] = oy * p.stride - p.pad;
+      b_ix[j] = ox * p.stride - p.pad;
+      b_off[j] = (uint32_t)(((img * p.hi + b_iy[j]) * p.wi + b_ix[j]) * p.cs) * ESZ + (uint32_t)c * 16u;
+    } else {
+      b_iy[j] = -(1 << 28);  // never in range
+      b_ix[j] = 0;
+      b_off[j] = 0;
+    }
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+  auto issue = [&](int s) {  // stage s -> ring slot s % 3
+    const uint32_t base = lds0 + (uint32_t)((s % 3) * BUF);
+    const int ti = s / nck, cc = s - ti * nck;
+    const int tap = p.taps[ti];
+    const int ky = tap / p.kw, kx = tap - ky * p.kw;
+    const uint32_t wst = (uint32_t)(tap * nck + cc) * 8192u;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) dma16(rs_w, a_off[j] + wst, base + (uint32_t)((j * NW + wave) * 1024), 0);
+    const int dy = ky * p.dil, dx = kx * p.dil;
+    const int toff = ((dy * p.wi + dx) * p.cs + cc * 64) * ESZ;
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const bool ok = (unsigned)(b_iy[j] + dy) < (unsigned)p.hi && (unsigned)(b_ix[j] + dx) < (unsigned)p.wi;
+      dma16(rs_in, ok ? b_off[j] + (uint32_t)toff : GL_OOB, base + (uint32_t)(A_BYTES + (j * NW + wave) * 1024), 0);
+    }
+  };
+
+  // fragment addressing: lane (r16, g) reads row r16 of a 16-row sub-tile, chunk 4h + g
+  const int r16 = lane & 15, g = lane >> 4;
+  const int sw = (r16 >> 1) & 7;
+  const int fo0 = r16 * 128 + (((0 + g) ^ sw) << 4), fo1 = r16 * 128 + (((4 + g) ^ sw) << 4);
+  const int a_base = wm * 64 * 128, b_base = A_BYTES + wn * (BN / 4) * 128;
+
+  f32x4_g acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4_g{0.f, 0.f, 0.f, 0.f};
+
+  if (s_begin < s_end) issue(s_begin);
+  if (s_begin + 1 < s_end) issue(s_begin + 1);
+  for (int s = s_begin; s < s_end; ++s) {
+    // stage s landed (stage s + 1 may stay in flight); the barrier also ends every wave's reads of slot (s + 2) % 3
+    if (s + 1 < s_end) vm_wait<NINS>(); else vm_wait<0>();
+    lds_barrier();
+    if (s + 2 < s_end) issue(s + 2);
+    const char* base = lds + (s % 3) * BUF;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int fo = h ? fo1 : fo0;
+      u32x4_g a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = *(const u32x4_g*)(base + a_base + i * 16 * 128 + fo);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = *(const u32x4_g*)(base + b_base + j * 16 * 128 + fo);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          if constexpr (DT == NST_DT_F16)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_g, a[i]),
+                                                               __builtin_bit_cast(f16x8_g, b[j]), acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_g, a[i]),
+                                                                __builtin_bit_cast(bf16x8_g, b[j]), acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+  vm_wait<0>();  // no DMA lands after the workgroup releases its LDS
+
+  // ---- epilogue (as gemm_conv_kernel's): lane owns output channels co..co+3 of one pixel per sub-tile ----
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int px = pix0 + wn * (BN / 4) + j * 16 + r16;
+    if (px >= p.npix) continue;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int co = row0 + wm * 64 + i * 16 + 4 * g;
+      if (co >= p.cout_store) continue;
+      if (p.ksplit > 1) {
+        *(f32x4_g*)(p.partial + ((size_t)blockIdx.z * p.npix + px) * p.cout_store + co) = acc[i][j];
+        continue;
+      }
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = acc[i][j][q] * p.scale[co + q] + p.shift[co + q];
+      if (p.res) {
+        const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
+        v[0] += h_to_f((uint16_t)(r.x & 0xffff), DT); v[1] += h_to_f((uint16_t)(r.x >> 16), DT);
+        v[2] += h_to_f((uint16_t)(r.y & 0xffff), DT); v[3] += h_to_f((uint16_t)(r.y >> 16), DT);
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      }
+      const size_t o = (size_t)px * p.out_cs + p.out_off + co;
+      if (p.out_f32) {
+        *(float4*)((float*)p.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 w;
+        w.x = (uint32_t)f_to_h(v[0], DT) | ((uint32_t)f_to_h(v[1], DT) << 16);
+        w.y = (uint32_t)f_to_h(v[2], DT) | ((uint32_t)f_to_h(v[3], DT) << 16);
+        *(uint2*)((uint16_t*)p.out + o) = w;
+      }
+    }
+  }
+}
+
 // split-K epilogue: sum the K slices in slice order, then scale/shift, residual, ReLU, store (as the
 // single-pass epilogue does)
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmConvParams p, int dt) {
@@ -279,25 +442,64 @@ void live_taps(GemmConvParams& p) {
   }
 }
 
+// launch shape.  16-bit: the LDS-DMA kernel (128 x 256 tiles when they fill the chip, else 128 x 128, split in
+// K up to about a wave of the chip) unless the tensors exceed its 32-bit buffer offsets or the GEMM is too
+// small to fill half the chip that way.  Otherwise (and fp32) the register-staged kernel: 128x128 tiles when
+// they fill the chip, split in K over them for deep K when they fill a quarter of it (Gatys 512^2 1.74 -> 1.47 ms
+// per Adam step from VGG conv4_x; DeepLab's shorter-K layers measured slower that way, hence the floor), else
+// 64x64 tiles, split when fewer than a wave of the chip.
+#ifndef NST_GEMM_GLDS
+#define NST_GEMM_GLDS 1
+#endif
+#ifndef NST_GEMM_BIG_SPLIT_MIN_STAGES
+#define NST_GEMM_BIG_SPLIT_MIN_STAGES 64
+#endif
+enum GemmKind { GK_REG64 = 0, GK_REG128 = 1, GK_GLDS256 = 2, GK_GLDS128 = 3 };
 struct GemmShape {
-  bool big;
+  int kind;
   int ksplit;
 };
 GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
   const int nstage = p.ntaps * (p.cin / gemm_stage_channels(dtype));
-  GemmShape g;
-  // 128x128 tiles when they alone fill the chip's 256 CUs; 64x64 otherwise
-  g.big = (long)((p.npix + 127) / 128) * ((p.cout_store + 127) / 128) >= 256;
-  g.ksplit = 1;
-  if (!g.big) {  // fewer 64x64 tiles than a wave of the chip and a long K loop: split K (at most 8 slices)
-    const long tiles = (long)((p.npix + 63) / 64) * ((p.cout_store + 63) / 64);
-    if (tiles < 240 && nstage >= 16) {
-      long k = (480 + tiles - 1) / tiles;
-      k = std::min<long>(k, std::min<long>(8, nstage / 8));
-      g.ksplit = (int)std::max<long>(k, 1);
+  const long mt = (p.cout_store + 127) / 128;
+  GemmShape g{GK_REG64, 1};
+  if (NST_GEMM_GLDS && dtype != NST_DT_F32) {
+    const long n_img = p.npix / std::max(1, p.ho * p.wo);
+    const double in_b = (double)n_img * p.hi * p.wi * p.cs * 2.0;
+    const double w_b = (double)((p.cout_store + 63) / 64) * p.kh * p.kw * (p.cin / 64) * 8192.0;
+    if (in_b < 2147483648.0 && w_b < 2147483648.0) {
+      const long t256 = (long)((p.npix + 255) / 256) * mt, t128 = (long)((p.npix + 127) / 128) * mt;
+      if (t256 >= 200) return GemmShape{GK_GLDS256, 1};
+      long k = 1;
+      if (t128 < 200 && nstage >= 16) k = std::max<long>(1, std::min<long>((256 + t128 - 1) / t128, std::min<long>(8, nstage / 8)));
+      if (t128 * k >= 128) return GemmShape{GK_GLDS128, (int)k};
     }
   }
+  const long tiles128 = (long)((p.npix + 127) / 128) * mt;
+  if (tiles128 >= 256) return GemmShape{GK_REG128, 1};
+  if (tiles128 >= 64 && nstage >= NST_GEMM_BIG_SPLIT_MIN_STAGES) {
+    long k = (480 + tiles128 - 1) / tiles128;
+    k = std::min<long>(k, std::min<long>(8, nstage / 8));
+    if (k > 1) return GemmShape{GK_REG128, (int)k};
+  }
+  // fewer 64x64 tiles than a wave of the chip and a long K loop: split K (at most 8 slices)
+  const long tiles = (long)((p.npix + 63) / 64) * ((p.cout_store + 63) / 64);
+  if (tiles < 240 && nstage >= 16) {
+    long k = (480 + tiles - 1) / tiles;
+    k = std::min<long>(k, std::min<long>(8, nstage / 8));
+    g.ksplit = (int)std::max<long>(k, 1);
+  }
   return g;
+}
+
+template <int BN>
+void launch_glds(int dt, const GemmConvParams& p, hipStream_t st) {
+  const long n_img = p.npix / std::max(1, p.ho * p.wo);
+  const uint32_t in_b = (uint32_t)(n_img * p.hi * p.wi * p.cs * 2);
+  const uint32_t w_b = (uint32_t)((p.cout_store + 63) / 64) * (uint32_t)(p.kh * p.kw * (p.cin / 64)) * 8192u;
+  const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + 127) / 128), (unsigned)p.ksplit);
+  if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_glds_kernel<BN, NST_DT_F16>), grid, dim3(512), 0, st, p, w_b, in_b);
+  else hipLaunchKernelGGL((gemm_glds_kernel<BN, NST_DT_BF16>), grid, dim3(512), 0, st, p, w_b, in_b);
 }
 
 }  // namespace
@@ -318,7 +520,9 @@ hipError_t launch_gemm_conv(int dtype, GemmConvParams& p, hipStream_t st) {
   if (p.ntaps == 0) return hipErrorInvalidValue;
   const GemmShape g = gemm_shape(dtype, p);
   p.ksplit = p.partial ? g.ksplit : 1;
-  if (g.big) launch_tile<128, 128>(dtype, p, st);
+  if (g.kind == GK_GLDS256) launch_glds<256>(dtype, p, st);
+  else if (g.kind == GK_GLDS128) launch_glds<128>(dtype, p, st);
+  else if (g.kind == GK_REG128) launch_tile<128, 128>(dtype, p, st);
   else launch_tile<64, 64>(dtype, p, st);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ksplit == 1) return e;

@@ -731,6 +731,13 @@ struct GramT<float> {
   static constexpr int KM = 4, VEC = 4, KB = 64, RS = 272;
 };
 
+// ds_read_b64_tr_b16 (gfx950): per 16-lane group a 4-row x 16-column block of 16-bit elements, delivered column-major
+__device__ __forceinline__ uint2 tr_read16(const char* p) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)p);
+  return __builtin_bit_cast(uint2, v);
+}
+
 template <typename T, int TI, bool HWC, bool RELU>
 __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int c, int hw, int kslice,
                                                    float* __restrict__ out, size_t slice_stride) {
@@ -739,6 +746,10 @@ __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int 
   constexpr int MI = TI / 32, MJ = TI / 64;                // 16 x 16 fragments per wave
   constexpr int CPS = TI * KB / VEC;                        // 16-B chunks per side and fill
   constexpr int CPT = (CPS + 511) / 512;                    // per thread
+  // 16-bit HWC side image: KB pixel rows x TI channels, row pitch = 32 mod 256 bytes, so the 8 rows of a 32-lane
+  // half's transposed read (4 per 16-lane group) fall on 8 distinct 8-bank groups
+  constexpr int RST = TI * 2 + 32;
+  constexpr bool TR = HWC && sizeof(T) == 2;
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int tt = (c + TI - 1) / TI;
@@ -749,7 +760,7 @@ __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int 
   const int k0 = blockIdx.y * kslice, k1 = min(hw, k0 + kslice);
   const T* Fb = F + (size_t)b * c * hw;
   char* sa = gsm;
-  char* sb = diag ? gsm : gsm + TI * RS;
+  char* sb = diag ? gsm : gsm + (TR ? KB * RST : TI * RS);
 
   // chunk q of a side: CHW: row q / (KB/VEC), pixels (q % (KB/VEC)) * VEC ..; HWC: pixel q / (TI/VEC),
   // channels (q % (TI/VEC)) * VEC ..
@@ -781,9 +792,10 @@ __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int 
       const int px = q / (TI / VEC), row = (q % (TI / VEC)) * VEC;
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
       if constexpr (sizeof(T) == 2) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          *(uint16_t*)(side + (row + e) * RS + px * 2) = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+        // 16-bit HWC: the fill keeps the [pixel][channel] rows (one 16-B write); the fragments are read
+        // transposed (ds_read_b64_tr_b16, below)
+        *(uint4*)(side + px * RST + row * 2) = v;
+        (void)w;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) *(uint32_t*)(side + (row + e) * RS + px * 4) = w[e];
@@ -826,7 +838,32 @@ __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int 
     }
 #pragma unroll
     for (int kk = 0; kk < KB; kk += KM) {
-      if constexpr (sizeof(T) == 2) {
+      if constexpr (TR) {
+        // transposed reads of the [pixel][channel] image: lane 4q + p of 16-lane group g addresses pixel row
+        // kk + 16h + 4g + q, channels c0 + 4p .. +3, and receives channel c0 + (lane & 15) of those 4 pixels.
+        // K element e of group g is pixel kk + 16 (e >> 2) + 4g + (e & 3) for both operands (a permutation of
+        // the 32 pixels of the step: the same products are summed)
+        const int q = (lane & 15) >> 2, pp = lane & 3;
+        uint4 fa[MI], fb[MJ];
+#pragma unroll
+        for (int m = 0; m < MI; ++m) {
+          const char* a0 = sa + (kk + 4 * g + q) * RST + (ra + 16 * m + 4 * pp) * 2;
+          const uint2 lo = tr_read16(a0), hi = tr_read16(a0 + 16 * RST);
+          fa[m] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
+#pragma unroll
+        for (int n = 0; n < MJ; ++n) {
+          const char* b0 = sb + (kk + 4 * g + q) * RST + (cb + 16 * n + 4 * pp) * 2;
+          const uint2 lo = tr_read16(b0), hi = tr_read16(b0 + 16 * RST);
+          fb[n] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
+#pragma unroll
+        for (int m = 0; m < MI; ++m)
+#pragma unroll
+          for (int n = 0; n < MJ; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[m]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[n]), acc[m][n], 0, 0, 0);
+      } else if constexpr (sizeof(T) == 2) {
         uint4 fa[MI], fb[MJ];
 #pragma unroll
         for (int m = 0; m < MI; ++m) fa[m] = *(const uint4*)(sa + (ra + 16 * m + row) * RS + (kk + 8 * g) * 2);
@@ -929,7 +966,7 @@ hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, i
   float* dst = g.slices > 1 ? (float*)ws : G;  // one slice: the reduce pass divides G in place
   dim3 grid(g.tt * g.tt, g.slices, n);
   const int rs = dtype == NST_DT_BF16 ? GramT<__bf16>::RS : GramT<float>::RS;
-  const size_t lds = (size_t)2 * g.ti * rs;
+  const size_t lds = std::max((size_t)2 * g.ti * rs, (size_t)2 * 64 * (g.ti * 2 + 32));  // CHW / 16-bit HWC images
 #define NST_GRAM_GO(T, TI, HWC, RL)                                                                      \
   do {                                                                                                   \
     static const hipError_t attr = hipFuncSetAttribute((const void*)gram_kernel<T, TI, HWC, RL>,        \

@@ -110,19 +110,23 @@ __global__ __launch_bounds__(256) void vgg_relu_bwd_kernel(const uint4* __restri
 
 // ---- Gram (style) gradient, fused with the ReLU backward and the other gradient terms:
 //   gz[p][i] = z[p][i] > 0 ? ga[p][i] + sum_j ReLU(z[p][j]) M[j][i] + cw * (ReLU(z[p][i]) - P[p][i]) : 0
-// M = 4 beta w_l (G - A) / (c^3 hw), symmetric (so row i of M is column i).  MFMA 16x16x32 bf16:
-// A = 16 pixels x 32 channels of ReLU(z), B = 32 x 16 of M (bf16, rounded once by vgg_style_delta_kernel).  Workgroup = 4
-// waves = 64 pixels x 64 channels, each wave 16 pixels x 64 channels.
+// M = 4 beta w_l (G - A) / (c^3 hw), symmetric (so row i of M is column i).  MFMA 16x16x32 bf16 with M as the A
+// operand (16 channels x 32) and ReLU(z) as B (32 x 16 pixels): lane (pixel, g) ends with 4 consecutive channels of
+// one pixel.  Workgroup = 4 waves = 64 pixels x 64 channels, each wave 16 pixels x 64 channels.  The product goes
+// through an LDS tile [64 px][64 ch] so the fused epilogue reads z / ga / P and writes gz as whole 16-byte
+// chunks (8 channels of a pixel per thread, full 128-B channel runs per pixel), not 2-byte elements.
 template <int C>
 __global__ __launch_bounds__(256) void vgg_gram_bwd_kernel(const __bf16* __restrict__ z, const __bf16* __restrict__ ga,
                                                            const __bf16* __restrict__ P, float cw,
                                                            const __bf16* __restrict__ Mb, int hw,
                                                            __bf16* __restrict__ gz) {
+  constexpr int TP = 64 + 4;  // floats per staged pixel row (16-B pad: the float4 writes of a 16-lane group spread)
+  __shared__ __attribute__((aligned(16))) float tile[64 * TP];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int row = lane & 15, g = lane >> 4;
+  const int col = lane & 15, g = lane >> 4;
   const int p0 = blockIdx.x * 64 + wv * 16;
   const int i0 = blockIdx.y * 64;
-  const int pa = min(p0 + row, hw - 1);  // A row (pixel) of this lane
+  const int pb = min(p0 + col, hw - 1);  // B column (pixel) of this lane
   f32x4_t acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
@@ -131,32 +135,41 @@ __global__ __launch_bounds__(256) void vgg_gram_bwd_kernel(const __bf16* __restr
 #pragma unroll
   for (int k = 0; k < C; k += 32) {
     float f[8];
-    unpack8(*(const uint4*)(z + (size_t)pa * C + k + 8 * g), f);
+    unpack8(*(const uint4*)(z + (size_t)pb * C + k + 8 * g), f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-    const uint4 a = pack8(f);
+    const uint4 b = pack8(f);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const uint4 b = *(const uint4*)(Mb + (size_t)(i0 + 16 * t + row) * C + k + 8 * g);
+      const uint4 a = *(const uint4*)(Mb + (size_t)(i0 + 16 * t + col) * C + k + 8 * g);
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
                                                        acc[t], 0, 0, 0);
     }
   }
-  // D[4g + r][lane & 15]: pixel p0 + 4g + r, channel i0 + 16t + (lane & 15)
+  // D[16t + 4g + r][col]: channel i0 + 16t + 4g + r of pixel p0 + col
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int ch = i0 + 16 * t + row;
+  for (int t = 0; t < 4; ++t) *(f32x4_t*)(tile + (wv * 16 + col) * TP + 16 * t + 4 * g) = acc[t];
+  __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int p = p0 + 4 * g + r;
-      if (p >= hw) continue;
-      const size_t o = (size_t)p * C + ch;
-      const float zv = (float)z[o];
-      float v = acc[t][r];
-      if (ga) v = v + (float)ga[o];
-      if (P) v = v + cw * (fmaxf(zv, 0.f) - (float)P[o]);
-      gz[o] = (__bf16)(zv > 0.f ? v : 0.f);
+  for (int k = 0; k < 2; ++k) {
+    const int q = k * 256 + threadIdx.x;  // 64 pixels x 8 chunks of 8 channels
+    const int pl = q >> 3, cq = q & 7;
+    const int p = blockIdx.x * 64 + pl;
+    if (p >= hw) continue;
+    const size_t o = (size_t)p * C + i0 + 8 * cq;
+    float zv[8], gv[8], pv[8], o8[8];
+    unpack8(*(const uint4*)(z + o), zv);
+    if (ga) unpack8(*(const uint4*)(ga + o), gv);
+    if (P) unpack8(*(const uint4*)(P + o), pv);
+    const f32x4_t m0 = *(const f32x4_t*)(tile + pl * TP + 8 * cq), m1 = *(const f32x4_t*)(tile + pl * TP + 8 * cq + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = j < 4 ? m0[j] : m1[j - 4];
+      if (ga) v = v + gv[j];
+      if (P) v = v + cw * (fmaxf(zv[j], 0.f) - pv[j]);
+      o8[j] = zv[j] > 0.f ? v : 0.f;
     }
+    *(uint4*)(gz + o) = pack8(o8);
   }
 }
 

@@ -256,7 +256,8 @@ def test_gram_vgg_shapes_deterministic(c, hw):
     """nst_gram at the VGG-19 style layers of a 512x512 image (relu1_1..relu5_1: c = 64..512, hw =
     512^2 / 4^k) and ragged shapes: fp32 within 1e-5 of an fp64 Gram (utils.py:80-83 arithmetic);
     bf16 within 1e-5 of the fp64 Gram of the bf16-rounded features (products exact, fp32
-    accumulation); bit-identical across runs and between the CHW and HWC layouts."""
+    accumulation); bit-identical across runs; the fp32 HWC layout bit-identical to CHW, the bf16 HWC layout (read
+    through transposed LDS reads, which sum each 32-pixel step's products in another order) within the same 1e-5."""
     from neuralstyletransferv1_amd import _lib
     from neuralstyletransferv1_amd.utils import gram_matrix, gram_raw
     g = torch.Generator().manual_seed(c + hw)
@@ -273,9 +274,12 @@ def test_gram_vgg_shapes_deterministic(c, hw):
     assert relb < 1e-5, relb
     assert torch.equal(Gb, gram_matrix(Fb.cuda().view(2, c, hw, 1)))  # deterministic
     assert torch.equal(G32, gram_matrix(Fd))
-    if c % 8 == 0:  # the NHWC activation layout gives the same fills, so the same bits
+    if c % 8 == 0:  # the NHWC activation layout
         hwc = Fb.transpose(1, 2).contiguous().cuda()
-        assert torch.equal(gram_raw(hwc, _lib.NST_DT_BF16, _lib.NST_GRAM_HWC, 2, c, hw), Gb)
+        Gh = gram_raw(hwc, _lib.NST_DT_BF16, _lib.NST_GRAM_HWC, 2, c, hw)
+        relh = float((Gh.cpu().double() - refb).abs().max() / refb.abs().max())
+        assert relh < 1e-5, relh
+        assert torch.equal(Gh, gram_raw(hwc, _lib.NST_DT_BF16, _lib.NST_GRAM_HWC, 2, c, hw))
         hwc32 = F.transpose(1, 2).contiguous().cuda()
         assert torch.equal(gram_raw(hwc32, _lib.NST_DT_F32, _lib.NST_GRAM_HWC, 2, c, hw), G32)
 

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Variant builds of libnst_hip.so for A/B sweeps on the GPU (tools/*_bench.py select one with NST_HIP_LIB):
+#   bash tools/build_variants.sh <source.hip> <name>=<"-D flags"> ...
+# recompiles <source> with the flags and links it with the default objects into sweep/libnst_hip_<name>.so
+set -e
+cd "$(dirname "$0")/.."
+make -j8 >/dev/null
+SRC=$1; shift
+base=$(basename "$SRC")
+mkdir -p build/var sweep
+for spec in "$@"; do
+  name=${spec%%=*}; flags=${spec#*=}
+  objs=$(ls build/obj/*.o | grep -v "/$base.o")
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function \
+    -Iinclude -Ineuralstyletransferv1_amd/csrc $flags -c "$SRC" -o "build/var/${base}_$name.o" &
+  pids="$pids $!"
+done
+for p in $pids; do wait $p; done
+for spec in "$@"; do
+  name=${spec%%=*}
+  objs=$(ls build/obj/*.o | grep -v "/$base.o")
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "sweep/libnst_hip_$name.so" $objs "build/var/${base}_$name.o"
+  echo "built sweep/libnst_hip_$name.so"
+done
