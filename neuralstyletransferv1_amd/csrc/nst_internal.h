@@ -152,10 +152,6 @@ hipError_t launch_vgg_relu_bwd(const void* z, const void* ga, const void* P, flo
                                hipStream_t st);
 hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, float cw, const void* Mb, int hw, int c,
                                void* gz, hipStream_t st);
-// Mb: bf16 [c][c] = k (G - A); loss_out = sum (G - A)^2; parts: VGG_STYLE_PARTS floats of scratch
-constexpr int VGG_STYLE_PARTS = 256;
-hipError_t launch_vgg_style_delta(const float* G, const float* A, int c, float k, void* Mb, float* loss_out,
-                                  float* parts, hipStream_t st);
 int vgg_content_parts(size_t elems);
 hipError_t launch_vgg_losses(const void* z, const void* P, size_t elems, float* part, const float* style_raw,
                              float cscale, const float* sscale, float* losses, hipStream_t st);
@@ -198,8 +194,19 @@ hipError_t launch_prepad_encode(int dtype, const ConvParams& p, int in_kind, int
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b,
                         float omb, uint8_t* out, int n, int hw, hipStream_t st, const uint8_t* mask8 = nullptr);
 size_t gram_workspace_bytes(int n, int c, int hw);
-// relu: Gram of ReLU(F) (bf16 HWC only: the VGG program's stored pre-activations)
+// The Gatys style term fused into the Gram's reduce pass: Mb = bf16(k (G - A)) and loss_out = sum (G - A)^2
+// (per-block partials in `parts`, <= GRAM_DELTA_MAX_PARTS = c*c/64 of them, summed in block order)
+constexpr int GRAM_DELTA_MAX_PARTS = 512 * 512 / 64;
+struct GramDelta {
+  const float* A;
+  float k;
+  __bf16* Mb;
+  float* parts;
+  float* loss_out;
+};
+hipError_t launch_vgg_sum_parts(const float* parts, int n, float* out, hipStream_t st);
+// relu: Gram of ReLU(F) (bf16 HWC only: the VGG program's stored pre-activations); delta: see GramDelta
 hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, int hw, float* G, void* ws,
-                       hipStream_t st, int relu = 0);
+                       hipStream_t st, int relu = 0, const GramDelta* delta = nullptr);
 
 }  // namespace nst

@@ -907,8 +907,12 @@ __global__ __launch_bounds__(512) void gram_kernel(const T* __restrict__ F, int 
 // consecutive entries; its 16 lane groups each sum a contiguous 1/16 of the slices with four interleaved
 // accumulators (independent loads in flight: the slices are read at HBM rate instead of one dependent load at a
 // time), combined ((a0 + a1) + (a2 + a3)), then the 16 group sums are added in group order.
+// DELTA (the Gatys style loss, vgg_gatys.cpp): also Mb = bf16(k (G - A)) and one partial of sum (G - A)^2 per block
+// (a fixed-order xor tree over the block's 64 entries), which launch_vgg_sum_parts adds in block order
+template <bool DELTA>
 __global__ __launch_bounds__(1024) void gram_reduce_kernel(const float* __restrict__ part, int slices,
-                                                           size_t slice_stride, float denom, float* __restrict__ G) {
+                                                           size_t slice_stride, float denom, float* __restrict__ G,
+                                                           GramDelta gd) {
   __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const size_t e = (size_t)blockIdx.x * 64 + lane;
@@ -925,10 +929,23 @@ __global__ __launch_bounds__(1024) void gram_reduce_kernel(const float* __restri
   }
   red[grp][lane] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
-  if (grp == 0 && e < slice_stride) {
-    float t = red[0][lane];
-    for (int g = 1; g < 16; ++g) t += red[g][lane];
-    G[e] = t / denom;
+  if (grp == 0) {
+    float d2 = 0.f;
+    if (e < slice_stride) {
+      float t = red[0][lane];
+      for (int g = 1; g < 16; ++g) t += red[g][lane];
+      G[e] = t / denom;
+      if constexpr (DELTA) {
+        const float d = t / denom - gd.A[e];
+        gd.Mb[e] = (__bf16)(gd.k * d);
+        d2 = d * d;
+      }
+    }
+    if constexpr (DELTA) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) d2 = d2 + __shfl_xor(d2, o);
+      if (lane == 0) gd.parts[blockIdx.x] = d2;
+    }
   }
 }
 
@@ -959,7 +976,7 @@ GramPlan gram_plan(int n, int c, int hw) {
 size_t gram_workspace_bytes(int n, int c, int hw) { return gram_plan(n, c, hw).ws_bytes; }
 
 hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, int hw, float* G, void* ws,
-                       hipStream_t st, int relu) {
+                       hipStream_t st, int relu, const GramDelta* delta) {
   const GramPlan g = gram_plan(n, c, hw);
   const size_t slice = (size_t)n * c * c;
   const float denom = (float)((double)c * (double)hw);
@@ -993,8 +1010,15 @@ hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, i
 #undef NST_GRAM_GO
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((slice + 63) / 64)), dim3(1024), 0, st, dst, g.slices, slice,
-                     denom, G);
+  const unsigned nb = (unsigned)((slice + 63) / 64);
+  if (delta) {
+    if (nb > (unsigned)GRAM_DELTA_MAX_PARTS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gram_reduce_kernel<true>, dim3(nb), dim3(1024), 0, st, dst, g.slices, slice, denom, G, *delta);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_vgg_sum_parts(delta->parts, (int)nb, delta->loss_out, st);
+  }
+  hipLaunchKernelGGL(gram_reduce_kernel<false>, dim3(nb), dim3(1024), 0, st, dst, g.slices, slice, denom, G, GramDelta{});
   return hipGetLastError();
 }
 

@@ -160,7 +160,7 @@ VggPlan vgg_plan(int h, int w) {
     gws = std::max(gws, gram_workspace_bytes(1, c, P.ch[ci] * P.cw[ci]));
   }
   P.gram_ws = off; off += al(std::max<size_t>(gws, 256));
-  P.part = off; off += al(512 * 4);
+  P.part = off; off += al(std::max(512, GRAM_DELTA_MAX_PARTS) * 4);
   P.raw = off; off += al(8 * 4);
   P.losses = off; off += al(4 * 4);
   // split-K scratch of the GEMM-conv layers (forward and input gradient), the largest one
@@ -420,10 +420,10 @@ int gatys_grad_impl(nst_vgg* v, const float* image, int h, int w, const float* s
   for (int l = 0; l < 5; ++l) {
     const int i = kStyle[l], c = kConvs[i].cout, hw = P.ch[i] * P.cw[i];
     const float wl = style_layer_weights ? style_layer_weights[l] : 1.f;
-    VGG_CHECK(launch_gram(ws + P.z[i], NST_DT_BF16, 1, 1, c, hw, (float*)(ws + P.gram[l]), ws + P.gram_ws, st, 1));
     const double k = 4.0 * style_weight * wl / ((double)c * c * c * hw);
-    VGG_CHECK(launch_vgg_style_delta((const float*)(ws + P.gram[l]), (const float*)(sp + P.sA[l]), c, (float)k,
-                                     ws + P.M[l], (float*)(ws + P.raw) + l, (float*)(ws + P.part), st));
+    const GramDelta gd{(const float*)(sp + P.sA[l]), (float)k, (__bf16*)(ws + P.M[l]), (float*)(ws + P.part),
+                       (float*)(ws + P.raw) + l};
+    VGG_CHECK(launch_gram(ws + P.z[i], NST_DT_BF16, 1, 1, c, hw, (float*)(ws + P.gram[l]), ws + P.gram_ws, st, 1, &gd));
     sscale[l] = (float)(style_weight * wl / ((double)c * c));
   }
   const size_t nc = (size_t)P.ch[kContent] * P.cw[kContent] * 512;

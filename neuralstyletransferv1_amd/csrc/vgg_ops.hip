@@ -173,28 +173,8 @@ __global__ __launch_bounds__(256) void vgg_gram_bwd_kernel(const __bf16* __restr
   }
 }
 
-// ---- style delta + loss: Mb = bf16(k (G - A)) (the gram-gradient GEMM's operand), per-block partial sums of
-// (G - A)^2, then one block adds the partials in block order (fixed order: deterministic) ----
-__global__ __launch_bounds__(256) void vgg_style_delta_kernel(const float* __restrict__ G, const float* __restrict__ A,
-                                                               int cc, float k, __bf16* __restrict__ Mb,
-                                                               float* __restrict__ part) {
-  __shared__ float red[256];
-  float s = 0.f;
-  for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < cc; i += gridDim.x * 256 * 4) {
-    const float4 gv = *(const float4*)(G + i), av = *(const float4*)(A + i);
-    const float d[4] = {gv.x - av.x, gv.y - av.y, gv.z - av.z, gv.w - av.w};
-    *(uint2*)(Mb + i) = make_uint2(bf_pack(k * d[0], k * d[1]), bf_pack(k * d[2], k * d[3]));
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s = s + d[j] * d[j];
-  }
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
-}
+// ---- block partials summed in block order (deterministic): the style loss (gram_reduce_kernel<true>) and the
+// content loss ----
 __global__ __launch_bounds__(256) void vgg_sum_parts_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
   __shared__ float red[256];
   float s = 0.f;
@@ -312,14 +292,8 @@ hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, flo
   }
   return hipGetLastError();
 }
-// parts: scratch of VGG_STYLE_PARTS floats
-hipError_t launch_vgg_style_delta(const float* G, const float* A, int c, float k, void* Mb, float* loss_out,
-                                  float* parts, hipStream_t st) {
-  const int cc = c * c;
-  if (cc % 4 != 0) return hipErrorInvalidValue;
-  const int nb = std::min(VGG_STYLE_PARTS, (cc / 4 + 255) / 256);
-  hipLaunchKernelGGL(vgg_style_delta_kernel, dim3((unsigned)nb), dim3(256), 0, st, G, A, cc, k, (__bf16*)Mb, parts);
-  hipLaunchKernelGGL(vgg_sum_parts_kernel, dim3(1), dim3(256), 0, st, parts, nb, loss_out);
+hipError_t launch_vgg_sum_parts(const float* parts, int n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(vgg_sum_parts_kernel, dim3(1), dim3(256), 0, st, parts, n, out);
   return hipGetLastError();
 }
 int vgg_content_parts(size_t elems) { return (int)std::min<size_t>(512, (elems / 8 + 255) / 256); }
