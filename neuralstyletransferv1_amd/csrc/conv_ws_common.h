@@ -46,6 +46,23 @@ __device__ __forceinline__ void mfma_tied(f32x4_t& c, const uint4& a, const uint
   }
 }
 
+// the same with C = cinit for a tile row's first MFMA (the conv bias: the epilogue then adds nothing)
+template <typename T>
+__device__ __forceinline__ void mfma_tied_c(f32x4_t& c, const uint4& a, const uint4& bop, bool first, const f32x4_t& cinit) {
+  const u32x4_t av = __builtin_bit_cast(u32x4_t, a), bv = __builtin_bit_cast(u32x4_t, bop);
+  if constexpr (IS_F16<T>) {
+    if (first)
+      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %3" : "=&v"(c) : "v"(av), "v"(bv), "v"(cinit));
+    else
+      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
+  } else {
+    if (first)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %3" : "=&v"(c) : "v"(av), "v"(bv), "v"(cinit));
+    else
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
+  }
+}
+
 // cache policy of the activation stores: nt (streaming).  A store holds vmcnt until the L2 has taken
 // it, and every later unit wait counts it (in-order), so the trunk's output and residual-stream
 // stores sit in front of the next tile's loads; streaming stores measured ~1 % faster per step.

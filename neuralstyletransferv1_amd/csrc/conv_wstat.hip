@@ -35,6 +35,15 @@ namespace nst {
 constexpr int WS_RING = 3;  // operand reads in flight ahead of the MFMAs
 constexpr int WS_SPLIT = 1;  // read steps between a unit's staging read and its transform (0: back to back)
 constexpr uint32_t OOB = 0xFFFFFF00u;  // buffer offset past every launch's records: loads 0, stores dropped
+// the conv bias enters as the C operand of each tile row's first MFMA (bias + the K sum in the accumulator, one
+// rounding per MFMA as before) instead of 32 epilogue adds per wave and tile
+#ifndef NST_WS_BIAS_C
+#define NST_WS_BIAS_C 1
+#endif
+// the epilogue's InstanceNorm sums as packed f32 pairs (v_pk_add_f32 / v_pk_fma_f32, no MFMA of this wave in flight)
+#ifndef NST_WS_PK_STATS
+#define NST_WS_PK_STATS 1
+#endif
 
 template <int TH, int FILL>
 struct WsCfg {
@@ -271,9 +280,14 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   // The hazards hipcc cannot see are covered by construction: each tile's first MFMA of a row
   // takes C = 0 (no VALU write feeds an MFMA), operands come from loads it waits for, an
   // accumulation chain needs no wait states, and mfma_drain() pads before the epilogue reads.
-  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) { mfma_tied<T>(c, a, bop, first); };
   auto kloop = [&](Acc& acc, auto&& hook, auto&& bound) {
     constexpr int NI = 4 * PRD, D = WS_RING;
+    f32x4_t bias0;
+    if constexpr (NST_WS_BIAS_C) bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 * wv + 4 * g) * 4);
+    auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
+      if constexpr (NST_WS_BIAS_C) mfma_tied_c<T>(c, a, bop, first, bias0);
+      else mfma_tied<T>(c, a, bop, first);
+    };
     uint4 ring[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) ring[i] = bread(i);
@@ -308,7 +322,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
     // the last MFMAs' results: 8-pass XDL write -> VALU read needs >= 12 wait states (20 here)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     const int c0 = 16 * wv + 4 * g;
-    const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
+    const f32x4_t bias = NST_WS_BIAS_C ? (f32x4_t){0.f, 0.f, 0.f, 0.f} : *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
     const __amdgpu_buffer_rsrc_t ors = launch_rsrc(p.out, ob);
     const int ox = wk.tx0 + px;
     const uint32_t row_bytes = (uint32_t)p.ow * p.cout_stride * 2;
@@ -322,7 +336,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
 #pragma unroll
       for (int r = 0; r < TH; ++r) {
         const bool valid = decltype(all_valid)::value || (wk.ty0 + r < p.oh && ox < p.ow);
-        const f32x4_t v = add4(acc[r], bias);
+        const f32x4_t v = NST_WS_BIAS_C ? acc[r] : add4(acc[r], bias);
         const u32x2_t pk = {pack16<T>(v[0], v[1]), pack16<T>(v[2], v[3])};
         if constexpr (C::OST) {
           *(u32x2_t*)(smem + obase + r * C::TW * 256) = pk;
@@ -330,7 +344,17 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
           __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row_bytes : OOB, 0, ST_AUX);
         }
         const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
-        stat4(s1, s2, x);
+        if constexpr (NST_WS_PK_STATS) {
+          if (r == 0) {
+            s1 = x;
+            s2 = x * x;
+          } else {
+            s1 = s1 + x;
+            s2 = __builtin_elementwise_fma(x, x, s2);
+          }
+        } else {
+          stat4(s1, s2, x);
+        }
       }
     };
     // every tile but those on the bottom / right edge: no per-row validity
