@@ -35,7 +35,24 @@ $(BUILD)/%.cpp.o: $(CSRC)/%.cpp $(CSRC)/nst_internal.h $(CSRC)/seg_internal.h $(
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
-clean:
-	rm -rf $(BUILD) $(LIB)
+# Host-side AddressSanitizer build of the C ABI (tools/asan/nst_asan_driver.cpp): the host translation units
+# with -fsanitize=address on the host side only (no device sanitizer on this pool), the kernels as built above
+ASAN_HOST := nst_api.cpp vgg_gatys.cpp seg_deeplab.cpp region_api.cpp flow_api.cpp
+ASAN_OBJS := $(patsubst %,build/asan/%.o,$(ASAN_HOST))
+ASAN_BIN := tools/asan/nst_asan_driver
+ASAN_FLAGS := -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer
 
-.PHONY: all clean
+build/asan/%.cpp.o: $(CSRC)/%.cpp $(CSRC)/nst_internal.h $(CSRC)/seg_internal.h $(CSRC)/post_common.h $(CSRC)/region_internal.h $(CSRC)/flow_internal.h include/nst_hip.h
+	@mkdir -p build/asan
+	$(HIPCC) $(CXXFLAGS) $(ASAN_FLAGS) -x hip -c $< -o $@
+
+$(ASAN_BIN): tools/asan/nst_asan_driver.cpp $(ASAN_OBJS) $(filter-out $(patsubst %,$(BUILD)/%.o,$(ASAN_HOST)),$(OBJS))
+	$(HIPCC) $(CXXFLAGS) $(ASAN_FLAGS) -x hip tools/asan/nst_asan_driver.cpp -x none $(ASAN_OBJS) \
+	  $(filter-out $(patsubst %,$(BUILD)/%.o,$(ASAN_HOST)),$(OBJS)) -o $@
+
+asan: $(ASAN_BIN)
+
+clean:
+	rm -rf $(BUILD) $(LIB) build/asan $(ASAN_BIN)
+
+.PHONY: all clean asan

@@ -558,7 +558,10 @@ struct WstatInst {
   }
 };
 
-constexpr int WSTAT_TH = 8;  // tile rows
+#ifndef NST_WSTAT_TH
+#define NST_WSTAT_TH 8
+#endif
+constexpr int WSTAT_TH = NST_WSTAT_TH;  // tile rows
 #define E(...) WstatInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wstat(int* count) {
   static const ConvKernelInfo table[] = {

@@ -1,0 +1,159 @@
+// Host-side AddressSanitizer run of the C ABI ("ASan host build of the C-ABI").
+//
+// Built by `make asan`: the host translation units that implement the C ABI (nst_api.cpp, vgg_gatys.cpp,
+// seg_deeplab.cpp, region_api.cpp, flow_api.cpp) are compiled with -fsanitize=address on the HOST side only
+// (device code is unchanged: GPU sanitizers are not available on the pool) and linked with the normal kernel
+// objects into this driver.  It exercises handle creation and weight packing, planning, workspace sizing, the
+// forward of every architecture in every compute dtype on small ragged frames, the Gram entry point, and the
+// argument-validation / error paths, then destroys everything; ASan reports any heap overflow, use-after-free or
+// double free in that host code.
+//
+//   nst_asan_driver <params.bin>...   (tools/asan/make_params.py writes one file per architecture:
+//                                       int32 arch, int32 count, then per tensor: int32 name length, name,
+//                                       int64 numel, numel float32)
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nst_hip.h"
+
+namespace {
+int g_fail = 0;
+void expect(bool ok, const char* what) {
+  if (!ok) {
+    std::fprintf(stderr, "FAIL: %s (%s)\n", what, nst_last_error());
+    ++g_fail;
+  }
+}
+
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "FAIL: %s: %s\n", what, hipGetErrorString(e));
+    ++g_fail;
+  }
+}
+#define HC(expr) hip_ok((expr), #expr)
+
+struct Params {
+  int arch = -1;
+  std::vector<std::string> names;
+  std::vector<std::vector<float>> data;
+  std::vector<nst_param> view;
+};
+
+bool load(const char* path, Params& P) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return false;
+  int32_t arch = 0, count = 0;
+  bool ok = std::fread(&arch, 4, 1, f) == 1 && std::fread(&count, 4, 1, f) == 1 && count > 0;
+  P.arch = arch;
+  for (int i = 0; ok && i < count; ++i) {
+    int32_t len = 0;
+    int64_t numel = 0;
+    ok = std::fread(&len, 4, 1, f) == 1 && len > 0 && len < 4096;
+    std::string name(ok ? len : 0, '\0');
+    ok = ok && std::fread(&name[0], 1, len, f) == (size_t)len && std::fread(&numel, 8, 1, f) == 1 && numel > 0;
+    std::vector<float> d(ok ? numel : 0);
+    ok = ok && std::fread(d.data(), 4, numel, f) == (size_t)numel;
+    P.names.push_back(name);
+    P.data.push_back(std::move(d));
+  }
+  std::fclose(f);
+  for (size_t i = 0; ok && i < P.names.size(); ++i) P.view.push_back(nst_param{P.names[i].c_str(), P.data[i].data(), (int64_t)P.data[i].size()});
+  return ok;
+}
+
+void run_arch(const Params& P) {
+  const int dtypes[] = {NST_DT_F32, NST_DT_BF16, NST_DT_F16, NST_DT_F32S};
+  const int n = 2, h = 45, w = 58;  // ragged (the output fit path of Johnson / ReCoNet), above NST's 40-px pre-reflect
+  std::vector<uint8_t> frames((size_t)n * h * w * 3);
+  for (size_t i = 0; i < frames.size(); ++i) frames[i] = (uint8_t)((i * 2654435761u) >> 24);
+  uint8_t *x = nullptr, *y = nullptr;
+  float* yf = nullptr;
+  HC(hipMalloc(&x, frames.size()));
+  HC(hipMalloc(&y, frames.size()));
+  HC(hipMemcpy(x, frames.data(), frames.size(), hipMemcpyHostToDevice));
+  for (int dt : dtypes) {
+    nst_handle* hd = nullptr;
+    expect(nst_create(P.arch, P.view.data(), (int)P.view.size(), dt, 0, &hd) == NST_OK && hd, "nst_create");
+    if (!hd) continue;
+    int oh = 0, ow = 0;
+    expect(nst_output_hw(hd, h, w, &oh, &ow) == NST_OK && oh > 0 && ow > 0, "nst_output_hw");
+    size_t ws_bytes = 0;
+    expect(nst_workspace_bytes(hd, n, h, w, &ws_bytes) == NST_OK && ws_bytes > 0, "nst_workspace_bytes");
+    void* ws = nullptr;
+    HC(hipMalloc(&ws, ws_bytes));
+    HC(hipMalloc(&yf, (size_t)n * 3 * oh * ow * 4));
+    // raw model tensor out (any size), then uint8 frames when the output keeps the input size
+    expect(nst_forward(hd, x, NST_IO_U8_NHWC, n, h, w, NST_PRESET_IMAGENET_255, yf, NST_IO_F32_NCHW, ws, ws_bytes,
+                       nullptr) == NST_OK, "nst_forward u8 -> f32");
+    if (oh == h && ow == w)
+      expect(nst_forward(hd, x, NST_IO_U8_NHWC, n, h, w, NST_PRESET_IMAGENET_255, y, NST_IO_U8_NHWC, ws, ws_bytes,
+                         nullptr) == NST_OK, "nst_forward u8 -> u8");
+    // error paths: too small a workspace, bad preset, null handle, u8 output of another size
+    expect(nst_forward(hd, x, NST_IO_U8_NHWC, n, h, w, NST_PRESET_IMAGENET_255, yf, NST_IO_F32_NCHW, ws, ws_bytes - 1,
+                       nullptr) == NST_E_WORKSPACE, "workspace too small is rejected");
+    expect(nst_forward(hd, x, NST_IO_U8_NHWC, n, h, w, 99, yf, NST_IO_F32_NCHW, ws, ws_bytes, nullptr) == NST_E_INVALID,
+           "unknown preset is rejected");
+    expect(nst_forward(nullptr, x, NST_IO_U8_NHWC, n, h, w, NST_PRESET_IMAGENET_255, yf, NST_IO_F32_NCHW, ws, ws_bytes,
+                       nullptr) == NST_E_INVALID, "null handle is rejected");
+    expect(nst_num_layers(hd) > 0 && nst_layer_name(hd, 0) != nullptr, "layer names");
+    expect(hipDeviceSynchronize() == hipSuccess, "device sync");
+    HC(hipFree(ws));
+    HC(hipFree(yf));
+    yf = nullptr;
+    nst_destroy(hd);
+  }
+  HC(hipFree(x));
+  HC(hipFree(y));
+}
+
+void run_gram() {
+  const int n = 2, c = 64, hw = 1000;
+  std::vector<float> F((size_t)n * c * hw);
+  for (size_t i = 0; i < F.size(); ++i) F[i] = (float)((i * 2654435761u) >> 24) / 255.f;
+  float *dF = nullptr, *dG = nullptr;
+  HC(hipMalloc(&dF, F.size() * 4));
+  HC(hipMalloc(&dG, (size_t)n * c * c * 4));
+  HC(hipMemcpy(dF, F.data(), F.size() * 4, hipMemcpyHostToDevice));
+  size_t wsb = 0;
+  expect(nst_gram_workspace_bytes(n, c, hw, &wsb) == NST_OK, "nst_gram_workspace_bytes");
+  void* ws = nullptr;
+  if (wsb) HC(hipMalloc(&ws, wsb));
+  expect(nst_gram(dF, NST_DT_F32, NST_GRAM_CHW, n, c, hw, dG, ws, wsb, nullptr) == NST_OK, "nst_gram");
+  std::vector<float> G((size_t)n * c * c);
+  HC(hipMemcpy(G.data(), dG, G.size() * 4, hipMemcpyDeviceToHost));
+  double ref = 0;  // G[0][0][0] on the host
+  for (int p = 0; p < hw; ++p) ref += (double)F[p] * F[p];
+  ref /= (double)c * hw;
+  expect(std::abs(G[0] - ref) <= 1e-5 * ref, "gram value");
+  if (ws) HC(hipFree(ws));
+  HC(hipFree(dF));
+  HC(hipFree(dG));
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    std::fprintf(stderr, "no GPU\n");
+    return 2;
+  }
+  expect(nst_create(0, nullptr, 0, NST_DT_BF16, 0, nullptr) == NST_E_INVALID, "nst_create without params is rejected");
+  for (int i = 1; i < argc; ++i) {
+    Params P;
+    if (!load(argv[i], P)) {
+      std::fprintf(stderr, "cannot read %s\n", argv[i]);
+      return 2;
+    }
+    run_arch(P);
+    std::printf("arch %d: %zu tensors, 4 dtypes\n", P.arch, P.view.size());
+  }
+  run_gram();
+  std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "ok", g_fail);
+  return g_fail ? 1 : 0;
+}
