@@ -231,14 +231,15 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, BUF = A_BYTES + B_BYTES;
   constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;  // DMA instructions per wave and stage
   constexpr int NINS = A_INS + B_INS;
-  constexpr int ESZ = 2;
+  constexpr bool F32 = DT == NST_DT_F32;
+  constexpr int ESZ = F32 ? 4 : 2, CK = 128 / ESZ;  // bytes per element, channels per stage
   __shared__ __attribute__((aligned(16))) char lds[3 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
   const int pix0 = blockIdx.x * BN, row0 = blockIdx.y * BM;
-  const int nck = p.cin / 64;
+  const int nck = p.cin / CK;
   const int nstage_all = p.kh * p.kw * nck;
   const int nstage = p.ntaps * nck;
   const int s_begin = (int)(((long)nstage * blockIdx.z) / p.ksplit);
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
 #pragma unroll
     for (int j = 0; j < A_INS; ++j) dma16(rs_w, a_off[j] + wst, base + (uint32_t)((j * NW + wave) * 1024), 0);
     const int dy = ky * p.dil, dx = kx * p.dil;
-    const int toff = ((dy * p.wi + dx) * p.cs + cc * 64) * ESZ;
+    const int toff = ((dy * p.wi + dx) * p.cs + cc * CK) * ESZ;
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
       const bool ok = (unsigned)(b_iy[j] + dy) < (unsigned)p.hi && (unsigned)(b_ix[j] + dx) < (unsigned)p.wi;
@@ -326,7 +327,12 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          if constexpr (DT == NST_DT_F16)
+          if constexpr (F32) {  // 16x16x4 f32 over the 16-B fragment: the same K permutation for A and B
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].x), __uint_as_float(b[j].x), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].y), __uint_as_float(b[j].y), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].z), __uint_as_float(b[j].z), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].w), __uint_as_float(b[j].w), acc[i][j], 0, 0, 0);
+          } else if constexpr (DT == NST_DT_F16)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_g, a[i]),
                                                                __builtin_bit_cast(f16x8_g, b[j]), acc[i][j], 0, 0, 0);
           else
@@ -354,16 +360,21 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = acc[i][j][q] * p.scale[co + q] + p.shift[co + q];
       if (p.res) {
-        const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
-        v[0] += h_to_f((uint16_t)(r.x & 0xffff), DT); v[1] += h_to_f((uint16_t)(r.x >> 16), DT);
-        v[2] += h_to_f((uint16_t)(r.y & 0xffff), DT); v[3] += h_to_f((uint16_t)(r.y >> 16), DT);
+        if constexpr (F32) {
+          const float4 r = *(const float4*)((const float*)p.res + (size_t)px * p.res_cs + co);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        } else {
+          const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
+          v[0] += h_to_f((uint16_t)(r.x & 0xffff), DT); v[1] += h_to_f((uint16_t)(r.x >> 16), DT);
+          v[2] += h_to_f((uint16_t)(r.y & 0xffff), DT); v[3] += h_to_f((uint16_t)(r.y >> 16), DT);
+        }
       }
       if (p.relu) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
       }
       const size_t o = (size_t)px * p.out_cs + p.out_off + co;
-      if (p.out_f32) {
+      if (F32 || p.out_f32) {
         *(float4*)((float*)p.out + o) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
         uint2 w;
@@ -451,6 +462,11 @@ void live_taps(GemmConvParams& p) {
 #ifndef NST_GEMM_GLDS
 #define NST_GEMM_GLDS 1
 #endif
+// fp32 on the LDS-DMA kernel: measured slower for the configs[4] mask at its 256-px working size (4.07 -> 4.65 ms,
+// tools/gpu_gemm_sweep.sh), slightly faster at full 1080p (91 -> 98 TFLOP/s): off
+#ifndef NST_GEMM_GLDS_F32
+#define NST_GEMM_GLDS_F32 0
+#endif
 #ifndef NST_GEMM_BIG_SPLIT_MIN_STAGES
 #define NST_GEMM_BIG_SPLIT_MIN_STAGES 64
 #endif
@@ -463,10 +479,11 @@ GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
   const int nstage = p.ntaps * (p.cin / gemm_stage_channels(dtype));
   const long mt = (p.cout_store + 127) / 128;
   GemmShape g{GK_REG64, 1};
-  if (NST_GEMM_GLDS && dtype != NST_DT_F32) {
+  if (NST_GEMM_GLDS && (dtype != NST_DT_F32 || NST_GEMM_GLDS_F32)) {
+    const int esz = dtype == NST_DT_F32 ? 4 : 2;
     const long n_img = p.npix / std::max(1, p.ho * p.wo);
-    const double in_b = (double)n_img * p.hi * p.wi * p.cs * 2.0;
-    const double w_b = (double)((p.cout_store + 63) / 64) * p.kh * p.kw * (p.cin / 64) * 8192.0;
+    const double in_b = (double)n_img * p.hi * p.wi * p.cs * esz;
+    const double w_b = (double)((p.cout_store + 63) / 64) * p.kh * p.kw * (p.cin / (128 / esz)) * 8192.0;
     if (in_b < 2147483648.0 && w_b < 2147483648.0) {
       const long t256 = (long)((p.npix + 255) / 256) * mt, t128 = (long)((p.npix + 127) / 128) * mt;
       if (t256 >= 200) return GemmShape{GK_GLDS256, 1};
@@ -494,11 +511,13 @@ GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
 
 template <int BN>
 void launch_glds(int dt, const GemmConvParams& p, hipStream_t st) {
+  const int esz = dt == NST_DT_F32 ? 4 : 2;
   const long n_img = p.npix / std::max(1, p.ho * p.wo);
-  const uint32_t in_b = (uint32_t)(n_img * p.hi * p.wi * p.cs * 2);
-  const uint32_t w_b = (uint32_t)((p.cout_store + 63) / 64) * (uint32_t)(p.kh * p.kw * (p.cin / 64)) * 8192u;
+  const uint32_t in_b = (uint32_t)(n_img * p.hi * p.wi * p.cs * esz);
+  const uint32_t w_b = (uint32_t)((p.cout_store + 63) / 64) * (uint32_t)(p.kh * p.kw * (p.cin / (128 / esz))) * 8192u;
   const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + 127) / 128), (unsigned)p.ksplit);
   if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_glds_kernel<BN, NST_DT_F16>), grid, dim3(512), 0, st, p, w_b, in_b);
+  else if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_glds_kernel<BN, NST_DT_F32>), grid, dim3(512), 0, st, p, w_b, in_b);
   else hipLaunchKernelGGL((gemm_glds_kernel<BN, NST_DT_BF16>), grid, dim3(512), 0, st, p, w_b, in_b);
 }
 
