@@ -94,45 +94,48 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restr
 
 // One-launch form for layers with few tiles per frame (the 270x480 trunk: ~1k): grid (n, cstride/16), block
 // 1024 = 16 channels x 64 tile phases, each thread sums tiles phase, phase + 64, ... in fp64 (<= 32 loads,
-// all in flight), then a fixed-order LDS tree over the 64 phases and the finalize.  Deterministic; half
-// the launches of the two-stage form, whose second launch is pure latency at this size.
+// all in flight), a wave's 4 phases by xor shuffles, the 16 waves through LDS in wave order, then the finalize.
+// Deterministic; half the launches of the two-stage form, whose second launch is pure latency at this size.
 constexpr int IN_ONE_PH = 64, IN_ONE_CH = 16, IN_ONE_MAX_TILES = 2048;
 __global__ __launch_bounds__(1024) void in_stats_kernel(const float* __restrict__ partial, int tiles, int cstride,
                                                         double count, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps, int frn,
                                                         float2* __restrict__ out) {
-  __shared__ double red[IN_ONE_PH][IN_ONE_CH][2];
+  __shared__ double red[IN_ONE_PH / 4][IN_ONE_CH][2];
   const int n = blockIdx.x;
   const int cl = threadIdx.x & (IN_ONE_CH - 1), q = threadIdx.x / IN_ONE_CH;
-  const int c = blockIdx.y * IN_ONE_CH + cl;
+  const int c = min(blockIdx.y * IN_ONE_CH + cl, cstride - 1);
+  const float2* p = (const float2*)partial + (size_t)n * tiles * cstride + c;
+  // every load in flight at once: indices clamped into range (always a valid address), the extra ones zeroed after
+  float2 v[IN_ONE_MAX_TILES / IN_ONE_PH];
+#pragma unroll
+  for (int k = 0; k < IN_ONE_MAX_TILES / IN_ONE_PH; ++k) v[k] = p[(size_t)min(q + k * IN_ONE_PH, tiles - 1) * cstride];
   double s1 = 0.0, s2 = 0.0;
-  if (c < cstride) {
-    const float2* p = (const float2*)partial + (size_t)n * tiles * cstride + c;
-    float2 v[IN_ONE_MAX_TILES / IN_ONE_PH];
 #pragma unroll
-    for (int k = 0; k < IN_ONE_MAX_TILES / IN_ONE_PH; ++k) {
-      const int t = q + k * IN_ONE_PH;
-      v[k] = t < tiles ? p[(size_t)t * cstride] : make_float2(0.f, 0.f);
-    }
-#pragma unroll
-    for (int k = 0; k < IN_ONE_MAX_TILES / IN_ONE_PH; ++k) {
-      s1 += (double)v[k].x;
-      s2 += (double)v[k].y;
-    }
+  for (int k = 0; k < IN_ONE_MAX_TILES / IN_ONE_PH; ++k) {
+    const bool in = q + k * IN_ONE_PH < tiles;
+    s1 += in ? (double)v[k].x : 0.0;
+    s2 += in ? (double)v[k].y : 0.0;
   }
-  red[q][cl][0] = s1;
-  red[q][cl][1] = s2;
+  // the wave's 4 tile phases (lanes cl, cl + 16, cl + 32, cl + 48), then the 16 waves in LDS, fixed order
+#pragma unroll
+  for (int o = 16; o <= 32; o <<= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < IN_ONE_CH) {
+    red[wv][cl][0] = s1;
+    red[wv][cl][1] = s2;
+  }
   __syncthreads();
-  for (int h = IN_ONE_PH / 2; h >= 1; h >>= 1) {
-    if (q < h) {
-      red[q][cl][0] += red[q + h][cl][0];
-      red[q][cl][1] += red[q + h][cl][1];
-    }
-    __syncthreads();
-  }
-  if (q != 0 || c >= cstride) return;
+  if (threadIdx.x >= IN_ONE_CH || blockIdx.y * IN_ONE_CH + cl >= cstride) return;
   s1 = red[0][cl][0];
   s2 = red[0][cl][1];
+  for (int w = 1; w < IN_ONE_PH / 4; ++w) {
+    s1 += red[w][cl][0];
+    s2 += red[w][cl][1];
+  }
   const double mean = frn ? 0.0 : s1 / count;  // FRN: mean(x^2) only (frn.py:71-74)
   double var = s2 / count - mean * mean;
   var = var < 0.0 ? 0.0 : var;
