@@ -69,6 +69,7 @@ struct W9Cfg {
 };
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
 
 template <typename T, int NW>
 __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
@@ -152,7 +153,15 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
     int fb = buf * C::HALO + (16 * wv + px + 2 * g) * 8;  // row-r operand: + r * RS
     int kb = buf * C::HALO + (16 * wv + px + 8) * 8;      // column-8 operand rows r + g (clamped)
     asm volatile("" : "+v"(fb), "+v"(kb));
-    auto fread = [&](int r) { return *(const uint4*)(smem + fb + r * C::RS); };
+    // the row operand of lane (px, g) starts at pixel 16 wv + px + 2g: 8-byte aligned, not 16.  A ds_read_b128 off
+    // its 16-byte alignment is replayed at ~64 cycles per wave-instruction (cdna_hip_programming.md Guideline
+    // 17), which made this kernel LDS-bound (SQ_LDS_IDX_ACTIVE ~0.8 of its cycles): two naturally aligned
+    // ds_read_b64 instead (volatile: never merged into a ds_read2_b64)
+    auto fread = [&](int r) {
+      const char* a = smem + fb + r * C::RS;
+      const uint64_t lo = *(const volatile lds_u64*)a, hi = *(const volatile lds_u64*)(a + 8);
+      return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+    };
     // rows past the halo only meet zero weights (kernel rows 9..11): read row HR - 1 instead
     typedef uint2 KOp;
     auto kread = [&](int r) {
