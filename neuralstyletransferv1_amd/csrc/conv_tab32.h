@@ -28,6 +28,12 @@
 #ifndef NST_T32_OUT
 #define NST_T32_OUT 8, 32, 4, 1
 #endif
+// the 3-channel output conv as x-shift rows (5 shifts x 3 channels per 16-row MFMA block instead of 3 of 16 rows):
+// fp32 parity mode 162.5 -> 186.7 frames/s (output conv 11.9 -> 5.5 ms per batch of 8), split-fp16 297.5 -> 312.2
+// (6.1 -> 4.8 ms); 8-row or 8-wave x-shift tiles exceed the LDS budget for 4-byte entries
+#ifndef NST_T32_XS
+#define NST_T32_XS 4, 80, 4, 1
+#endif
 
 namespace nst {
 template <typename F>
