@@ -36,10 +36,22 @@
 
 namespace nst {
 
-constexpr int WS9_TH = 8;    // output rows per tile (each wave's rows)
-constexpr int WS9_OCC = 2;   // waves per SIMD the register allocation must allow (two 4-wave workgroups per CU)
-constexpr int WS9_NW = 4;    // waves per workgroup: 4 = two workgroups per CU drifting out of phase
-constexpr int WS9_RING = 2;  // input-row operands in flight ahead of the MFMAs
+#ifndef NST_WS9_TH
+#define NST_WS9_TH 8
+#endif
+constexpr int WS9_TH = NST_WS9_TH;    // output rows per tile (each wave's rows)
+#ifndef NST_WS9_OCC
+#define NST_WS9_OCC 2
+#endif
+constexpr int WS9_OCC = NST_WS9_OCC;   // waves per SIMD the register allocation must allow (two 4-wave workgroups per CU)
+#ifndef NST_WS9_NW
+#define NST_WS9_NW 4
+#endif
+constexpr int WS9_NW = NST_WS9_NW;    // waves per workgroup: 4 = two workgroups per CU drifting out of phase
+#ifndef NST_WS9_RING
+#define NST_WS9_RING 2
+#endif
+constexpr int WS9_RING = NST_WS9_RING;  // input-row operands in flight ahead of the MFMAs
 
 template <int NW_>
 struct W9Cfg {
