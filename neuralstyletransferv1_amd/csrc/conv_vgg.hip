@@ -8,6 +8,16 @@
 // layer's gradient leaves as fp32 NCHW.
 #include "conv_impl.h"
 
+#ifndef NST_VGG_T12
+#define NST_VGG_T12 8, 16, 2, 2  // conv1_2 forward (64 -> 64 @ the full image)
+#endif
+#ifndef NST_VGG_T11
+#define NST_VGG_T11 8, 32, 4, 1  // conv1_1 forward (the normalised image)
+#endif
+#ifndef NST_VGG_TB1
+#define NST_VGG_TB1 8, 32, 4, 1  // conv1_1 backward (-> the image gradient)
+#endif
+
 namespace nst {
 typedef __bf16 B;
 #define E(...) ConvInst<__VA_ARGS__>::info()
@@ -16,15 +26,15 @@ const ConvKernelInfo* conv_table_vgg(int* count) {
   static const ConvKernelInfo table[] = {
       //  T  MODE KS S CINP BN TH TW WM WN  IN           OUT
       // forward
-      E(B, SD, 3, 1, 4, 64, 8, 32, 4, 1, IN_F32_NCHW, OUT_ACT),   // conv1_1 (normalised image)
-      E(B, SD, 3, 1, 64, 64, 8, 16, 2, 2, IN_ACT, OUT_ACT),       // conv1_2
+      E(B, SD, 3, 1, 4, 64, NST_VGG_T11, IN_F32_NCHW, OUT_ACT),   // conv1_1 (normalised image)
+      E(B, SD, 3, 1, 64, 64, NST_VGG_T12, IN_ACT, OUT_ACT),       // conv1_2
       E(B, SD, 3, 1, 64, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),      // conv2_1
       E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // conv2_2, conv3_1 (2 channel blocks); backward 2_2
       E(B, SD, 3, 1, 256, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // conv3_2..3_4, conv4_1; backward 3_1..3_4
       E(B, SD, 3, 1, 512, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),     // conv4_2..5_1; backward 4_1..5_1
       // backward
       E(B, SD, 3, 1, 128, 64, 8, 16, 2, 2, IN_ACT, OUT_ACT),      // conv2_1 -> 64 input channels
-      E(B, SD, 3, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_F32_NCHW),  // conv1_1 -> the image gradient (3 of 16)
+      E(B, SD, 3, 1, 64, 16, NST_VGG_TB1, IN_ACT, OUT_F32_NCHW),  // conv1_1 -> the image gradient (3 of 16)
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;
