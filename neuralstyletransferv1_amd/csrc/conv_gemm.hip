@@ -213,31 +213,36 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
   }
 }
 
-// ---- LDS-DMA form (bf16 / fp16): 128 x BN tiles, 8 waves, one workgroup per CU ----
+// ---- LDS-DMA form (bf16 / fp16): BM x BN tiles (BM 128, or 64 for 64-channel outputs), 8 waves, one workgroup per CU ----
 // The register-staged kernel above keeps one stage in flight and spends VGPRs and ds_writes on the staging; here
 // every stage lands in LDS by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPR destination, zero for any offset past
 // the buffer = the im2col's zero padding) into a 3-slot ring, two stages ahead of the MFMAs, with counted vmcnt
 // waits and one raw barrier per stage (MI355X_MICROARCH / cdna_hip_programming 'glds ... 3 LDS buffers').
-//   * LDS image of a stage: rows (A: 128 output channels, B: BN pixels) x 128 B, lane-linear per DMA
+//   * LDS image of a stage: rows (A: BM output channels, B: BN pixels) x 128 B, lane-linear per DMA
 //     instruction (8 rows x 8 16-B slots); slot s of row r holds K chunk s ^ ((r >> 1) & 7), so the four 16-lane
 //     groups of every fragment ds_read_b128 (16 consecutive rows, chunk 4h + g) hit 16 distinct bank slots.
-//   * waves 2 (M) x 4 (N): 64 channels x BN/4 pixels each, v_mfma_f32_16x16x32_{bf16,f16}; the same epilogue
-//     (and split-K partials) as the register-staged kernel.
+//   * waves BM/64 (M) x 8/(BM/64) (N): 64 channels x BN/WN pixels each, v_mfma_f32_16x16x32_{bf16,f16}; the same
+//     epilogue (and split-K partials) as the register-staged kernel.  BM = 64 serves 64-channel outputs (VGG's
+//     conv1_2 and the dgrads into 64-channel maps) without a half-empty A tile: half the MFMAs and a quarter fewer
+//     fragment reads per output than 128 x 256.
 constexpr uint32_t GL_OOB = 0xFFFFFF00u;
-template <int BN, int DT>
+template <int BM, int BN, int DT, int RING>
 __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32_t w_bytes, uint32_t in_bytes) {
-  constexpr int BM = 128, NW = 8;
-  constexpr int MI = 4, NI = BN / 64;                  // 16x16 sub-tiles per wave
+  constexpr int NW = 8, WM = BM / 64, WN = NW / WM;   // wave grid
+  constexpr int MI = 4, NI = BN / (16 * WN);           // 16x16 sub-tiles per wave
+  static_assert(BM == 64 || BM == 128, "BM");
+  static_assert(NI >= 1 && BN % (16 * WN) == 0, "BN");
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, BUF = A_BYTES + B_BYTES;
   constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;  // DMA instructions per wave and stage
   constexpr int NINS = A_INS + B_INS;
   constexpr bool F32 = DT == NST_DT_F32;
   constexpr int ESZ = F32 ? 4 : 2, CK = 128 / ESZ;  // bytes per element, channels per stage
-  __shared__ __attribute__((aligned(16))) char lds[3 * BUF];
+  static_assert(RING == 3 || RING == 4, "ring");
+  __shared__ __attribute__((aligned(16))) char lds[RING * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % WM, wn = wave / WM;
   const int pix0 = blockIdx.x * BN, row0 = blockIdx.y * BM;
   const int nck = p.cin / CK;
   const int nstage_all = p.kh * p.kw * nck;
@@ -278,8 +283,8 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
     }
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
-  auto issue = [&](int s) {  // stage s -> ring slot s % 3
-    const uint32_t base = lds0 + (uint32_t)((s % 3) * BUF);
+  auto issue = [&](int s) {  // stage s -> ring slot s % RING
+    const uint32_t base = lds0 + (uint32_t)((s % RING) * BUF);
     const int ti = s / nck, cc = s - ti * nck;
     const int tap = p.taps[ti];
     const int ky = tap / p.kw, kx = tap - ky * p.kw;
@@ -299,7 +304,7 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
   const int r16 = lane & 15, g = lane >> 4;
   const int sw = (r16 >> 1) & 7;
   const int fo0 = r16 * 128 + (((0 + g) ^ sw) << 4), fo1 = r16 * 128 + (((4 + g) ^ sw) << 4);
-  const int a_base = wm * 64 * 128, b_base = A_BYTES + wn * (BN / 4) * 128;
+  const int a_base = wm * 64 * 128, b_base = A_BYTES + wn * (BN / WN) * 128;
 
   f32x4_g acc[MI][NI];
 #pragma unroll
@@ -309,12 +314,17 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
 
   if (s_begin < s_end) issue(s_begin);
   if (s_begin + 1 < s_end) issue(s_begin + 1);
+  if (RING == 4 && s_begin + 2 < s_end) issue(s_begin + 2);
   for (int s = s_begin; s < s_end; ++s) {
-    // stage s landed (stage s + 1 may stay in flight); the barrier also ends every wave's reads of slot (s + 2) % 3
-    if (s + 1 < s_end) vm_wait<NINS>(); else vm_wait<0>();
+    // stage s landed (the RING - 2 stages after it may stay in flight); the barrier also ends every wave's reads
+    // of slot (s + RING - 1) % RING
+    const int later = s_end - 1 - s;
+    if (RING == 4 && later >= 2) vm_wait<2 * NINS>();
+    else if (later >= 1) vm_wait<NINS>();
+    else vm_wait<0>();
     lds_barrier();
-    if (s + 2 < s_end) issue(s + 2);
-    const char* base = lds + (s % 3) * BUF;
+    if (s + RING - 1 < s_end) issue(s + RING - 1);
+    const char* base = lds + (s % RING) * BUF;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int fo = h ? fo1 : fo0;
@@ -344,44 +354,56 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
   vm_wait<0>();  // no DMA lands after the workgroup releases its LDS
 
   // ---- epilogue (as gemm_conv_kernel's): lane owns output channels co..co+3 of one pixel per sub-tile ----
+  auto finish = [&](int px, int co, const f32x4_g& a) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = a[q] * p.scale[co + q] + p.shift[co + q];
+    if (p.res) {
+      if constexpr (F32) {
+        const float4 r = *(const float4*)((const float*)p.res + (size_t)px * p.res_cs + co);
+        v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+      } else {
+        const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
+        v[0] += h_to_f((uint16_t)(r.x & 0xffff), DT); v[1] += h_to_f((uint16_t)(r.x >> 16), DT);
+        v[2] += h_to_f((uint16_t)(r.y & 0xffff), DT); v[3] += h_to_f((uint16_t)(r.y >> 16), DT);
+      }
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+    }
+    const size_t o = (size_t)px * p.out_cs + p.out_off + co;
+    if (F32 || p.out_f32) {
+      *(float4*)((float*)p.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      uint2 w;
+      w.x = (uint32_t)f_to_h(v[0], DT) | ((uint32_t)f_to_h(v[1], DT) << 16);
+      w.y = (uint32_t)f_to_h(v[2], DT) | ((uint32_t)f_to_h(v[3], DT) << 16);
+      *(uint2*)((uint16_t*)p.out + o) = w;
+    }
+  };
+  if (p.ksplit == 1) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int px = pix0 + wn * (BN / WN) + j * 16 + r16;
+      if (px >= p.npix) continue;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int co = row0 + wm * 64 + i * 16 + 4 * g;
+        if (co < p.cout_store) finish(px, co, acc[i][j]);
+      }
+    }
+    return;
+  }
+  // split K: this slice's fp32 partial (gemm_splitk_reduce sums the slices in slice order)
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int px = pix0 + wn * (BN / 4) + j * 16 + r16;
+    const int px = pix0 + wn * (BN / WN) + j * 16 + r16;
     if (px >= p.npix) continue;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int co = row0 + wm * 64 + i * 16 + 4 * g;
-      if (co >= p.cout_store) continue;
-      if (p.ksplit > 1) {
-        *(f32x4_g*)(p.partial + ((size_t)blockIdx.z * p.npix + px) * p.cout_store + co) = acc[i][j];
-        continue;
-      }
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = acc[i][j][q] * p.scale[co + q] + p.shift[co + q];
-      if (p.res) {
-        if constexpr (F32) {
-          const float4 r = *(const float4*)((const float*)p.res + (size_t)px * p.res_cs + co);
-          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
-        } else {
-          const uint2 r = *(const uint2*)((const uint16_t*)p.res + (size_t)px * p.res_cs + co);
-          v[0] += h_to_f((uint16_t)(r.x & 0xffff), DT); v[1] += h_to_f((uint16_t)(r.x >> 16), DT);
-          v[2] += h_to_f((uint16_t)(r.y & 0xffff), DT); v[3] += h_to_f((uint16_t)(r.y >> 16), DT);
-        }
-      }
-      if (p.relu) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-      }
-      const size_t o = (size_t)px * p.out_cs + p.out_off + co;
-      if (F32 || p.out_f32) {
-        *(float4*)((float*)p.out + o) = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        uint2 w;
-        w.x = (uint32_t)f_to_h(v[0], DT) | ((uint32_t)f_to_h(v[1], DT) << 16);
-        w.y = (uint32_t)f_to_h(v[2], DT) | ((uint32_t)f_to_h(v[3], DT) << 16);
-        *(uint2*)((uint16_t*)p.out + o) = w;
-      }
+      if (co < p.cout_store) *(f32x4_g*)(p.partial + ((size_t)blockIdx.z * p.npix + px) * p.cout_store + co) = acc[i][j];
     }
   }
 }
@@ -470,7 +492,16 @@ void live_taps(GemmConvParams& p) {
 #ifndef NST_GEMM_BIG_SPLIT_MIN_STAGES
 #define NST_GEMM_BIG_SPLIT_MIN_STAGES 64
 #endif
-enum GemmKind { GK_REG64 = 0, GK_REG128 = 1, GK_GLDS256 = 2, GK_GLDS128 = 3 };
+#ifndef NST_GEMM_RING_32K  // ring depth for tiles whose stage is 32 KB (128 x 128); 4 (three stages in flight) measured
+#define NST_GEMM_RING_32K 3   // 1.161 -> 1.169 ms per Gatys step (r03_m2)
+#endif
+#ifndef NST_GEMM_SPLIT256  // 128 x 256 tiles split in K where 128 x 128 tiles would run unsplit / less split
+#define NST_GEMM_SPLIT256 1
+#endif
+#ifndef NST_GEMM_BM64  // 64 x 256 LDS-DMA tiles for outputs of at most 64 channels
+#define NST_GEMM_BM64 1
+#endif
+enum GemmKind { GK_REG64 = 0, GK_REG128 = 1, GK_GLDS256 = 2, GK_GLDS128 = 3, GK_GLDS64x256 = 4 };
 struct GemmShape {
   int kind;
   int ksplit;
@@ -486,7 +517,12 @@ GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
     const double w_b = (double)((p.cout_store + 63) / 64) * p.kh * p.kw * (p.cin / (128 / esz)) * 8192.0;
     if (in_b < 2147483648.0 && w_b < 2147483648.0) {
       const long t256 = (long)((p.npix + 255) / 256) * mt, t128 = (long)((p.npix + 127) / 128) * mt;
-      if (t256 >= 200) return GemmShape{GK_GLDS256, 1};
+      if (t256 >= 200) return GemmShape{NST_GEMM_BM64 && p.cout_store <= 64 ? GK_GLDS64x256 : GK_GLDS256, 1};
+      if (NST_GEMM_SPLIT256 && p.cout_store > 64 && t256 >= 32 && nstage >= 16) {
+        // a 128 x 256 tile reads a third less LDS per output than 128 x 128 (64 x 64 per wave instead of 64 x 32)
+        const long k2 = std::max<long>(1, std::min<long>((256 + t256 - 1) / t256, std::min<long>(8, nstage / 8)));
+        if (t256 * k2 >= 200) return GemmShape{GK_GLDS256, (int)k2};
+      }
       long k = 1;
       if (t128 < 200 && nstage >= 16) k = std::max<long>(1, std::min<long>((256 + t128 - 1) / t128, std::min<long>(8, nstage / 8)));
       if (t128 * k >= 128) return GemmShape{GK_GLDS128, (int)k};
@@ -509,16 +545,17 @@ GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
   return g;
 }
 
-template <int BN>
+template <int BM, int BN>
 void launch_glds(int dt, const GemmConvParams& p, hipStream_t st) {
   const int esz = dt == NST_DT_F32 ? 4 : 2;
   const long n_img = p.npix / std::max(1, p.ho * p.wo);
   const uint32_t in_b = (uint32_t)(n_img * p.hi * p.wi * p.cs * esz);
   const uint32_t w_b = (uint32_t)((p.cout_store + 63) / 64) * (uint32_t)(p.kh * p.kw * (p.cin / (128 / esz))) * 8192u;
-  const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + 127) / 128), (unsigned)p.ksplit);
-  if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_glds_kernel<BN, NST_DT_F16>), grid, dim3(512), 0, st, p, w_b, in_b);
-  else if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_glds_kernel<BN, NST_DT_F32>), grid, dim3(512), 0, st, p, w_b, in_b);
-  else hipLaunchKernelGGL((gemm_glds_kernel<BN, NST_DT_BF16>), grid, dim3(512), 0, st, p, w_b, in_b);
+  const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM), (unsigned)p.ksplit);
+  constexpr int RING = BM * 128 + BN * 128 <= 32768 ? NST_GEMM_RING_32K : 3;  // 4 x 32 KB stages fit the LDS, 4 x 48 KB do not
+  if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_F16, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
+  else if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_F32, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
+  else hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_BF16, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
 }
 
 }  // namespace
@@ -539,8 +576,9 @@ hipError_t launch_gemm_conv(int dtype, GemmConvParams& p, hipStream_t st) {
   if (p.ntaps == 0) return hipErrorInvalidValue;
   const GemmShape g = gemm_shape(dtype, p);
   p.ksplit = p.partial ? g.ksplit : 1;
-  if (g.kind == GK_GLDS256) launch_glds<256>(dtype, p, st);
-  else if (g.kind == GK_GLDS128) launch_glds<128>(dtype, p, st);
+  if (g.kind == GK_GLDS64x256) launch_glds<64, 256>(dtype, p, st);
+  else if (g.kind == GK_GLDS256) launch_glds<128, 256>(dtype, p, st);
+  else if (g.kind == GK_GLDS128) launch_glds<128, 128>(dtype, p, st);
   else if (g.kind == GK_REG128) launch_tile<128, 128>(dtype, p, st);
   else launch_tile<64, 64>(dtype, p, st);
   hipError_t e = hipGetLastError();
