@@ -8,8 +8,16 @@ make -j8 >/dev/null
 SRC=$1; shift
 base=$(basename "$SRC")
 mkdir -p build/var sweep
+# the Makefile's per-file flags (without them the persistent kernels' K loops stay rolled and their
+# accumulators go to scratch, whose loads break the hand-counted vmcnt waits)
+case "$base" in
+  conv_bf16_wl.hip) extra="-mllvm -pragma-unroll-threshold=200000" ;;
+  conv_wstat.hip|conv_ws2.hip|conv_ws9.hip) extra="-mllvm -pragma-unroll-threshold=5000000" ;;
+  conv_wphase.hip) extra="-mllvm -pragma-unroll-threshold=5000000 -fslp-vectorize" ;;
+  *) extra="" ;;
+esac
 for spec in "$@"; do
-  name=${spec%%=*}; flags=${spec#*=}
+  name=${spec%%=*}; flags="$extra ${spec#*=}"
   objs=$(ls build/obj/*.o | grep -v "/$base.o")
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function \
     -Iinclude -Ineuralstyletransferv1_amd/csrc $flags -c "$SRC" -o "build/var/${base}_$name.o" &
