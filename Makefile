@@ -17,7 +17,10 @@ all: $(LIB)
 
 $(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h $(CSRC)/conv_tab16.h $(CSRC)/conv_tab32.h $(CSRC)/nst_internal.h $(CSRC)/seg_internal.h $(CSRC)/post_common.h $(CSRC)/region_internal.h $(CSRC)/flow_internal.h include/nst_hip.h
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+	$(if $(NOSCRATCH),$(HIPCC) $(CXXFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $@.rem && python3 tools/check_scratch.py $@.rem || { rm -f $@; exit 1; },$(HIPCC) $(CXXFLAGS) -c $< -o $@)
+
+# kernels with hand-counted vmcnt waits: report any scratch use (tools/check_scratch.py; NST_STRICT_SCRATCH=1 fails)
+$(BUILD)/conv_wstat.hip.o $(BUILD)/conv_wphase.hip.o $(BUILD)/conv_ws9.hip.o $(BUILD)/conv_gemm.hip.o: NOSCRATCH = 1
 
 # the persistent kernels fully unroll a long K loop (static register / LDS indices): lift the
 # pragma-unroll size cap for that translation unit only

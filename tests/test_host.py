@@ -199,3 +199,26 @@ def test_feather_restatement_properties():
     m[15, 15] = 255
     f = O.feather_mask_u8(m, 4).astype(int)
     assert np.array_equal(f, f[::-1, ::-1]) and np.array_equal(f, f.T)
+
+
+def test_check_scratch_flags_spills(tmp_path):
+    """tools/check_scratch.py (run by the Makefile on the counted-vmcnt kernels): a kernel with scratch is reported
+    (and fails the build under NST_STRICT_SCRATCH=1), a clean remarks file passes, compiler warnings are echoed."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    rem = "x.hip:1:1: remark: {} [-Rpass-analysis=kernel-resource-usage]\n"
+    ok = tmp_path / "ok.rem"
+    ok.write_text(rem.format("Function Name: k0") + "    1 | __global__ void k0()\n      | ^\n"
+                  + rem.format("    ScratchSize [bytes/lane]: 0") + "x.hip:2:1: warning: unused\n")
+    bad = tmp_path / "bad.rem"
+    bad.write_text(rem.format("Function Name: k1") + rem.format("    ScratchSize [bytes/lane]: 20"))
+    r = subprocess.run([sys.executable, str(root / "tools/check_scratch.py"), str(ok)], capture_output=True, text=True)
+    assert r.returncode == 0 and "warning: unused" in r.stderr and "__global__" not in r.stderr
+    r = subprocess.run([sys.executable, str(root / "tools/check_scratch.py"), str(bad)], capture_output=True, text=True)
+    assert r.returncode == 0 and "k1 uses 20 bytes/lane" in r.stderr
+    env = dict(os.environ, NST_STRICT_SCRATCH="1")
+    r = subprocess.run([sys.executable, str(root / "tools/check_scratch.py"), str(bad)], capture_output=True, text=True,
+                       env=env)
+    assert r.returncode == 1

@@ -19,8 +19,13 @@ esac
 for spec in "$@"; do
   name=${spec%%=*}; flags="$extra ${spec#*=}"
   objs=$(ls build/obj/*.o | grep -v "/$base.o")
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function \
-    -Iinclude -Ineuralstyletransferv1_amd/csrc $flags -c "$SRC" -o "build/var/${base}_$name.o" &
+  ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function \
+    -Iinclude -Ineuralstyletransferv1_amd/csrc $flags -Rpass-analysis=kernel-resource-usage -c "$SRC" \
+    -o "build/var/${base}_$name.o" 2> "build/var/${base}_$name.rem" &&
+    case "$base" in  # the Makefile's scratch check for the counted-vmcnt kernels
+      conv_wstat.hip|conv_wphase.hip|conv_ws9.hip|conv_gemm.hip) python3 tools/check_scratch.py "build/var/${base}_$name.rem" ;;
+      *) true ;;
+    esac || { rm -f "build/var/${base}_$name.o"; echo "variant $name failed"; exit 1; } ) &
   pids="$pids $!"
 done
 for p in $pids; do wait $p; done
