@@ -153,8 +153,11 @@ hipError_t launch_vgg_relu_bwd(const void* z, const void* ga, const void* P, flo
 hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, float cw, const void* Mb, int hw, int c,
                                void* gz, hipStream_t st);
 int vgg_content_parts(size_t elems);
-hipError_t launch_vgg_losses(const void* z, const void* P, size_t elems, float* part, const float* style_raw,
-                             float cscale, const float* sscale, float* losses, hipStream_t st);
+// spart (nullable): the 5 style layers' Gram-reduce block partials at stride sstride floats, snparts[l] each; their
+// sums land in style_raw (else style_raw holds them already)
+hipError_t launch_vgg_losses(const void* z, const void* P, size_t elems, float* part, float* style_raw,
+                             float cscale, const float* sscale, float* losses, hipStream_t st,
+                             const float* spart = nullptr, const int* snparts = nullptr, int sstride = 0);
 hipError_t launch_adam(float* x, const float* g, float* m, float* v, int hw, int n, const float* inv_std, float lr,
                        float b1, float b2, float eps, float bc1, float bc2, int clamp01, hipStream_t st);
 
@@ -202,7 +205,7 @@ struct GramDelta {
   float k;
   __bf16* Mb;
   float* parts;
-  float* loss_out;
+  float* loss_out;  // nullptr: the caller sums `parts` itself (launch_vgg_losses' spart)
 };
 hipError_t launch_vgg_sum_parts(const float* parts, int n, float* out, hipStream_t st);
 // relu: Gram of ReLU(F) (bf16 HWC only: the VGG program's stored pre-activations); delta: see GramDelta

@@ -1019,7 +1019,7 @@ hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, i
     hipLaunchKernelGGL(gram_reduce_kernel<true>, dim3(nb), dim3(1024), 0, st, dst, g.slices, slice, denom, G, *delta);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_vgg_sum_parts(delta->parts, (int)nb, delta->loss_out, st);
+    return delta->loss_out ? launch_vgg_sum_parts(delta->parts, (int)nb, delta->loss_out, st) : hipSuccess;
   }
   hipLaunchKernelGGL(gram_reduce_kernel<false>, dim3(nb), dim3(1024), 0, st, dst, g.slices, slice, denom, G, GramDelta{});
   return hipGetLastError();

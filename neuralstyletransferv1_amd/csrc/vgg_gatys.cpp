@@ -116,7 +116,7 @@ namespace {
 struct VggPlan {
   int h = 0, w = 0;
   int ch[13], cw[13];  // conv output extents
-  size_t z[13], pool[4], ga, gb, gimg, gram[5], M[5], gram_ws, part, raw, losses, gpart, end;  // workspace offsets
+  size_t z[13], pool[4], ga, gb, gimg, gram[5], M[5], gram_ws, part, raw, losses, gpart, spart, end;  // workspace offsets
   size_t gpart_bytes;
   size_t sP, sA[5], send;                                                              // state offsets
 };
@@ -162,6 +162,7 @@ VggPlan vgg_plan(int h, int w) {
   P.gram_ws = off; off += al(std::max<size_t>(gws, 256));
   P.part = off; off += al(std::max(512, GRAM_DELTA_MAX_PARTS) * 4);
   P.raw = off; off += al(8 * 4);
+  P.spart = off; off += al((size_t)5 * GRAM_DELTA_MAX_PARTS * 4);  // the style layers' Gram-reduce partials
   P.losses = off; off += al(4 * 4);
   // split-K scratch of the GEMM-conv layers (forward and input gradient), the largest one
   size_t gp = 0;
@@ -417,18 +418,22 @@ int gatys_grad_impl(nst_vgg* v, const float* image, int h, int w, const float* s
   if (rc != NST_OK) return rc;
   // style: G_l, M_l = 4 beta w_l (G - A) / (c^3 hw), raw sum (G - A)^2
   float sscale[5];
+  int snparts[5];
   for (int l = 0; l < 5; ++l) {
     const int i = kStyle[l], c = kConvs[i].cout, hw = P.ch[i] * P.cw[i];
     const float wl = style_layer_weights ? style_layer_weights[l] : 1.f;
     const double k = 4.0 * style_weight * wl / ((double)c * c * c * hw);
-    const GramDelta gd{(const float*)(sp + P.sA[l]), (float)k, (__bf16*)(ws + P.M[l]), (float*)(ws + P.part),
-                       (float*)(ws + P.raw) + l};
+    // partials per layer, summed by the loss kernel below (one launch for the five layers)
+    const GramDelta gd{(const float*)(sp + P.sA[l]), (float)k, (__bf16*)(ws + P.M[l]),
+                       (float*)(ws + P.spart) + (size_t)l * GRAM_DELTA_MAX_PARTS, nullptr};
+    snparts[l] = (int)(((size_t)c * c + 63) / 64);  // launch_gram's reduce blocks
     VGG_CHECK(launch_gram(ws + P.z[i], NST_DT_BF16, 1, 1, c, hw, (float*)(ws + P.gram[l]), ws + P.gram_ws, st, 1, &gd));
     sscale[l] = (float)(style_weight * wl / ((double)c * c));
   }
   const size_t nc = (size_t)P.ch[kContent] * P.cw[kContent] * 512;
-  VGG_CHECK(launch_vgg_losses(ws + P.z[kContent], sp + P.sP, nc, (float*)(ws + P.part), (const float*)(ws + P.raw),
-                              (float)(content_weight / (double)nc), sscale, losses, st));
+  VGG_CHECK(launch_vgg_losses(ws + P.z[kContent], sp + P.sP, nc, (float*)(ws + P.part), (float*)(ws + P.raw),
+                              (float)(content_weight / (double)nc), sscale, losses, st, (const float*)(ws + P.spart),
+                              snparts, GRAM_DELTA_MAX_PARTS));
   // backward, top to bottom, through two ping-pong gradient buffers (each step reads `cur` and
   // writes the other one).  `ready`: cur already holds dL/dz of conv i (the pool backward folds the
   // producer's ReLU backward in); otherwise cur holds dL/d ReLU(z_i) (none above conv5_1).

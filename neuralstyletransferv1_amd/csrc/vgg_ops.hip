@@ -216,11 +216,29 @@ __global__ __launch_bounds__(256) void vgg_content_partial_kernel(const uint4* _
 struct LossArgs {
   float cscale;          // alpha / numel(content features)
   float sscale[5];       // beta * w_l / c_l^2
+  int snparts[5];        // spart: each style layer's Gram-reduce block partials (vgg_sum_parts_kernel's sums)
+  int sstride;
 };
+// spart: the style layers' raw sums are summed here from their block partials (one launch instead of one
+// vgg_sum_parts_kernel per layer, the same fixed-order arithmetic) and written to style_raw; else style_raw is read
 __global__ __launch_bounds__(256) void vgg_loss_final_kernel(const float* __restrict__ part, int nparts,
-                                                             const float* __restrict__ style_raw, LossArgs a,
-                                                             float* __restrict__ losses) {
+                                                             const float* __restrict__ spart, float* __restrict__ style_raw,
+                                                             LossArgs a, float* __restrict__ losses) {
   __shared__ float red[256];
+  if (spart != nullptr) {
+    for (int l = 0; l < 5; ++l) {
+      float s = 0.f;
+      for (int i = threadIdx.x; i < a.snparts[l]; i += 256) s = s + spart[l * a.sstride + i];
+      red[threadIdx.x] = s;
+      __syncthreads();
+      for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + w];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) style_raw[l] = red[0];
+      __syncthreads();
+    }
+  }
   float s = 0.f;
   for (int i = threadIdx.x; i < nparts; i += 256) s = s + part[i];
   red[threadIdx.x] = s;
@@ -297,15 +315,20 @@ hipError_t launch_vgg_sum_parts(const float* parts, int n, float* out, hipStream
   return hipGetLastError();
 }
 int vgg_content_parts(size_t elems) { return (int)std::min<size_t>(512, (elems / 8 + 255) / 256); }
-hipError_t launch_vgg_losses(const void* z, const void* P, size_t elems, float* part, const float* style_raw,
-                             float cscale, const float* sscale, float* losses, hipStream_t st) {
+hipError_t launch_vgg_losses(const void* z, const void* P, size_t elems, float* part, float* style_raw,
+                             float cscale, const float* sscale, float* losses, hipStream_t st, const float* spart,
+                             const int* snparts, int sstride) {
   const int parts = vgg_content_parts(elems);
   hipLaunchKernelGGL(vgg_content_partial_kernel, dim3(parts), dim3(256), 0, st, (const uint4*)z, (const uint4*)P,
                      elems / 8, part);
   LossArgs a;
   a.cscale = cscale;
-  for (int l = 0; l < 5; ++l) a.sscale[l] = sscale[l];
-  hipLaunchKernelGGL(vgg_loss_final_kernel, dim3(1), dim3(256), 0, st, part, parts, style_raw, a, losses);
+  for (int l = 0; l < 5; ++l) {
+    a.sscale[l] = sscale[l];
+    a.snparts[l] = spart ? snparts[l] : 0;
+  }
+  a.sstride = sstride;
+  hipLaunchKernelGGL(vgg_loss_final_kernel, dim3(1), dim3(256), 0, st, part, parts, spart, style_raw, a, losses);
   return hipGetLastError();
 }
 hipError_t launch_adam(float* x, const float* g, float* m, float* v, int hw, int n, const float* inv_std, float lr,
