@@ -63,6 +63,11 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=3, help="timed 1080p frames per CPU configuration")
     ap.add_argument("--no-fp16", action="store_true", help="skip the fp16-mode timing")
     ap.add_argument("--no-fp32s", action="store_true", help="skip the split-fp16 (fp32s) mode timing")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend for --gpus N > 1 (nccl = RCCL over xGMI; gloo stages the exchange "
+                         "through host memory, so N ranks can rehearse the multi-GPU command on one GPU)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="GPU index for this rank (default LOCAL_RANK); e.g. 0 to put every rank on one GPU")
     return ap.parse_args()
 
 
@@ -166,10 +171,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = args.device if args.device is not None else (local if world > 1 else 0)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     from neuralstyletransferv1_amd import synthetic
@@ -226,7 +235,7 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el, out
@@ -345,6 +354,8 @@ def main():
             "frame_hw": [H, W],
             "parallelism": f"frames round-robin over {world} GPU(s), " +
                            ("point-to-point gather to rank 0" if args.gather else "no data-path collective"),
+            "dist_backend": args.dist_backend if world > 1 else None,
+            "ranks_per_gpu": (world if args.device is not None else 1) if world > 1 else 1,
         },
         "roofline": {
             "bound": "mfma",

@@ -95,8 +95,12 @@ def trunk_kernel_sha() -> str:
     for rel in TRUNK_KERNEL_SOURCES:
         with open(os.path.join(_HERE, rel), "rb") as f:
             h.update(f.read())
-    with open(os.path.join(_HERE, "..", "Makefile")) as f:  # the compiler and flags the kernel is built with
-        h.update("".join(l for l in f if re.match(r"(HIPCC|ARCH|SLP|CXXFLAGS) |\$\(BUILD\)/conv_wstat", l)).encode())
+    # the compiler and the code-generation flags of conv_wstat.hip's own translation unit: the global
+    # HIPCC / ARCH / SLP / CXXFLAGS definitions and target-specific CXXFLAGS / SLP assignments naming that
+    # object alone (diagnostic-only rules such as the multi-target NOSCRATCH remark pass do not change code)
+    pat = r"(HIPCC|ARCH|SLP|CXXFLAGS) |\$\(BUILD\)/conv_wstat\.hip\.o: *(CXXFLAGS|SLP) "
+    with open(os.path.join(_HERE, "..", "Makefile")) as f:
+        h.update("".join(l for l in f if re.match(pat, l)).encode())
     return h.hexdigest()[:16]
 
 

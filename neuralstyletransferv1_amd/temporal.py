@@ -80,6 +80,15 @@ class DisScratch:
         return self.buf
 
 
+def dis_supported(h: int, w: int) -> bool:
+    """Whether nst_flow_dis accepts h x w grays (the frame-size limits of dis_check_shape: a coarsest pyramid
+    level at or above the finest, a stripe buffer that fits LDS); host-side, no GPU work."""
+    if h <= 0 or w <= 0:
+        return False
+    sz = ctypes.c_size_t()
+    return lib().nst_flow_dis_scratch_bytes(1, h, w, ctypes.byref(sz)) == _lib.NST_OK
+
+
 def dis(prev_gray: torch.Tensor, gray: torch.Tensor, scratch: Optional[DisScratch] = None) -> torch.Tensor:
     """cv2.DISOpticalFlow_create(PRESET_FAST).calc of frame pairs: [n,h,w] (or [h,w]) uint8 x 2 -> flow
     [n,h,w,2] (or [h,w,2]) float32 (dx, dy)."""
@@ -157,13 +166,21 @@ class FlowSmoother:
         self.method = method
         self.scratch = FlowScratch()
         self.dis_scratch = DisScratch()
+        self._warned = False
         self.reset()
 
-    def flows(self, prev_gray: torch.Tensor, grays: torch.Tensor) -> torch.Tensor:
+    def flows(self, prev_gray: torch.Tensor, grays: torch.Tensor) -> Optional[torch.Tensor]:
         """Flows of the pairs (prev, grays[0]), (grays[0], grays[1]), ... -> [n,h,w,2] (pipeline.py:1886-1923:
-        optional INTER_AREA reduction by ds, the flow, INTER_LINEAR back x ds)."""
+        optional INTER_AREA reduction by ds, the flow, INTER_LINEAR back x ds), or None when DIS cannot run on
+        the (reduced) frame size: the reference wraps dis.calc in try/except and skips the flow for that frame
+        (pipeline.py:1903-1917), so the frames pass through unfused."""
         prevs = torch.cat([prev_gray[None], grays[:-1]], dim=0)
         n, h, w = grays.shape
+        if self.method == "dis" and not dis_supported(h // self.ds, w // self.ds):
+            if not self._warned:
+                print(f"[flow][warn] DIS cannot run on {w // self.ds}x{h // self.ds} frames; skipping the flow")
+                self._warned = True
+            return None
         if self.ds > 1:
             prevs = torch.stack([downscale_gray(g, self.ds) for g in prevs])
             cur = torch.stack([downscale_gray(g, self.ds) for g in grays])
@@ -187,7 +204,7 @@ class FlowSmoother:
             fl = self.flows(self.prev_gray, grays)
         elif self.enabled and n > 1:
             fl = self.flows(grays[0], grays[1:])
-            fl = [None] + list(fl)
+            fl = None if fl is None else [None] + list(fl)
         fused, flows = [], []
         for k in range(n):
             f = None if fl is None else fl[k]
@@ -213,10 +230,10 @@ class FlowSmoother:
         gray = gray_u8(orig_u8[None])[0]
         self.last_flow = None
         if self.enabled and self.prev_gray is not None and self.prev_styled is not None:
-            if self.prev_gray.shape == gray.shape:
-                flow = self.flows(self.prev_gray, gray[None])[0]
-                out01 = fuse(out01, self.prev_styled, flow, self.alpha)
-                self.last_flow = flow
+            fl = self.flows(self.prev_gray, gray[None]) if self.prev_gray.shape == gray.shape else None
+            if fl is not None:
+                out01 = fuse(out01, self.prev_styled, fl[0], self.alpha)
+                self.last_flow = fl[0]
         self.prev_gray = gray
         self.prev_styled = out01
         return out01

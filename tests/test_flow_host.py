@@ -65,3 +65,14 @@ def test_dis_restatement_recovers_translation():
         fl = DO.dis_flow(prev, nxt)[16:-16, 16:-16]
         assert abs(float(np.median(fl[..., 0])) - dx) < 0.2 and abs(float(np.median(fl[..., 1])) - dy) < 0.2
     assert DO.coarsest_scale(1080, 1920) == 6 and DO.coarsest_scale(96, 128) == 2
+
+
+def test_dis_supported_frame_limits():
+    """The host-side size check the flow EMA consults before DIS (temporal.dis_supported; no GPU work): frames
+    whose coarsest pyramid level would lie below the finest scale are skipped like the reference's dis.calc
+    failures (pipeline.py:1903-1917); 1080p and the usual downscaled sizes run."""
+    from neuralstyletransferv1_amd import temporal as T
+    assert not T.dis_supported(30, 40)
+    assert not T.dis_supported(0, 64)
+    for h, w in ((1080, 1920), (540, 960), (270, 480), (96, 128)):
+        assert T.dis_supported(h, w), (h, w)

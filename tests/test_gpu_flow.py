@@ -271,3 +271,27 @@ def test_cli_flow_downscale_non_divisor(tmp_path):
     assert np.quantile(d, 0.999) <= 1e-3 and d.max() <= 0.05
     # no translation check here: DIS PRESET_FAST on the 93 x 127 reduced gray does not recover the 2 x -1 px
     # shift (its finest scale is 2, so 4-px patches on a ~46 x 63 grid); the restatement's field is the same
+
+
+def test_cli_flow_ema_dis_small_frames_pass_through(tmp_path):
+    """--flow_ema (DIS) on frames too small for DIS PRESET_FAST (80 x 60 with --flow_downscale 2 -> 40 x 30 grays):
+    the reference's dis.calc try/except skips the flow for the frame (pipeline.py:1903-1917), so every frame is
+    written unfused, equal to the same run without --flow_ema."""
+    sd = synthetic.make_state_dict("johnson", 5)
+    ck = tmp_path / "m.pth"
+    torch.save(sd, ck)
+    d_in = tmp_path / "in"
+    d_in.mkdir()
+    for i, f in enumerate(synthetic.make_frames(3, 60, 80, seed=52)):
+        Image.fromarray(f).save(d_in / f"frame_{i + 1:04d}.png")
+    assert not T.dis_supported(30, 40)
+    outs = {}
+    for tag, extra in (("flow", ["--flow_ema", "--flow_downscale", "2"]), ("plain", [])):
+        d_out = tmp_path / f"out_{tag}"
+        assert P.main(["--input_dir", str(d_in), "--output_dir", str(d_out), "--work_dir", str(tmp_path / f"w_{tag}"),
+                       "--model", str(ck), "--io_preset", "imagenet_255", "--batch", "2"] + extra) == 0
+        outs[tag] = [np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png")) for i in range(3)]
+    for a, b in zip(outs["flow"], outs["plain"]):
+        d = np.abs(a.astype(int) - b.astype(int))
+        print("differing values", int((d > 0).sum()), "max", int(d.max()))
+        assert d.max() <= 1  # the --flow_ema path truncates the fp32 out01 on its own kernel (same arithmetic)

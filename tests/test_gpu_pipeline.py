@@ -299,3 +299,32 @@ def test_multi_gpu_orchestration_gloo_matches_single(tmp_path):
         outs[gpus] = [np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png")) for i in range(7)]
     for i in range(7):
         assert np.array_equal(outs[1][i], outs[2][i]), i
+
+
+def test_bench_two_ranks_under_torchrun_gloo(tmp_path):
+    """The driver's multi-GPU bench command (python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N),
+    rehearsed on this one-GPU box: 2 ranks, both on GPU 0 (--device 0), gloo (exchange through host memory), with
+    the ordered gather to rank 0 (--gather).  torchrun is started as a child process (no exec from this process);
+    rank 0 prints ONE JSON line with n_gpus 2 and the whole-job frame count.  Scaling itself is not measured here."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--gather", "--dist-backend", "gloo", "--device", "0", "--frame", "960x540",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
+                       env=dict(os.environ, OMP_NUM_THREADS="4"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["dist_backend"] == "gloo"
+    from neuralstyletransferv1_amd.frames import rank0_share
+    assert d["config"]["global_batch"] == rank0_share(2, 8) + 8
+    assert d["value"] > 0 and abs(d["value"] - d["config"]["global_batch"] * 3 / (d["ms_per_step"] * 3e-3)) < 1e-3 * d["value"]

@@ -52,11 +52,30 @@ def test_plan_groups_and_round_robin_shard():
     assert F.shard([4], 2, 1) == []
 
 
-def _gather_worker(rank, world, port, q):
+def test_owners_with_caps():
+    """owners(): round-robin over the ranks that still have room (rank 0's lighter share, frames.rank0_share)."""
+    assert F.owners(5, 2) == [0, 1, 0, 1, 0]
+    assert F.owners(5, 2, [1, 4]) == [0, 1, 1, 1, 1]
+    assert F.owners(7, 3, [1, 3, 3]) == [0, 1, 2, 1, 2, 1, 2]
+    assert F.owners(3, 3, [1, 3, 3]) == [0, 1, 2]  # a short last group: every rank's first slot in order
+    assert F.owners(2, 3, [0, 3, 3]) == [1, 2]
+    with pytest.raises(ValueError):
+        F.owners(8, 3, [1, 3, 3])
+    for world, batch in ((2, 8), (3, 8), (8, 8), (8, 2)):
+        caps = [F.rank0_share(world, batch)] + [batch] * (world - 1)
+        own = F.owners(sum(caps), world, caps)
+        assert [own.count(r) for r in range(world)] == caps
+    assert F.rank0_share(8, 8) == 6 and F.rank0_share(1, 8) == 8
+    g = F.plan_groups([(4, 4)] * 9 + [(8, 8)] * 2, world=2, batch=3, rank0_batch=1)
+    assert g == [[0, 1, 2, 3], [4, 5, 6, 7], [8], [9, 10]]
+
+
+def _gather_worker(rank, world, port, q, caps=None):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     seen = []
-    groups = F.plan_groups([(2, 3)] * 7 + [(5, 1)] * 2, world, batch=2)
+    groups = F.plan_groups([(2, 3)] * 7 + [(5, 1)] * 2, world, batch=2 if caps is None else caps[1],
+                           rank0_batch=None if caps is None else caps[0])
 
     def stylize(idx):
         if not idx:
@@ -67,21 +86,23 @@ def _gather_worker(rank, world, port, q):
     def consume(g, full):
         seen.append((g, [int(full[j].flatten()[0]) for j in range(full.shape[0])]))
 
-    F.run_sharded(groups, world, rank, stylize, consume)
+    F.run_sharded(groups, world, rank, stylize, consume, caps=caps)
     dist.barrier()
     dist.destroy_process_group()
     q.put((rank, seen))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_ordered_gather_gloo(world):
+@pytest.mark.parametrize("world,caps", [(2, None), (3, None), (2, [1, 3]), (3, [1, 2, 2]), (3, [2, 3, 3])])
+def test_ordered_gather_gloo(world, caps):
+    """Frames come back to rank 0 in order: equal shares, and the pipeline's caps (rank 0 lighter) with a short
+    last group and a frame-size change (7 frames of one size, then 2 of another)."""
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q, caps)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
@@ -95,10 +116,10 @@ def test_ordered_gather_gloo(world):
         assert vals == g  # frame j of each group is the frame itself, in order
 
 
-def _failing_worker(rank, world, port, fail_rank, fail_in, q):
+def _failing_worker(rank, world, port, fail_rank, fail_in, q, caps=None):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    groups = F.plan_groups([(2, 3)] * 8, world, batch=2)
+    groups = F.plan_groups([(2, 3)] * 8, world, batch=2, rank0_batch=None if caps is None else caps[0])
     consumed = []
 
     def stylize(idx):
@@ -114,7 +135,7 @@ def _failing_worker(rank, world, port, fail_rank, fail_in, q):
         consumed.append(list(g))
 
     try:
-        F.run_sharded(groups, world, rank, stylize, consume)
+        F.run_sharded(groups, world, rank, stylize, consume, caps=caps)
         outcome = "ok"
     except F.RankFailed:
         outcome = "RankFailed"
@@ -124,10 +145,12 @@ def _failing_worker(rank, world, port, fail_rank, fail_in, q):
     q.put((rank, outcome, consumed))
 
 
-@pytest.mark.parametrize("fail_in,fail_rank", [("stylize", 1), ("stylize", 0), ("consume", 0)])
-def test_sharded_failure_reaches_every_rank(fail_in, fail_rank):
+@pytest.mark.parametrize("fail_in,fail_rank,caps", [("stylize", 1, None), ("stylize", 0, None), ("consume", 0, None),
+                                                    ("stylize", 2, [1, 2, 2]), ("consume", 0, [1, 2, 2])])
+def test_sharded_failure_reaches_every_rank(fail_in, fail_rank, caps):
     """A rank whose stylize (or rank 0 whose consume) raises must not leave the others blocked in the
-    point-to-point exchange: every rank stops (the failing one with its own error)."""
+    point-to-point exchange: every rank stops (the failing one with its own error); also with rank 0's lighter
+    share (caps: groups of 5 frames, 1 of them on rank 0)."""
     import torch.multiprocessing as mp
     world = 3
     with socket.socket() as s:
@@ -135,7 +158,8 @@ def test_sharded_failure_reaches_every_rank(fail_in, fail_rank):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, fail_rank, fail_in, q)) for r in range(world)]
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, fail_rank, fail_in, q, caps))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {r: (o, c) for r, o, c in (q.get(timeout=120) for _ in range(world))}
@@ -144,7 +168,9 @@ def test_sharded_failure_reaches_every_rank(fail_in, fail_rank):
     own = "ValueError" if fail_in == "stylize" else "OSError"
     for r in range(world):
         assert res[r][0] == (own if r == fail_rank else "RankFailed"), (r, res[r])
-    assert res[0][1] == [[0, 1, 2, 3, 4, 5]]  # the group before the failure was consumed, nothing after
+    # the group before the failure was consumed, nothing after (groups of 6 frames; 5 with caps [1, 2, 2], where
+    # the failing group is [5..7], whose frames >= 4 fail on every rank holding one)
+    assert res[0][1] == ([[0, 1, 2, 3, 4, 5]] if caps is None else [[0, 1, 2, 3, 4]])
 
 
 def test_run_videos_env_mapping(monkeypatch):
