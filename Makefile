@@ -19,8 +19,9 @@ $(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h $(C
 	@mkdir -p $(BUILD)
 	$(if $(NOSCRATCH),$(HIPCC) $(CXXFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $@.rem && python3 tools/check_scratch.py $@.rem || { rm -f $@; exit 1; },$(HIPCC) $(CXXFLAGS) -c $< -o $@)
 
-# kernels with hand-counted vmcnt waits: report any scratch use (tools/check_scratch.py; NST_STRICT_SCRATCH=1 fails)
-$(BUILD)/conv_wstat.hip.o $(BUILD)/conv_wphase.hip.o $(BUILD)/conv_ws9.hip.o $(BUILD)/conv_gemm.hip.o: NOSCRATCH = 1
+# kernels with hand-counted vmcnt waits: the build fails on any scratch use (tools/check_scratch.py; NST_STRICT_SCRATCH=0
+# reports instead, for experiment builds)
+$(BUILD)/conv_wstat.hip.o $(BUILD)/conv_wphase.hip.o $(BUILD)/conv_ws9.hip.o $(BUILD)/conv_gemm.hip.o $(BUILD)/conv_ws2.hip.o: NOSCRATCH = 1
 
 # the persistent kernels fully unroll a long K loop (static register / LDS indices): lift the
 # pragma-unroll size cap for that translation unit only

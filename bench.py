@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=3, help="timed 1080p frames per CPU configuration")
     ap.add_argument("--no-fp16", action="store_true", help="skip the fp16-mode timing")
     ap.add_argument("--no-fp32s", action="store_true", help="skip the split-fp16 (fp32s) mode timing")
+    ap.add_argument("--no-fp16m", action="store_true", help="skip the split-head fp16 (fp16m) mode timing")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="process-group backend for --gpus N > 1 (nccl = RCCL over xGMI; gloo stages the exchange "
                          "through host memory, so N ranks can rehearse the multi-GPU command on one GPU)")
@@ -158,6 +159,57 @@ def _measured_peaks():
                 "what": "v_mfma_f32_16x16x32_bf16 back to back on random operands at two waves per SIMD; streaming copy"}
     except (OSError, KeyError, ValueError):
         return None
+
+
+def layer_flops(H: int, W: int) -> dict:
+    """Algorithmic FLOP per frame of each Johnson layer (transformer_net.py:4-41): 2 cin cout k^2
+    per output pixel (the up-convs at the upsampled resolution)."""
+    h2, w2, h4, w4 = (H + 1) // 2, (W + 1) // 2, (H + 3) // 4, (W + 3) // 4
+    f = {"conv1.conv2d": 2 * 3 * 32 * 81 * H * W, "conv2.conv2d": 2 * 32 * 64 * 9 * h2 * w2,
+         "conv3.conv2d": 2 * 64 * 128 * 9 * h4 * w4, "deconv1.conv2d": 2 * 128 * 64 * 9 * h2 * w2,
+         "deconv2.conv2d": 2 * 64 * 32 * 9 * H * W, "deconv3.conv2d": 2 * 32 * 3 * 81 * H * W}
+    for r in range(1, 6):
+        for c in (1, 2):
+            f[f"res{r}.conv{c}.conv2d"] = 2 * 128 * 128 * 9 * h4 * w4
+    return f
+
+
+# NST_DT_F16M's split-precision layers and their MFMA issue cost per algorithmic product (nst_api.cpp layer_kdt):
+# the first layer 2 fp16 MFMAs (Wh x + Wl x), the down-convs and the first residual block 3 (Wh xh + Wh xl + Wl xh;
+# the generic kernels of the first residual block issue 4: two per 16-channel K step)
+F16M_MFMA_PER_PRODUCT = {"conv1.conv2d": 2, "conv2.conv2d": 3, "conv3.conv2d": 3, "res1.conv1.conv2d": 4,
+                         "res1.conv2.conv2d": 4}
+# bytes per element each F16M layer reads / writes (fp32 activations in the split head)
+F16M_IO_BYTES = {"conv1.conv2d": (2, 4), "conv2.conv2d": (4, 4), "conv3.conv2d": (4, 4), "res1.conv1.conv2d": (4, 4),
+                 "res1.conv2.conv2d": (4, 4)}
+
+
+def mode_roofline(eng, frames, H: int, W: int, nloc: int) -> dict:
+    """The dominant kernel of a precision mode (largest share of a profiled step): its algorithmic FLOP per launch /
+    its average launch time (HIP events on the forward's stream) against the fp16 MFMA peak divided by the MFMA
+    issues per product of its arithmetic, and its algorithmic HBM bytes per launch."""
+    eng.profile_begin()
+    torch.cuda.synchronize(frames.device)
+    for _ in range(3):
+        eng.stylize_u8(frames, PRESET)
+    torch.cuda.synchronize(frames.device)
+    prof = eng.profile_end()
+    name, ms, cnt = max(prof, key=lambda t: t[1])
+    avg_ms = ms / max(cnt, 1)
+    fl = layer_flops(H, W)[name] * nloc
+    mpp = F16M_MFMA_PER_PRODUCT.get(name, 1)
+    peak = MFMA_BF16_PEAK_TFLOPS / mpp
+    ach = fl / (avg_ms * 1e-3) / 1e12
+    cin, cout = {"conv1.conv2d": (3, 32), "conv2.conv2d": (32, 64), "conv3.conv2d": (64, 128),
+                 "deconv1.conv2d": (128, 64), "deconv2.conv2d": (64, 32), "deconv3.conv2d": (32, 3)}.get(name, (128, 128))
+    ib, ob = F16M_IO_BYTES.get(name, (2, 2))
+    stride_in = {"conv2.conv2d": 2, "conv3.conv2d": 2, "deconv1.conv2d": 0.5, "deconv2.conv2d": 0.5}.get(name, 1)
+    opix = fl / nloc / (2 * cin * cout * (81 if name in ("conv1.conv2d", "deconv3.conv2d") else 9))
+    byts = nloc * opix * (cin * ib * stride_in * stride_in + cout * ob)
+    return {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": None, "avg_launch_ms": round(avg_ms, 4),
+            "flop_per_launch": fl, "mfma_issues_per_product": mpp, "algorithmic_bytes_per_launch": int(byts),
+            "per_layer_avg_ms": {n: round(t / max(c, 1), 4) for n, t, c in prof}}
 
 
 def _kernel_sha() -> str:
@@ -272,6 +324,9 @@ def main():
     for key, dt, skip, what in (
             ("fp16_mode", "fp16", args.no_fp16,
              "NST_DT_F16: the bench kernels with fp16 weights/activations (fp16 MFMA, fp32 accumulate)"),
+            ("fp16m_mode", "fp16m", args.no_fp16m,
+             "NST_DT_F16M: split-fp16 operands and weights (fp32 activations) on the first layer, the down-convs and "
+             "the first residual block, fp16 kernels elsewhere: the +-1 LSB bar at most of the fp16 rate"),
             ("fp32s_mode", "fp32s", args.no_fp32s,
              "NST_DT_F32S: fp32 activations, every conv operand an fp16 hi/lo pair (two fp16 MFMAs per K step, "
              "generic kernels): the fp32 parity mode's +-1 LSB bar")):
@@ -283,6 +338,8 @@ def main():
         t_alt = time_steps(lambda: e_alt.stylize_u8(frames, PRESET), max(3, min(args.steps, 10)))
         alt_modes[key] = (e_alt, {"frames_per_s": round(nloc / t_alt, 2), "ms_per_step": round(t_alt * 1e3, 4),
                                   "what": what})
+        if dt == "fp16m":
+            alt_modes[key][1]["roofline"] = mode_roofline(e_alt, frames, H, W, nloc)
 
     # profiled pass: per-conv HIP events on the forward's stream
     kp = max(3, min(args.steps, 10))

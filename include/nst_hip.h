@@ -50,6 +50,12 @@ extern "C" {
                          v = hi + lo in LDS (weights at pack time), and two v_mfma_f32_16x16x32_f16 per K step give
                          Wh*(xh + xl) + Wl*xh: ~22 significant bits per product (the fp32 parity bar) at a quarter of
                          the exact-f32 MFMA cycles.  Conv inputs must stay inside the fp16 range (|v| <= 65504) */
+#define NST_DT_F16M 4 /* split-precision head + fp16 trunk (Johnson / NST nets): the first layer takes the raw bytes
+                         (exact) against fp16 hi/lo weight pairs, the two down-convs and the first residual block
+                         run split-fp16 operands and weights (Wh*xh + Wh*xl + Wl*xh) with fp32 activations, and the
+                         rest of the net runs the fp16 mode's kernels.  The layers whose rounding reaches the frame
+                         most (tests/precision_study.py) keep ~22-bit products: 1080p frames within +-1 LSB of the
+                         fp32 reference at about 3/4 of the fp16 mode's rate.  ReCoNet: NST_E_INVALID */
 
 /* ---- I/O formats for nst_forward ---- */
 #define NST_IO_F32_NCHW 0 /* raw model tensor [n,3,h,w] fp32 (TransformerNet.forward(X) surface) */
@@ -104,7 +110,9 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
 #define NST_KSEL_NO_PREPAD 0x20           /* first layer over the pre-padded encoded frame (conv_prep.hip) */
 #define NST_KSEL_NO_PERSISTENT 0x40       /* generic persistent LDS-weight-ring kernels */
 #define NST_KSEL_UNFUSED_RESIDUAL 0x80    /* residual add as a separate kernel */
-#define NST_KSEL_ALL 0xff
+#define NST_KSEL_NO_FOLD 0x100            /* uint8 frames: stage the encoded value instead of the raw byte with the
+                                             io_preset encode folded into the first layer's weights */
+#define NST_KSEL_ALL 0x1ff
 int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                   unsigned flags, nst_handle** out);
 void nst_destroy(nst_handle* h);
@@ -155,7 +163,11 @@ typedef struct nst_op_desc {
   int out_h, out_w; /* stored output extent */
   int cin_stride, cout_stride;
   int kernel_mode;  /* internal kernel family (0 generic, 1 phase, 2 x-shift, 3 out9, 4 wstat, 5 wphase, 6 ws2, 7 ws9) */
-  int elem_bytes;   /* 2 (bf16) or 4 (fp32) */
+  int elem_bytes;   /* bytes per element of what the op writes (act[i]): 2 (bf16 / fp16) or 4 (fp32) */
+  int in_elem_bytes;  /* bytes per element of src (NST_BUF_INPUT: the staged first-layer operand, 2 or 4) */
+  int res_elem_bytes; /* bytes per element of the joined residual stream (res_buf / res_out), 0 if none */
+  int kernel_dtype;   /* the op's arithmetic: an NST_DT_* value, or 16 / 17 (fp16 operand x fp16 hi/lo weight
+                         pairs, fp32 / fp16 output) and 18 / 19 (split fp16 operand and weights, fp32 / fp16 output) */
 } nst_op_desc;
 int nst_num_ops(const nst_handle* h);
 int nst_op_describe(const nst_handle* h, int n, int in_h, int in_w, int op, nst_op_desc* out);

@@ -16,7 +16,9 @@ LIB_PATH = os.environ.get("NST_HIP_LIB", os.path.join(_HERE, "libnst_hip.so"))
 
 NST_OK = 0
 NST_ARCH_JOHNSON, NST_ARCH_NST, NST_ARCH_RECONET, NST_ARCH_RECONET_FRN = 0, 1, 2, 3
-NST_DT_F32, NST_DT_BF16, NST_DT_F16, NST_DT_F32S = 0, 1, 2, 3
+NST_DT_F32, NST_DT_BF16, NST_DT_F16, NST_DT_F32S, NST_DT_F16M = 0, 1, 2, 3, 4
+# kernel dtypes of the NST_DT_F16M split-precision layers (nst_op_desc.kernel_dtype)
+NST_KDT_SW_O32, NST_KDT_SW_O16, NST_KDT_SPLIT_O32, NST_KDT_SPLIT_O16 = 16, 17, 18, 19
 NST_VGG_GENERIC_ONLY = 0x1
 NST_IO_F32_NCHW, NST_IO_U8_NHWC = 0, 1
 PRESETS = {
@@ -55,7 +57,7 @@ NST_GRAM_CHW, NST_GRAM_HWC = 0, 1
 # nst_create_ex kernel-selection flags (include/nst_hip.h NST_KSEL_*)
 KSEL = {
     "no_wstat": 0x1, "no_wphase": 0x2, "no_ws2": 0x4, "no_ws9": 0x8, "no_kyrot": 0x10, "no_prepad": 0x20,
-    "no_persistent": 0x40, "unfused_residual": 0x80,
+    "no_persistent": 0x40, "unfused_residual": 0x80, "no_fold": 0x100,
 }
 NST_BUF_INPUT, NST_BUF_OUTPUT = -1, -2
 
@@ -68,7 +70,7 @@ class NstOpDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "kind", "layer", "src", "dst", "in_norm", "in_relu", "res_buf", "res_norm", "res_out", "relu_out",
         "in_h", "in_w", "conv_h", "conv_w", "out_h", "out_w", "cin_stride", "cout_stride", "kernel_mode",
-        "elem_bytes")]
+        "elem_bytes", "in_elem_bytes", "res_elem_bytes", "kernel_dtype")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -1333,6 +1333,7 @@ struct ConvInst {
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
+    std::memset(&k, 0, sizeof(k));  // fields this mapping does not set (wbytes, tanh_out, in/out_esz, ...) are 0
     k.dtype = dtype_code<T>();
     k.mode = MODE;
     k.ks = KS; k.stride = S; k.cinp = CINP; k.bn = BN; k.th = TH; k.tw = TW; k.wm = WM; k.wn = WN;

@@ -8,7 +8,9 @@
 // 8 bytes per pixel, so the conv fill is plain 16-byte loads (two pixels per LDS entry) with an
 // identity coordinate map.  Arithmetic per element is the reference's: x01 = byte / 255 (ToTensor),
 // ((x01 * a) - b) / d, one RNE rounding to the 16-bit format — bit-identical to the fused encode it replaces
-// (for uint8 frames through a per-block table of the 3 x 256 possible values).
+// (for uint8 frames through a per-block table of the 3 x 256 possible values).  With p.enc_raw the staged value
+// is byte / 256 (exact in either format) and the first layer's weights carry the encode instead
+// (nst_api.cpp fold_first_layer): the operand then adds no rounding at all.
 #include <algorithm>
 
 #include "conv_impl.h"
@@ -51,7 +53,8 @@ __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int
   for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
     const int ch = i >> 8, b = i & 255;
     const float x01 = (float)b / 255.0f;  // ToTensor: .float().div(255)
-    const float v = ((x01 * p.enc_a[ch]) - p.enc_b[ch]) / p.enc_d[ch];
+    // enc_raw: the byte itself, scaled by 2^-8 (exact); the encode is folded into the layer's weights and bias
+    const float v = p.enc_raw ? (float)b * 0.00390625f : ((x01 * p.enc_a[ch]) - p.enc_b[ch]) / p.enc_d[ch];
     lut[ch][b] = (uint16_t)(pack16<T>(v, 0.f) & 0xffffu);
   }
   __syncthreads();

@@ -449,10 +449,10 @@ struct WphaseInst {
       const int nb = std::min(p.n_work, cus());
       const bool zp = p.axis_mode == AX_ZERO;  // ConvTranspose: zeros past the edge
       if constexpr (RES) {
-        if (p.res_rnorm != nullptr)
-          zp ? go<WF_RESRN, true>(p, nb, st) : go<WF_RESRN, false>(p, nb, st);
-        else
-          zp ? go<WF_RES, true>(p, nb, st) : go<WF_RES, false>(p, nb, st);
+        // the join of a normalised stream (WF_RESRN) is not instantiated: it spilled (12-16 B of scratch per lane
+        // in a counted-vmcnt kernel) and no program reaches it (the up-conv joins the stored x_5; nst_api rejects
+        // a normalised residual for this kernel before launching)
+        if (p.res_rnorm == nullptr) zp ? go<WF_RES, true>(p, nb, st) : go<WF_RES, false>(p, nb, st);
       } else {
         if (p.in_norm != nullptr)
           zp ? go<WF_NORM, true>(p, nb, st) : go<WF_NORM, false>(p, nb, st);

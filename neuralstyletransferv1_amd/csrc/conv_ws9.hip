@@ -53,9 +53,16 @@ constexpr int WS9_NW = NST_WS9_NW;    // waves per workgroup: 4 = two workgroups
 #endif
 constexpr int WS9_RING = NST_WS9_RING;  // input-row operands in flight ahead of the MFMAs
 
-template <int NW_>
+// SW (split weights, the split-precision modes' first layer): the exact raw-byte operand of conv_prep.hip's
+// enc_raw staging against fp16 hi / lo weight pairs (Wh = RNE(w), Wl = RNE(w - Wh)): the two MFMAs the plain
+// kernel spends on the two 16-channel M tiles go to Wh and Wl of ONE M tile, into separate accumulators added in
+// the epilogue, so a wave covers 16 output channels (wave w: channel half w / (NW/2), 16-column strip w % (NW/2))
+// and a tile is half as wide.  O32: fp32 output (the next layer reads it as a split hi / lo operand).
+template <int NW_, bool SW = false, bool O32 = false>
 struct W9Cfg {
-  static constexpr int NW = NW_, NT = 64 * NW, TH = WS9_TH, TW = 16 * NW, COUT = 32;
+  static constexpr int NW = NW_, NT = 64 * NW, TH = WS9_TH, COUT = 32;
+  static constexpr int NSTRIP = SW ? NW / 2 : NW;  // 16-column strips per tile
+  static constexpr int TW = 16 * NSTRIP;
   static constexpr int HR = TH + 8;                 // halo rows
   // 16-B chunks per halo row: TW + 8 px used, rounded up so the row stride is == 32 mod 64 dwords
   // (the column-8 operand's four rows land in disjoint bank halves)
@@ -64,32 +71,38 @@ struct W9Cfg {
   static constexpr int HALO = HR * RS;
   static constexpr int NCHK = HR * RCH;
   static constexpr int NREQ = (NCHK + NT - 1) / NT; // request slots per thread (the last partial)
-  static constexpr int PIXB = COUT * 2;             // 64 B per output pixel
+  static constexpr int PIXB = COUT * (O32 ? 4 : 2);  // bytes per output pixel
   static constexpr int OUT_OFF = 2 * HALO;
   static constexpr int OUTB = TH * TW * PIXB;       // the LDS output tile
   static constexpr int NST = TH * TW * PIXB / (NT * 16);  // 16-B stores per thread
+  static constexpr int PXS = NT * 16 / PIXB;        // output pixels per store instruction
   static constexpr int PART_OFF = OUT_OFF + OUTB;
   static constexpr int BIAS_OFF = PART_OFF + NW * 64 * 4;
   static constexpr int LDS = BIAS_OFF + COUT * 4;
   static constexpr int NWM = 9 * 2;                 // 16x16x32 weight fragments (ky, m)
   static constexpr int NWK = 3 * 2;                 // 16x16x16 weight fragments (j, m)
-  static constexpr int WBYTES = NWM * 64 * 16 + NWK * 64 * 8;
+  static constexpr int WHALF = NWM * 64 * 16 + NWK * 64 * 8;  // one weight set (SW: one channel half)
+  static constexpr int WBYTES = (SW ? 2 : 1) * WHALF;
   static_assert(NCHK % 64 == 0, "whole-wave DMA requests");
   static_assert(2 * RCH >= TW + 8 && (RS / 4) % 64 == 32, "halo row");
   static_assert(NST * NT * 16 == TH * TW * PIXB, "whole 16-B stores per thread");
+  static_assert(PXS % TW == 0, "a store instruction covers whole tile rows (a thread's column is fixed)");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 
-template <typename T, int NW>
+template <typename T, int NW, bool SW, bool O32>
 __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
-  using C = W9Cfg<NW>;
+  using C = W9Cfg<NW, SW, O32>;
+  static_assert(!SW || IS_F16<T>, "split weights are fp16 pairs");
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, px = lane & 15;
+  const int strip = SW ? wv % C::NSTRIP : wv;  // the wave's 16 output columns
+  const int mh = SW ? wv / C::NSTRIP : 0;      // SW: the wave's 16 output channels 16 mh ..
 
   struct Work {
     int n, tile, oy0, ox0;
@@ -109,14 +122,16 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   const int w0 = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
   if (w0 >= p.n_work) return;
 
-  // ---- the whole weight tensor, resident for the launch (same in every wave) ----
+  // ---- the whole weight tensor (SW: the wave's channel half, hi and lo), resident for the launch ----
+  // wm[2 ky + m]: M tile m (plain) or weight part m = hi / lo of channel half mh (SW); wk likewise
   uint4 wm[C::NWM];
   uint2 wk[C::NWK];
   {
-    const uint4* src = (const uint4*)p.wpk + lane;
+    const char* wbase = (const char*)p.wpk + (size_t)mh * C::WHALF;
+    const uint4* src = (const uint4*)wbase + lane;
 #pragma unroll
     for (int s = 0; s < C::NWM; ++s) wm[s] = src[s * 64];
-    const uint2* srck = (const uint2*)((const char*)p.wpk + C::NWM * 64 * 16) + lane;
+    const uint2* srck = (const uint2*)(wbase + C::NWM * 64 * 16) + lane;
 #pragma unroll
     for (int s = 0; s < C::NWK; ++s) wk[s] = srck[s * 64];
   }
@@ -162,8 +177,8 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   };
   // ---- K loop over the wave's 16 halo rows ----
   auto kloop = [&](Acc& acc, int buf) {
-    int fb = buf * C::HALO + (16 * wv + px + 2 * g) * 8;  // row-r operand: + r * RS
-    int kb = buf * C::HALO + (16 * wv + px + 8) * 8;      // column-8 operand rows r + g (clamped)
+    int fb = buf * C::HALO + (16 * strip + px + 2 * g) * 8;  // row-r operand: + r * RS
+    int kb = buf * C::HALO + (16 * strip + px + 8) * 8;      // column-8 operand rows r + g (clamped)
     asm volatile("" : "+v"(fb), "+v"(kb));
     // the row operand of lane (px, g) starts at pixel 16 wv + px + 2g: 8-byte aligned, not 16.  A ds_read_b128 off
     // its 16-byte alignment is replayed at ~64 cycles per wave-instruction (cdna_hip_programming.md Guideline
@@ -217,61 +232,117 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
 
   // ---- epilogue: bias, 16-bit values into the LDS output tile, IN partials from the fp32 values ----
   auto epilogue = [&](const Work& wk_, Acc& acc) {
-    const f32x4_t bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (4 * g) * 4);
-    const f32x4_t bias1 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 + 4 * g) * 4);
-    const int e = 2 * ((px >> 2) & 3);  // slot swizzle of this lane's pixel
-    int obase = C::OUT_OFF + (16 * wv + px) * C::PIXB;
-    asm volatile("" : "+v"(obase));
-    const int o0 = ((0 + g) ^ e) * 8, o1 = ((4 + g) ^ e) * 8;
-    f32x4_t s1a = {0.f, 0.f, 0.f, 0.f}, s2a = s1a, s1b = s1a, s2b = s1a;
-    // interior tiles (all but the frame's last row / column of tiles) take the select-free copy
-    auto rows = [&](auto masked) {
+    if constexpr (!SW) {
+      const f32x4_t bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (4 * g) * 4);
+      const f32x4_t bias1 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 + 4 * g) * 4);
+      const int e = 2 * ((px >> 2) & 3);  // slot swizzle of this lane's pixel
+      int obase = C::OUT_OFF + (16 * wv + px) * C::PIXB;
+      asm volatile("" : "+v"(obase));
+      const int o0 = ((0 + g) ^ e) * 8, o1 = ((4 + g) ^ e) * 8;
+      f32x4_t s1a = {0.f, 0.f, 0.f, 0.f}, s2a = s1a, s1b = s1a, s2b = s1a;
+      // interior tiles (all but the frame's last row / column of tiles) take the select-free copy
+      auto rows = [&](auto masked) {
 #pragma unroll
-      for (int y = 0; y < C::TH; ++y) {
-        const f32x4_t va = add4(acc[y][0], bias0), vb = add4(acc[y][1], bias1);
-        const u32x2_t pa = {pack16<T>(va[0], va[1]), pack16<T>(va[2], va[3])};
-        const u32x2_t pb = {pack16<T>(vb[0], vb[1]), pack16<T>(vb[2], vb[3])};
-        *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o0) = pa;
-        *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o1) = pb;
-        f32x4_t xa = va, xb = vb;
-        if constexpr (decltype(masked)::value) {
-          const bool valid = wk_.oy0 + y < p.oh && wk_.ox0 + 16 * wv + px < p.ow;
-          const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
-          xa = valid ? va : z;
-          xb = valid ? vb : z;
+        for (int y = 0; y < C::TH; ++y) {
+          const f32x4_t va = add4(acc[y][0], bias0), vb = add4(acc[y][1], bias1);
+          const u32x2_t pa = {pack16<T>(va[0], va[1]), pack16<T>(va[2], va[3])};
+          const u32x2_t pb = {pack16<T>(vb[0], vb[1]), pack16<T>(vb[2], vb[3])};
+          *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o0) = pa;
+          *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o1) = pb;
+          f32x4_t xa = va, xb = vb;
+          if constexpr (decltype(masked)::value) {
+            const bool valid = wk_.oy0 + y < p.oh && wk_.ox0 + 16 * wv + px < p.ow;
+            const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+            xa = valid ? va : z;
+            xb = valid ? vb : z;
+          }
+          stat4(s1a, s2a, xa);
+          stat4(s1b, s2b, xb);
         }
-        stat4(s1a, s2a, xa);
-        stat4(s1b, s2b, xb);
-      }
-    };
-    if (wk_.oy0 + C::TH <= p.oh && wk_.ox0 + C::TW <= p.ow)
-      rows(std::false_type{});
-    else
-      rows(std::true_type{});
-    // value v = 8 m + 2 c + k (channel 16 m + 4 g + c, k = sum / sum of squares); after the
-    // reduce-scatter over the 16 pixel lanes lane px holds the row total of value px
-    const float vv[16] = {s1a[0], s2a[0], s1a[1], s2a[1], s1a[2], s2a[2], s1a[3], s2a[3],
-                          s1b[0], s2b[0], s1b[1], s2b[1], s1b[2], s2b[2], s1b[3], s2b[3]};
-    float a8[8], a4[4], a2[2], a1[1];
-    rs_step<8, 0x140>(vv, a8, px >= 8);
-    rs_step<4, 0x141>(a8, a4, (px & 4) != 0);
-    rs_step<2, 0x1b>(a4, a2, (px & 2) != 0);
-    rs_step<1, 0xb1>(a2, a1, (px & 1) != 0);
-    const int ch = 16 * (px >> 3) + 4 * g + ((px >> 1) & 3);
-    ((float*)(smem + C::PART_OFF))[wv * 64 + ch * 2 + (px & 1)] = a1[0];
+      };
+      if (wk_.oy0 + C::TH <= p.oh && wk_.ox0 + C::TW <= p.ow)
+        rows(std::false_type{});
+      else
+        rows(std::true_type{});
+      // value v = 8 m + 2 c + k (channel 16 m + 4 g + c, k = sum / sum of squares); after the
+      // reduce-scatter over the 16 pixel lanes lane px holds the row total of value px
+      const float vv[16] = {s1a[0], s2a[0], s1a[1], s2a[1], s1a[2], s2a[2], s1a[3], s2a[3],
+                            s1b[0], s2b[0], s1b[1], s2b[1], s1b[2], s2b[2], s1b[3], s2b[3]};
+      float a8[8], a4[4], a2[2], a1[1];
+      rs_step<8, 0x140>(vv, a8, px >= 8);
+      rs_step<4, 0x141>(a8, a4, (px & 4) != 0);
+      rs_step<2, 0x1b>(a4, a2, (px & 2) != 0);
+      rs_step<1, 0xb1>(a2, a1, (px & 1) != 0);
+      const int ch = 16 * (px >> 3) + 4 * g + ((px >> 1) & 3);
+      ((float*)(smem + C::PART_OFF))[wv * 64 + ch * 2 + (px & 1)] = a1[0];
+    } else {
+      // hi + lo partial sums of channels 16 mh + 4 g .. + 3, + bias (fp32), into the staged tile
+      const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 * mh + 4 * g) * 4);
+      int obase = C::OUT_OFF + (16 * strip + px) * C::PIXB;
+      asm volatile("" : "+v"(obase));
+      // O32: 16-B chunk 4 mh + g of the 8-chunk pixel, XOR-swizzled by pixel (2-way at most); 16-bit: 8-B slot
+      const int oo = O32 ? (((4 * mh + g) ^ (px & 7)) * 16) : (((4 * mh + g) ^ (2 * ((px >> 2) & 3))) * 8);
+      f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
+      auto rows = [&](auto masked) {
+#pragma unroll
+        for (int y = 0; y < C::TH; ++y) {
+          const f32x4_t v = add4(add4(acc[y][0], acc[y][1]), bias);
+          if constexpr (O32) {
+            *(f32x4_t*)(smem + obase + y * C::TW * C::PIXB + oo) = v;
+          } else {
+            const u32x2_t pv = {pack16<T>(v[0], v[1]), pack16<T>(v[2], v[3])};
+            *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + oo) = pv;
+          }
+          f32x4_t x = v;
+          if constexpr (decltype(masked)::value) {
+            const bool valid = wk_.oy0 + y < p.oh && wk_.ox0 + 16 * strip + px < p.ow;
+            x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+          }
+          stat4(s1, s2, x);
+        }
+      };
+      if (wk_.oy0 + C::TH <= p.oh && wk_.ox0 + C::TW <= p.ow)
+        rows(std::false_type{});
+      else
+        rows(std::true_type{});
+      // reduce-scatter of the 8 statistics over the 16 pixel lanes, then the xor-1 partner: lane px (even)
+      // ends with statistic idx & 1 of channel 4 g + (idx >> 1) of the half, idx = 4 (px >= 8) + 2 (px & 4) + (px & 2) / 2
+      const float vv[8] = {s1[0], s2[0], s1[1], s2[1], s1[2], s2[2], s1[3], s2[3]};
+      float a4[4], a2[2], a1[1];
+      rs_step<4, 0x140>(vv, a4, px >= 8);
+      rs_step<2, 0x141>(a4, a2, (px & 4) != 0);
+      rs_step<1, 0x1b>(a2, a1, (px & 2) != 0);
+      const float t = a1[0] + dpp_f<0xb1>(a1[0]);
+      const int idx = (px >= 8 ? 4 : 0) + ((px & 4) ? 2 : 0) + ((px & 2) ? 1 : 0);
+      if ((px & 1) == 0) ((float*)(smem + C::PART_OFF))[wv * 64 + (4 * g + (idx >> 1)) * 2 + (idx & 1)] = t;
+    }
   };
-  // wave 0: the tile's partial row (fixed-order sum over the NW waves); all: whole-pixel stores
-  // store k of thread t: tile row k, pixel column t / 4, bytes 16 (t % 4) .. + 15 (NT / 4 == TW)
-  static_assert(C::NT / 4 == C::TW && C::NST == C::TH, "one tile row per store");
-  const int sx = tid >> 2, scb = (tid & 3) * 16;
-  int srd = C::OUT_OFF + sx * C::PIXB + (((scb >> 3) ^ (2 * ((sx >> 2) & 3))) << 3);
+  // wave 0: the tile's partial row (fixed-order sum over the waves of a channel half); all: whole-pixel stores.
+  // store k of thread t covers tile bytes (k NT + t) 16 .. + 15: pixel (k NT + t) / (PIXB / 16), chunk (t % (PIXB / 16))
+  constexpr int CPP = C::PIXB / 16;  // 16-B chunks per pixel
+  const int sq = tid / CPP, scb = (tid % CPP) * 16;  // pixel (within a store's PXS) and byte of this thread
+  auto lds_chunk = [&](int pp) {  // LDS address of this thread's chunk of tile pixel pp (row-major, TW per row)
+    const int x = pp % C::TW;
+    if constexpr (SW && O32) return C::OUT_OFF + pp * C::PIXB + (((scb >> 4) ^ (x & 7)) << 4);
+    return C::OUT_OFF + pp * C::PIXB + (((scb >> 3) ^ (2 * ((x >> 2) & 3))) << 3);
+  };
+  const int sx = sq % C::TW;  // this thread's tile column in every store
+  int srd = lds_chunk(sq);
   asm volatile("" : "+v"(srd));
   auto store_out = [&](const Work& wk_) {
     if (wv == 0) {
-      const float* pp = (const float*)(smem + C::PART_OFF) + lane;
-      float t = pp[0];
+      const float* pp = (const float*)(smem + C::PART_OFF);
+      float t;
+      if constexpr (!SW) {
+        t = pp[lane];
 #pragma unroll
-      for (int w = 1; w < C::NW; ++w) t += pp[w * 64];
+        for (int w = 1; w < C::NW; ++w) t += pp[w * 64 + lane];
+      } else {
+        const int ch = lane >> 1, h = ch >> 4, e = (ch & 15) * 2 + (lane & 1);
+        t = pp[(h * C::NSTRIP) * 64 + e];
+#pragma unroll
+        for (int s2 = 1; s2 < C::NSTRIP; ++s2) t += pp[(h * C::NSTRIP + s2) * 64 + e];
+      }
       const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * 64), (short)0, 256, 0x00020000);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (uint32_t)(lane * 4), 0, 0);
@@ -281,10 +352,11 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
         (void*)((char*)p.out + (size_t)wk_.n * obytes), (short)0, (int)obytes, 0x00020000);
     const uint32_t voff = (wk_.ox0 + sx < p.ow) ? (uint32_t)((wk_.ox0 + sx) * C::PIXB + scb) : 0x80000000u;
 #pragma unroll
-    for (int k = 0; k < C::NST; ++k) {  // store k = tile row k
-      const u32x4_t v = *(const u32x4_t*)(smem + srd + k * C::TW * C::PIXB);
-      if (wk_.oy0 + k < p.oh)
-        __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + k) * p.ow * C::PIXB, ST_AUX);
+    for (int k = 0; k < C::NST; ++k) {  // store k: tile rows (k PXS + sq) / TW
+      const int row = (k * C::PXS + sq) / C::TW;
+      const u32x4_t v = *(const u32x4_t*)(smem + srd + k * C::PXS * C::PIXB);
+      if (wk_.oy0 + row < p.oh)
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + row) * p.ow * C::PIXB, ST_AUX);
     }
   };
 
@@ -316,9 +388,9 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   vm_wait<0>();
 }
 
-template <typename T, int NW>
+template <typename T, int NW, bool SW = false, bool O32 = false>
 struct Ws9Inst {
-  using C = W9Cfg<NW>;
+  using C = W9Cfg<NW, SW, O32>;
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;
@@ -333,14 +405,17 @@ struct Ws9Inst {
     ConvParams p = p0;
     p.n_work = (int)grid.x * (int)grid.y;
     const int nb = std::min(p.n_work, cus() * (8 / NW));  // 8 waves per CU (VGPRs)
-    hipLaunchKernelGGL((ws9_kernel<T, NW>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((ws9_kernel<T, NW, SW, O32>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
     std::memset(&k, 0, sizeof(k));
-    k.dtype = dtype_code<T>();
+    k.dtype = SW ? (O32 ? NST_KDT_SW_O32 : NST_KDT_SW_O16) : dtype_code<T>();
     k.mode = MODE_WS9;
     k.ks = 9; k.stride = 1; k.cinp = 4; k.bn = C::COUT; k.th = C::TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
+    k.in_esz = 2;
+    k.out_esz = O32 ? 4 : 2;
+    k.split_w = SW ? 1 : 0;
     k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
     k.cpc = 4; k.nch = 1; k.lds_bytes = C::LDS;
     k.wbytes = C::WBYTES;
@@ -353,8 +428,10 @@ struct Ws9Inst {
 };
 
 const ConvKernelInfo* conv_table_ws9(int* count) {
-  static const ConvKernelInfo table[] = {Ws9Inst<__bf16, WS9_NW>::info(), Ws9Inst<_Float16, WS9_NW>::info()};
-  *count = 2;
+  static const ConvKernelInfo table[] = {Ws9Inst<__bf16, WS9_NW>::info(), Ws9Inst<_Float16, WS9_NW>::info(),
+                                         Ws9Inst<_Float16, WS9_NW, true, true>::info(),
+                                         Ws9Inst<_Float16, WS9_NW, true, false>::info()};
+  *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;
 }
 

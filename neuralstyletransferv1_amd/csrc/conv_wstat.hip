@@ -281,7 +281,9 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   // takes C = 0 (no VALU write feeds an MFMA), operands come from loads it waits for, an
   // accumulation chain needs no wait states, and mfma_drain() pads before the epilogue reads.
   auto kloop = [&](Acc& acc, auto&& hook, auto&& bound) {
-    constexpr int NI = 4 * PRD, D = WS_RING;
+    // the zero-padded join (NST_Train's trunk) keeps one operand read fewer in flight: at three it spilled 8 B
+    // per lane in this counted-vmcnt kernel (ring depth 2 / 3 / 4 measured within noise on the reflect trunk)
+    constexpr int NI = 4 * PRD, D = (RES && ZPAD) ? 2 : WS_RING;
     f32x4_t bias0;
     if constexpr (NST_WS_BIAS_C) bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 * wv + 4 * g) * 4);
     auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {

@@ -86,6 +86,12 @@ struct Layer {
   float eps = 1e-5f;  // InstanceNorm2d eps, or |FRN.eps|
   int frn = 0;        // statistics: mean / variance (InstanceNorm) or mean square (FRN, frn.py:71)
   bool prepad = false;  // image layer reading the pre-padded encoded input (conv_prep.hip)
+  int kdt = 0;                   // the layer's arithmetic (NST_DT_* / NST_KDT_*): the handle's dtype except in NST_DT_F16M
+  int in_esz = 2, out_esz = 2;   // activation element bytes it reads / writes
+  // image layer over pre-padded uint8 frames: weights / bias with the io_preset encode folded in, per preset
+  // (fold_first_layer; nullptr where the fold does not hold), used with the raw-byte staging (ConvParams::enc_raw)
+  void* wpk_fold[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  float* bias_fold[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 // Program steps
@@ -98,6 +104,7 @@ struct Op {
   int in_norm;   // OP_CONV: layer whose IN+ReLU the prologue applies (-1: identity); with res_buf: IN of src, no ReLU
   int r_buf, r_norm, r_relu, relu_out;  // OP_RESADD; OP_CONV with res_buf >= 0: the residual join in the fill
   int res_buf = -1, res_out = -1;       // OP_CONV: residual stream r (joined into the fill) / where it is written
+  int out_esz = 0;                      // OP_RESADD: element bytes of the stream it writes (0: the handle's)
 };
 
 static int round_up(int v, int a) { return (v + a - 1) / a * a; }
@@ -105,7 +112,11 @@ static bool is_reconet(int arch) { return arch == NST_ARCH_RECONET || arch == NS
 
 // x0_export (with fuse_res): block 1's conv1 also writes x_0 = ReLU(IN_2(C)) from its fill (only the
 // weight-stationary trunk kernel does), so block 2's join reads a stored x_0 like every later join
-static void build_program(int arch, bool fuse_res, bool x0_export, std::vector<LayerDef>& L, std::vector<Op>& P) {
+// split_head (NST_DT_F16M): the first residual block runs unfused on the split-precision generic kernels (fp32
+// activations) and a separate residual add writes x_1 = IN(y) + ReLU(IN_2(C)) as the fp16 stream; blocks 2..5 are
+// the fused fp16 program from that stored stream (block 2's conv1 reads x_1 as is, later joins read it)
+static void build_program(int arch, bool fuse_res, bool x0_export, std::vector<LayerDef>& L, std::vector<Op>& P,
+                          bool split_head = false) {
   L.clear();
   P.clear();
   auto conv = [&](int layer, int src, int dst, int in_norm) {
@@ -167,7 +178,25 @@ static void build_program(int arch, bool fuse_res, bool x0_export, std::vector<L
   conv(0, B_IMG, B_A, -1);
   conv(1, B_A, B_B, 0);
   conv(2, B_B, B_C, 1);
-  if (!fuse_res) {
+  if (split_head) {
+    conv(3, B_C, B_D, 2);
+    conv(4, B_D, B_E, 3);
+    resadd(4, B_E, B_F, B_C, 2, relu_out);
+    P.back().out_esz = 2;
+    int xbuf = B_F;
+    for (int r = 1; r < nres; ++r) {
+      const int l1 = 3 + 2 * r, l2 = 4 + 2 * r;
+      if (r == 1) {
+        conv(l1, B_F, B_D, -1);  // x_1 as stored: the fill applies nothing
+      } else {
+        const int xout = xbuf == B_F ? B_G : B_F;
+        convres(l1, B_E, l2 - 2, xbuf, -1, xout, relu_out, B_D);
+        xbuf = xout;
+      }
+      conv(l2, B_D, B_E, l1);
+    }
+    convres(u1, B_E, u1 - 1, xbuf, -1, -1, relu_out, B_A);
+  } else if (!fuse_res) {
     // residual stream lives in B_C; block k's input is C (block 1: IN+ReLU of layer 2, lazily)
     for (int r = 0; r < nres; ++r) {
       const int l1 = 3 + 2 * r, l2 = 4 + 2 * r;
@@ -319,6 +348,37 @@ std::vector<float> pack_weights(const ConvKernelInfo& k, const LayerDef& d, cons
             }
           }
         }
+  return out;
+}
+
+// Split-weight layouts (ConvKernelInfo::split_w): every 16-bit weight fragment f of the plain packing becomes
+// the pair (hi, lo) = (RNE16(w), w - RNE16(w)) — hi as its exact fp32 value, lo left in fp32 for
+// upload_weights(NST_DT_F16) to round, so Wl = RNE16(w - Wh).  Orders (what the kernels load):
+//   MODE_WS9 (conv_ws9.hip SW): [channel half mh][ky][hi, lo] 16x16x32 fragments, then [mh][j][hi, lo] 16x16x16
+//   MODE_WS2 (conv_ws2.hip SPL): [channel group cg][hi | lo][step]
+std::vector<float> split_weight_frags(const ConvKernelInfo& k, const std::vector<float>& pk) {
+  std::vector<float> out(pk.size() * 2);
+  size_t o = 0;
+  auto put = [&](const float* f, size_t n, bool lo) {
+    for (size_t i = 0; i < n; ++i) {
+      const float hi = f16_to_f32(f32_to_f16_rne(f[i]));
+      out[o++] = lo ? f[i] - hi : hi;
+    }
+  };
+  if (k.mode == MODE_WS9) {
+    const size_t fm = 64 * 8, fk = 64 * 4;  // elements per 16x16x32 / 16x16x16 fragment
+    const float* k8 = pk.data() + 18 * fm;
+    for (int mh = 0; mh < 2; ++mh) {
+      for (int ky = 0; ky < 9; ++ky)
+        for (int hl = 0; hl < 2; ++hl) put(pk.data() + (2 * ky + mh) * fm, fm, hl == 1);
+      for (int j = 0; j < 3; ++j)
+        for (int hl = 0; hl < 2; ++hl) put(k8 + (2 * j + mh) * fk, fk, hl == 1);
+    }
+  } else {  // MODE_WS2: [cg][step][lane][8] -> [cg][hl][step][lane][8]
+    const size_t per_cg = pk.size() / (k.bn / 16);
+    for (int cg = 0; cg < k.bn / 16; ++cg)
+      for (int hl = 0; hl < 2; ++hl) put(pk.data() + cg * per_cg, per_cg, hl == 1);
+  }
   return out;
 }
 
@@ -511,6 +571,8 @@ struct Plan {
   std::string err;
   // per op: input and output dims
   std::vector<int> ih, iw, oh, ow, ch, cw;  // ch/cw: conv extent (before crop)
+  // per op: element bytes of its source, its output and the residual stream it joins / writes (0: none)
+  std::vector<int> in_esz, out_esz, res_esz;
   size_t buf_bytes[NBUF] = {0, 0, 0, 0, 0, 0, 0};
   size_t partial_floats = 0;
   int out_h = 0, out_w = 0;
@@ -535,10 +597,11 @@ void tile_grid(const ConvKernelInfo& k, int sh, int sw, int oh, int ow, int* tx,
 
 Plan make_plan(const nst_handle* h, int n, int H, int W) {
   Plan P;
-  const size_t esz = act_elem_bytes(h->dtype);
-  int bh[NBUF], bw[NBUF];
+  int bh[NBUF], bw[NBUF], be[NBUF];  // extent and element bytes of what each buffer holds
+  for (int b = 0; b < NBUF; ++b) be[b] = (int)act_elem_bytes(h->dtype);
   const size_t nops = h->prog.size();
   P.ih.resize(nops); P.iw.resize(nops); P.oh.resize(nops); P.ow.resize(nops); P.ch.resize(nops); P.cw.resize(nops);
+  P.in_esz.assign(nops, 0); P.out_esz.assign(nops, 0); P.res_esz.assign(nops, 0);
   for (size_t i = 0; i < nops; ++i) {
     const Op& op = h->prog[i];
     const Layer& Ly = h->layers[op.layer];
@@ -554,8 +617,16 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
       // the conv kernels address a frame (a launch's frames, for the weight-stationary ones) with
       // 32-bit buffer offsets, 0x80000000 and up reserved as the out-of-range offset: one frame's
       // activation must stay below 2^31 bytes (a 16-bit 128-channel map of 8.4 Gpx / 4)
-      const size_t fin = (size_t)sh * sw * (op.src == B_IMG ? 8 : Ly.cinp) * esz;
-      const size_t fout = (size_t)ch * cw * Ly.coutp * esz;
+      const int iesz = op.src == B_IMG ? 2 : be[op.src];
+      if (op.src != B_IMG && iesz != Ly.in_esz) {
+        P.err = "internal: layer " + Ly.d.conv + " reads " + std::to_string(iesz) + "-byte activations, its kernel " +
+                std::to_string(Ly.in_esz);
+        return P;
+      }
+      P.in_esz[i] = iesz;
+      P.out_esz[i] = Ly.out_esz;
+      const size_t fin = (size_t)sh * sw * (op.src == B_IMG ? 4 : Ly.cinp) * iesz;
+      const size_t fout = (size_t)ch * cw * Ly.coutp * Ly.out_esz;
       if (std::max(fin, fout) >= (size_t)0x7FFFFF00u) {
         P.err = "input " + std::to_string(H) + "x" + std::to_string(W) + " too large: layer " + Ly.d.conv +
                 " needs " + std::to_string(std::max(fin, fout)) + " bytes per frame (limit 2^31)";
@@ -568,9 +639,11 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         const size_t pb = ((size_t)n * (ch + Ly.d.ks - 1) + prepad_slack_rows(wpad)) * wpad * 8;
         if (pb > P.pre_bytes) P.pre_bytes = pb;
       }
-      if (op.res_out >= 0) {  // the joined residual stream: same geometry as the conv input
-        bh[op.res_out] = sh; bw[op.res_out] = sw;
-        const size_t rb = (size_t)n * sh * sw * Ly.cinp * esz;
+      if (op.res_buf >= 0) P.res_esz[i] = be[op.res_buf];
+      if (op.res_out >= 0) {  // the joined residual stream: same geometry and format as the conv input
+        bh[op.res_out] = sh; bw[op.res_out] = sw; be[op.res_out] = iesz;
+        P.res_esz[i] = iesz;
+        const size_t rb = (size_t)n * sh * sw * Ly.cinp * iesz;
         if (rb > P.buf_bytes[op.res_out]) P.buf_bytes[op.res_out] = rb;
       }
       P.ih[i] = sh; P.iw[i] = sw; P.ch[i] = ch; P.cw[i] = cw;
@@ -583,8 +656,8 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         P.out_h = P.oh[i]; P.out_w = P.ow[i];
       } else {
         P.oh[i] = ch; P.ow[i] = cw;
-        bh[op.dst] = ch; bw[op.dst] = cw;
-        const size_t bytes = (size_t)n * ch * cw * Ly.coutp * esz;
+        bh[op.dst] = ch; bw[op.dst] = cw; be[op.dst] = Ly.out_esz;
+        const size_t bytes = (size_t)n * ch * cw * Ly.coutp * Ly.out_esz;
         if (bytes > P.buf_bytes[op.dst]) P.buf_bytes[op.dst] = bytes;
         int ttx, tty;
         tile_grid(*Ly.k_main, sh, sw, ch, cw, &ttx, &tty);
@@ -597,6 +670,12 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
     } else {
       P.ih[i] = P.oh[i] = bh[op.src];
       P.iw[i] = P.ow[i] = bw[op.src];
+      P.in_esz[i] = be[op.src];
+      P.res_esz[i] = be[op.r_buf];
+      P.out_esz[i] = op.out_esz ? op.out_esz : be[op.src];
+      be[op.dst] = P.out_esz[i];
+      const size_t rb = (size_t)n * bh[op.src] * bw[op.src] * Ly.coutp * P.out_esz[i];
+      if (rb > P.buf_bytes[op.dst]) P.buf_bytes[op.dst] = rb;
       bh[op.dst] = bh[op.src];
       bw[op.dst] = bw[op.src];
     }
@@ -655,6 +734,39 @@ bool preset_consts(int preset, PresetConsts& c) {
       return true;
     default: return false;
   }
+}
+
+// The first layer over uint8 frames with the io_preset encode folded into its weights: the reference feeds
+// x_c = ((byte[perm c] / 255) * a_c - b_c) / d_c (pipeline.py:1445-1486) to the conv; the engine stages
+// o_c = byte[perm c] / 256, exact in bf16 and fp16, so conv(W, x) = conv(W', o) + sum W b_c / d_c with
+//   W'[.][c] = W[.][c] * 256 a_c / (255 d_c),   bias' = bias - sum_{c,ky,kx} W[.][c][ky][kx] b_c / d_c
+// (fp64, then fp32; the reference's own fp32 rounding of x_c is ~2^-24 relative).  The operand then carries no
+// rounding at all, which in the 16-bit modes was the largest single source of output error (tests/precision_study.py).
+// The constant b_c / d_c survives reflection padding but not zero padding, so zero-padded first layers fold only
+// presets with b = 0 (raw_01 / raw_255 / tanh's b = 1 does not).  false: no fold for this preset.
+bool fold_first_layer(const LayerDef& d, const float* W, const float* b, int preset, std::vector<float>& Wf,
+                      std::vector<float>& bf) {
+  PresetConsts pc;
+  if (preset == NST_PRESET_NONE || !preset_consts(preset, pc)) return false;
+  if (d.axis_mode != AX_REFLECT)
+    for (int c = 0; c < 3; ++c)
+      if (pc.eb[c] != 0.f) return false;
+  const int kk = d.ks * d.ks;
+  Wf.assign(W, W + (size_t)d.cout * d.cin * kk);
+  bf.assign(b, b + d.cout);
+  for (int o = 0; o < d.cout; ++o) {
+    double sb = b[o];
+    for (int c = 0; c < d.cin; ++c) {
+      const double sc = 256.0 * (double)pc.ea[c] / (255.0 * (double)pc.ed[c]), sh = (double)pc.eb[c] / (double)pc.ed[c];
+      for (int t = 0; t < kk; ++t) {
+        const size_t i = ((size_t)o * d.cin + c) * kk + t;
+        Wf[i] = (float)((double)W[i] * sc);
+        sb -= (double)W[i] * sh;
+      }
+    }
+    bf[o] = (float)sb;
+  }
+  return true;
 }
 
 }  // namespace
@@ -755,11 +867,24 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
 int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                   unsigned flags, nst_handle** out) {
   if (!out || arch < 0 || arch > 3 || (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16 && compute_dtype != NST_DT_F16 &&
-                                           compute_dtype != NST_DT_F32S) ||
+                                           compute_dtype != NST_DT_F32S && compute_dtype != NST_DT_F16M) ||
       (flags & ~(unsigned)NST_KSEL_ALL) != 0) {
     set_error("nst_create: invalid arguments");
     return NST_E_INVALID;
   }
+  const bool f16m = compute_dtype == NST_DT_F16M;
+  if (f16m && (is_reconet(arch) || (flags & (NST_KSEL_UNFUSED_RESIDUAL | NST_KSEL_NO_WS9 | NST_KSEL_NO_WS2 | NST_KSEL_NO_PREPAD)))) {
+    set_error("nst_create: NST_DT_F16M is built for the Johnson / NST nets with the default kernel selection");
+    return NST_E_INVALID;
+  }
+  // per-layer arithmetic of NST_DT_F16M (tests/precision_study.py: these layers' roundings reach the frame most)
+  auto layer_kdt = [&](size_t li) -> int {
+    if (!f16m) return compute_dtype;
+    if (li == 0) return NST_KDT_SW_O32;            // raw-byte operand x fp16 hi / lo weights, fp32 out
+    if (li == 1 || li == 2) return NST_KDT_SPLIT_O32;  // split operand and weights, fp32 out
+    if (li == 3 || li == 4) return NST_DT_F32S;    // first residual block: the split-fp16 generic kernels
+    return NST_DT_F16;
+  };
   const bool no_pers = (flags & NST_KSEL_NO_PERSISTENT) != 0;
   *out = nullptr;
   std::map<std::string, const nst_param*> byname;
@@ -781,7 +906,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
   h->arch = arch; h->dtype = compute_dtype; h->device = device;
   std::vector<LayerDef> defs;
   const bool fuse_res = (flags & NST_KSEL_UNFUSED_RESIDUAL) == 0;
-  build_program(arch, fuse_res, fuse_res, defs, h->prog);
+  build_program(arch, fuse_res, fuse_res, defs, h->prog, f16m);
   // layers whose fill joins the residual stream run the VAR_RES instantiation
   std::vector<int> res_layer(defs.size(), 0);
   for (const Op& op : h->prog)
@@ -789,7 +914,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
   // activation channel padding: fp32 chunks hold 4 channels (K step 16); bf16 chunks 8 (K step 32),
   // and bf16 tiles above 32 channels come in multiples of 64 (48->64, 96->128)
   auto pad_ch = [&](int c) {
-    if (f32_storage(compute_dtype)) return round_up(c, 16);
+    if (f32_storage(compute_dtype)) return round_up(c, 16);  // (NST_DT_F16M: 32 / 64 / 128 either way)
     return c <= 32 ? 32 : round_up(c, 64);
   };
   int rc = NST_OK;
@@ -797,6 +922,8 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     Layer Ly;
     Ly.d = defs[li];
     const LayerDef& d = Ly.d;
+    const int kdt = layer_kdt(li);
+    Ly.kdt = kdt;
     const bool image_in = li == 0;
     const bool final_layer = d.norm.empty();
     Ly.cinp = image_in ? 4 : pad_ch(d.cin);
@@ -831,17 +958,17 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       // weight-stationary 9x9 kernel (conv_ws9.hip) where compiled, else the generic one
       Ly.k_main = (flags & NST_KSEL_NO_WS9)
                       ? nullptr
-                      : find_conv_kernel(compute_dtype, MODE_WS9, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0, no_pers);
+                      : find_conv_kernel(kdt, MODE_WS9, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0, no_pers);
       if (Ly.k_main) Ly.mode = MODE_WS9;
-      else Ly.k_main = find_conv_kernel(compute_dtype, MODE_STD, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0, no_pers);
+      else Ly.k_main = find_conv_kernel(kdt, MODE_STD, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_ACT, outk, 0, no_pers);
       if (Ly.k_main && d.stride == 1) { Ly.prepad = true; Ly.k_alt = Ly.k_main; modes.clear(); }
       else Ly.k_main = nullptr;
     }
     for (int mode : modes) {
-      Ly.k_main = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk, res_layer[li], no_pers);
+      Ly.k_main = find_conv_kernel(kdt, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, outk, res_layer[li], no_pers);
       Ly.k_alt = nullptr;
-      if (image_in) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk, 0, no_pers);
-      if (final_layer) Ly.k_alt = find_conv_kernel(compute_dtype, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW, 0, no_pers);
+      if (image_in) Ly.k_alt = find_conv_kernel(kdt, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, IN_F32_NCHW, outk, 0, no_pers);
+      if (final_layer) Ly.k_alt = find_conv_kernel(kdt, mode, d.ks, d.stride, Ly.cinp, Ly.coutp, ink, OUT_F32_NCHW, 0, no_pers);
       const bool tanh_ok = mode != MODE_KYROT || !Ly.k_main ||
                            (Ly.k_main->tanh_out == (is_reconet(arch) ? 1 : 0) && Ly.k_alt &&
                             Ly.k_alt->tanh_out == Ly.k_main->tanh_out);
@@ -870,8 +997,11 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       Ly.frn = final_layer ? 0 : 1;
     }
     auto upload_packed = [&](const std::vector<float>& pk, void** dst) -> int {
-      return upload_weights(compute_dtype, pk, dst);
+      if (Ly.k_main->split_w) return upload_weights(NST_DT_F16, split_weight_frags(*Ly.k_main, pk), dst);
+      return upload_weights(kdt, pk, dst);
     };
+    Ly.in_esz = Ly.k_main->in_esz ? Ly.k_main->in_esz : (int)act_elem_bytes(kdt);
+    Ly.out_esz = Ly.k_main->out_esz ? Ly.k_main->out_esz : (int)act_elem_bytes(kdt);
     if (Ly.mode == MODE_KYROT) {
       if ((rc = upload_packed(pack_kyrot_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if (Ly.mode == MODE_WSTAT) {
@@ -884,6 +1014,19 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       if ((rc = upload_packed(pack_ws9_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if ((rc = upload_packed(pack_weights(*Ly.k_main, d, W, Ly.coutp), &Ly.wpk)) != NST_OK) {
       break;
+    }
+    if (Ly.prepad && !f32_storage(compute_dtype) && !(flags & NST_KSEL_NO_FOLD)) {
+      for (int pr = 1; pr < 8 && rc == NST_OK; ++pr) {
+        std::vector<float> Wf, bfo;
+        if (!fold_first_layer(d, W, b, pr, Wf, bfo)) continue;
+        std::vector<float> pk = Ly.mode == MODE_WS9 ? pack_ws9_weights(*Ly.k_main, d, Wf.data())
+                                                    : pack_weights(*Ly.k_main, d, Wf.data(), Ly.coutp);
+        std::vector<float> bpad(Ly.coutp, 0.f);
+        std::copy(bfo.begin(), bfo.end(), bpad.begin());
+        if ((rc = upload_packed(pk, &Ly.wpk_fold[pr])) != NST_OK) break;
+        rc = upload(bpad.data(), bpad.size() * 4, (void**)&Ly.bias_fold[pr]);
+      }
+      if (rc != NST_OK) break;
     }
     std::vector<float> bp(Ly.coutp, 0.f), gp(Ly.coutp, 0.f), btp(Ly.coutp, 0.f);
     for (int c = 0; c < d.cout; ++c) {
@@ -910,7 +1053,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
   }
   // x_0 export needs block 1's conv1 on the weight-stationary kernel; otherwise block 2's join
   // normalises conv3's output itself (the same layers and residual layers either way)
-  if (fuse_res && h->layers[3].mode != MODE_WSTAT) build_program(arch, true, false, defs, h->prog);
+  if (fuse_res && !f16m && h->layers[3].mode != MODE_WSTAT) build_program(arch, true, false, defs, h->prog);
   *out = h;
   return NST_OK;
 }
@@ -925,6 +1068,10 @@ void nst_destroy(nst_handle* h) {
     if (Ly.bias) (void)hipFree(Ly.bias);
     if (Ly.gamma) (void)hipFree(Ly.gamma);
     if (Ly.beta) (void)hipFree(Ly.beta);
+    for (int pr = 0; pr < 8; ++pr) {
+      if (Ly.wpk_fold[pr]) (void)hipFree(Ly.wpk_fold[pr]);
+      if (Ly.bias_fold[pr]) (void)hipFree(Ly.bias_fold[pr]);
+    }
   }
   delete h;
 }
@@ -983,7 +1130,6 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
   }
   DeviceGuard guard(h->device);
   hipStream_t st = (hipStream_t)stream;
-  const size_t esz = act_elem_bytes(h->dtype);
   char* ws = (char*)workspace;
   void* bufs[NBUF];
   for (int b = 0; b < NBUF; ++b) bufs[b] = ws + P.off_buf[b];
@@ -996,22 +1142,23 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       off += align256((size_t)n * h->layers[li].coutp * 8);
     }
   }
-  // run op i over frames f0 .. f0 + n - 1 (every activation buffer holds its frames contiguously at the
-  // op's shape, every IN table is [frame][channel])
-  auto run_op = [&](size_t i, int f0, int n) -> int {
+  // run op i over the batch (every activation buffer holds its frames contiguously at the op's shape, every IN
+  // table is [frame][channel])
+  auto run_op = [&](size_t i) -> int {
     const Op& op = h->prog[i];
     const Layer& Ly = h->layers[op.layer];
-    const size_t in_fb = (size_t)P.ih[i] * P.iw[i] * Ly.cinp * esz, out_fb = (size_t)P.oh[i] * P.ow[i] * Ly.coutp * esz;
-    auto buf_in = [&](int b) { return (void*)((char*)bufs[b] + f0 * in_fb); };
-    auto buf_out = [&](int b) { return (void*)((char*)bufs[b] + f0 * out_fb); };
-    auto tab = [&](int layer) { return layer >= 0 ? stats[layer] + (size_t)f0 * h->layers[layer].coutp : nullptr; };
+    auto tab = [&](int layer) { return layer >= 0 ? stats[layer] : nullptr; };
     if (op.kind == OP_RESADD) {
       const int hw = P.oh[i] * P.ow[i];
-      hipError_t e = launch_residual(h->dtype, buf_out(op.src), tab(op.layer), buf_out(op.r_buf), tab(op.r_norm), op.r_relu,
-                                     op.relu_out, buf_out(op.dst), n, hw, Ly.coutp, st);
+      hipError_t e = (P.in_esz[i] == 4 && P.res_esz[i] == 4 && P.out_esz[i] == 2)
+                         ? launch_residual_f32_to_f16(bufs[op.src], tab(op.layer), bufs[op.r_buf], tab(op.r_norm),
+                                                      op.r_relu, op.relu_out, bufs[op.dst], n, hw, Ly.coutp, st)
+                         : launch_residual(h->dtype, bufs[op.src], tab(op.layer), bufs[op.r_buf], tab(op.r_norm), op.r_relu,
+                                           op.relu_out, bufs[op.dst], n, hw, Ly.coutp, st);
       if (e != hipSuccess) { set_error(std::string("residual launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
       if (cap && cap->act && cap->act[i])
-        NST_HIP_CHECK(hipMemcpyAsync(cap->act[i], bufs[op.dst], (size_t)n * hw * Ly.coutp * esz, hipMemcpyDeviceToDevice, st));
+        NST_HIP_CHECK(hipMemcpyAsync(cap->act[i], bufs[op.dst], (size_t)n * hw * Ly.coutp * P.out_esz[i],
+                                     hipMemcpyDeviceToDevice, st));
       return NST_OK;
     }
     const bool image_in = op.src == B_IMG, final_out = op.dst == B_OUT;
@@ -1020,7 +1167,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     if (final_out && y_fmt == NST_IO_F32_NCHW) k = Ly.k_alt;
     ConvParams p;
     std::memset(&p, 0, sizeof(p));
-    p.in = image_in ? x : buf_in(op.src);
+    p.in = image_in ? x : bufs[op.src];
     p.hs = P.ih[i];
     p.ws = P.iw[i];
     p.cs = image_in ? 3 : Ly.cinp;
@@ -1038,11 +1185,11 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     p.in_norm = tab(op.in_norm);
     p.in_relu = op.in_norm >= 0 && op.res_buf < 0 ? 1 : 0;
     if (op.res_buf >= 0) {
-      p.res_r = buf_in(op.res_buf);
+      p.res_r = bufs[op.res_buf];
       p.res_rnorm = tab(op.r_norm);
       p.res_relu = op.relu_out;
     }
-    p.res_out = op.res_out >= 0 ? buf_in(op.res_out) : nullptr;
+    p.res_out = op.res_out >= 0 ? bufs[op.res_out] : nullptr;
     for (int c = 0; c < 3; ++c) {
       p.enc_a[c] = pc.ea[c]; p.enc_b[c] = pc.eb[c]; p.enc_d[c] = pc.ed[c]; p.enc_perm[c] = pc.eperm[c];
       p.dec_p[c] = pc.dp[c]; p.dec_q[c] = pc.dq[c]; p.dec_r[c] = pc.dr[c]; p.dec_s[c] = pc.ds[c]; p.dec_perm[c] = pc.dperm[c];
@@ -1050,12 +1197,18 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     if (image_in && x_fmt == NST_IO_F32_NCHW && preset == NST_PRESET_NONE) {
       for (int c = 0; c < 3; ++c) { p.enc_a[c] = 1.f; p.enc_b[c] = 0.f; p.enc_d[c] = 1.f; p.enc_perm[c] = c; }
     }
+    // uint8 frames through a first layer with this preset folded in: stage the raw bytes (exact operand)
+    const bool fold = image_in && Ly.prepad && x_fmt == NST_IO_U8_NHWC && preset >= 0 && preset < 8 &&
+                      Ly.wpk_fold[preset] != nullptr;
+    p.enc_raw = fold ? 1 : 0;
     if (image_in && Ly.prepad) {
       // resolve padding + encode once into the workspace, then run the conv over it with an
       // identity coordinate map (pad 0, no reflection)
       const int hp = P.ch[i] + Ly.d.ks - 1, wp = P.cw[i] + Ly.d.ks - 1;
       void* pre = ws + P.off_pre;
-      hipError_t e = launch_prepad_encode(h->dtype, p, x_fmt == NST_IO_U8_NHWC ? IN_U8_NHWC : IN_F32_NCHW, n, hp, wp, pre, st);
+      // the staged operand's format: bf16, or fp16 (the fp16 mode and NST_DT_F16M's split-weight first layer)
+      const int pdt = (Ly.kdt == NST_DT_F16 || Ly.kdt == NST_KDT_SW_O32 || Ly.kdt == NST_KDT_SW_O16) ? NST_DT_F16 : NST_DT_BF16;
+      hipError_t e = launch_prepad_encode(pdt, p, x_fmt == NST_IO_U8_NHWC ? IN_U8_NHWC : IN_F32_NCHW, n, hp, wp, pre, st);
       if (e != hipSuccess) { set_error(std::string("prepad launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
       p.in = pre;
       p.hs = hp;
@@ -1066,8 +1219,8 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       p.pre = 0;
     }
     p.dec_tanh = (is_reconet(h->arch) && final_out) ? 1 : 0;
-    p.wpk = Ly.wpk;
-    p.bias = Ly.bias;
+    p.wpk = fold ? Ly.wpk_fold[preset] : Ly.wpk;
+    p.bias = fold ? Ly.bias_fold[preset] : Ly.bias;
     if (Ly.mode == MODE_XSHIFT && final_out && y_fmt == NST_IO_U8_NHWC && pc.dperm[0] == 2) {
       p.wpk = Ly.wpk_rev;  // decode channel c from model channel 2-c (caffe_bgr)
       p.bias = Ly.bias_rev;
@@ -1078,7 +1231,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     p.ow = P.ow[i];
     p.crop_y = (P.ch[i] - P.oh[i]) / 2;
     p.crop_x = (P.cw[i] - P.ow[i]) / 2;
-    p.out = final_out ? y : buf_out(op.dst);
+    p.out = final_out ? y : bufs[op.dst];
     p.cout_real = Ly.d.cout;
     p.cout_stride = Ly.coutp;
     tile_grid(*k, p.hs, p.ws, p.oh, p.ow, &p.tiles_x, &p.tiles_y);
@@ -1103,7 +1256,8 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       set_error("conv " + Ly.d.conv + ": weight-stationary kernels store whole pixels of bn channels");
       return NST_E_SHAPE;
     }
-    if (Ly.mode == MODE_WPHASE && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out != nullptr || p.res_relu)) {
+    if (Ly.mode == MODE_WPHASE && p.res_r != nullptr &&
+        (p.in_norm == nullptr || p.res_out != nullptr || p.res_relu || p.res_rnorm != nullptr)) {
       set_error("conv " + Ly.d.conv + ": weight-stationary phase kernel joins IN(y) + r without writing the stream");
       return NST_E_SHAPE;
     }
@@ -1130,10 +1284,10 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     }
     if (cap && !final_out) {
       if (cap->act && cap->act[i])
-        NST_HIP_CHECK(hipMemcpyAsync(cap->act[i], bufs[op.dst], (size_t)n * P.oh[i] * P.ow[i] * Ly.coutp * esz,
+        NST_HIP_CHECK(hipMemcpyAsync(cap->act[i], bufs[op.dst], (size_t)n * P.oh[i] * P.ow[i] * Ly.coutp * P.out_esz[i],
                                      hipMemcpyDeviceToDevice, st));
       if (cap->res && cap->res[i] && op.res_out >= 0)
-        NST_HIP_CHECK(hipMemcpyAsync(cap->res[i], bufs[op.res_out], (size_t)n * P.ih[i] * P.iw[i] * Ly.cinp * esz,
+        NST_HIP_CHECK(hipMemcpyAsync(cap->res[i], bufs[op.res_out], (size_t)n * P.ih[i] * P.iw[i] * Ly.cinp * P.res_esz[i],
                                      hipMemcpyDeviceToDevice, st));
       if (cap->stats && cap->stats[i])
         NST_HIP_CHECK(hipMemcpyAsync(cap->stats[i], stats[op.layer], (size_t)n * Ly.coutp * 8, hipMemcpyDeviceToDevice, st));
@@ -1141,7 +1295,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     return NST_OK;
   };
   for (size_t i = 0; i < h->prog.size(); ++i) {
-    const int rc = run_op(i, 0, n);
+    const int rc = run_op(i);
     if (rc != NST_OK) return rc;
   }
   return NST_OK;
@@ -1203,7 +1357,10 @@ int nst_op_describe(const nst_handle* h, int n, int in_h, int in_w, int op_index
   out->cin_stride = op.src == B_IMG ? 3 : Ly.cinp;
   out->cout_stride = Ly.coutp;
   out->kernel_mode = Ly.mode;
-  out->elem_bytes = act_elem_bytes(h->dtype);
+  out->elem_bytes = P.out_esz[op_index];
+  out->in_elem_bytes = P.in_esz[op_index];
+  out->res_elem_bytes = P.res_esz[op_index];
+  out->kernel_dtype = op.kind == OP_CONV ? Ly.kdt : h->dtype;
   return NST_OK;
 }
 

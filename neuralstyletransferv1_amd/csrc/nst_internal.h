@@ -98,6 +98,9 @@ struct ConvParams {
   // image-input preset encode: x_in[c] = ((x01[perm[c]] * a[c]) - b[c]) / d[c]
   float enc_a[3], enc_b[3], enc_d[3];
   int enc_perm[3];
+  // pre-padded uint8 frames only (conv_prep.hip): stage x_in[c] = byte[perm[c]] / 256 (exact in bf16 / fp16) and
+  // let the first layer's folded weights carry the encode (nst_api.cpp fold_first_layer)
+  int enc_raw;
   // weights
   const void* wpk;     // packed fragments (see pack_conv_weights)
   const float* bias;   // [cout_pad]
@@ -119,9 +122,15 @@ struct ConvParams {
   int ph_off[2];  // MODE_PHASE / MODE_WPHASE: LDS row/col offset of sub-pixel phase 0/1 ({0,1} nearest-up, {1,1} ConvTranspose)
 };
 
+// Kernel dtype codes of the split-precision layers (ConvKernelInfo::dtype only; not in the ABI):
+//   SW:    fp16 operand (the first layer's exact raw bytes) x fp16 hi / lo weight pairs
+//   SPLIT: fp32 input staged as an fp16 hi / lo operand pair x fp16 hi / lo weight pairs (Wh xh + Wh xl + Wl xh)
+//   O32 / O16: fp32 / fp16 output storage
+enum KernelDtype { NST_KDT_SW_O32 = 16, NST_KDT_SW_O16 = 17, NST_KDT_SPLIT_O32 = 18, NST_KDT_SPLIT_O16 = 19 };
+
 // Static description of one compiled conv kernel instantiation.
 struct ConvKernelInfo {
-  int dtype;  // NST_DT_*
+  int dtype;  // NST_DT_* or NST_KDT_*
   int mode;   // ConvMode
   int ks, stride, cinp, bn, th, tw, wm, wn, in_kind, out_kind;
   // derived
@@ -132,6 +141,8 @@ struct ConvKernelInfo {
   int wbytes;      // MODE_KYROT: bytes of the packed weight table
   int res;         // fill joins the residual stream (VAR_RES)
   int tanh_out;    // MODE_KYROT: tanh compiled into the output (ReCoNet); other kernels: p.dec_tanh
+  int in_esz, out_esz;  // activation element bytes read / written (0: the dtype's own, act_elem_bytes)
+  int split_w;          // packed weights are fp16 hi / lo pairs (pack functions place w and w - RNE16(w))
   void (*launch)(const ConvParams&, dim3 grid, hipStream_t);
 };
 
@@ -171,6 +182,10 @@ hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstrid
 hipError_t launch_residual(int dtype, const void* y, const float2* ys, const void* r,
                            const float2* rs, int r_relu, int relu_out, void* out, int n, int hw,
                            int c, hipStream_t st);
+// NST_DT_F16M's first residual join: y, r fp32 (the split-precision block's output and the producer conv's raw
+// output, normalised + ReLU'd as rs / r_relu say) -> the fp16 stream out = rr + (y * ys.x + ys.y) [+ ReLU]
+hipError_t launch_residual_f32_to_f16(const void* y, const float2* ys, const void* r, const float2* rs, int r_relu,
+                                      int relu_out, void* out, int n, int hw, int c, hipStream_t st);
 hipError_t launch_decode_resize_u8(const float* y, int n, int h, int w, const float* p,
                                    const float* q, const float* r, const float* s, const int* perm,
                                    uint8_t* out, int oh, int ow, hipStream_t st);

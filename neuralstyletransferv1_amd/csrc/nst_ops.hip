@@ -272,6 +272,64 @@ hipError_t launch_residual(int dtype, const void* y, const float2* ys, const voi
   return hipGetLastError();
 }
 
+// y, r fp32 -> out fp16, 8 channels per thread (two 16-B loads of each input, one 16-B store); the fp32
+// arithmetic of residual_kernel<float> (product, then sum, no contraction), one RNE rounding to fp16
+__global__ __launch_bounds__(256) void residual_f32_to_f16_kernel(const float* __restrict__ y, const float2* __restrict__ ys,
+                                                                  const float* __restrict__ r, const float2* __restrict__ rs,
+                                                                  int r_relu, int relu_out, _Float16* __restrict__ out,
+                                                                  int hw, int c) {
+  const int cv_n = c / 8;
+  const int tpp = blockDim.x / cv_n;
+  const int cv = threadIdx.x % cv_n, pl = threadIdx.x / cv_n;
+  const int n = blockIdx.y, ch0 = cv * 8;
+  float ysc[8], ysh[8], rsc[8], rsh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float2 a = ys[(size_t)n * c + ch0 + j];
+    ysc[j] = a.x; ysh[j] = a.y;
+    rsc[j] = 1.f; rsh[j] = 0.f;
+    if (rs) { const float2 b = rs[(size_t)n * c + ch0 + j]; rsc[j] = b.x; rsh[j] = b.y; }
+  }
+  const size_t base = (size_t)n * hw * c + ch0;
+  for (int px = blockIdx.x * tpp + pl; px < hw; px += gridDim.x * tpp) {
+    const float4* yp = (const float4*)(y + base + (size_t)px * c);
+    const float4* rp = (const float4*)(r + base + (size_t)px * c);
+    const float4 y0 = yp[0], y1 = yp[1], r0 = rp[0], r1 = rp[1];
+    const float vy[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+    const float vr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      float o[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        float rr = vr[j + k];
+        if (rs) {
+          rr = rr * rsc[j + k] + rsh[j + k];
+          if (r_relu) rr = fmaxf(rr, 0.f);
+        }
+        float v = vy[j + k] * ysc[j + k] + ysh[j + k];
+        v = rr + v;
+        if (relu_out) v = fmaxf(v, 0.f);
+        o[k] = v;
+      }
+      w[j / 2] = pack16<_Float16>(o[0], o[1]);
+    }
+    *(uint4*)(out + base + (size_t)px * c) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+hipError_t launch_residual_f32_to_f16(const void* y, const float2* ys, const void* r, const float2* rs, int r_relu,
+                                      int relu_out, void* out, int n, int hw, int c, hipStream_t st) {
+  const int cv_n = c / 8;
+  if (c % 8 != 0 || cv_n > 256) return hipErrorInvalidValue;
+  const int tpp = 256 / cv_n;
+  const int blocks = std::min((hw + tpp - 1) / tpp, 2048);
+  hipLaunchKernelGGL(residual_f32_to_f16_kernel, dim3((unsigned)blocks, (unsigned)n), dim3((unsigned)(tpp * cv_n)), 0, st,
+                     (const float*)y, ys, (const float*)r, rs, r_relu, relu_out, (_Float16*)out, hw, c);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 // Output fit: preset decode + clamp(0,1) of the raw model output (pipeline.py:1445-1486),
 // bilinear resize to the content size with align_corners=False (pipeline.py:1512-1516,

@@ -18,7 +18,7 @@ from . import _lib
 from ._lib import NstError, NstParam, check, lib
 
 _DTYPES = {"fp32": _lib.NST_DT_F32, "float32": _lib.NST_DT_F32, "bf16": _lib.NST_DT_BF16, "bfloat16": _lib.NST_DT_BF16,
-           "fp16": _lib.NST_DT_F16, "float16": _lib.NST_DT_F16, "fp32s": _lib.NST_DT_F32S}
+           "fp16": _lib.NST_DT_F16, "float16": _lib.NST_DT_F16, "fp32s": _lib.NST_DT_F32S, "fp16m": _lib.NST_DT_F16M}
 
 
 class Engine:
@@ -118,20 +118,25 @@ class Engine:
             y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=self.device)
             yf = _lib.NST_IO_F32_NCHW
         ops = self.op_descs(n, h, w)
-        dt = {_lib.NST_DT_BF16: torch.bfloat16, _lib.NST_DT_F16: torch.float16}.get(self.dtype, torch.float32)
+        half = torch.bfloat16 if self.dtype == _lib.NST_DT_BF16 else torch.float16
+
+        def dt_of(esz):  # a 2-byte activation is the handle's 16-bit format, a 4-byte one fp32
+            return torch.float32 if esz == 4 else half
         caps = []
         k = len(ops)
         act, res, st = (ctypes.c_void_p * k)(), (ctypes.c_void_p * k)(), (ctypes.c_void_p * k)()
         for i, d in enumerate(ops):
             c = {"act": None, "res": None, "stats": None}
             if d["dst"] != _lib.NST_BUF_OUTPUT:
-                c["act"] = torch.empty((n, d["out_h"], d["out_w"], d["cout_stride"]), dtype=dt, device=self.device)
+                c["act"] = torch.empty((n, d["out_h"], d["out_w"], d["cout_stride"]), dtype=dt_of(d["elem_bytes"]),
+                                       device=self.device)
                 act[i] = c["act"].data_ptr()
                 if d["kind"] == 0:
                     c["stats"] = torch.empty((n, d["cout_stride"], 2), dtype=torch.float32, device=self.device)
                     st[i] = c["stats"].data_ptr()
                 if d["res_out"] >= 0:
-                    c["res"] = torch.empty((n, d["in_h"], d["in_w"], d["cin_stride"]), dtype=dt, device=self.device)
+                    c["res"] = torch.empty((n, d["in_h"], d["in_w"], d["cin_stride"]), dtype=dt_of(d["res_elem_bytes"]),
+                                           device=self.device)
                     res[i] = c["res"].data_ptr()
             caps.append(c)
         ws = self.workspace(n, h, w)
@@ -196,7 +201,9 @@ class StylizationNet(nn.Module):
         # "fp32": parity mode (exact-f32 MFMA); "bf16": throughput mode (bf16 MFMA, fp32 accumulate);
         # "fp16": fp16 MFMA at the bf16 rate (11 significant bits); "fp32s": fp32 activations with
         # every conv operand split into an fp16 hi/lo pair (two fp16 MFMAs per K step, ~22 bits): the
-        # parity mode's +-1 LSB at a quarter of its MFMA cycles
+        # parity mode's +-1 LSB at a quarter of its MFMA cycles; "fp16m": the split-fp16 arithmetic on the layers
+        # whose rounding reaches the frame most (first layer, down-convs, first residual block), fp16 elsewhere:
+        # 1080p frames within +-1 LSB at ~3/4 of the fp16 rate (Johnson / NST nets)
         self.compute_dtype = "fp32"
         # kernel selection (names of _lib.KSEL): e.g. {"no_wstat"} runs the residual trunk on the
         # generic kernel instead of the weight-stationary one; empty = the fastest mapping
@@ -217,7 +224,7 @@ class StylizationNet(nn.Module):
             device = torch.device("cuda", torch.cuda.current_device())
         dtype = dtype or self.compute_dtype
         if dtype not in _DTYPES:
-            raise NstError(f"compute_dtype must be fp32, fp32s, bf16 or fp16, got {dtype!r}")
+            raise NstError(f"compute_dtype must be fp32, fp32s, fp16m, bf16 or fp16, got {dtype!r}")
         flags = 0
         for name in self.kernel_select:
             if name not in _lib.KSEL:

@@ -190,18 +190,27 @@ class Gatys:
 
     def run(self, content: torch.Tensor, style: torch.Tensor, steps: int = 300, lr: float = 0.02,
             content_weight: float = 1.0, style_weight: float = 1e6, init: Optional[torch.Tensor] = None,
-            record_every: int = 0):
+            record_every: int = 0, trajectory: bool = False):
         """Optimise from `init` (default: the content image) for `steps` Adam updates.
-        -> (image, list of (step, total, content, style) recorded every `record_every` steps)."""
+        -> (image, list of (step, total, content, style) recorded every `record_every` steps); with
+        `trajectory` every step's losses are kept on the device (no host synchronisation inside the loop) and
+        returned as the list instead."""
         self.set_targets(content, style)
         x = (content if init is None else init).detach().to(self.device, torch.float32).clone().contiguous()
         m, v = torch.zeros_like(x), torch.zeros_like(x)
         hist = []
+        traj = None
         for t in range(1, steps + 1):
             g, losses = self.grad(x, content_weight, style_weight)
-            if record_every and (t == 1 or t % record_every == 0):
+            if trajectory:
+                if traj is None:
+                    traj = torch.empty((steps, losses.numel()), dtype=losses.dtype, device=losses.device)
+                traj[t - 1].copy_(losses)
+            elif record_every and (t == 1 or t % record_every == 0):
                 hist.append((t - 1,) + tuple(float(z) for z in losses.cpu()))
             self.adam(x, g, m, v, t, lr)
+        if traj is not None:
+            hist = [(i,) + tuple(float(z) for z in row) for i, row in enumerate(traj.cpu())]
         return x, hist
 
 

@@ -10,9 +10,10 @@ per-frame loop (`style_frames`, pipeline.py:527-2122, standard path :1409-1519 +
     -> LAB EMA (LUT, frame order) -> mask composite -> uniform blend --D2H--> host: PIL encode.
 
 Additions: --gpus N (frames round-robin over N GPUs, ordered gather to rank 0 over RCCL),
---batch B (frames per GPU step), --dtype {fp32,fp32s,bf16,fp16} (fp32 = parity with the reference's
+--batch B (frames per GPU step), --dtype {fp32,fp32s,fp16m,bf16,fp16} (fp32 = parity with the reference's
 arithmetic, default; fp32s = fp32 activations on split-fp16 MFMAs, the parity bar at several times
-fp32's speed; bf16 = throughput mode; fp16 = near bf16's speed with 3 more mantissa bits),
+fp32's speed; fp16m = split-fp16 on the layers whose rounding reaches the frame, fp16 elsewhere: +-1 LSB
+at most of the fp16 rate; bf16 = throughput mode; fp16 = near bf16's speed with 3 more mantissa bits),
 --synthetic WxH / --synthetic_frames N (an
 in-memory synthetic frame stream instead of files; config 4 of BASELINE.json).
 
@@ -152,13 +153,21 @@ def build_parser() -> argparse.ArgumentParser:
                     help="--gpus > 1 process group: nccl (RCCL over xGMI, one GPU per rank) or gloo (host-staged "
                          "exchange; ranks may share a GPU, used by the tests)")
     ap.add_argument("--dist_timeout", type=float, default=600.0, help="seconds before a blocked exchange aborts")
-    ap.add_argument("--dtype", choices=["fp32", "fp32s", "bf16", "fp16"], default="fp32",
+    ap.add_argument("--dtype", choices=["fp32", "fp32s", "fp16m", "bf16", "fp16"], default="fp32",
                     help="fp32 = parity with the reference arithmetic; fp32s = fp32 activations on split-fp16 "
-                         "MFMAs (the same +-1 LSB parity, faster; conv inputs < 65504); bf16 = throughput mode; "
+                         "MFMAs (the same +-1 LSB parity, faster; conv inputs < 65504); fp16m = split-fp16 on the "
+                         "first layers, fp16 elsewhere (+-1 LSB on 1080p frames, most of fp16's speed; ReCoNet runs "
+                         "fp32s); bf16 = throughput mode; "
                          "fp16 = near the throughput mode's speed with 3 more mantissa bits (activations < 65504)")
     ap.add_argument("--synthetic", type=str, default=None, help="WxH: stylize an in-memory synthetic frame stream")
     ap.add_argument("--synthetic_frames", type=int, default=16)
     ap.add_argument("--no_save", action="store_true", help="do not encode/write outputs (throughput runs)")
+    ap.add_argument("--keep_staged", action="store_true",
+                    help="--input_dir: also write the staged frame copies (the reference's work_dir/frames files); the "
+                         "frames are staged in memory either way, with the same pixels")
+    ap.add_argument("--png_compress_level", type=int, default=None, choices=range(10), metavar="0-9",
+                    help="zlib level of the PNG outputs (default: PIL's, as the reference saves them); the pixels "
+                         "are the same at every level, only the file size and the encode time change")
     return ap
 
 
@@ -355,6 +364,9 @@ def load_model(path: str, model_type: str, device, dtype: str, slot: str = "A", 
         model = TransformerNet()
     _load_checkpoint_compat(model, path)
     model = model.to(device).eval()
+    if dtype == "fp16m" and arch == "reconet":  # the split-precision head is built for the 128-channel nets
+        _log("[backend] fp16m is built for the Johnson / NST nets; ReCoNet runs fp32s (the same +-1 LSB bar)")
+        dtype = "fp32s"
     model.compute_dtype = dtype
     _log(f"[backend] {slot}: type={model_type} path={path} device={device} arch={arch} dtype={dtype}")
     return model, arch
@@ -362,10 +374,12 @@ def load_model(path: str, model_type: str, device, dtype: str, slot: str = "A", 
 
 # ----------------------------------------------------------------------------- the frame loop
 class FrameSource:
-    """Frames by index: files (PIL decode, optional --inference_res LANCZOS) or a synthetic stream."""
+    """Frames by index: files (PIL decode, optional --inference_res LANCZOS), --input_dir sources staged in memory
+    (`staged`: (source path, JPEG quality or None) per frame), or a synthetic stream."""
 
-    def __init__(self, files: Optional[List[Path]] = None, synthetic=None, infer_res: int = 0):
-        self.files = files
+    def __init__(self, files: Optional[List[Path]] = None, synthetic=None, infer_res: int = 0, staged=None):
+        self.files = files if files is not None else ([s for s, _ in staged] if staged is not None else None)
+        self.staged = staged
         self.synthetic = synthetic  # (n, h, w)
         self.infer_res = infer_res
 
@@ -378,7 +392,28 @@ class FrameSource:
         from PIL import Image
         with Image.open(self.files[i]) as im:
             w, h = im.size
+            if self.staged is not None:  # the staged copy is EXIF-upright: orientations 6 / 8 swap the sides
+                tags = getattr(im, "_getexif", lambda: None)() or {}
+                if _EXIF_UPRIGHT.get(tags.get(0x0112)) in (90, 270):
+                    w, h = h, w
         return (h, w)
+
+    def _open_rgb(self, i: int):
+        from PIL import Image
+        if self.staged is None:
+            return Image.open(self.files[i]).convert("RGB")
+        # the reference's --input_dir staging (pipeline.py:2577-2586): EXIF-upright RGB, re-saved as the staged
+        # frame -- PNG (lossless: the decoded frame is that RGB image itself) or JPEG at --jpeg_quality, whose
+        # encode -> decode round trip runs here in memory (the same bytes PIL writes, so the same pixels)
+        src, q = self.staged[i]
+        pil = _get_image_with_exif_pil(str(src))
+        if q is None:
+            return pil
+        import io
+        buf = io.BytesIO()
+        pil.save(buf, format="JPEG", quality=q)
+        buf.seek(0)
+        return Image.open(buf).convert("RGB")
 
     def load(self, i: int):
         """-> (original uint8 HxWx3, model-input uint8 hxwx3)."""
@@ -387,7 +422,7 @@ class FrameSource:
             f = make_frames(1, self.synthetic[1], self.synthetic[2], seed=10_000 + i)[0]
             return f, f
         from PIL import Image
-        pil_rgb = Image.open(self.files[i]).convert("RGB")
+        pil_rgb = self._open_rgb(i)
         pil_src = pil_rgb
         if self.infer_res > 0:  # pipeline.py:1089-1097
             w0, h0 = pil_rgb.size
@@ -465,17 +500,24 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         src = FrameSource(synthetic=(n_syn, int(m.group(2)), int(m.group(1))))
         names = [f"frame_{i + 1:04d}" for i in range(n_syn)]
     else:
-        files = sorted(p for p in frames_dir.iterdir() if p.is_file() and p.name.startswith("frame_")
-                       and p.suffix.lower() in {".png", ".jpg", ".jpeg"})
+        staged = getattr(args, "_staged_sources", None)
+        if staged is not None:  # --input_dir: frame_{i:04d} staged in memory (prepare)
+            entries = [(f"frame_{i:04d}", s) for i, s in enumerate(staged, start=1)]
+        else:
+            files = sorted(p for p in frames_dir.iterdir() if p.is_file() and p.name.startswith("frame_")
+                           and p.suffix.lower() in {".png", ".jpg", ".jpeg"})
+            entries = [(p.stem, p) for p in files]
         if stride and stride > 1:
-            files = files[::stride]
+            entries = entries[::stride]
         if max_frames:
-            files = files[:max_frames]
-        if not files:
+            entries = entries[:max_frames]
+        if not entries:
             _log(f"[error] No frames found to style in: {frames_dir}")
             sys.exit(1)
-        src = FrameSource(files=files, infer_res=int(getattr(args, "inference_res", 0) or 0))
-        names = [p.stem for p in files]
+        ir = int(getattr(args, "inference_res", 0) or 0)
+        src = (FrameSource(staged=[e[1] for e in entries], infer_res=ir) if staged is not None
+               else FrameSource(files=[e[1] for e in entries], infer_res=ir))
+        names = [e[0] for e in entries]
     _log(f"[debug] found {len(src)} staged frame(s)")
 
     if getattr(args, "mask_dir", None) and not getattr(args, "mask", None) and not args.synthetic:
@@ -497,6 +539,20 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     flow_mode = bool(getattr(args, "flow_ema", False))
     need_orig = blend < 1.0 or bool(args.mask or args.mask_dir) or (flow_mode and bool(getattr(args, "motion_blend", False)))
 
+    # host decode runs ahead of the GPU: this rank's next group(s) are loading on the pool while a group is
+    # stylized (and the previous group's encodes drain), so decode, GPU step and encode overlap
+    from .frames import shard
+    my_shards = [shard(g, world, rank, caps) for g in groups]
+    shard_pos = {tuple(sh): k for k, sh in enumerate(my_shards) if sh}
+    loads = {}
+    prefetch_depth = 2
+
+    def _submit(k):
+        if 0 <= k < len(my_shards):
+            for f in my_shards[k]:
+                if f not in loads:
+                    loads[f] = pool.submit(src.load, f)
+
     # the reference fits model A's output to the content size; with --inference_res the model
     # input is smaller than the content
     def stylize(idx: List[int]):
@@ -505,7 +561,10 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             if flow_mode:
                 return torch.empty((0, 15 * h0 * w0), dtype=torch.uint8, device=dev)
             return torch.empty((0, h0, w0, 6 if need_orig else 3), dtype=torch.uint8, device=dev)
-        loaded = list(pool.map(src.load, idx))
+        k = shard_pos.get(tuple(idx), -1)
+        for j in range(k, k + 1 + prefetch_depth):
+            _submit(j)
+        loaded = [(loads.pop(f) if f in loads else pool.submit(src.load, f)).result() for f in idx]
         orig = torch.from_numpy(np.stack([a for a, _ in loaded])).to(dev, non_blocking=True)
         xin = orig if loaded[0][1] is loaded[0][0] else torch.from_numpy(np.stack([b for _, b in loaded])).to(dev)
         h0, w0 = orig.shape[1], orig.shape[2]
@@ -658,6 +717,8 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             out_path = (base / f"{output_prefix}_{idx_str}").with_suffix(".jpg" if save_as_jpg else ".png")
         if save_as_jpg:
             out_img.save(out_path, format="JPEG", quality=int(jpeg_quality))
+        elif getattr(args, "png_compress_level", None) is not None:
+            out_img.save(out_path, compress_level=int(args.png_compress_level))
         else:
             out_img.save(out_path)
         return str(out_path)
@@ -805,21 +866,26 @@ def prepare(args):
             sys.exit(2)
         Path(args.output_dir).mkdir(parents=True, exist_ok=True)
 
-        def stage(i_f):  # the reference's per-file staging copy (decode with EXIF transpose, re-encode)
-            i, f = i_f
-            src = Path(f).resolve()
-            ext = src.suffix.lower()
-            dst = frames_dir / f"frame_{i:04d}{ext}"
-            pil = _get_image_with_exif_pil(str(src))
-            if ext in (".jpg", ".jpeg"):
-                pil.save(dst, format="JPEG", quality=max(1, min(95, int(args.jpeg_quality))))
-            else:
-                pil.save(dst)
-
-        # the same files the reference writes one after another (pipeline.py:2560-2590), encoded in parallel: PIL's
-        # codecs release the GIL, and the staging encode was ~90 % of a PNG directory run's wall time
-        with ThreadPoolExecutor(max_workers=max(1, int(getattr(args, "threads", 1) or 1))) as ex:
-            list(ex.map(stage, enumerate(in_files, start=1)))
+        # the reference's per-file staging copy (pipeline.py:2560-2590: EXIF-upright RGB re-saved as
+        # frames/frame_{i:04d}{ext}, JPEG at --jpeg_quality) happens in memory when the frame is loaded
+        # (FrameSource._open_rgb): a PNG copy decodes to that RGB image itself, a JPEG copy is re-encoded and
+        # decoded from memory -- the same pixels without writing the staged files (--keep_staged writes them too)
+        q = max(1, min(95, int(args.jpeg_quality)))
+        args._staged_sources = [(Path(f).resolve(), q if Path(f).suffix.lower() in (".jpg", ".jpeg") else None)
+                                for f in in_files]
+        if getattr(args, "keep_staged", False):
+            def stage(i_f):
+                i, f = i_f
+                src = Path(f).resolve()
+                ext = src.suffix.lower()
+                pil = _get_image_with_exif_pil(str(src))
+                dst = frames_dir / f"frame_{i:04d}{ext}"
+                if ext in (".jpg", ".jpeg"):
+                    pil.save(dst, format="JPEG", quality=q)
+                else:
+                    pil.save(dst)
+            with ThreadPoolExecutor(max_workers=max(1, int(getattr(args, "threads", 1) or 1))) as ex:
+                list(ex.map(stage, enumerate(in_files, start=1)))
         for i, f in enumerate(in_files, start=1):
             src = Path(f).resolve()
             ext = src.suffix.lower()

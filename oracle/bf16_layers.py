@@ -144,6 +144,48 @@ def fill_operand(y: torch.Tensor, ys: Optional[torch.Tensor], in_relu: bool, r: 
     return rnd(v)
 
 
+# io_preset encode constants as the engine rounds them to fp32 (nst_api.cpp preset_consts; pipeline.py:1445-1486):
+# x_c = ((byte[perm c] / 255) * a_c - b_c) / d_c
+def _f32(v):
+    return float(np.float32(v))
+
+
+PRESET_ENC = {
+    "tanh": ((2.0,) * 3, (1.0,) * 3, (1.0,) * 3, (0, 1, 2)),
+    "imagenet_01": ((1.0,) * 3, tuple(_f32(m) for m in (0.485, 0.456, 0.406)), tuple(_f32(s) for s in (0.229, 0.224, 0.225)),
+                    (0, 1, 2)),
+    "imagenet_255": ((255.0,) * 3, tuple(_f32(np.float32(m) * np.float32(255.0)) for m in (0.485, 0.456, 0.406)),
+                     tuple(_f32(np.float32(s) * np.float32(255.0)) for s in (0.229, 0.224, 0.225)), (0, 1, 2)),
+    "caffe_bgr": ((255.0,) * 3, tuple(_f32(c) for c in (103.939, 116.779, 123.68)), (1.0,) * 3, (2, 1, 0)),
+    "raw_255": ((255.0,) * 3, (0.0,) * 3, (1.0,) * 3, (0, 1, 2)),
+    "raw_01": ((1.0,) * 3, (0.0,) * 3, (1.0,) * 3, (0, 1, 2)),
+}
+
+
+def fold_first_layer(W: torch.Tensor, b: torch.Tensor, preset: str, axis: int):
+    """The engine's first layer over uint8 frames (nst_api.cpp fold_first_layer): operand o_c = byte[perm c] / 256
+    (exact), W'[.][c] = W * 256 a_c / (255 d_c), bias' = bias - sum W b_c / d_c (fp64 -> fp32), or None where the
+    fold does not hold (zero padding with b != 0)."""
+    if preset not in PRESET_ENC:
+        return None
+    a, bb, d, _ = PRESET_ENC[preset]
+    if axis != REFLECT and any(v != 0.0 for v in bb):
+        return None
+    Wd = W.double()
+    sc = torch.tensor([256.0 * a[c] / (255.0 * d[c]) for c in range(3)], dtype=torch.float64)
+    sh = torch.tensor([bb[c] / d[c] for c in range(3)], dtype=torch.float64)
+    Wf = (Wd * sc[None, :, None, None]).float()
+    bf = (b.double() - (Wd * sh[None, :, None, None]).sum(dim=(1, 2, 3))).float()
+    return Wf, bf
+
+
+def raw_operand(frames_u8: np.ndarray, preset: str) -> torch.Tensor:
+    """The staged first-layer operand with the fold: [n,3,h,w] byte[perm c] / 256 (exact in bf16 / fp16)."""
+    perm = list(PRESET_ENC[preset][3])
+    x = torch.from_numpy(np.ascontiguousarray(frames_u8)).permute(0, 3, 1, 2).float()
+    return x[:, perm] / 256.0
+
+
 def encode_operand(frames_u8: np.ndarray, preset: str, round_bf16: bool = True, fmt: str = "bf16") -> torch.Tensor:
     """First-layer operand: encode(ToTensor(frame)) in the preset's fp32 arithmetic (+ 16-bit rounding)."""
     v = O.encode(O.to_tensor01(frames_u8), preset).float()

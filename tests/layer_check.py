@@ -28,6 +28,10 @@ ULP1_FRAC_MAX_F16 = 8e-3
 STATS_REL = 1e-5         # IN scale/shift vs the oracle's statistics of its fp32 values (measured <= 4e-7)
 RAW_REL = 5e-6           # output conv raw fp32, relative to max |y| (measured <= 1.1e-6)
 U8_EXACT_MIN = 0.9999    # decoded u8 frames: >= 99.99 % identical, the rest 1 LSB (truncation boundary)
+# split-precision layers (NST_DT_F16M: fp16 hi / lo operand and weight pairs, ~22-bit products, fp32 output) against
+# the exact (fp64) conv of the same fp32 operand: within this fraction of the layer's max |value|
+SPLIT_REL = 2e-5
+SPLIT_KDT = (3, 16, 17, 18, 19)  # NST_DT_F32S and the NST_KDT_* split kernels (nst_op_desc.kernel_dtype)
 
 
 def _nchw(t: torch.Tensor, c: int) -> torch.Tensor:
@@ -90,7 +94,7 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
     """-> one record per op.  bands: None = every output row; else [(fraction, rows)] row bands
     (start = fraction of the output height, rounded down to even) checked per op (4K frames)."""
     arch = {0: "johnson", 1: "nst", 2: "reconet", 3: "reconet_frn"}[net.ARCH]
-    fmt = "fp16" if net.compute_dtype in ("fp16", "float16") else "bf16"
+    fmt = "fp16" if net.compute_dtype in ("fp16", "float16", "fp16m") else "bf16"
     ulp1_max = ULP1_FRAC_MAX_F16 if fmt == "fp16" else ULP1_FRAC_MAX
     frn = arch == "reconet_frn"
     sd = {k: v.detach().float().cpu() for k, v in net.state_dict().items()}
@@ -112,9 +116,34 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
     recs = []
     x_enc = None
     for i, d in enumerate(ops):
-        if d["kind"] != 0:
-            raise AssertionError("unfused residual ops are not part of the default program")
         conv, norm, cin, cout, ks, st, axis, pad, pre = layers[d["layer"]]
+        split = d["kernel_dtype"] in SPLIT_KDT
+        if d["kind"] != 0:
+            # NST_DT_F16M's first residual join (fp32 y and r -> the fp16 stream): the fp32 arithmetic of the
+            # reference's ResidualBlock (product, then sum), one fp16 rounding
+            if d["elem_bytes"] != 2 or d["in_elem_bytes"] != 4:
+                raise AssertionError("only the split-precision program has a separate residual op")
+            j, kind = writer[d["src"]]
+            y = _nchw(host[j][kind], cout)
+            jr, kr = writer[d["res_buf"]]
+            r = _nchw(host[jr][kr], cout)
+            ys = host[layer_op[d["in_norm"]]]["stats"][:, :cout]
+            if d["res_norm"] >= 0:
+                rs = host[layer_op[d["res_norm"]]]["stats"][:, :cout]
+                r = r * rs[..., 0][:, :, None, None] + rs[..., 1][:, :, None, None]
+                r = r.clamp_min(0.0)
+            v = r + (y * ys[..., 0][:, :, None, None] + ys[..., 1][:, :, None, None])
+            if d["relu_out"]:
+                v = v.clamp_min(0.0)
+            ref = v.to(torch.float16)
+            got = host[i]["act"].permute(0, 3, 1, 2)[:, :cout].contiguous()
+            ulp = B.bf16_ulp_diff(got, ref)
+            rec = {"op": i, "layer": conv + " (join)", "mode": -1, "elements": ref.numel(), "ulp_max": int(ulp.max()),
+                   "ulp1_frac": float((ulp >= 1).float().mean())}
+            assert rec["ulp_max"] <= 1 and rec["ulp1_frac"] <= 1e-4, rec
+            writer[d["dst"]] = (i, "act")
+            recs.append(rec)
+            continue
 
         def stats_of(layer):
             return host[layer_op[layer]]["stats"][:, :, :]
@@ -123,10 +152,18 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
             j, kind = writer[buf]
             return _nchw(host[j][kind], cin)
 
+        W, bias = sd[conv + ".weight"], sd[conv + ".bias"]
+        folded = B.fold_first_layer(W, bias, preset, axis) if d["src"] == -1 else None
         if d["src"] == -1:
-            if x_enc is None:
-                x_enc = B.encode_operand(frames_u8, preset, fmt=fmt)
-            src = x_enc
+            if folded is not None:  # uint8 frames: raw bytes / 256 and the encode in the weights (nst_api.cpp)
+                W, bias = folded
+                src = B.raw_operand(frames_u8, preset)
+            else:
+                if x_enc is None:
+                    x_enc = B.encode_operand(frames_u8, preset, fmt=fmt)
+                src = x_enc
+            if split:
+                src = src.double()
 
             def get_rows(idx, src=src):
                 return src.index_select(2, idx)
@@ -139,9 +176,11 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
                 r = buf_rows(d["res_buf"])
                 rs = stats_of(d["res_norm"])[:, :cin] if d["res_norm"] >= 0 else None
 
-            def get_rows(idx, ysrc=ysrc, ys=ys, r=r, rs=rs, d=d):
-                return B.fill_operand(ysrc.index_select(2, idx), ys, bool(d["in_relu"]),
-                                      None if r is None else r.index_select(2, idx), rs, bool(d["relu_out"]), fmt=fmt)
+            def get_rows(idx, ysrc=ysrc, ys=ys, r=r, rs=rs, d=d, split=split):
+                v = B.fill_operand(ysrc.index_select(2, idx), ys, bool(d["in_relu"]),
+                                   None if r is None else r.index_select(2, idx), rs, bool(d["relu_out"]),
+                                   round_bf16=not split, fmt=fmt)
+                return v.double() if split else v
             Hs = ysrc.shape[2]
             if d["res_out"] >= 0:  # the joined stream the op wrote for its own pixels: bit-exact
                 joined = get_rows(torch.arange(Hs))
@@ -162,11 +201,11 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
         row_sets = [(0, ch)] if bands is None else sorted({
             (r0, min(ch, r0 + k)) for f, k in bands for r0 in [min(max(0, int(f * ch)) // 2 * 2, max(0, ch - k) // 2 * 2)]})
         rec = {"op": i, "layer": conv, "mode": d["kernel_mode"], "elements": 0}
-        W, bias = sd[conv + ".weight"], sd[conv + ".bias"]
         if frn:  # TLU outputs are stored shifted by -tau: the bias absorbs sum W tau
             bias = _frn_bias(sd, d["layer"], W, bias)
         for (r0, r1) in row_sets:
-            z = B.conv_layer(get_rows, Hs, n, cin, W, bias, ks, st, axis, pad, pre, True, (r0, r1), acc, fmt)
+            z = B.conv_layer(get_rows, Hs, n, cin, W, bias, ks, st, axis, pad, pre, not split, (r0, r1),
+                             torch.float64 if split else acc, fmt)
             if final:
                 if arch.startswith("reconet"):
                     z = torch.tanh(z)
@@ -193,6 +232,20 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
             got = got_full[:, r0:r1].permute(0, 3, 1, 2)[:, :cout].contiguous()
             pad_ch = got_full[:, r0:r1, :, cout:]
             assert (pad_ch.float() == 0).all(), f"op {i} ({conv}): padded channels not zero"
+            if split:  # fp32 (or fp16) output of ~22-bit products vs the exact conv
+                zr = z if d["elem_bytes"] == 4 else z.to(torch.float16).float()
+                rel = float((got.float() - zr.float()).abs().max() / zr.abs().max().clamp_min(1e-12))
+                rec["elements"] += zr.numel()
+                rec["split_rel"] = max(rec.get("split_rel", 0.0), rel)
+                lim = SPLIT_REL if d["elem_bytes"] == 4 else 1e-3
+                assert rel <= lim, f"op {i} ({conv}) rows {r0}:{r1}: split-precision output rel err {rel:.2e} > {lim}"
+                if bands is None:
+                    s_ref = B.in_stats(z.float(), sd[norm + ".weight"], sd[norm + ".bias"])
+                    s_got = host[i]["stats"][:, :cout]
+                    err = (s_got - s_ref).abs() / s_ref.abs().amax(dim=1, keepdim=True).clamp_min(1e-6)
+                    rec["stats_rel"] = float(err.max())
+                    assert rec["stats_rel"] <= STATS_REL, (i, conv, rec["stats_rel"])
+                continue
             ref = z.to(B.TORCH16[fmt])
             ulp = B.bf16_ulp_diff(got, ref)
             diff = (got.float() - ref.float()).abs()

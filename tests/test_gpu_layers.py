@@ -40,12 +40,17 @@ def _report(recs):
     ("reconet", 1, 61, 90, "tanh"),           # 48/96/192 channels: generic bf16 kernels + tanh output
     ("reconet_frn", 1, 61, 90, "tanh"),       # FRN + TLU: mean-square statistics, tau folded into biases / shifts
 ])
-@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp16m"])
 def test_16bit_layers_small(arch, n, h, w, preset, dtype):
+    if dtype == "fp16m" and arch.startswith("reconet"):
+        pytest.skip("NST_DT_F16M is built for the Johnson / NST nets")
     frames = synthetic.make_frames(n, h, w, seed=40 + h)
     recs = LC.check_layers(_net(arch, 11, dtype), frames, preset, acc=torch.float64)
     _report(recs)
-    assert len(recs) == (14 if arch.startswith("reconet") else 16)
+    # fp16m: the first residual block runs unfused (+1 op: the join writing the fp16 stream)
+    assert len(recs) == (14 if arch.startswith("reconet") else 16) + (1 if dtype == "fp16m" else 0)
+    if dtype == "fp16m":  # the split-precision head: ~22-bit products (measured rel error reported)
+        assert sum(1 for r in recs if "split_rel" in r) == 5
 
 
 def test_bf16_layers_1080p():
@@ -66,6 +71,19 @@ def test_fp16_layers_1080p():
     recs = LC.check_layers(_net("johnson", 0, "fp16"), frames, "imagenet_255")
     _report(recs)
     assert max(r.get("absmax", 0.0) for r in recs) < 65504
+
+
+def test_fp16m_layers_1080p():
+    """NST_DT_F16M at configs[1]'s frame size: the split-precision head (first layer, down-convs, first residual
+    block: fp32 outputs against the exact conv of the same operand), the fp16 join and the fp16 trunk / up-convs /
+    output conv, every output row of every layer."""
+    frames = synthetic.make_frames(1, 1080, 1920, seed=1000)
+    recs = LC.check_layers(_net("johnson", 0, "fp16m"), frames, "imagenet_255")
+    _report(recs)
+    modes = {r["layer"]: r["mode"] for r in recs}
+    assert modes["conv1.conv2d"] == 7 and modes["conv2.conv2d"] == 6 and modes["conv3.conv2d"] == 6
+    assert modes["res3.conv1.conv2d"] == 4 and modes["deconv1.conv2d"] == 5 and modes["deconv3.conv2d"] == 3
+    assert max(r.get("split_rel", 0.0) for r in recs) <= LC.SPLIT_REL
 
 
 def test_bf16_layers_4k_bands():

@@ -328,3 +328,54 @@ def test_bench_two_ranks_under_torchrun_gloo(tmp_path):
     from neuralstyletransferv1_amd.frames import rank0_share
     assert d["config"]["global_batch"] == rank0_share(2, 8) + 8
     assert d["value"] > 0 and abs(d["value"] - d["config"]["global_batch"] * 3 / (d["ms_per_step"] * 3e-3)) < 1e-3 * d["value"]
+
+
+def test_input_dir_staging_in_memory_jpeg_exif_png(tmp_path):
+    """--input_dir staging (pipeline.py:2560-2590) done in memory: a JPEG source is EXIF-uprighted and re-encoded at
+    --jpeg_quality before it is stylised, a PNG source is used as its EXIF-upright RGB image.  fp32 CLI without the
+    LAB stage vs the oracle on exactly those staged pixels: within +-1 LSB; --keep_staged writes the staged copies
+    (decoding them gives the same pixels) and does not change the outputs; a PNG level other than PIL's default
+    changes only the file, not the pixels."""
+    import io
+    ck, sd = _ckpt(tmp_path, "johnson", 3)
+    frames = synthetic.make_frames(3, 64, 96, seed=77)
+    d_in = tmp_path / "in"
+    d_in.mkdir()
+    staged = []
+    for i, f in enumerate(frames):
+        im = Image.fromarray(f)
+        if i == 1:  # EXIF orientation 6: the reference rotates 270 (upright), so the staged frame is 96 x 64
+            exif = Image.Exif()
+            exif[0x0112] = 6
+            im.save(d_in / f"frame_{i + 1:04d}.jpg", format="JPEG", quality=92, exif=exif)
+            up = Image.open(d_in / f"frame_{i + 1:04d}.jpg").convert("RGB").rotate(270, expand=True)
+        elif i == 0:
+            im.save(d_in / f"frame_{i + 1:04d}.jpg", format="JPEG", quality=92)
+            up = Image.open(d_in / f"frame_{i + 1:04d}.jpg").convert("RGB")
+        else:
+            im.save(d_in / f"frame_{i + 1:04d}.png")
+            up = im
+        if i < 2:  # the staged JPEG copy at --jpeg_quality 85, decoded
+            buf = io.BytesIO()
+            up.save(buf, format="JPEG", quality=85)
+            buf.seek(0)
+            up = Image.open(buf).convert("RGB")
+        staged.append(np.array(up))
+    outs = {}
+    for tag, extra in (("mem", []), ("keep", ["--keep_staged", "--png_compress_level", "1"])):
+        d_out = tmp_path / f"out_{tag}"
+        assert P.main(["--input_dir", str(d_in), "--output_dir", str(d_out), "--model", ck, "--io_preset", "imagenet_255",
+                       "--pattern", "frame_*", "--no-smooth_lightness", "--batch", "1", "--work_dir",
+                       str(tmp_path / f"w_{tag}")] + extra) == 0
+        outs[tag] = [np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png")) for i in range(3)]
+    for i in range(3):
+        ref = _oracle_chain([("johnson", sd)], [1.0], [staged[i]], "imagenet_255", smooth=False)[0]
+        assert outs["mem"][i].shape == staged[i].shape
+        d = np.abs(outs["mem"][i].astype(int) - ref.astype(int))
+        print(f"frame {i}: {staged[i].shape}, max |d| {d.max()}")
+        assert d.max() <= 1
+        assert np.array_equal(outs["mem"][i], outs["keep"][i])
+    kept = sorted((tmp_path / "w_keep").rglob("frame_*"))
+    assert len(kept) == 3
+    for i, p in enumerate(kept):
+        assert np.array_equal(np.array(Image.open(p).convert("RGB")), staged[i])

@@ -228,8 +228,8 @@ def test_feather_restatement_properties():
 
 
 def test_check_scratch_flags_spills(tmp_path):
-    """tools/check_scratch.py (run by the Makefile on the counted-vmcnt kernels): a kernel with scratch is reported
-    (and fails the build under NST_STRICT_SCRATCH=1), a clean remarks file passes, compiler warnings are echoed."""
+    """tools/check_scratch.py (run by the Makefile on the counted-vmcnt kernels): a kernel with scratch fails the
+    build (NST_STRICT_SCRATCH=0 only reports it), a clean remarks file passes, compiler warnings are echoed."""
     import subprocess
     import sys
     from pathlib import Path
@@ -242,9 +242,10 @@ def test_check_scratch_flags_spills(tmp_path):
     bad.write_text(rem.format("Function Name: k1") + rem.format("    ScratchSize [bytes/lane]: 20"))
     r = subprocess.run([sys.executable, str(root / "tools/check_scratch.py"), str(ok)], capture_output=True, text=True)
     assert r.returncode == 0 and "warning: unused" in r.stderr and "__global__" not in r.stderr
-    r = subprocess.run([sys.executable, str(root / "tools/check_scratch.py"), str(bad)], capture_output=True, text=True)
-    assert r.returncode == 0 and "k1 uses 20 bytes/lane" in r.stderr
-    env = dict(os.environ, NST_STRICT_SCRATCH="1")
+    env = {k: v for k, v in os.environ.items() if k != "NST_STRICT_SCRATCH"}
     r = subprocess.run([sys.executable, str(root / "tools/check_scratch.py"), str(bad)], capture_output=True, text=True,
                        env=env)
-    assert r.returncode == 1
+    assert r.returncode == 1 and "k1 uses 20 bytes/lane" in r.stderr
+    r = subprocess.run([sys.executable, str(root / "tools/check_scratch.py"), str(bad)], capture_output=True, text=True,
+                       env=dict(env, NST_STRICT_SCRATCH="0"))
+    assert r.returncode == 0

@@ -23,7 +23,7 @@ for spec in "$@"; do
     -Iinclude -Ineuralstyletransferv1_amd/csrc $flags -Rpass-analysis=kernel-resource-usage -c "$SRC" \
     -o "build/var/${base}_$name.o" 2> "build/var/${base}_$name.rem" &&
     case "$base" in  # the Makefile's scratch check for the counted-vmcnt kernels
-      conv_wstat.hip|conv_wphase.hip|conv_ws9.hip|conv_gemm.hip) python3 tools/check_scratch.py "build/var/${base}_$name.rem" ;;
+      conv_wstat.hip|conv_wphase.hip|conv_ws9.hip|conv_gemm.hip|conv_ws2.hip) python3 tools/check_scratch.py "build/var/${base}_$name.rem" ;;
       *) true ;;
     esac || { rm -f "build/var/${base}_$name.o"; echo "variant $name failed"; exit 1; } ) &
   pids="$pids $!"
