@@ -9,7 +9,7 @@ BUILD := build/obj
 SLP ?= -fno-slp-vectorize
 CXXFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off $(SLP) -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
-SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_f32s.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/conv_gemm.hip $(CSRC)/seg_ops.hip $(CSRC)/region_ops.hip $(CSRC)/flow_ops.hip $(CSRC)/dis_ops.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp $(CSRC)/seg_deeplab.cpp $(CSRC)/region_api.cpp $(CSRC)/flow_api.cpp
+SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_ws1s.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_f32s.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/conv_gemm.hip $(CSRC)/seg_ops.hip $(CSRC)/region_ops.hip $(CSRC)/flow_ops.hip $(CSRC)/dis_ops.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp $(CSRC)/seg_deeplab.cpp $(CSRC)/region_api.cpp $(CSRC)/flow_api.cpp
 OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
 LIB := $(PKG)/libnst_hip.so
 
@@ -21,7 +21,7 @@ $(BUILD)/%.hip.o: $(CSRC)/%.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h $(C
 
 # kernels with hand-counted vmcnt waits: the build fails on any scratch use (tools/check_scratch.py; NST_STRICT_SCRATCH=0
 # reports instead, for experiment builds)
-$(BUILD)/conv_wstat.hip.o $(BUILD)/conv_wphase.hip.o $(BUILD)/conv_ws9.hip.o $(BUILD)/conv_gemm.hip.o $(BUILD)/conv_ws2.hip.o: NOSCRATCH = 1
+$(BUILD)/conv_wstat.hip.o $(BUILD)/conv_wphase.hip.o $(BUILD)/conv_ws9.hip.o $(BUILD)/conv_gemm.hip.o $(BUILD)/conv_ws2.hip.o $(BUILD)/conv_ws1s.hip.o: NOSCRATCH = 1
 
 # the persistent kernels fully unroll a long K loop (static register / LDS indices): lift the
 # pragma-unroll size cap for that translation unit only
@@ -31,6 +31,7 @@ $(BUILD)/conv_wphase.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 $(BUILD)/conv_wphase.hip.o: SLP =
 $(BUILD)/conv_ws2.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 $(BUILD)/conv_ws9.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
+$(BUILD)/conv_ws1s.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 
 $(BUILD)/%.cpp.o: $(CSRC)/%.cpp $(CSRC)/nst_internal.h $(CSRC)/seg_internal.h $(CSRC)/post_common.h $(CSRC)/region_internal.h $(CSRC)/flow_internal.h include/nst_hip.h
 	@mkdir -p $(BUILD)

@@ -51,9 +51,10 @@ extern "C" {
                          Wh*(xh + xl) + Wl*xh: ~22 significant bits per product (the fp32 parity bar) at a quarter of
                          the exact-f32 MFMA cycles.  Conv inputs must stay inside the fp16 range (|v| <= 65504) */
 #define NST_DT_F16M 4 /* split-precision head + fp16 trunk (Johnson / NST nets): the first layer takes the raw bytes
-                         (exact) against fp16 hi/lo weight pairs, the two down-convs and the first residual block
-                         run split-fp16 operands and weights (Wh*xh + Wh*xl + Wl*xh) with fp32 activations, and the
-                         rest of the net runs the fp16 mode's kernels.  The layers whose rounding reaches the frame
+                         (exact) against fp16 hi/lo weight pairs, the two down-convs run split-fp16 operands and
+                         weights (Wh*xh + Wh*xl + Wl*xh), the first two residual blocks split-fp16 operands against
+                         fp16 weights (Wh*xh + Wh*xl), all with fp32 activations, and the rest of the net runs the
+                         fp16 mode's kernels.  The layers whose rounding reaches the frame
                          most (tests/precision_study.py) keep ~22-bit products: 1080p frames within +-1 LSB of the
                          fp32 reference at about 3/4 of the fp16 mode's rate.  ReCoNet: NST_E_INVALID */
 
@@ -167,7 +168,8 @@ typedef struct nst_op_desc {
   int in_elem_bytes;  /* bytes per element of src (NST_BUF_INPUT: the staged first-layer operand, 2 or 4) */
   int res_elem_bytes; /* bytes per element of the joined residual stream (res_buf / res_out), 0 if none */
   int kernel_dtype;   /* the op's arithmetic: an NST_DT_* value, or 16 / 17 (fp16 operand x fp16 hi/lo weight
-                         pairs, fp32 / fp16 output) and 18 / 19 (split fp16 operand and weights, fp32 / fp16 output) */
+                         pairs, fp32 / fp16 output), 18 / 19 (split fp16 operand and weights, fp32 / fp16 output),
+                         20 (split fp16 operand x fp16 weights, fp32 output) */
 } nst_op_desc;
 int nst_num_ops(const nst_handle* h);
 int nst_op_describe(const nst_handle* h, int n, int in_h, int in_w, int op, nst_op_desc* out);
@@ -320,7 +322,8 @@ int nst_adam_step(float* x, const float* grad, float* m, float* v, int c, int hw
  * ASPP (modeling/aspp.py:34-78), decoder (modeling/decoder.py:7-43).  Parameters by their state_dict
  * names without the "module." prefix (sky_swap.py:150 strips it), e.g. "backbone.layer3.22.conv2.weight",
  * "aspp.global_avg_pool.1.weight", "decoder.last_conv.8.bias"; running_mean / running_var are used,
- * num_batches_tracked is ignored.  NHWC activations in the compute dtype, fp32 accumulation. */
+ * num_batches_tracked is ignored.  NHWC activations in the compute dtype, fp32 accumulation; compute_dtype
+ * NST_DT_F32S keeps fp32 activations and splits every conv's operands into fp16 pairs (the split-fp16 GEMM). */
 typedef struct nst_seg nst_seg;
 int nst_seg_create(const nst_param* params, int n_params, int num_classes, int compute_dtype, int device,
                    nst_seg** out);

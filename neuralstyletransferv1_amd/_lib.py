@@ -18,7 +18,7 @@ NST_OK = 0
 NST_ARCH_JOHNSON, NST_ARCH_NST, NST_ARCH_RECONET, NST_ARCH_RECONET_FRN = 0, 1, 2, 3
 NST_DT_F32, NST_DT_BF16, NST_DT_F16, NST_DT_F32S, NST_DT_F16M = 0, 1, 2, 3, 4
 # kernel dtypes of the NST_DT_F16M split-precision layers (nst_op_desc.kernel_dtype)
-NST_KDT_SW_O32, NST_KDT_SW_O16, NST_KDT_SPLIT_O32, NST_KDT_SPLIT_O16 = 16, 17, 18, 19
+NST_KDT_SW_O32, NST_KDT_SW_O16, NST_KDT_SPLIT_O32, NST_KDT_SPLIT_O16, NST_KDT_SPLITO_O32 = 16, 17, 18, 19, 20
 NST_VGG_GENERIC_ONLY = 0x1
 NST_IO_F32_NCHW, NST_IO_U8_NHWC = 0, 1
 PRESETS = {

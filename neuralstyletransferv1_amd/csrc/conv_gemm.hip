@@ -48,10 +48,29 @@ __device__ __forceinline__ uint16_t f_to_h(float f, int dt) {
   return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
-// DT: the compute dtype (NST_DT_F32 = the exact-f32 parity mode, NST_DT_BF16, NST_DT_F16)
+// DT: the compute dtype (NST_DT_F32 = the exact-f32 parity mode, NST_DT_BF16, NST_DT_F16, or NST_DT_F32S: the fp32
+// layout of the parity mode with each 16-B operand fragment (4 fp32 values of A and of B) split into fp16 pairs in
+// registers, v = RNE16(v) + RNE16(v - RNE16(v)), and two v_mfma_f32_16x16x32_f16 per fragment pair instead of four
+// v_mfma_f32_16x16x4_f32: [Ah Ah] x [Bh Bl] + [Al 0] x [Bh Bl] = Ah Bh + Ah Bl + Al Bh over the same 4 products per
+// lane group (Al Bl, ~2^-22 of the product, dropped): ~22-bit products, fp32 accumulation)
+__device__ __forceinline__ void split4(const u32x4_g& v, uint2& hi, uint2& lo) {
+  float f[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+  _Float16 h[4], l[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    h[k] = (_Float16)f[k];
+    l[k] = (_Float16)(f[k] - (float)h[k]);
+  }
+  auto pk = [](_Float16 a, _Float16 b) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  };
+  hi = make_uint2(pk(h[0], h[1]), pk(h[2], h[3]));
+  lo = make_uint2(pk(l[0], l[1]), pk(l[2], l[3]));
+}
 template <int BM, int BN, int DT>
 __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
-  constexpr bool F32 = DT == NST_DT_F32;
+  constexpr bool SPL = DT == NST_DT_F32S;
+  constexpr bool F32 = DT == NST_DT_F32 || SPL;  // fp32 activations and weights in memory and LDS
   constexpr int MI = BM / 32, NI = BN / 32;      // 16x16 sub-tiles per wave along rows / columns
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, BUF = A_BYTES + B_BYTES;
   constexpr int A_TPR = 256 / BM, A_CPT = 8 / A_TPR;  // loader threads per row, 16-B chunks per thread
@@ -148,6 +167,32 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
       for (int i = 0; i < MI; ++i) a[i] = *(const u32x4_g*)(base + half * (BM * 64) + a_off + i * 16 * 64);
 #pragma unroll
       for (int j = 0; j < NI; ++j) b[j] = *(const u32x4_g*)(base + half * (BN * 64) + b_off + j * 16 * 64);
+      if constexpr (SPL) {
+        u32x4_g ah[MI], al[MI], bb[NI];  // [Ah Ah], [Al 0], [Bh Bl] operand fragments
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          uint2 h, l;
+          split4(a[i], h, l);
+          ah[i] = u32x4_g{h.x, h.y, h.x, h.y};
+          al[i] = u32x4_g{l.x, l.y, 0u, 0u};
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          uint2 h, l;
+          split4(b[j], h, l);
+          bb[j] = u32x4_g{h.x, h.y, l.x, l.y};
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_g, ah[i]),
+                                                               __builtin_bit_cast(f16x8_g, bb[j]), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_g, al[i]),
+                                                               __builtin_bit_cast(f16x8_g, bb[j]), acc[i][j], 0, 0, 0);
+          }
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -411,7 +456,7 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
 // split-K epilogue: sum the K slices in slice order, then scale/shift, residual, ReLU, store (as the
 // single-pass epilogue does)
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmConvParams p, int dt) {
-  const bool f32 = dt == NST_DT_F32;
+  const bool f32 = dt == NST_DT_F32 || dt == NST_DT_F32S;
   const int groups = p.cout_store >> 2;
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (size_t)p.npix * groups) return;
@@ -450,6 +495,7 @@ template <int BM, int BN>
 void launch_tile(int dt, const GemmConvParams& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM), (unsigned)p.ksplit);
   if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F32>), grid, dim3(256), 0, st, p);
+  else if (dt == NST_DT_F32S) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F32S>), grid, dim3(256), 0, st, p);
   else if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F16>), grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_BF16>), grid, dim3(256), 0, st, p);
 }
@@ -507,6 +553,7 @@ struct GemmShape {
   int ksplit;
 };
 GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
+  if (dtype == NST_DT_F32S) dtype = NST_DT_F32;  // the fp32 layout and launch shapes (register-staged kernel)
   const int nstage = p.ntaps * (p.cin / gemm_stage_channels(dtype));
   const long mt = (p.cout_store + 127) / 128;
   GemmShape g{GK_REG64, 1};

@@ -164,12 +164,20 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   };
 
   typedef f32x4_t Acc[C::TH][2];
+  // SW: asm MFMAs (accumulators tied in place: the builtins let hipcc allocate a destination over an operand,
+  // mfma16x16x16_tied); the epilogue then drains the MFMA pipe before its VALU reads
   auto mfma32 = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) {
+    if constexpr (SW) {
+      mfma_tied<T>(c, a, bop, first);
+      return;
+    }
     const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
     c = mfma16x16x32<T>(a, bop, first ? z : c);
   };
   auto mfma16 = [&](f32x4_t& c, const uint2& a, const uint2& bop) {
-    if constexpr (IS_F16<T>)
+    if constexpr (SW)
+      mfma16x16x16_tied<T>(c, a, bop);
+    else if constexpr (IS_F16<T>)
       c = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4_t, a), __builtin_bit_cast(f16x4_t, bop), c, 0, 0, 0);
     else
       c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4_t, a), __builtin_bit_cast(s16x4_t, bop), c,
@@ -276,6 +284,7 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
       const int ch = 16 * (px >> 3) + 4 * g + ((px >> 1) & 3);
       ((float*)(smem + C::PART_OFF))[wv * 64 + ch * 2 + (px & 1)] = a1[0];
     } else {
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // asm MFMA results -> VALU reads
       // hi + lo partial sums of channels 16 mh + 4 g .. + 3, + bias (fp32), into the staged tile
       const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 * mh + 4 * g) * 4);
       int obase = C::OUT_OFF + (16 * strip + px) * C::PIXB;

@@ -46,6 +46,19 @@ __device__ __forceinline__ void mfma_tied(f32x4_t& c, const uint4& a, const uint
   }
 }
 
+// v_mfma_f32_16x16x16_{f16,bf16} accumulating in place (asm: the accumulator is tied, so hipcc cannot give the
+// destination a register of the A / B operands -- conv_ws9.hip's split-weight variant got
+// v_mfma_f32_16x16x16_f16 v[178:181], v[92:93], v[178:179], ... from the builtin and two result values came out
+// wrong; tools/check_mfma_overlap.py)
+template <typename T>
+__device__ __forceinline__ void mfma16x16x16_tied(f32x4_t& c, const uint2& a, const uint2& bop) {
+  const u32x2_t av = __builtin_bit_cast(u32x2_t, a), bv = __builtin_bit_cast(u32x2_t, bop);
+  if constexpr (IS_F16<T>)
+    asm volatile("v_mfma_f32_16x16x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
+  else
+    asm volatile("v_mfma_f32_16x16x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(av), "v"(bv));
+}
+
 // the same with C = cinit for a tile row's first MFMA (the conv bias: the epilogue then adds nothing)
 template <typename T>
 __device__ __forceinline__ void mfma_tied_c(f32x4_t& c, const uint4& a, const uint4& bop, bool first, const f32x4_t& cinit) {

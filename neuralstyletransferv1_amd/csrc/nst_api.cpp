@@ -34,6 +34,7 @@ const ConvKernelInfo* conv_table_wstat(int* count);
 const ConvKernelInfo* conv_table_wphase(int* count);
 const ConvKernelInfo* conv_table_ws2(int* count);
 const ConvKernelInfo* conv_table_ws9(int* count);
+const ConvKernelInfo* conv_table_ws1s(int* count);
 
 // first match wins: the persistent / LDS-weight-ring table is searched before the plain one
 const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, int cinp, int bn, int in_kind,
@@ -41,12 +42,12 @@ const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, 
   typedef const ConvKernelInfo* (*TableFn)(int*);
   // 16-bit formats (bf16, fp16) share the specialised tables; an entry matches only its own dtype
   const TableFn tables_16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_ws9,
-                               conv_table_out9, conv_table_bf16, conv_table_f16};
+                               conv_table_out9, conv_table_bf16, conv_table_f16, conv_table_ws1s};
   // 4-byte activation formats (fp32, split-fp16): the generic kernels only
   const TableFn tables_f32[] = {conv_table_f32, conv_table_f32s};
   const bool h16 = !f32_storage(dtype);
   const TableFn* tables = h16 ? tables_16 : tables_f32;
-  const int ntables = h16 ? 8 : 2;
+  const int ntables = h16 ? 9 : 2;
   for (int ti = (h16 && no_persistent) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
     const ConvKernelInfo* t = tables[ti](&count);
@@ -112,9 +113,9 @@ static bool is_reconet(int arch) { return arch == NST_ARCH_RECONET || arch == NS
 
 // x0_export (with fuse_res): block 1's conv1 also writes x_0 = ReLU(IN_2(C)) from its fill (only the
 // weight-stationary trunk kernel does), so block 2's join reads a stored x_0 like every later join
-// split_head (NST_DT_F16M): the first residual block runs unfused on the split-precision generic kernels (fp32
-// activations) and a separate residual add writes x_1 = IN(y) + ReLU(IN_2(C)) as the fp16 stream; blocks 2..5 are
-// the fused fp16 program from that stored stream (block 2's conv1 reads x_1 as is, later joins read it)
+// split_head (NST_DT_F16M): the first two residual blocks run unfused on the split-operand kernel (fp32
+// activations), separate residual adds write x_1 (fp32) and x_2 (the fp16 stream); blocks 3..5 are the fused fp16
+// program from that stored stream (block 3's conv1 reads x_2 as is, later joins read it)
 static void build_program(int arch, bool fuse_res, bool x0_export, std::vector<LayerDef>& L, std::vector<Op>& P,
                           bool split_head = false) {
   L.clear();
@@ -179,15 +180,21 @@ static void build_program(int arch, bool fuse_res, bool x0_export, std::vector<L
   conv(1, B_A, B_B, 0);
   conv(2, B_B, B_C, 1);
   if (split_head) {
+    // blocks 1-2 unfused on fp32 activations: x_1 = IN(y) + ReLU(IN_2(C)) as fp32 in F, x_2 = IN(y) + x_1 as the
+    // fp16 stream in G; blocks 3..5 fused from G (block 3's conv1 reads x_2 as is)
     conv(3, B_C, B_D, 2);
     conv(4, B_D, B_E, 3);
     resadd(4, B_E, B_F, B_C, 2, relu_out);
+    P.back().out_esz = 4;
+    conv(5, B_F, B_D, -1);
+    conv(6, B_D, B_E, 5);
+    resadd(6, B_E, B_G, B_F, -1, relu_out);
     P.back().out_esz = 2;
-    int xbuf = B_F;
-    for (int r = 1; r < nres; ++r) {
+    int xbuf = B_G;
+    for (int r = 2; r < nres; ++r) {
       const int l1 = 3 + 2 * r, l2 = 4 + 2 * r;
-      if (r == 1) {
-        conv(l1, B_F, B_D, -1);  // x_1 as stored: the fill applies nothing
+      if (r == 2) {
+        conv(l1, B_G, B_D, -1);  // x_2 as stored: the fill applies nothing
       } else {
         const int xout = xbuf == B_F ? B_G : B_F;
         convres(l1, B_E, l2 - 2, xbuf, -1, xout, relu_out, B_D);
@@ -882,7 +889,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     if (!f16m) return compute_dtype;
     if (li == 0) return NST_KDT_SW_O32;            // raw-byte operand x fp16 hi / lo weights, fp32 out
     if (li == 1 || li == 2) return NST_KDT_SPLIT_O32;  // split operand and weights, fp32 out
-    if (li == 3 || li == 4) return NST_DT_F32S;    // first residual block: the split-fp16 generic kernels
+    if (li >= 3 && li <= 6) return NST_KDT_SPLITO_O32;  // residual blocks 1-2: split operand, fp16 weights, fp32
     return NST_DT_F16;
   };
   const bool no_pers = (flags & NST_KSEL_NO_PERSISTENT) != 0;
@@ -951,6 +958,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     // stride-2 down-convs: weight-stationary kernel (conv_ws2.hip) where compiled
     if (!up && !final_layer && !image_in && d.ks == 3 && d.stride == 2 && !(flags & NST_KSEL_NO_WS2))
       modes.push_back(MODE_WS2);
+    if (kdt == NST_KDT_SPLITO_O32) modes.insert(modes.begin(), MODE_WS1S);
     modes.push_back(MODE_STD);
     // image layer: prefer the conv over the pre-padded encoded input (one streaming pre-pass, plain
     // 16-byte fill loads) when it is compiled for this shape; it serves u8 and f32 inputs alike
@@ -998,7 +1006,8 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     }
     auto upload_packed = [&](const std::vector<float>& pk, void** dst) -> int {
       if (Ly.k_main->split_w) return upload_weights(NST_DT_F16, split_weight_frags(*Ly.k_main, pk), dst);
-      return upload_weights(kdt, pk, dst);
+      // the split-operand kernels (NST_KDT_*) take plain fp16 weights
+      return upload_weights(kdt >= NST_KDT_SW_O32 ? NST_DT_F16 : kdt, pk, dst);
     };
     Ly.in_esz = Ly.k_main->in_esz ? Ly.k_main->in_esz : (int)act_elem_bytes(kdt);
     Ly.out_esz = Ly.k_main->out_esz ? Ly.k_main->out_esz : (int)act_elem_bytes(kdt);
@@ -1008,7 +1017,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       if ((rc = upload_packed(pack_wstat_weights(d, W), &Ly.wpk)) != NST_OK) break;
     } else if (Ly.mode == MODE_WPHASE) {
       if ((rc = upload_packed(pack_wphase_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
-    } else if (Ly.mode == MODE_WS2) {
+    } else if (Ly.mode == MODE_WS2 || Ly.mode == MODE_WS1S) {  // [channel group][step][lane][8]: the same order
       if ((rc = upload_packed(pack_ws2_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
     } else if (Ly.mode == MODE_WS9) {
       if ((rc = upload_packed(pack_ws9_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
@@ -1150,10 +1159,12 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     auto tab = [&](int layer) { return layer >= 0 ? stats[layer] : nullptr; };
     if (op.kind == OP_RESADD) {
       const int hw = P.oh[i] * P.ow[i];
+      // element formats of y / r / out: all the handle's, all fp32 (NST_DT_F16M's first join), or fp32 -> fp16
+      const int rdt = P.out_esz[i] == 4 ? NST_DT_F32 : h->dtype;
       hipError_t e = (P.in_esz[i] == 4 && P.res_esz[i] == 4 && P.out_esz[i] == 2)
                          ? launch_residual_f32_to_f16(bufs[op.src], tab(op.layer), bufs[op.r_buf], tab(op.r_norm),
                                                       op.r_relu, op.relu_out, bufs[op.dst], n, hw, Ly.coutp, st)
-                         : launch_residual(h->dtype, bufs[op.src], tab(op.layer), bufs[op.r_buf], tab(op.r_norm), op.r_relu,
+                         : launch_residual(rdt, bufs[op.src], tab(op.layer), bufs[op.r_buf], tab(op.r_norm), op.r_relu,
                                            op.relu_out, bufs[op.dst], n, hw, Ly.coutp, st);
       if (e != hipSuccess) { set_error(std::string("residual launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
       if (cap && cap->act && cap->act[i])
@@ -1252,7 +1263,12 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
       set_error("conv " + Ly.d.conv + ": weight-stationary 9x9 kernel reads the pre-padded frame, uncropped");
       return NST_E_SHAPE;
     }
-    if ((Ly.mode == MODE_WPHASE || Ly.mode == MODE_WSTAT || Ly.mode == MODE_WS2 || Ly.mode == MODE_WS9) && p.cout_stride != k->bn) {
+    if (Ly.mode == MODE_WS1S && (p.res_r != nullptr || p.res_out != nullptr || p.crop_x || p.crop_y)) {
+      set_error("conv " + Ly.d.conv + ": split-operand trunk kernel runs plain convs, uncropped");
+      return NST_E_SHAPE;
+    }
+    if ((Ly.mode == MODE_WPHASE || Ly.mode == MODE_WSTAT || Ly.mode == MODE_WS2 || Ly.mode == MODE_WS9 ||
+         Ly.mode == MODE_WS1S) && p.cout_stride != k->bn) {
       set_error("conv " + Ly.d.conv + ": weight-stationary kernels store whole pixels of bn channels");
       return NST_E_SHAPE;
     }

@@ -77,7 +77,8 @@ enum OutKind { OUT_ACT = 0, OUT_U8_NHWC = 1, OUT_F32_NCHW = 2 };
 enum AxisMode { AX_REFLECT = 0, AX_REFLECT_UP2 = 1, AX_ZERO = 2, AX_ZERO_PREREFLECT = 3, AX_ZINSERT = 4, AX_CLAMP = 5 };
 
 // conv_kernel mappings (see conv_impl.h)
-enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2, MODE_KYROT = 3, MODE_WSTAT = 4, MODE_WPHASE = 5, MODE_WS2 = 6, MODE_WS9 = 7 };  // KYROT: conv_out9.hip, WSTAT: conv_wstat.hip, WPHASE: conv_wphase.hip, WS2: conv_ws2.hip, WS9: conv_ws9.hip
+enum ConvMode { MODE_STD = 0, MODE_PHASE = 1, MODE_XSHIFT = 2, MODE_KYROT = 3, MODE_WSTAT = 4, MODE_WPHASE = 5, MODE_WS2 = 6, MODE_WS9 = 7,
+                MODE_WS1S = 8 };  // WS1S: conv_ws1s.hip (split-operand stride-1 trunk conv)  // KYROT: conv_out9.hip, WSTAT: conv_wstat.hip, WPHASE: conv_wphase.hip, WS2: conv_ws2.hip, WS9: conv_ws9.hip
 
 struct ConvParams {
   // input
@@ -126,7 +127,9 @@ struct ConvParams {
 //   SW:    fp16 operand (the first layer's exact raw bytes) x fp16 hi / lo weight pairs
 //   SPLIT: fp32 input staged as an fp16 hi / lo operand pair x fp16 hi / lo weight pairs (Wh xh + Wh xl + Wl xh)
 //   O32 / O16: fp32 / fp16 output storage
-enum KernelDtype { NST_KDT_SW_O32 = 16, NST_KDT_SW_O16 = 17, NST_KDT_SPLIT_O32 = 18, NST_KDT_SPLIT_O16 = 19 };
+//   SPLITO: fp32 input staged as an fp16 hi / lo operand pair x fp16 weights (Wh xh + Wh xl), fp32 output
+enum KernelDtype { NST_KDT_SW_O32 = 16, NST_KDT_SW_O16 = 17, NST_KDT_SPLIT_O32 = 18, NST_KDT_SPLIT_O16 = 19,
+                   NST_KDT_SPLITO_O32 = 20 };
 
 // Static description of one compiled conv kernel instantiation.
 struct ConvKernelInfo {

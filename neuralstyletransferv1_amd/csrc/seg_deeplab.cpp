@@ -146,6 +146,9 @@ int out_extent(int in, int k, int s, int d, int p) { return (in + 2 * p - d * (k
 
 struct nst_seg {
   int device = 0, dtype = NST_DT_BF16, nc = 0, ncs = 0;
+  // the GEMM convs' arithmetic: dtype, or NST_DT_F32S with dtype = NST_DT_F32 (the fp32 layout everywhere, each
+  // conv's operands split into fp16 pairs in registers: conv_gemm.hip gemm_conv_kernel)
+  int gemm_dt = NST_DT_BF16;
   int cache_n = 0, cache_h = 0, cache_w = 0;  // geometry of the cached workspace plan
   size_t cache_partial = 0;
   SegConv stem;
@@ -232,7 +235,7 @@ hipError_t run(const nst_seg* s, SegRun& R, const SegConv& L, const void* in, in
     return hipSuccess;
   }
   p.partial = (need && need <= R.partial_bytes) ? R.partial : nullptr;
-  return launch_gemm_conv(s->dtype, p, st);
+  return launch_gemm_conv(s->gemm_dt, p, st);
 }
 
 #define SEG_CHECK(expr)                                                                            \
@@ -404,7 +407,8 @@ extern "C" {
 int nst_seg_create(const nst_param* params, int n_params, int num_classes, int compute_dtype, int device,
                    nst_seg** out) {
   if (!params || n_params <= 0 || !out || num_classes < 2 || num_classes > 256 ||
-      (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16 && compute_dtype != NST_DT_F16)) {
+      (compute_dtype != NST_DT_F32 && compute_dtype != NST_DT_BF16 && compute_dtype != NST_DT_F16 &&
+       compute_dtype != NST_DT_F32S)) {
     set_error("nst_seg_create: invalid arguments");
     return NST_E_INVALID;
   }
@@ -417,6 +421,8 @@ int nst_seg_create(const nst_param* params, int n_params, int num_classes, int c
   if (hipSetDevice(device) != hipSuccess) { set_error("nst_seg_create: bad device"); return NST_E_INVALID; }
   auto* s = new nst_seg();
   s->device = device;
+  s->gemm_dt = compute_dtype;
+  if (compute_dtype == NST_DT_F32S) compute_dtype = NST_DT_F32;  // layout, packing and the non-GEMM kernels: fp32
   s->dtype = compute_dtype;
   s->nc = num_classes;
   s->ncs = (num_classes + 3) / 4 * 4;

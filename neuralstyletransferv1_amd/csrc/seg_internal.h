@@ -49,7 +49,7 @@ hipError_t launch_gemm_conv(int dtype, GemmConvParams& p, hipStream_t st);
 // bytes of split-K scratch the launch of this conv would use (0: no split)
 size_t gemm_partial_bytes(int dtype, const GemmConvParams& p);
 // stage width in channels for a dtype (64 bf16 / fp16, 32 fp32)
-inline int gemm_stage_channels(int dtype) { return dtype == NST_DT_F32 ? 32 : 64; }
+inline int gemm_stage_channels(int dtype) { return (dtype == NST_DT_F32 || dtype == NST_DT_F32S) ? 32 : 64; }
 
 // ---- seg_ops.hip ----
 // Stem im2col for the 7x7/2 pad-3 first conv: source = frames u8 NHWC [n][h][w][3] normalised as

@@ -24,7 +24,7 @@ from . import _lib
 from ._lib import NstError, NstParam, check, lib
 
 _DTYPES = {"fp32": _lib.NST_DT_F32, "float32": _lib.NST_DT_F32, "bf16": _lib.NST_DT_BF16, "bfloat16": _lib.NST_DT_BF16,
-           "fp16": _lib.NST_DT_F16, "float16": _lib.NST_DT_F16}
+           "fp16": _lib.NST_DT_F16, "float16": _lib.NST_DT_F16, "fp32s": _lib.NST_DT_F32S}
 
 # resnet.py:153 ResNet101 blocks per layer; :50-56 output stride 16 strides / dilations; :50 multi-grid
 RESNET101_LAYERS = (3, 4, 23)
@@ -121,7 +121,7 @@ class SegEngine:
         if device.type != "cuda":
             raise NstError("libnst_hip runs on MI355X (cuda) devices only; there is no CPU path")
         if dtype not in _DTYPES:
-            raise NstError(f"compute_dtype must be fp32, bf16 or fp16, got {dtype!r}")
+            raise NstError(f"compute_dtype must be fp32, fp32s, bf16 or fp16, got {dtype!r}")
         self.device = device
         self.num_classes = int(num_classes)
         self.dtype = _DTYPES[dtype]

@@ -54,17 +54,20 @@ def _margin(y):
     return s[:, -1] - s[:, -2]
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "fp32s"])
 @pytest.mark.parametrize("case", CASES)
-def test_forward_fp32_vs_reference(case):
+def test_forward_fp32_vs_reference(case, dtype):
+    """Logits vs the reference modules' (goldens): exact-f32 GEMMs, and the split-fp16 GEMMs (fp32s) held to the
+    same fp32 bars."""
     z = np.load(os.path.join(GOLDEN, case))
-    m = _model(int(z["num_classes"]), int(z["seed"]), "fp32")
+    m = _model(int(z["num_classes"]), int(z["seed"]), dtype)
     y = m(torch.from_numpy(z["x"]).to(DEV)).cpu().numpy()
     ref = z["y"]
     assert y.shape == ref.shape
     rel = float(np.abs(y - ref).max() / np.abs(ref).max())
     decided = _margin(ref) > 1e-4 * np.abs(ref).max()
     agree = (y.argmax(1) == ref.argmax(1))
-    print(case, f"fp32 max rel {rel:.2e}, argmax agreement {agree.mean():.6f}, on decided pixels {agree[decided].mean()}")
+    print(case, f"{dtype} max rel {rel:.2e}, argmax agreement {agree.mean():.6f}, on decided pixels {agree[decided].mean()}")
     assert rel <= 1e-4, rel
     assert agree[decided].all()
 
@@ -88,7 +91,7 @@ def test_forward_16bit_vs_reference(case, dtype):
     assert agree >= 0.98, agree
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("dtype", ["fp32", "fp32s", "bf16", "fp16"])
 def test_forward_deterministic(dtype):
     m = _model(19, 0, dtype)
     x = torch.randn(2, 3, 72, 96, generator=torch.Generator().manual_seed(5)).to(DEV)
@@ -163,12 +166,14 @@ def test_mask_post_vs_oracle(params):
             assert d.max() == 0
 
 
-def test_mask_engine_1080p_vs_oracle():
-    """configs[4]'s mask producer on two 1080p frames (working size 256x144): GPU (fp32) vs the oracle chain
-    (Pillow LANCZOS -> preprocess -> DeepLab -> argmax -> select / close / feather -> INTER_LINEAR)."""
-    m = _model(19, 0, "fp32")
+@pytest.mark.parametrize("dtype", ["fp32", "fp32s"])
+def test_mask_engine_1080p_vs_oracle(dtype):
+    """configs[4]'s mask producer on two 1080p frames (working size 256x144): GPU vs the oracle chain (Pillow
+    LANCZOS -> preprocess -> DeepLab -> argmax -> select / close / feather -> INTER_LINEAR), in the exact-f32 mode
+    and the split-fp16 GEMM mode (fp32 activations, fp16 operand pairs): the same bars."""
+    m = _model(19, 0, dtype)
     frames = synthetic.make_frames(2, 1080, 1920, seed=21)
-    me = deeplab.MaskEngine(m, DEV, resolution=256, dtype="fp32")
+    me = deeplab.MaskEngine(m, DEV, resolution=256, dtype=dtype)
     ids = [8, 11, 18]
     masks, pred = me.masks(torch.from_numpy(frames).to(DEV), ids, feather_px=3, return_pred=True)
     masks, pred = masks.cpu().numpy(), pred.cpu().numpy()
