@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "conv_ws_common.h"
 #include "nst_hip.h"
@@ -275,14 +276,14 @@ template <int BM, int BN, int DT, int RING>
 __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32_t w_bytes, uint32_t in_bytes) {
   constexpr int NW = 8, WM = BM / 64, WN = NW / WM;   // wave grid
   constexpr int MI = 4, NI = BN / (16 * WN);           // 16x16 sub-tiles per wave
-  static_assert(BM == 64 || BM == 128, "BM");
+  static_assert(BM == 64 || BM == 128 || BM == 256, "BM");
   static_assert(NI >= 1 && BN % (16 * WN) == 0, "BN");
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, BUF = A_BYTES + B_BYTES;
   constexpr int A_INS = A_BYTES / 1024 / NW, B_INS = B_BYTES / 1024 / NW;  // DMA instructions per wave and stage
   constexpr int NINS = A_INS + B_INS;
   constexpr bool F32 = DT == NST_DT_F32;
   constexpr int ESZ = F32 ? 4 : 2, CK = 128 / ESZ;  // bytes per element, channels per stage
-  static_assert(RING == 3 || RING == 4, "ring");
+  static_assert(RING >= 2 && RING <= 4, "ring");
   __shared__ __attribute__((aligned(16))) char lds[RING * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -357,15 +358,15 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4_g{0.f, 0.f, 0.f, 0.f};
 
-  if (s_begin < s_end) issue(s_begin);
-  if (s_begin + 1 < s_end) issue(s_begin + 1);
-  if (RING == 4 && s_begin + 2 < s_end) issue(s_begin + 2);
+#pragma unroll
+  for (int k = 0; k < RING - 1; ++k)
+    if (s_begin + k < s_end) issue(s_begin + k);
   for (int s = s_begin; s < s_end; ++s) {
     // stage s landed (the RING - 2 stages after it may stay in flight); the barrier also ends every wave's reads
     // of slot (s + RING - 1) % RING
-    const int later = s_end - 1 - s;
-    if (RING == 4 && later >= 2) vm_wait<2 * NINS>();
-    else if (later >= 1) vm_wait<NINS>();
+    const int ahead = std::min(RING - 2, s_end - 1 - s);
+    if (ahead >= 2) vm_wait<2 * NINS>();
+    else if (ahead == 1) vm_wait<NINS>();
     else vm_wait<0>();
     lds_barrier();
     if (s + RING - 1 < s_end) issue(s + RING - 1);
@@ -547,7 +548,16 @@ void live_taps(GemmConvParams& p) {
 #ifndef NST_GEMM_BM64  // 64 x 256 LDS-DMA tiles for outputs of at most 64 channels
 #define NST_GEMM_BM64 1
 #endif
-enum GemmKind { GK_REG64 = 0, GK_REG128 = 1, GK_GLDS256 = 2, GK_GLDS128 = 3, GK_GLDS64x256 = 4 };
+// 256 x 256 LDS-DMA tiles (a 128 x 64 block per wave: a quarter fewer LDS fragment bytes per MFMA than 128 x 256,
+// one stage in flight in a 2 x 64 KB ring), split in K to fill the chip: NST_GEMM_T256=1 enables them
+enum GemmKind { GK_REG64 = 0, GK_REG128 = 1, GK_GLDS256 = 2, GK_GLDS128 = 3, GK_GLDS64x256 = 4, GK_GLDS256x256 = 5 };
+int gemm_t256() {
+  static const int v = [] {
+    const char* e = std::getenv("NST_GEMM_T256");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 struct GemmShape {
   int kind;
   int ksplit;
@@ -564,6 +574,11 @@ GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
     const double w_b = (double)((p.cout_store + 63) / 64) * p.kh * p.kw * (p.cin / (128 / esz)) * 8192.0;
     if (in_b < 2147483648.0 && w_b < 2147483648.0) {
       const long t256 = (long)((p.npix + 255) / 256) * mt, t128 = (long)((p.npix + 127) / 128) * mt;
+      if (gemm_t256() && p.cout_store > 128 && nstage >= 16) {
+        const long tt = (long)((p.npix + 255) / 256) * ((p.cout_store + 255) / 256);
+        const long k = std::max<long>(1, std::min<long>((256 + tt - 1) / tt, std::min<long>(8, nstage / 8)));
+        if (tt * k >= 128) return GemmShape{GK_GLDS256x256, (int)k};
+      }
       if (t256 >= 200) return GemmShape{NST_GEMM_BM64 && p.cout_store <= 64 ? GK_GLDS64x256 : GK_GLDS256, 1};
       if (NST_GEMM_SPLIT256 && p.cout_store > 64 && t128 < 200 && t256 >= 32 && nstage >= 16) {
         // a 128 x 256 tile reads a third less LDS per output than 128 x 128 (64 x 64 per wave instead of 64 x 32);
@@ -601,7 +616,8 @@ void launch_glds(int dt, const GemmConvParams& p, hipStream_t st) {
   const uint32_t in_b = (uint32_t)(n_img * p.hi * p.wi * p.cs * esz);
   const uint32_t w_b = (uint32_t)((p.cout_store + 63) / 64) * (uint32_t)(p.kh * p.kw * (p.cin / (128 / esz))) * 8192u;
   const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM), (unsigned)p.ksplit);
-  constexpr int RING = BM * 128 + BN * 128 <= 32768 ? NST_GEMM_RING_32K : 3;  // 4 x 32 KB stages fit the LDS, 4 x 48 KB do not
+  // 4 x 32 KB stages fit the LDS, 4 x 48 KB do not, 2 x 64 KB (256 x 256) do
+  constexpr int RING = BM * 128 + BN * 128 <= 32768 ? NST_GEMM_RING_32K : (BM * 128 + BN * 128 <= 49152 ? 3 : 2);
   if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_F16, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
   else if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_F32, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
   else hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_BF16, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
@@ -625,7 +641,8 @@ hipError_t launch_gemm_conv(int dtype, GemmConvParams& p, hipStream_t st) {
   if (p.ntaps == 0) return hipErrorInvalidValue;
   const GemmShape g = gemm_shape(dtype, p);
   p.ksplit = p.partial ? g.ksplit : 1;
-  if (g.kind == GK_GLDS64x256) launch_glds<64, 256>(dtype, p, st);
+  if (g.kind == GK_GLDS256x256) launch_glds<256, 256>(dtype, p, st);
+  else if (g.kind == GK_GLDS64x256) launch_glds<64, 256>(dtype, p, st);
   else if (g.kind == GK_GLDS256) launch_glds<128, 256>(dtype, p, st);
   else if (g.kind == GK_GLDS128) launch_glds<128, 128>(dtype, p, st);
   else if (g.kind == GK_REG128) launch_tile<128, 128>(dtype, p, st);

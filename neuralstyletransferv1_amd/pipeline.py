@@ -58,6 +58,11 @@ IO_PRESETS_AUTO = {  # pipeline.py:2518-2523
 SLOTS = ["b", "c", "d", "e", "f", "g", "h"]
 
 
+# the last style_frames run on this process: frames, seconds of the frame loop (decode -> GPU -> encode, from the
+# first frame load to the last file written) and seconds of setup before it (model load, plans, size scan)
+LAST_RUN_STATS: Dict[str, float] = {}
+
+
 def _log(msg: str) -> None:
     print(msg, flush=True)
 
@@ -165,9 +170,13 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--keep_staged", action="store_true",
                     help="--input_dir: also write the staged frame copies (the reference's work_dir/frames files); the "
                          "frames are staged in memory either way, with the same pixels")
+    ap.add_argument("--png_writer", choices=["fast", "pil"], default="fast",
+                    help="PNG outputs: 'fast' = Up filter + zlib RLE deflate (pngio.py: ~6x faster than Pillow's "
+                         "default encoder, files within a few percent of its size), 'pil' = Pillow's encoder at its "
+                         "defaults, byte-identical to the reference's files.  The pixels are identical either way")
     ap.add_argument("--png_compress_level", type=int, default=None, choices=range(10), metavar="0-9",
-                    help="zlib level of the PNG outputs (default: PIL's, as the reference saves them); the pixels "
-                         "are the same at every level, only the file size and the encode time change")
+                    help="Pillow's PNG encoder at this zlib level (overrides --png_writer); the pixels are the same "
+                         "at every level, only the file size and the encode time change")
     return ap
 
 
@@ -409,11 +418,14 @@ class FrameSource:
         pil = _get_image_with_exif_pil(str(src))
         if q is None:
             return pil
-        import io
-        buf = io.BytesIO()
-        pil.save(buf, format="JPEG", quality=q)
-        buf.seek(0)
-        return Image.open(buf).convert("RGB")
+        # the round trip goes through an anonymous in-memory file with a real descriptor: Pillow encodes to a
+        # descriptor with the GIL released (to a BytesIO it holds the GIL, so a thread pool would serialise)
+        with os.fdopen(os.memfd_create("nst_stage"), "w+b") as f:
+            pil.save(f, format="JPEG", quality=q)
+            f.seek(0)
+            im = Image.open(f)
+            im.load()
+            return im if im.mode == "RGB" else im.convert("RGB")
 
     def load(self, i: int):
         """-> (original uint8 HxWx3, model-input uint8 hxwx3)."""
@@ -444,6 +456,7 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     from PIL import Image
 
     from .frames import plan_groups, rank0_share, run_sharded
+    t_setup = time.perf_counter()
     from .postproc import LabSmoother, blend_frames
 
     # one GPU per rank (several ranks may share a device with --dist_backend gloo: tests)
@@ -719,6 +732,9 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             out_img.save(out_path, format="JPEG", quality=int(jpeg_quality))
         elif getattr(args, "png_compress_level", None) is not None:
             out_img.save(out_path, compress_level=int(args.png_compress_level))
+        elif getattr(args, "png_writer", "fast") == "fast":  # same pixels as Pillow's file (pngio docstring)
+            from .pngio import write_png
+            write_png(out_path, img)
         else:
             out_img.save(out_path)
         return str(out_path)
@@ -727,8 +743,9 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     for p in pending:
         p.result()
     pool.shutdown()
+    el = time.perf_counter() - t_start
+    LAST_RUN_STATS.update(frames=len(src), seconds=el, setup_seconds=t_start - t_setup)
     if rank == 0:
-        el = time.perf_counter() - t_start
         _log(f"Styled {len(src)}/{len(src)} frames in {el:.2f}s ({len(src) / max(el, 1e-9):.2f} frames/s)")
 
 
@@ -897,11 +914,13 @@ def prepare(args):
     return frames_dir, model_path, save_map, (image_single or image_batch), video
 
 
-def _worker(rank: int, world: int, argv: List[str], port: int, prep):
+def _worker(rank: int, world: int, argv: List[str], port: int, prep, staged=None):
     import torch
     import torch.distributed as dist
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     args = build_parser().parse_args(argv)
+    if staged is not None:  # --input_dir sources staged in memory by the parent's prepare()
+        args._staged_sources = staged
     dev = torch.device("cuda", rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     if args.dist_backend == "nccl":  # RCCL over xGMI, one GPU per rank
@@ -940,7 +959,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = s.getsockname()[1]
-        mp.start_processes(_worker, args=(args.gpus, resolved, port, prep), nprocs=args.gpus, start_method="spawn")
+        mp.start_processes(_worker, args=(args.gpus, resolved, port, prep, getattr(args, "_staged_sources", None)), nprocs=args.gpus, start_method="spawn")
     else:
         _run_style(args, frames_dir, model_path, save_map, image_mode)
     if video:

@@ -335,7 +335,7 @@ def test_input_dir_staging_in_memory_jpeg_exif_png(tmp_path):
     --jpeg_quality before it is stylised, a PNG source is used as its EXIF-upright RGB image.  fp32 CLI without the
     LAB stage vs the oracle on exactly those staged pixels: within +-1 LSB; --keep_staged writes the staged copies
     (decoding them gives the same pixels) and does not change the outputs; a PNG level other than PIL's default
-    changes only the file, not the pixels."""
+    changes only the file, not the pixels, and so does the fast PNG writer (pngio) against Pillow's."""
     import io
     ck, sd = _ckpt(tmp_path, "johnson", 3)
     frames = synthetic.make_frames(3, 64, 96, seed=77)
@@ -362,7 +362,8 @@ def test_input_dir_staging_in_memory_jpeg_exif_png(tmp_path):
             up = Image.open(buf).convert("RGB")
         staged.append(np.array(up))
     outs = {}
-    for tag, extra in (("mem", []), ("keep", ["--keep_staged", "--png_compress_level", "1"])):
+    for tag, extra in (("mem", []), ("keep", ["--keep_staged", "--png_compress_level", "1"]),
+                       ("pil", ["--png_writer", "pil"])):
         d_out = tmp_path / f"out_{tag}"
         assert P.main(["--input_dir", str(d_in), "--output_dir", str(d_out), "--model", ck, "--io_preset", "imagenet_255",
                        "--pattern", "frame_*", "--no-smooth_lightness", "--batch", "1", "--work_dir",
@@ -375,6 +376,7 @@ def test_input_dir_staging_in_memory_jpeg_exif_png(tmp_path):
         print(f"frame {i}: {staged[i].shape}, max |d| {d.max()}")
         assert d.max() <= 1
         assert np.array_equal(outs["mem"][i], outs["keep"][i])
+        assert np.array_equal(outs["mem"][i], outs["pil"][i])
     kept = sorted((tmp_path / "w_keep").rglob("frame_*"))
     assert len(kept) == 3
     for i, p in enumerate(kept):

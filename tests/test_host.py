@@ -249,3 +249,27 @@ def test_check_scratch_flags_spills(tmp_path):
     r = subprocess.run([sys.executable, str(root / "tools/check_scratch.py"), str(bad)], capture_output=True, text=True,
                        env=dict(env, NST_STRICT_SCRATCH="0"))
     assert r.returncode == 0
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 3), (1, 7, 3), (5, 1, 3), (37, 53, 3), (64, 96, 4), (33, 17)])
+def test_fast_png_writer_decodes_to_the_same_pixels(shape, tmp_path):
+    """pngio.encode_png (Up filter + zlib RLE; the CLI's default PNG writer) decodes with Pillow to exactly the
+    array it was given: noise, flat and ramp content, RGB / RGBA / grey, one-pixel rows and columns."""
+    from PIL import Image
+    from neuralstyletransferv1_amd import pngio
+    rng = np.random.default_rng(sum(shape))
+    for kind in ("noise", "flat", "ramp"):
+        if kind == "noise":
+            a = rng.integers(0, 256, size=shape, dtype=np.uint8)
+        elif kind == "flat":
+            a = np.full(shape, 200, np.uint8)
+        else:
+            a = (np.arange(int(np.prod(shape))) % 251).astype(np.uint8).reshape(shape)
+        p = tmp_path / f"{kind}.png"
+        pngio.write_png(p, a)
+        with Image.open(p) as im:
+            assert im.size == (shape[1], shape[0])
+            got = np.array(im)
+        assert got.dtype == np.uint8 and np.array_equal(got, a), kind
+    with pytest.raises(ValueError):
+        pngio.encode_png(np.zeros((4, 4, 3), np.float32))

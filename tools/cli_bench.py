@@ -1,19 +1,31 @@
-"""End-to-end CLI frames/s at 1080p on one GPU: the reference's frame-directory
-path (pipeline.py --input_dir: PIL decode -> stylize -> LAB EMA -> blend -> PIL encode, pipeline.py:1080-2119) through
-this engine's pipeline.main, for PNG and JPEG frames, beside the host decode / encode rates alone (the same thread
-count) and the GPU step rate -- so the host I/O share of the wall time is measured, not assumed.
+"""End-to-end CLI frames/s at 1080p on one GPU: the reference's frame paths
+through this engine's pipeline, for PNG and JPEG frames, beside the host decode / encode rates alone (the same
+thread count), so the host I/O share of the wall time is measured, not assumed.
 
-  python tools/cli_bench.py [--frames 48] [--threads 16]
+Two paths per format:
+  * "input_dir": pipeline.main --input_dir (image batch mode, pipeline.py:2575-2606): each source is staged (EXIF
+    upright, JPEG re-encoded at --jpeg_quality, in memory here), stylized, LAB-smoothed, blended and saved.
+    A JPEG frame costs four host codec operations (decode, staging encode + decode, output encode).
+  * "frames_dir": the video path's per-frame loop after ffmpeg has extracted the frames (pipeline.py:1080-2119:
+    decode -> stylize -> LAB EMA -> blend -> encode), run on a directory of frame_*.{png,jpg} files.
+
+Default CLI settings (bf16, --batch 8, --blend 0.9, --smooth_alpha 0.65, staged/output JPEG at the default
+--jpeg_quality 85 from quality-95 source files, PNG through the default fast writer) on synthetic frames (smooth gradients + shapes + ~5 LSB
+noise, neuralstyletransferv1_amd/synthetic.py).  The timed run excludes the model load (a warm-up run first).
+
+  python tools/cli_bench.py [--frames 240] [--threads 16] [--png_writer fast|pil]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
 import sys
 import tempfile
 import time
 from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
 
 import numpy as np
 import torch
@@ -25,48 +37,91 @@ sys.path.insert(0, REPO)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=48)
+    ap.add_argument("--frames", type=int, default=240)
     ap.add_argument("--threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--png_writer", default="fast", choices=["fast", "pil"])
+    ap.add_argument("--formats", default="jpg,png")
+    ap.add_argument("--paths", default="frames_dir,input_dir")
     args = ap.parse_args()
     from neuralstyletransferv1_amd import pipeline as P
-    from neuralstyletransferv1_amd import synthetic
+    from neuralstyletransferv1_amd import pngio, synthetic
 
     tmp = tempfile.mkdtemp(prefix="nst_cli_")
     ck = os.path.join(tmp, "johnson.pth")
     torch.save(synthetic.make_state_dict("johnson", 0), ck)
     frames = synthetic.make_frames(8, 1080, 1920, seed=300)
-    res = {"frames": args.frames, "threads": args.threads, "frame_hw": [1080, 1920]}
+    res = {"frames": args.frames, "threads": args.threads, "frame_hw": [1080, 1920], "png_writer": args.png_writer,
+           "data": "synthetic 1080p frames (8 distinct, cycled)"}
     pool = ThreadPoolExecutor(args.threads)
-    for ext in ("png", "jpg"):
+    for ext in args.formats.split(","):
         d_in = os.path.join(tmp, f"in_{ext}")
         os.makedirs(d_in)
         paths = [os.path.join(d_in, f"frame_{i + 1:04d}.{ext}") for i in range(args.frames)]
 
-        def enc(i):
-            im = Image.fromarray(frames[i % len(frames)])
+        def enc_in(i):
             if ext == "png":
-                im.save(paths[i])
+                pngio.write_png(paths[i], frames[i % len(frames)])
             else:
-                im.save(paths[i], format="JPEG", quality=85)
-        t0 = time.perf_counter()
-        list(pool.map(enc, range(args.frames)))
-        t_enc = time.perf_counter() - t0
+                Image.fromarray(frames[i % len(frames)]).save(paths[i], format="JPEG", quality=95)
+        list(pool.map(enc_in, range(args.frames)))
+        host = {}
         t0 = time.perf_counter()
         list(pool.map(lambda p: np.asarray(Image.open(p).convert("RGB")), paths))
-        t_dec = time.perf_counter() - t0
-        d_out = os.path.join(tmp, f"out_{ext}")
-        argv = ["--input_dir", d_in, "--output_dir", d_out, "--model", ck, "--io_preset", "imagenet_255",
-                "--dtype", "bf16", "--batch", "8", "--blend", "0.9", "--smooth_alpha", "0.65", "--image_ext", ext,
-                "--threads", str(args.threads), "--work_dir", os.path.join(tmp, f"w_{ext}")]
-        P.main(argv[:4] + ["--max_frames", "8"] + argv[4:])  # warm-up: model load, kernels, LAB tables
+        host["host_decode_frames_per_s"] = round(args.frames / (time.perf_counter() - t0), 1)
+        d_enc = os.path.join(tmp, f"enc_{ext}")
+        os.makedirs(d_enc)
+
+        def enc_out(i):
+            p = os.path.join(d_enc, f"o_{i:04d}.{ext}")
+            if ext == "jpg":
+                Image.fromarray(frames[i % len(frames)]).save(p, format="JPEG", quality=95)
+            elif args.png_writer == "fast":
+                pngio.write_png(p, frames[i % len(frames)])
+            else:
+                Image.fromarray(frames[i % len(frames)]).save(p)
         t0 = time.perf_counter()
-        rc = P.main(argv)
-        t_cli = time.perf_counter() - t0
-        assert rc == 0
-        res[ext] = {"cli_frames_per_s": round(args.frames / t_cli, 2), "cli_s": round(t_cli, 3),
-                    "host_encode_frames_per_s": round(args.frames / t_enc, 2),
-                    "host_decode_frames_per_s": round(args.frames / t_dec, 2)}
-        print(ext, json.dumps(res[ext]), flush=True)
+        list(pool.map(enc_out, range(args.frames)))
+        host["host_encode_frames_per_s"] = round(args.frames / (time.perf_counter() - t0), 1)
+        shutil.rmtree(d_enc)
+        res[ext] = dict(host)
+        common = ["--model", ck, "--io_preset", "imagenet_255", "--dtype", "bf16", "--batch", "8", "--blend", "0.9",
+                  "--smooth_alpha", "0.65", "--image_ext", ext, "--threads", str(args.threads),
+                  "--png_writer", args.png_writer]
+        for path in args.paths.split(","):
+            if path == "input_dir":
+                d_out = os.path.join(tmp, f"out_{ext}")
+                argv = ["--input_dir", d_in, "--output_dir", d_out, "--work_dir", os.path.join(tmp, f"w_{ext}")] + common
+                P.main(argv[:4] + ["--max_frames", "8"] + argv[4:])  # warm-up: model load, kernels, LAB tables
+                t0 = time.perf_counter()
+                rc = P.main(argv)
+                t_cli = time.perf_counter() - t0
+                assert rc == 0
+                n_out = len(list(Path(d_out).glob(f"*.{ext}")))
+            else:
+                # the video path after extraction: style_frames over work_dir/frames (frame_*.ext), outputs
+                # styled_frame_*.ext beside them (pipeline.py:1080-2119)
+                wd = Path(tmp) / f"v_{ext}"
+                fd = wd / "frames"
+                fd.mkdir(parents=True)
+                for p in paths:
+                    os.link(p, fd / os.path.basename(p))
+                a = P.build_parser().parse_args(["--input_video", "x", "--output_video", "y", "--work_dir", str(wd)]
+                                                + common)
+                a.model_type = "transformer"
+                P._run_style(a, fd, Path(ck), {}, False)  # warm-up (writes the outputs once)
+                t0 = time.perf_counter()
+                P._run_style(a, fd, Path(ck), {}, False)
+                t_cli = time.perf_counter() - t0
+                n_out = len(list(fd.glob(f"styled_frame_*.{ext}")))
+            assert n_out == args.frames, (path, n_out)
+            st = dict(P.LAST_RUN_STATS)
+            # wall time of the whole call (model load and plans included), and the frame loop's own rate
+            res[ext][path] = {"cli_frames_per_s": round(args.frames / t_cli, 2), "cli_s": round(t_cli, 3),
+                              "loop_frames_per_s": round(st["frames"] / st["seconds"], 2),
+                              "setup_s": round(st["setup_seconds"], 3)}
+            print(ext, path, json.dumps(res[ext][path]), flush=True)
+        shutil.rmtree(d_in)
+    shutil.rmtree(tmp, ignore_errors=True)
     print(json.dumps(res))
 
 

@@ -61,7 +61,7 @@ def timed(fn, steps):
 
 
 # the mask program's dtype in the configs[4] step: sky_swap.py's default
-MASK_DT = "fp32"
+MASK_DT = os.environ.get("SEG_MASK_DT", "fp32")
 
 
 def main():
@@ -78,7 +78,7 @@ def main():
     out = {"workload": "configs[4]: DeepLab v3+ mask (256-px working size) + Johnson stylization + mask composite, "
                        "1920x1080 batch 8, bf16", "frames_per_step": N}
     res = {}
-    for dtype in ("bf16", "fp16", "fp32"):
+    for dtype in ("bf16", "fp16", "fp32", "fp32s"):
         me = deeplab.MaskEngine(model, dev, resolution=256, dtype=dtype)
         res[dtype] = timed(lambda: me.masks(frames, ids, feather_px=3), STEPS)
     me = deeplab.MaskEngine(model, dev, resolution=256, dtype=MASK_DT)
@@ -89,7 +89,7 @@ def main():
     lanczos_ms = timed(lambda: me._resampler("lanczos", H, W, hw[1], hw[0])(frames), STEPS)
     g_work = deeplab_gflop(hw[1], hw[0]) * N
     out.update({"mask_dtype": MASK_DT, "mask_ms_bf16": round(res["bf16"], 3), "mask_ms_fp16": round(res["fp16"], 3),
-                "mask_ms_fp32": round(res["fp32"], 3),
+                "mask_ms_fp32": round(res["fp32"], 3), "mask_ms_fp32s": round(res["fp32s"], 3),
                 "lanczos_ms": round(lanczos_ms, 3), "deeplab_fwd_ms": round(fwd_ms, 3),
                 "deeplab_gflop_per_batch": round(g_work, 2),
                 "deeplab_tflops_working_size": round(g_work / fwd_ms, 1)})
@@ -107,7 +107,9 @@ def main():
     ms = timed(step, STEPS)
     styl_ms = timed(lambda: eng.stylize_u8(frames, "imagenet_255"), STEPS)
     out.update({"step_ms": round(ms, 3), "frames_per_s": round(N / ms * 1e3, 1), "stylize_ms": round(styl_ms, 3),
-                "mask_share": round(res[MASK_DT] / ms, 3)})
+                "mask_share": round(res[MASK_DT] / ms, 3),
+                # the step with each mask dtype: its mask time / (that + the rest of the step)
+                "mask_share_by_dtype": {d: round(t / (ms - res[MASK_DT] + t), 3) for d, t in res.items()}})
     print(json.dumps(out), flush=True)
 
 
