@@ -210,7 +210,8 @@ def _get_image_with_exif_pil(image_path: str):
     angle = _EXIF_UPRIGHT.get(tags.get(0x0112))
     if angle is not None:
         img = img.rotate(angle, expand=True)
-    return img.convert("RGB")
+    img.load()
+    return img if img.mode == "RGB" else img.convert("RGB")  # (convert of an RGB image is a copy)
 
 
 def sh(cmd: str, check=True):
@@ -410,7 +411,9 @@ class FrameSource:
     def _open_rgb(self, i: int):
         from PIL import Image
         if self.staged is None:
-            return Image.open(self.files[i]).convert("RGB")
+            im = Image.open(self.files[i])
+            im.load()
+            return im if im.mode == "RGB" else im.convert("RGB")
         # the reference's --input_dir staging (pipeline.py:2577-2586): EXIF-upright RGB, re-saved as the staged
         # frame -- PNG (lossless: the decoded frame is that RGB image itself) or JPEG at --jpeg_quality, whose
         # encode -> decode round trip runs here in memory (the same bytes PIL writes, so the same pixels)
@@ -543,7 +546,9 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             _log(f"[mask][WARN] {len(missing)}/{len(names)} mask(s) missing under {md}.")
 
     pool = ThreadPoolExecutor(max_workers=max(1, threads))
-    sizes = [src.size(i) for i in range(len(src))]
+    prof = _PipeProf()
+    with prof("size_scan"):  # header reads (a PNG's EXIF lookup decodes it): on the pool
+        sizes = list(pool.map(src.size, range(len(src))))
     # rank 0 also runs every frame's ordered post chain: a lighter share of each group (frames.rank0_share)
     bsz = max(1, args.batch)
     r0 = rank0_share(world, bsz)
@@ -560,11 +565,28 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     loads = {}
     prefetch_depth = 2
 
+    pinned = {}  # shard k -> page-locked [n, h, w, 3] the loaders decode into (one H2D copy per group, async)
+
+    def _load_into(f, buf, j):
+        a, b = src.load(f)
+        np.copyto(buf[j], a)  # numpy releases the GIL for the copy
+        return None if b is a else b
+
     def _submit(k):
-        if 0 <= k < len(my_shards):
-            for f in my_shards[k]:
-                if f not in loads:
-                    loads[f] = pool.submit(src.load, f)
+        if 0 <= k < len(my_shards) and my_shards[k] and k not in pinned:
+            sh = my_shards[k]
+            h0, w0 = sizes[sh[0]]
+            if all(sizes[f] == (h0, w0) for f in sh):
+                buf = torch.empty((len(sh), h0, w0, 3), dtype=torch.uint8, pin_memory=True)
+                pinned[k] = buf
+                bn = buf.numpy()
+                for j, f in enumerate(sh):
+                    loads[f] = pool.submit(_load_into, f, bn, j)
+            else:
+                pinned[k] = None
+                for f in sh:
+                    if f not in loads:
+                        loads[f] = pool.submit(src.load, f)
 
     # the reference fits model A's output to the content size; with --inference_res the model
     # input is smaller than the content
@@ -577,9 +599,16 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         k = shard_pos.get(tuple(idx), -1)
         for j in range(k, k + 1 + prefetch_depth):
             _submit(j)
-        loaded = [(loads.pop(f) if f in loads else pool.submit(src.load, f)).result() for f in idx]
-        orig = torch.from_numpy(np.stack([a for a, _ in loaded])).to(dev, non_blocking=True)
-        xin = orig if loaded[0][1] is loaded[0][0] else torch.from_numpy(np.stack([b for _, b in loaded])).to(dev)
+        buf = pinned.pop(k, None)
+        with prof("wait_decode"):
+            loaded = [(loads.pop(f) if f in loads else pool.submit(src.load, f)).result() for f in idx]
+        with prof("h2d"):
+            if buf is not None:  # decoded straight into page-locked memory; loaded = the model inputs if different
+                orig = buf.to(dev, non_blocking=True)
+                xin = orig if loaded[0] is None else torch.from_numpy(np.stack(loaded)).to(dev)
+            else:
+                orig = torch.from_numpy(np.stack([a for a, _ in loaded])).to(dev, non_blocking=True)
+                xin = orig if loaded[0][1] is loaded[0][0] else torch.from_numpy(np.stack([b for _, b in loaded])).to(dev)
         h0, w0 = orig.shape[1], orig.shape[2]
         fids = [f + 1 for f in idx]  # the reference's 1-based frame index (animations, rotation)
         if flow_mode:  # the temporal stage needs out01 before the ToPILImage truncation (pipeline.py:1884-1943)
@@ -664,7 +693,11 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
                 for j, f in enumerate(g):
                     if motion[j] is not None and not _has_mask(f):
                         styled[j:j + 1] = blend_frames(styled_in[j:j + 1], orig[j:j + 1], 1.0, motion[j][None], "keep")
-        host = styled.cpu().numpy()
+        with prof("d2h"):  # page-locked: the saves read it after one stream sync
+            host_t = torch.empty(styled.shape, dtype=torch.uint8, pin_memory=True)
+            host_t.copy_(styled, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            host = host_t.numpy()
         if not args.no_save:
             for j, f in enumerate(g):
                 pending.append(pool.submit(_save, host[j], f))
@@ -740,13 +773,42 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         return str(out_path)
 
     run_sharded(groups, world, rank, stylize, consume, dev, caps)
-    for p in pending:
-        p.result()
+    with prof("drain_saves"):
+        for p in pending:
+            p.result()
     pool.shutdown()
+    prof.report(rank)
     el = time.perf_counter() - t_start
     LAST_RUN_STATS.update(frames=len(src), seconds=el, setup_seconds=t_start - t_setup)
     if rank == 0:
         _log(f"Styled {len(src)}/{len(src)} frames in {el:.2f}s ({len(src) / max(el, 1e-9):.2f} frames/s)")
+
+
+class _PipeProf:
+    """Wall time of the frame loop's host-side phases on the main thread (NST_PIPE_PROF=1 prints them)."""
+
+    def __init__(self):
+        self.on = os.environ.get("NST_PIPE_PROF", "0") == "1"
+        self.t: Dict[str, float] = {}
+
+    def __call__(self, name: str):
+        import contextlib
+
+        if not self.on:
+            return contextlib.nullcontext()
+
+        @contextlib.contextmanager
+        def cm():
+            t0 = time.perf_counter()
+            try:
+                yield
+            finally:
+                self.t[name] = self.t.get(name, 0.0) + time.perf_counter() - t0
+        return cm()
+
+    def report(self, rank: int):
+        if self.on:
+            _log(f"[pipe-prof rank {rank}] " + " ".join(f"{k}={v:.3f}s" for k, v in self.t.items()))
 
 
 def _slot_u8(model, preset, xin, h0, w0):

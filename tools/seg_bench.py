@@ -78,7 +78,7 @@ def main():
     out = {"workload": "configs[4]: DeepLab v3+ mask (256-px working size) + Johnson stylization + mask composite, "
                        "1920x1080 batch 8, bf16", "frames_per_step": N}
     res = {}
-    for dtype in ("bf16", "fp16", "fp32", "fp32s"):
+    for dtype in os.environ.get("SEG_DTYPES", "bf16,fp16,fp32,fp32s").split(","):
         me = deeplab.MaskEngine(model, dev, resolution=256, dtype=dtype)
         res[dtype] = timed(lambda: me.masks(frames, ids, feather_px=3), STEPS)
     me = deeplab.MaskEngine(model, dev, resolution=256, dtype=MASK_DT)
@@ -88,8 +88,7 @@ def main():
     fwd_ms = timed(lambda: seg.run(work, logits=False, pred=True), STEPS)
     lanczos_ms = timed(lambda: me._resampler("lanczos", H, W, hw[1], hw[0])(frames), STEPS)
     g_work = deeplab_gflop(hw[1], hw[0]) * N
-    out.update({"mask_dtype": MASK_DT, "mask_ms_bf16": round(res["bf16"], 3), "mask_ms_fp16": round(res["fp16"], 3),
-                "mask_ms_fp32": round(res["fp32"], 3), "mask_ms_fp32s": round(res["fp32s"], 3),
+    out.update({"mask_dtype": MASK_DT, **{f"mask_ms_{d}": round(t, 3) for d, t in res.items()},
                 "lanczos_ms": round(lanczos_ms, 3), "deeplab_fwd_ms": round(fwd_ms, 3),
                 "deeplab_gflop_per_batch": round(g_work, 2),
                 "deeplab_tflops_working_size": round(g_work / fwd_ms, 1)})
