@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -68,7 +69,15 @@ struct VggConv {
 };
 // the layers on the GEMM conv: every conv whose input has >= 64 channels and whose map is at most a
 // quarter of the image (conv2_1 onward); input gradients of the same layers
-bool vgg_gemm_layer(int i) { return i >= 2; }
+// (NST_VGG_GEMM_F / NST_VGG_GEMM_B: bitmasks of the layers whose forward / input gradient take the GEMM conv,
+// for sweeps; default conv2_1 onward for both)
+unsigned vgg_gemm_mask(bool fwd) {
+  static const unsigned m[2] = {
+      [] { const char* e = std::getenv("NST_VGG_GEMM_B"); return e ? (unsigned)std::strtoul(e, nullptr, 0) : 0x1ffcu; }(),
+      [] { const char* e = std::getenv("NST_VGG_GEMM_F"); return e ? (unsigned)std::strtoul(e, nullptr, 0) : 0x1ffcu; }()};
+  return m[fwd ? 1 : 0];
+}
+bool vgg_gemm_layer(int i) { return ((vgg_gemm_mask(true) | vgg_gemm_mask(false)) >> i) & 1u; }
 
 // W[cout][cin][3][3] fp32 -> the GEMM conv's bf16 fragments [coutp/64][stage = tap*nck + cc][64 rows][64]
 // (seg_internal.h GemmConvParams::wpk)
@@ -306,7 +315,8 @@ int nst_vgg_create_ex(const nst_param* params, int n_params, int device, unsigne
     if ((rc = pack_upload_conv(*L.kb, L.d.cout, L.d.cin, 3, Wt.data(), bcoutp, &L.wb)) != NST_OK) break;
     if ((rc = upload_floats(itb->second->data, L.d.cout, &L.bf)) != NST_OK) break;
     if (gemm_ok && vgg_gemm_layer(i)) {
-      L.gemm_f = L.gemm_b = true;
+      L.gemm_f = (vgg_gemm_mask(true) >> i) & 1u;
+      L.gemm_b = (vgg_gemm_mask(false) >> i) & 1u;
       const int cpb = (L.d.cin + 127) / 128 * 128;  // input-gradient outputs, padded to the 128-row tile
       std::vector<uint16_t> pf = pack_gemm(W, L.d.cout, L.d.cin, L.d.cout), pb = pack_gemm(Wt.data(), L.d.cin, L.d.cout, cpb);
       std::vector<float> one(512, 1.f), zero(512, 0.f), bias(512, 0.f);
