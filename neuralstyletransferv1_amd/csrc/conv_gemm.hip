@@ -37,6 +37,14 @@ typedef _Float16 f16x8_g __attribute__((ext_vector_type(8)));
 typedef float f32x4_g __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_g __attribute__((ext_vector_type(4)));
 
+// a use of the operand fragments after a stage's MFMAs: hipcc (ROCm 7.2) otherwise may allocate an MFMA's
+// destination partially over a source register that dies at that MFMA (tools/check_mfma_overlap.py), which the
+// matrix pipeline does not support
+template <int N>
+__device__ __forceinline__ void keep_live(const u32x4_g (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" ::"v"(v[i]));
+}
 __device__ __forceinline__ int chunk_swz(int row) { return ((row >> 3) & 1) << 1; }
 
 // 16-bit activation formats (dt = NST_DT_BF16 / NST_DT_F16): exact unpack, round-to-nearest-even pack
@@ -68,7 +76,7 @@ __device__ __forceinline__ void split4(const u32x4_g& v, uint2& hi, uint2& lo) {
   hi = make_uint2(pk(h[0], h[1]), pk(h[2], h[3]));
   lo = make_uint2(pk(l[0], l[1]), pk(l[2], l[3]));
 }
-template <int BM, int BN, int DT>
+template <int BM, int BN, int DT, bool PF2>
 __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
   constexpr bool SPL = DT == NST_DT_F32S;
   constexpr bool F32 = DT == NST_DT_F32 || SPL;  // fp32 activations and weights in memory and LDS
@@ -78,8 +86,13 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
   constexpr int B_TPR = 256 / BN, B_CPT = 8 / B_TPR;
   constexpr int ESZ = F32 ? 4 : 2;
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+  // the live-tap table in LDS: read from the kernel arguments with a dynamic index it is a vector memory load,
+  // and the wait for it would also wait for every K stage still in flight
+  __shared__ unsigned char s_taps[64];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 64) s_taps[tid] = p.taps[tid];
+  __syncthreads();
   const int wm = wave & 1, wn = wave >> 1;
   const int pix0 = blockIdx.x * BN, row0 = blockIdx.y * BM;
 
@@ -98,6 +111,13 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
   }
   const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
   const char* in_img = (const char*)p.in + (size_t)img * p.hi * p.wi * p.cs * ESZ + b_c0 * 16;
+  // PF2 (launched only when the input tensor is under 2 GiB): the same addresses as 32-bit buffer offsets
+  const uint32_t in_off0 = (uint32_t)((size_t)img * p.hi * p.wi * p.cs * ESZ + b_c0 * 16);
+  const int n_img_all = p.npix / (p.ho * p.wo);
+  const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.in, (short)0,
+      __builtin_amdgcn_readfirstlane((int)std::min<long long>((long long)n_img_all * p.hi * p.wi * p.cs * ESZ, 0x7fffffffLL)),
+      0x00020000);
   const int nck = p.cin / (128 / ESZ);
   const int nstage_all = p.kh * p.kw * nck;   // packed stages per 64-row block (every tap)
   const int nstage = p.ntaps * nck;           // stages this launch runs (live taps only)
@@ -109,24 +129,33 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
   const int s_end = (int)(((long)nstage * (blockIdx.z + 1)) / p.ksplit);
 
   u32x4_g ra[A_CPT], rb[B_CPT];
-  auto load_stage = [&](int s) {
+  auto load_into = [&](int s, u32x4_g (&ra)[A_CPT], u32x4_g (&rb)[B_CPT]) {
     const int ti = s / nck, cc = s - ti * nck;
-    const int tap = p.taps[ti];
+    const int tap = __builtin_amdgcn_readfirstlane(s_taps[ti]);
     const char* wa = wsrc + (size_t)(tap * nck + cc) * wstage;
 #pragma unroll
     for (int j = 0; j < A_CPT; ++j) ra[j] = *(const u32x4_g*)(wa + j * 16);
     const int ky = tap / p.kw, kx = tap - ky * p.kw;
     const int iy = iy0 + ky * p.dil, ix = ix0 + kx * p.dil;
     const bool ok = pvalid && (unsigned)iy < (unsigned)p.hi && (unsigned)ix < (unsigned)p.wi;
-    const char* src = in_img + ((size_t)iy * p.wi + ix) * p.cs * ESZ + cc * 128;
+    if constexpr (PF2) {
+      // buffer loads, zero past the tensor (offset 2^31): no branch around the loads, so the wait before a stage's
+      // LDS store counts only the older stage's loads and the newer stage's stay in flight
+      const uint32_t off = ok ? in_off0 + (uint32_t)(((iy * p.wi + ix) * p.cs) * ESZ + cc * 128) : 0x80000000u;
 #pragma unroll
-    for (int j = 0; j < B_CPT; ++j) {
-      u32x4_g v = {0u, 0u, 0u, 0u};
-      if (ok) v = *(const u32x4_g*)(src + j * 16);
-      rb[j] = v;
+      for (int j = 0; j < B_CPT; ++j)
+        rb[j] = __builtin_bit_cast(u32x4_g, __builtin_amdgcn_raw_buffer_load_b128(rs_in, off + j * 16, 0, 0));
+    } else {
+      const char* src = in_img + ((size_t)iy * p.wi + ix) * p.cs * ESZ + cc * 128;
+#pragma unroll
+      for (int j = 0; j < B_CPT; ++j) {
+        u32x4_g v = {0u, 0u, 0u, 0u};
+        if (ok) v = *(const u32x4_g*)(src + j * 16);
+        rb[j] = v;
+      }
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_from = [&](int buf, const u32x4_g (&ra)[A_CPT], const u32x4_g (&rb)[B_CPT]) {
     char* A = lds + buf * BUF;
     char* B = A + A_BYTES;
 #pragma unroll
@@ -153,14 +182,7 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4_g{0.f, 0.f, 0.f, 0.f};
 
-  load_stage(s_begin);
-  store_stage(0);
-  __syncthreads();
-  for (int s = s_begin; s < s_end; ++s) {
-    const int cur = (s - s_begin) & 1;
-    const bool more = s + 1 < s_end;
-    if (more) load_stage(s + 1);
-    const char* base = lds + cur * BUF;
+  auto compute = [&](const char* base) {
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       u32x4_g a[MI], b[NI];
@@ -192,6 +214,9 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_g, al[i]),
                                                                __builtin_bit_cast(f16x8_g, bb[j]), acc[i][j], 0, 0, 0);
           }
+        keep_live(ah);
+        keep_live(al);
+        keep_live(bb);
         continue;
       }
 #pragma unroll
@@ -211,9 +236,43 @@ __global__ __launch_bounds__(256, 2) void gemm_conv_kernel(GemmConvParams p) {
                                                                 __builtin_bit_cast(bf16x8_g, b[j]), acc[i][j], 0, 0, 0);
           }
         }
+      keep_live(a);
+      keep_live(b);
     }
-    if (more) store_stage(cur ^ 1);
+  };
+  if constexpr (PF2) {
+    // two stages in flight: stage s + 2's global loads go out before stage s's MFMAs, into the register set
+    // stage s left (stored to LDS one step earlier); the loop is unrolled by two so both sets stay in registers.
+    // The loads past the slice's end re-read its last stage (never stored).
+    u32x4_g ra2[A_CPT], rb2[B_CPT];
+    const int last = s_end - 1;
+    load_into(s_begin, ra, rb);
+    load_into(min(s_begin + 1, last), ra2, rb2);
+    store_from(0, ra, rb);
     __syncthreads();
+    for (int s = s_begin; s < s_end; s += 2) {
+      load_into(min(s + 2, last), ra, rb);
+      compute(lds);
+      if (s + 1 < s_end) store_from(1, ra2, rb2);
+      __syncthreads();
+      if (s + 1 >= s_end) break;
+      load_into(min(s + 3, last), ra2, rb2);
+      compute(lds + BUF);
+      if (s + 2 < s_end) store_from(0, ra, rb);
+      __syncthreads();
+    }
+  } else {
+    load_into(s_begin, ra, rb);
+    store_from(0, ra, rb);
+    __syncthreads();
+    for (int s = s_begin; s < s_end; ++s) {
+      const int cur = (s - s_begin) & 1;
+      const bool more = s + 1 < s_end;
+      if (more) load_into(s + 1, ra, rb);
+      compute(lds + cur * BUF);
+      if (more) store_from(cur ^ 1, ra, rb);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: lane owns output channels co..co+3 of one pixel per sub-tile ----
@@ -285,10 +344,15 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
   constexpr int ESZ = F32 ? 4 : 2, CK = 128 / ESZ;  // bytes per element, channels per stage
   static_assert(RING >= 2 && RING <= 4, "ring");
   __shared__ __attribute__((aligned(16))) char lds[RING * BUF];
+  // live-tap table in LDS (as gemm_conv_kernel): a kernel-argument read with a dynamic index is a vector memory
+  // load whose wait (vmcnt(0)) would drain every DMA stage in flight before each issue
+  __shared__ unsigned char s_taps[64];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM, wn = wave / WM;
+  if (tid < 64) s_taps[tid] = p.taps[tid];
+  __syncthreads();
   const int pix0 = blockIdx.x * BN, row0 = blockIdx.y * BM;
   const int nck = p.cin / CK;
   const int nstage_all = p.kh * p.kw * nck;
@@ -332,7 +396,7 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
   auto issue = [&](int s) {  // stage s -> ring slot s % RING
     const uint32_t base = lds0 + (uint32_t)((s % RING) * BUF);
     const int ti = s / nck, cc = s - ti * nck;
-    const int tap = p.taps[ti];
+    const int tap = __builtin_amdgcn_readfirstlane(s_taps[ti]);
     const int ky = tap / p.kw, kx = tap - ky * p.kw;
     const uint32_t wst = (uint32_t)(tap * nck + cc) * 8192u;
 #pragma unroll
@@ -395,6 +459,8 @@ __global__ __launch_bounds__(512) void gemm_glds_kernel(GemmConvParams p, uint32
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_g, a[i]),
                                                                 __builtin_bit_cast(bf16x8_g, b[j]), acc[i][j], 0, 0, 0);
         }
+      keep_live(a);
+      keep_live(b);
     }
   }
   vm_wait<0>();  // no DMA lands after the workgroup releases its LDS
@@ -492,13 +558,31 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmConvParams p, int 
   }
 }
 
+// register-staged kernel: two K stages in flight (NST_GEMM_PF2, default on) instead of one
+int gemm_pf2() {
+  static const int v = [] {
+    const char* e = std::getenv("NST_GEMM_PF2");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
 template <int BM, int BN>
 void launch_tile(int dt, const GemmConvParams& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM), (unsigned)p.ksplit);
-  if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F32>), grid, dim3(256), 0, st, p);
-  else if (dt == NST_DT_F32S) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F32S>), grid, dim3(256), 0, st, p);
-  else if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F16>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_BF16>), grid, dim3(256), 0, st, p);
+  // PF2: the 16-bit and split kernels (the exact-f32 one keeps one stage in flight: with two, hipcc allocated
+  // 16x16x4f32 MFMA destinations partially over a source, tools/check_mfma_overlap.py), inputs under 2 GiB
+  const long long in_bytes = (long long)(p.npix / std::max(1, p.ho * p.wo)) * p.hi * p.wi * p.cs *
+                             (dt == NST_DT_F32 || dt == NST_DT_F32S ? 4 : 2);
+  if (gemm_pf2() && dt != NST_DT_F32 && in_bytes < 0x7fffffffLL) {
+    if (dt == NST_DT_F32S) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F32S, true>), grid, dim3(256), 0, st, p);
+    else if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F16, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_BF16, true>), grid, dim3(256), 0, st, p);
+    return;
+  }
+  if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F32, false>), grid, dim3(256), 0, st, p);
+  else if (dt == NST_DT_F32S) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F32S, false>), grid, dim3(256), 0, st, p);
+  else if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_F16, false>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((gemm_conv_kernel<BM, BN, NST_DT_BF16, false>), grid, dim3(256), 0, st, p);
 }
 
 // taps whose source row AND column land inside the image for at least one output pixel
@@ -536,11 +620,27 @@ void live_taps(GemmConvParams& p) {
 #ifndef NST_GEMM_GLDS_F32
 #define NST_GEMM_GLDS_F32 0
 #endif
-#ifndef NST_GEMM_BIG_SPLIT_MIN_STAGES
-#define NST_GEMM_BIG_SPLIT_MIN_STAGES 64
-#endif
 #ifndef NST_GEMM_RING_32K  // ring depth for tiles whose stage is 32 KB (128 x 128); 4 (three stages in flight) measured
 #define NST_GEMM_RING_32K 3   // 1.161 -> 1.169 ms per Gatys step (r03_m2)
+#endif
+// sweep override of the 32 KB-stage ring depth (NST_GEMM_RING32=4)
+int gemm_ring32() {
+  static const int v = [] {
+    const char* e = std::getenv("NST_GEMM_RING32");
+    return e ? std::atoi(e) : NST_GEMM_RING_32K;
+  }();
+  return v;
+}
+// runtime override (NST_GEMM_GLDS_F32=1): fp32 / fp32s GEMMs on the LDS-DMA kernel (exact-f32 MFMAs)
+int gemm_glds_f32() {
+  static const int v = [] {
+    const char* e = std::getenv("NST_GEMM_GLDS_F32");
+    return e ? std::atoi(e) : NST_GEMM_GLDS_F32;
+  }();
+  return v;
+}
+#ifndef NST_GEMM_BIG_SPLIT_MIN_STAGES
+#define NST_GEMM_BIG_SPLIT_MIN_STAGES 64
 #endif
 #ifndef NST_GEMM_SPLIT256  // 128 x 256 tiles split in K where 128 x 128 tiles would run unsplit / less split
 #define NST_GEMM_SPLIT256 1
@@ -567,14 +667,14 @@ GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
   const int nstage = p.ntaps * (p.cin / gemm_stage_channels(dtype));
   const long mt = (p.cout_store + 127) / 128;
   GemmShape g{GK_REG64, 1};
-  if (NST_GEMM_GLDS && (dtype != NST_DT_F32 || NST_GEMM_GLDS_F32)) {
+  if (NST_GEMM_GLDS && (dtype != NST_DT_F32 || gemm_glds_f32())) {
     const int esz = dtype == NST_DT_F32 ? 4 : 2;
     const long n_img = p.npix / std::max(1, p.ho * p.wo);
     const double in_b = (double)n_img * p.hi * p.wi * p.cs * esz;
     const double w_b = (double)((p.cout_store + 63) / 64) * p.kh * p.kw * (p.cin / (128 / esz)) * 8192.0;
     if (in_b < 2147483648.0 && w_b < 2147483648.0) {
       const long t256 = (long)((p.npix + 255) / 256) * mt, t128 = (long)((p.npix + 127) / 128) * mt;
-      if (gemm_t256() && p.cout_store > 128 && nstage >= 16) {
+      if (gemm_t256() && dtype != NST_DT_F32 && p.cout_store > 128 && nstage >= 16) {
         const long tt = (long)((p.npix + 255) / 256) * ((p.cout_store + 255) / 256);
         const long k = std::max<long>(1, std::min<long>((256 + tt - 1) / tt, std::min<long>(8, nstage / 8)));
         if (tt * k >= 128) return GemmShape{GK_GLDS256x256, (int)k};
@@ -611,6 +711,7 @@ GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
 
 template <int BM, int BN>
 void launch_glds(int dt, const GemmConvParams& p, hipStream_t st) {
+  if (dt == NST_DT_F32S) dt = NST_DT_F32;  // the fp32 layout; exact-f32 MFMAs on this kernel
   const int esz = dt == NST_DT_F32 ? 4 : 2;
   const long n_img = p.npix / std::max(1, p.ho * p.wo);
   const uint32_t in_b = (uint32_t)(n_img * p.hi * p.wi * p.cs * esz);
@@ -618,8 +719,17 @@ void launch_glds(int dt, const GemmConvParams& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.npix + BN - 1) / BN), (unsigned)((p.cout_store + BM - 1) / BM), (unsigned)p.ksplit);
   // 4 x 32 KB stages fit the LDS, 4 x 48 KB do not, 2 x 64 KB (256 x 256) do
   constexpr int RING = BM * 128 + BN * 128 <= 32768 ? NST_GEMM_RING_32K : (BM * 128 + BN * 128 <= 49152 ? 3 : 2);
+  if constexpr (BM * 128 + BN * 128 <= 32768 && NST_GEMM_RING_32K != 4) {
+    if (gemm_ring32() == 4 && dt == NST_DT_BF16) {  // sweep override: three 32 KB stages in flight
+      hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_BF16, 4>), grid, dim3(512), 0, st, p, w_b, in_b);
+      return;
+    }
+  }
   if (dt == NST_DT_F16) hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_F16, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
-  else if (dt == NST_DT_F32) hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_F32, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
+  else if (dt == NST_DT_F32) {
+    // (no fp32 256 x 256 form: hipcc gives its 16x16x4f32 MFMAs partially overlapping registers)
+    if constexpr (BM < 256) hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_F32, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
+  }
   else hipLaunchKernelGGL((gemm_glds_kernel<BM, BN, NST_DT_BF16, RING>), grid, dim3(512), 0, st, p, w_b, in_b);
 }
 

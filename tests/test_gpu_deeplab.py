@@ -6,7 +6,8 @@ Pinned pieces and their bars:
     of max |logit| and the same argmax wherever the reference's top-2 margin exceeds 1e-4 (elsewhere the
     order of fp32 accumulation decides a near-tie); the 16-bit modes within their logit bar of max |logit|
     (bf16 3e-2, fp16 5e-3), the same argmax wherever the margin exceeds twice that bar, and >= 98 % argmax
-    agreement overall; 1080p masks: fp32 (sky_swap.py's default here) identical to the reference chain's; the
+    agreement overall; 1080p masks: fp32 and fp32s (split-fp16 GEMMs, sky_swap.py's default here) within 1 LSB of
+    the reference chain's (the same class maps wherever the reference's margin is decided); the
     16-bit modes within 1 LSB on >= 98.5 % of pixels in fp16 (measured 98.9 %) and >= 95 % in bf16 (measured
     95.3 %): a class flip at a near-tie of the 256-px working map becomes a blob of the 7.5x upscaled, closed,
     feathered mask, which is why neither 16-bit mode is the default.

@@ -61,7 +61,7 @@ def timed(fn, steps):
 
 
 # the mask program's dtype in the configs[4] step: sky_swap.py's default
-MASK_DT = os.environ.get("SEG_MASK_DT", "fp32")
+MASK_DT = os.environ.get("SEG_MASK_DT", "fp32s")
 
 
 def main():
