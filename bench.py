@@ -328,14 +328,20 @@ def main():
              "NST_DT_F16M: split-fp16 arithmetic (fp32 activations) on the first layer (weights), the down-convs "
              "(operands and weights) and the first two residual blocks (operands), fp16 kernels elsewhere: the +-1 "
              "LSB bar at most of the fp16 rate"),
+            ("fp16m_one_block_mode", "fp16m:f16m_one_block", args.no_fp16m,
+             "NST_DT_F16M with NST_KSEL_F16M_ONE_BLOCK: only the first residual block on the split-operand kernel "
+             "(tests/precision_study.py: live max 0.958 LSB instead of 0.920 on the bench frames)"),
             ("fp32s_mode", "fp32s", args.no_fp32s,
              "NST_DT_F32S: fp32 activations, every conv operand an fp16 hi/lo pair (two fp16 MFMAs per K step, "
              "generic kernels): the fp32 parity mode's +-1 LSB bar")):
         if skip or world != 1:
             continue
+        dt, _, ks = dt.partition(":")
         net.compute_dtype = dt
+        net.kernel_select = frozenset([ks] if ks else [])
         e_alt = net.engine(dev)
         net.compute_dtype = "bf16"
+        net.kernel_select = frozenset()
         t_alt = time_steps(lambda: e_alt.stylize_u8(frames, PRESET), max(3, min(args.steps, 10)))
         alt_modes[key] = (e_alt, {"frames_per_s": round(nloc / t_alt, 2), "ms_per_step": round(t_alt * 1e3, 4),
                                   "what": what})

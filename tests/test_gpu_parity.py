@@ -163,16 +163,18 @@ def _bench_frames_and_reference():
     return _BENCH8["frames"], _BENCH8["ref"]
 
 
-def test_1080p_fp16m_vs_oracle_8_frames():
+@pytest.mark.parametrize("ksel", [(), ("f16m_one_block",)])
+def test_1080p_fp16m_vs_oracle_8_frames(ksel):
     """NST_DT_F16M (split-fp16 head, fp16 trunk) on the bench's 8 1080p frames vs the CPU reference (pre-LAB
     uint8): EVERY value within +-1 LSB (north_star's bar; the rounding model of tests/precision_study.py puts the
     largest raw error at ~0.93 LSB on these frames).  The fp16 trunk's rounding (rms ~0.07 LSB in that model) moves
     values across a truncation boundary, so ~5.5 % of values are off by exactly one (measured 0.0554); the bar on
-    that fraction is 8 %."""
+    that fraction is 8 %.  With NST_KSEL_F16M_ONE_BLOCK (only residual block 1 split; the model's live max 0.958)
+    the same bars."""
     frames, ref = _bench_frames_and_reference()
-    out = _net("johnson", 0, "fp16m").stylize_frames(torch.from_numpy(frames).cuda(), "imagenet_255").cpu().numpy()
+    out = _net("johnson", 0, "fp16m", ksel).stylize_frames(torch.from_numpy(frames).cuda(), "imagenet_255").cpu().numpy()
     d = np.abs(out.astype(int) - ref.astype(int))
-    print(f"1080p x8 fp16m: max {d.max()} LSB, values off by one {(d > 0).mean():.6f}, values > 1 LSB "
+    print(f"1080p x8 fp16m {ksel}: max {d.max()} LSB, values off by one {(d > 0).mean():.6f}, values > 1 LSB "
           f"{int((d > 1).sum())}, ssim {min(O.ssim(out[i], ref[i]) for i in range(8)):.6f}")
     assert d.max() <= 1 and (d > 0).mean() < 0.08
 
