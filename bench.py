@@ -175,13 +175,13 @@ def layer_flops(H: int, W: int) -> dict:
 
 
 # NST_DT_F16M's split-precision layers and their MFMA issue cost per algorithmic product (nst_api.cpp layer_kdt):
-# the first layer 2 fp16 MFMAs (Wh x + Wl x), the down-convs 3 (Wh xh + Wh xl + Wl xh), the first two residual
-# blocks 2 (Wh xh + Wh xl, conv_ws1s.hip)
+# the first layer 2 fp16 MFMAs (Wh x + Wl x), the down-convs 3 (Wh xh + Wh xl + Wl xh), the first residual block 2
+# (Wh xh + Wh xl, conv_ws1s.hip; with NST_KSEL_F16M_TWO_BLOCKS the second block too)
 F16M_MFMA_PER_PRODUCT = {"conv1.conv2d": 2, "conv2.conv2d": 3, "conv3.conv2d": 3, "res1.conv1.conv2d": 2,
-                         "res1.conv2.conv2d": 2, "res2.conv1.conv2d": 2, "res2.conv2.conv2d": 2}
+                         "res1.conv2.conv2d": 2}
 # bytes per element each F16M layer reads / writes (fp32 activations in the split head)
 F16M_IO_BYTES = {"conv1.conv2d": (2, 4), "conv2.conv2d": (4, 4), "conv3.conv2d": (4, 4), "res1.conv1.conv2d": (4, 4),
-                 "res1.conv2.conv2d": (4, 4), "res2.conv1.conv2d": (4, 4), "res2.conv2.conv2d": (4, 4)}
+                 "res1.conv2.conv2d": (4, 4)}
 
 
 def mode_roofline(eng, frames, H: int, W: int, nloc: int) -> dict:
@@ -326,11 +326,11 @@ def main():
              "NST_DT_F16: the bench kernels with fp16 weights/activations (fp16 MFMA, fp32 accumulate)"),
             ("fp16m_mode", "fp16m", args.no_fp16m,
              "NST_DT_F16M: split-fp16 arithmetic (fp32 activations) on the first layer (weights), the down-convs "
-             "(operands and weights) and the first two residual blocks (operands), fp16 kernels elsewhere: the +-1 "
-             "LSB bar at most of the fp16 rate"),
-            ("fp16m_one_block_mode", "fp16m:f16m_one_block", args.no_fp16m,
-             "NST_DT_F16M with NST_KSEL_F16M_ONE_BLOCK: only the first residual block on the split-operand kernel "
-             "(tests/precision_study.py: live max 0.958 LSB instead of 0.920 on the bench frames)"),
+             "(operands and weights) and the first residual block (operands), fp16 kernels elsewhere: the +-1 "
+             "LSB bar at three quarters of the fp16 rate"),
+            ("fp16m_two_blocks_mode", "fp16m:f16m_two_blocks", args.no_fp16m,
+             "NST_DT_F16M with NST_KSEL_F16M_TWO_BLOCKS: residual blocks 1 and 2 on the split-operand kernel "
+             "(tests/precision_study.py: live max 0.920 LSB instead of 0.958 on the bench frames)"),
             ("fp32s_mode", "fp32s", args.no_fp32s,
              "NST_DT_F32S: fp32 activations, every conv operand an fp16 hi/lo pair (two fp16 MFMAs per K step, "
              "generic kernels): the fp32 parity mode's +-1 LSB bar")):

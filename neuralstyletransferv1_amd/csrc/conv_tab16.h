@@ -15,7 +15,9 @@
 #define NST_R_UP1_TILE 4, 32, 1, 4  // ReCoNet 192 -> 96 up-conv (phases): 2.24 -> 1.61 ms per batch of 8 vs 2 x 16
 #endif
 #ifndef NST_R_TRUNK_TILE
-#define NST_R_TRUNK_TILE 16, 16, 2, 2  // ReCoNet 192-channel trunk: 1.12 -> 0.96 ms per conv and batch of 8 vs 8 x 16
+#define NST_R_TRUNK_TILE 16, 16, 2, 4  // ReCoNet 192-channel trunk: 8 waves (2 x 4: 8 x 3 accumulator sub-tiles each,
+                                       // two waves per SIMD): 0.968 -> 0.735 ms per conv and batch of 8 (r04 sweep;
+                                       // 2 x 2 waves 0.968, 4 x 2 0.792, 4 x 1 0.978; r03: 8 x 16 tiles 1.12)
 #endif
 #ifndef NST_R_C1_TILE
 #define NST_R_C1_TILE 8, 32, 4, 1  // ReCoNet 9x9 first layer (48 -> 64 channels)

@@ -885,9 +885,9 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     return NST_E_INVALID;
   }
   const bool f16m = compute_dtype == NST_DT_F16M;
-  // residual blocks on the split-operand kernel (NST_KSEL_F16M_ONE_BLOCK: the first only; precision_study:
-  // live max 0.958 instead of 0.920 LSB on the bench frames)
-  const int split_blocks = !f16m ? 0 : ((flags & NST_KSEL_F16M_ONE_BLOCK) ? 1 : 2);
+  // residual blocks on the split-operand kernel: the first (tests/precision_study.py: live max 0.958 LSB on the
+  // bench frames; 1,114 frames/s), or the first two with NST_KSEL_F16M_TWO_BLOCKS (0.920 LSB; 1,014 frames/s)
+  const int split_blocks = !f16m ? 0 : ((flags & NST_KSEL_F16M_TWO_BLOCKS) ? 2 : 1);
   if (f16m && (is_reconet(arch) || (flags & (NST_KSEL_UNFUSED_RESIDUAL | NST_KSEL_NO_WS9 | NST_KSEL_NO_WS2 | NST_KSEL_NO_PREPAD)))) {
     set_error("nst_create: NST_DT_F16M is built for the Johnson / NST nets with the default kernel selection");
     return NST_E_INVALID;

@@ -23,6 +23,9 @@ def _net(arch, seed, dtype="bf16"):
     m = synthetic.build_module(arch)
     m.load_state_dict(synthetic.make_state_dict(arch, seed))
     m = m.to("cuda").eval()
+    if dtype == "fp16m2":  # NST_DT_F16M with residual blocks 1 and 2 split (NST_KSEL_F16M_TWO_BLOCKS)
+        dtype = "fp16m"
+        m.kernel_select = frozenset(["f16m_two_blocks"])
     m.compute_dtype = dtype
     return m
 
@@ -40,17 +43,19 @@ def _report(recs):
     ("reconet", 1, 61, 90, "tanh"),           # 48/96/192 channels: generic bf16 kernels + tanh output
     ("reconet_frn", 1, 61, 90, "tanh"),       # FRN + TLU: mean-square statistics, tau folded into biases / shifts
 ])
-@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp16m"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp16m", "fp16m2"])
 def test_16bit_layers_small(arch, n, h, w, preset, dtype):
-    if dtype == "fp16m" and arch.startswith("reconet"):
+    if dtype.startswith("fp16m") and arch.startswith("reconet"):
         pytest.skip("NST_DT_F16M is built for the Johnson / NST nets")
     frames = synthetic.make_frames(n, h, w, seed=40 + h)
     recs = LC.check_layers(_net(arch, 11, dtype), frames, preset, acc=torch.float64)
     _report(recs)
-    # fp16m: the first two residual blocks run unfused (+2 ops: the joins writing x_1 (fp32) and the fp16 stream x_2)
-    assert len(recs) == (14 if arch.startswith("reconet") else 16) + (2 if dtype == "fp16m" else 0)
-    if dtype == "fp16m":  # the split-precision head: ~22-bit products (measured rel error reported)
-        assert sum(1 for r in recs if "split_rel" in r) == 7
+    # fp16m: the split residual blocks run unfused (+1 op: the join writing the fp16 stream; two blocks: +2, the
+    # first join writing x_1 in fp32)
+    extra = {"fp16m": 1, "fp16m2": 2}.get(dtype, 0)
+    assert len(recs) == (14 if arch.startswith("reconet") else 16) + extra
+    if extra:  # the split-precision head: ~22-bit products (measured rel error reported)
+        assert sum(1 for r in recs if "split_rel" in r) == 3 + 2 * extra
 
 
 def test_bf16_layers_1080p():
@@ -74,15 +79,15 @@ def test_fp16_layers_1080p():
 
 
 def test_fp16m_layers_1080p():
-    """NST_DT_F16M at configs[1]'s frame size: the split-precision head (first layer, down-convs, first two residual
-    blocks: fp32 outputs against the conv of the same operand, exact / with the fp16 weights), the joins and the fp16
+    """NST_DT_F16M at configs[1]'s frame size: the split-precision head (first layer, down-convs, first residual
+    block: fp32 outputs against the conv of the same operand, exact / with the fp16 weights), the join and the fp16
     trunk / up-convs / output conv, every output row of every layer."""
     frames = synthetic.make_frames(1, 1080, 1920, seed=1000)
     recs = LC.check_layers(_net("johnson", 0, "fp16m"), frames, "imagenet_255")
     _report(recs)
     modes = {r["layer"]: r["mode"] for r in recs}
     assert modes["conv1.conv2d"] == 7 and modes["conv2.conv2d"] == 6 and modes["conv3.conv2d"] == 6
-    assert modes["res1.conv1.conv2d"] == 8 and modes["res2.conv2.conv2d"] == 8
+    assert modes["res1.conv1.conv2d"] == 8 and modes["res1.conv2.conv2d"] == 8 and modes["res2.conv1.conv2d"] == 4
     assert modes["res3.conv1.conv2d"] == 4 and modes["deconv1.conv2d"] == 5 and modes["deconv3.conv2d"] == 3
     assert max(r.get("split_rel", 0.0) for r in recs) <= LC.SPLIT_REL
 

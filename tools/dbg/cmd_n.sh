@@ -12,3 +12,4 @@ grep -E "1080p x8" gpurun_out/n_tests.log
 step n_bench 400 python -u bench.py --steps 20 --warmup 5
 python tools/bench_brief.py gpurun_out/n_bench.log | grep -E "fps|fp16m"
 step n_reconet 200 python -u tools/mode_profile.py bf16 reconet
+for v in t42 t24 t41; do NST_HIP_LIB=sweep/libnst_hip_$v.so step n_reconet_$v 200 python -u tools/mode_profile.py bf16 reconet; done
