@@ -44,6 +44,7 @@ namespace nst {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int reflect_idx(int v, int L) {
   v = v < 0 ? -v : v;
@@ -246,7 +247,7 @@ struct ConvCfg {
   static constexpr int PF = ROWED ? pf_div(PF_RAW, RS) : PF_RAW;
   static constexpr int NSTEP_P = ROWED ? NSTEP : (NSTEP + PF - 1) / PF * PF;     // loop trip (zero-padded)
   static constexpr int NSTEP_PACK = NSTEP_P + PF;                                 // packed steps (prefetch tail)
-  static constexpr int REDW = MODE == MODE_PHASE ? 4 : WM;                        // waves sharing a channel
+  static constexpr int REDW = MODE == MODE_PHASE ? 4 * WM : WM;                   // waves sharing a channel
   static constexpr int RED_BYTES = REDW * BN * 2 * 4;
   static constexpr int MAP_OFF = (LDS_BYTES + 15) / 16 * 16;                      // per-block row/col source maps
   static constexpr int MAP_BYTES = (LH + LW) * 4;
@@ -259,7 +260,8 @@ struct ConvCfg {
   static_assert(TW % COLS == 0 && MSUBT % WM == 0, "m-subtiles must split over WM waves");
   static_assert(BN % 16 == 0, "n-subtiles of 16 channels");
   static_assert(MODE == MODE_PHASE || (BN / 16) % WN == 0, "n-subtiles must split over WN waves");
-  static_assert(MODE != MODE_PHASE || (WM == 1 && WN == 4 && S == 1), "phase mode: one wave per phase");
+  static_assert(MODE != MODE_PHASE || ((WM == 1 || WM == 2) && WN == 4 && S == 1),
+                "phase mode: one wave per phase (WM = 2: two, splitting the tile's pixel sub-tiles)");
   static_assert(MODE != MODE_XSHIFT || (BN == 16 && WN == 1 && S == 1), "x-shift mode: 16 rows = 5x3 + 1");
   static_assert(PAIR || (CINP % CPC) == 0, "channel padding");
   static_assert(PAIR || NCH == 1 || NCH % 4 == 0, "chunks per pixel must be 1 or a multiple of 4");
@@ -822,6 +824,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
         }
       }
     }
+    // the step's operand fragments stay live past its MFMAs: hipcc (ROCm 7.2) otherwise may place an MFMA's
+    // destination partially over a source register that dies there (tools/check_mfma_overlap.py)
+#pragma unroll
+    for (int t = 0; t < NSUB * AF; ++t) asm volatile("" ::"v"(__builtin_bit_cast(u32x4_t, a[t])));
+#pragma unroll
+    for (int m = 0; m < MSUB; ++m) asm volatile("" ::"v"(__builtin_bit_cast(u32x4_t, b[m])));
   };
 
   // kloop(acc, rot, hook): rot = ring slot of this tile's stage 0 (PERS: the ring runs on across
@@ -1065,7 +1073,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
           for (int j = 0; j < 16; ++j) { v[2 * j] = s1[j]; v[2 * j + 1] = s2[j]; }
           float t1, t2;
           row_reduce_scatter32(v, px, t1, t2);
-          float* dst = p.partial + ((((size_t)n * ntile + wk.tile) * C::REDW + wm) * p.cout_stride + cbase + px) * 2;
+          const int rw = MODE == MODE_PHASE ? wave : wm;
+          float* dst = p.partial + ((((size_t)n * ntile + wk.tile) * C::REDW + rw) * p.cout_stride + cbase + px) * 2;
           *(float2*)dst = make_float2(t1, t2);
         }
         return;

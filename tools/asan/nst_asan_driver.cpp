@@ -4,7 +4,7 @@
 // seg_deeplab.cpp, region_api.cpp, flow_api.cpp) are compiled with -fsanitize=address on the HOST side only
 // (device code is unchanged: GPU sanitizers are not available on the pool) and linked with the normal kernel
 // objects into this driver.  It exercises handle creation and weight packing, planning, workspace sizing, the
-// forward of every architecture in every compute dtype on small ragged frames, the Gram entry point, and the
+// forward of every architecture in every compute dtype (and both NST_DT_F16M plans) on small ragged frames, the Gram entry point, and the
 // argument-validation / error paths, then destroys everything; ASan reports any heap overflow, use-after-free or
 // double free in that host code.
 //
@@ -68,7 +68,10 @@ bool load(const char* path, Params& P) {
 }
 
 void run_arch(const Params& P) {
-  const int dtypes[] = {NST_DT_F32, NST_DT_BF16, NST_DT_F16, NST_DT_F32S};
+  // NST_DT_F16M twice: the default one split residual block and NST_KSEL_F16M_TWO_BLOCKS (-1 below); the ReCoNet
+  // nets reject it (checked, then skipped)
+  const bool reconet = P.arch == NST_ARCH_RECONET || P.arch == NST_ARCH_RECONET_FRN;
+  const int dtypes[] = {NST_DT_F32, NST_DT_BF16, NST_DT_F16, NST_DT_F32S, NST_DT_F16M, -1};
   const int n = 2, h = 45, w = 58;  // ragged (the output fit path of Johnson / ReCoNet), above NST's 40-px pre-reflect
   std::vector<uint8_t> frames((size_t)n * h * w * 3);
   for (size_t i = 0; i < frames.size(); ++i) frames[i] = (uint8_t)((i * 2654435761u) >> 24);
@@ -77,9 +80,16 @@ void run_arch(const Params& P) {
   HC(hipMalloc(&x, frames.size()));
   HC(hipMalloc(&y, frames.size()));
   HC(hipMemcpy(x, frames.data(), frames.size(), hipMemcpyHostToDevice));
-  for (int dt : dtypes) {
+  for (int dt0 : dtypes) {
+    const int dt = dt0 < 0 ? NST_DT_F16M : dt0;
+    const unsigned flags = dt0 < 0 ? (unsigned)NST_KSEL_F16M_TWO_BLOCKS : 0u;
     nst_handle* hd = nullptr;
-    expect(nst_create(P.arch, P.view.data(), (int)P.view.size(), dt, 0, &hd) == NST_OK && hd, "nst_create");
+    if (reconet && dt == NST_DT_F16M) {
+      expect(nst_create_ex(P.arch, P.view.data(), (int)P.view.size(), dt, 0, flags, &hd) == NST_E_INVALID && !hd,
+             "NST_DT_F16M is rejected for ReCoNet");
+      continue;
+    }
+    expect(nst_create_ex(P.arch, P.view.data(), (int)P.view.size(), dt, 0, flags, &hd) == NST_OK && hd, "nst_create");
     if (!hd) continue;
     int oh = 0, ow = 0;
     expect(nst_output_hw(hd, h, w, &oh, &ow) == NST_OK && oh > 0 && ow > 0, "nst_output_hw");
@@ -151,7 +161,7 @@ int main(int argc, char** argv) {
       return 2;
     }
     run_arch(P);
-    std::printf("arch %d: %zu tensors, 4 dtypes\n", P.arch, P.view.size());
+    std::printf("arch %d: %zu tensors, 6 dtype / plan combinations\n", P.arch, P.view.size());
   }
   run_gram();
   std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "ok", g_fail);
