@@ -67,14 +67,16 @@ struct VggConv {
   void *gwf = nullptr, *gwb = nullptr;
   float *gscale = nullptr, *gshift = nullptr, *gzero = nullptr;
 };
-// the layers on the GEMM conv: every conv whose input has >= 64 channels and whose map is at most a
+// the layers that may take the GEMM conv: every conv whose input has >= 64 channels and whose map is at most a
 // quarter of the image (conv2_1 onward); input gradients of the same layers
-// (NST_VGG_GEMM_F / NST_VGG_GEMM_B: bitmasks of the layers whose forward / input gradient take the GEMM conv,
-// for sweeps; default conv2_1 onward for both)
+// (NST_VGG_GEMM_F / NST_VGG_GEMM_B: bitmasks of the layers whose forward / input gradient take the GEMM conv, for
+// sweeps.  Default: conv5_1 only, both ways (r04 sweep, profiles/r04_s_gatys_sweep.txt: with its operand fragments
+// kept live the halo-staged generic kernel beats the GEMM on conv2_1..conv4_4 too: 1.094 -> 1.007 ms per Adam step;
+// a GEMM-forward layer must follow a pool, since the GEMM reads a rectified input)
 unsigned vgg_gemm_mask(bool fwd) {
   static const unsigned m[2] = {
-      [] { const char* e = std::getenv("NST_VGG_GEMM_B"); return e ? (unsigned)std::strtoul(e, nullptr, 0) : 0x1ffcu; }(),
-      [] { const char* e = std::getenv("NST_VGG_GEMM_F"); return e ? (unsigned)std::strtoul(e, nullptr, 0) : 0x1ffcu; }()};
+      [] { const char* e = std::getenv("NST_VGG_GEMM_B"); return e ? (unsigned)std::strtoul(e, nullptr, 0) : 0x1000u; }(),
+      [] { const char* e = std::getenv("NST_VGG_GEMM_F"); return e ? (unsigned)std::strtoul(e, nullptr, 0) : 0x1000u; }()};
   return m[fwd ? 1 : 0];
 }
 bool vgg_gemm_layer(int i) { return ((vgg_gemm_mask(true) | vgg_gemm_mask(false)) >> i) & 1u; }

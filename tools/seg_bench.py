@@ -109,6 +109,27 @@ def main():
                 "mask_share": round(res[MASK_DT] / ms, 3),
                 # the step with each mask dtype: its mask time / (that + the rest of the step)
                 "mask_share_by_dtype": {d: round(t / (ms - res[MASK_DT] + t), 3) for d, t in res.items()}})
+    if os.environ.get("SEG_GRAPH", "0") == "1":
+        # launch-overhead probe: the mask program (MASK_DT) replayed from a captured HIP graph (static input / output
+        # buffers); the captured kernels are the same launches on the same stream
+        me_g = deeplab.MaskEngine(model, dev, resolution=256, dtype=MASK_DT)
+        static_in = frames.clone()
+        me_g.masks(static_in, ids, feather_px=3)  # allocations, plans, resamplers outside the capture
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            me_g.masks(static_in, ids, feather_px=3)
+            torch.cuda.synchronize(dev)
+            with torch.cuda.graph(graph, stream=s):
+                static_out = me_g.masks(static_in, ids, feather_px=3)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        g_ms = timed(lambda: graph.replay(), STEPS)
+        ref = me_g.masks(static_in, ids, feather_px=3)
+        graph.replay()
+        torch.cuda.synchronize(dev)
+        out.update({"mask_ms_graph": round(g_ms, 3), "graph_masks_identical": bool(torch.equal(ref, static_out))})
     print(json.dumps(out), flush=True)
 
 
