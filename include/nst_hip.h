@@ -33,6 +33,7 @@ extern "C" {
 #define NST_E_SHAPE (-3)     /* unsupported input/output geometry */
 #define NST_E_HIP (-4)       /* HIP runtime error */
 #define NST_E_WORKSPACE (-5) /* workspace too small */
+#define NST_E_RANGE (-6)     /* nst_set_range_check: a value left the compute dtype's range (non-finite result) */
 
 /* ---- architectures (pipeline.py:72-79 _detect_transformer_type, :598-603 reconet) ---- */
 #define NST_ARCH_JOHNSON 0 /* transformer_net.py:4-41 */
@@ -174,6 +175,11 @@ typedef struct nst_op_desc {
                          20 (split fp16 operand x fp16 weights, fp32 output) */
 } nst_op_desc;
 int nst_num_ops(const nst_handle* h);
+/* Optional range check (the 16-bit and split modes hold operands inside the fp16 range, |v| <= 65504):
+ * enabled, every nst_forward zeroes a device flag, checks each layer's InstanceNorm table (an overflowing operand
+ * turns into inf, then a non-finite statistic) and an fp32 output for non-finite values, waits for the stream and
+ * returns NST_E_RANGE if any was found.  Off by default (no extra launches, no synchronisation). */
+int nst_set_range_check(nst_handle* h, int enable);
 int nst_op_describe(const nst_handle* h, int n, int in_h, int in_w, int op, nst_op_desc* out);
 int nst_forward_capture(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset,
                         void* y, int y_fmt, void* workspace, size_t workspace_bytes, void* const* act,

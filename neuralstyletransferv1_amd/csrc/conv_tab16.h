@@ -20,7 +20,8 @@
                                        // 2 x 2 waves 0.968, 4 x 2 0.792, 4 x 1 0.978; r03: 8 x 16 tiles 1.12)
 #endif
 #ifndef NST_R_C1_TILE
-#define NST_R_C1_TILE 16, 32, 4, 2  // ReCoNet 9x9 first layer (48 -> 64 channels): 8 waves, 1.064 -> 1.008 ms (r04)
+#define NST_R_C1_TILE 16, 16, 4, 2  // ReCoNet 9x9 first layer (48 -> 64 channels): 8 waves on 16 x 16 tiles, 1.064 ->
+                                    // 0.93 ms (r04 sweeps: 16 x 32 1.008, 8 x 64 1.345)
 #endif
 #ifndef NST_R_DOWN2_TILE
 #define NST_R_DOWN2_TILE 8, 16, 2, 4  // ReCoNet 96 -> 192 stride-2 conv: 8 waves, 1.248 -> 0.774 ms (r04; r03: 4 x 32 tiles

@@ -247,6 +247,7 @@ using namespace nst;
 
 struct nst_handle {
   int arch, dtype, device;
+  int* range_flag = nullptr;  // nst_set_range_check: device flag raised by check_finite_kernel
   std::vector<Layer> layers;
   std::vector<Op> prog;
   // live profiling (nst_profile_begin/end)
@@ -1079,6 +1080,7 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
 void nst_destroy(nst_handle* h) {
   if (!h) return;
   DeviceGuard guard(h->device);
+  if (h->range_flag) (void)hipFree(h->range_flag);
   for (Layer& Ly : h->layers) {
     if (Ly.wpk) (void)hipFree(Ly.wpk);
     if (Ly.wpk_rev) (void)hipFree(Ly.wpk_rev);
@@ -1305,6 +1307,8 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     if (!final_out) {
       e = launch_in_finalize(partial, n, p.tiles_x * p.tiles_y * k->part_rows, Ly.coutp, (double)p.hconv * (double)p.wconv,
                              Ly.gamma, Ly.beta, Ly.eps, Ly.frn, tab(op.layer), ws + P.off_seg, st);
+      if (e == hipSuccess && h->range_flag)
+        e = launch_check_finite((const float*)tab(op.layer), (size_t)n * Ly.coutp * 2, h->range_flag, st);
       if (e != hipSuccess) { set_error(std::string("finalize launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
     }
     if (cap && !final_out) {
@@ -1319,9 +1323,22 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     }
     return NST_OK;
   };
+  if (h->range_flag) NST_HIP_CHECK(hipMemsetAsync(h->range_flag, 0, sizeof(int), st));
   for (size_t i = 0; i < h->prog.size(); ++i) {
     const int rc = run_op(i);
     if (rc != NST_OK) return rc;
+  }
+  if (h->range_flag) {  // synchronous: the caller asked for the verdict of this forward
+    if (y_fmt == NST_IO_F32_NCHW)
+      NST_HIP_CHECK(launch_check_finite((const float*)y, (size_t)n * 3 * P.out_h * P.out_w, h->range_flag, st));
+    int bad = 0;
+    NST_HIP_CHECK(hipMemcpyAsync(&bad, h->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    NST_HIP_CHECK(hipStreamSynchronize(st));
+    if (bad) {
+      set_error("nst_forward: a non-finite InstanceNorm statistic or output value (an activation left the range of "
+                "the compute dtype: fp16 / split-fp16 operands hold |v| <= 65504)");
+      return NST_E_RANGE;
+    }
   }
   return NST_OK;
 }
@@ -1340,6 +1357,22 @@ int nst_forward_capture(nst_handle* h, const void* x, int x_fmt, int n, int in_h
                         void* const* stats, void* stream) {
   const Capture cap{act, res, stats};
   return forward_impl(h, x, x_fmt, n, in_h, in_w, preset, y, y_fmt, workspace, workspace_bytes, stream, &cap);
+}
+
+int nst_set_range_check(nst_handle* h, int enable) {
+  if (!h) { set_error("nst_set_range_check: null handle"); return NST_E_INVALID; }
+  DeviceGuard guard(h->device);
+  if (enable && !h->range_flag) {
+    if (hipMalloc(&h->range_flag, sizeof(int)) != hipSuccess) {
+      h->range_flag = nullptr;
+      set_error("nst_set_range_check: hipMalloc failed");
+      return NST_E_HIP;
+    }
+  } else if (!enable && h->range_flag) {
+    (void)hipFree(h->range_flag);
+    h->range_flag = nullptr;
+  }
+  return NST_OK;
 }
 
 int nst_num_ops(const nst_handle* h) { return h ? (int)h->prog.size() : 0; }

@@ -179,6 +179,7 @@ hipError_t launch_adam(float* x, const float* g, float* m, float* v, int hw, int
 constexpr int IN_MAX_SEGMENTS = 128;
 int in_finalize_segments(int tiles);
 // seg_ws: n * IN_MAX_SEGMENTS * cstride * 16 bytes of scratch
+hipError_t launch_check_finite(const float* v, size_t n, int* flag, hipStream_t st);
 hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
                               const float* gamma, const float* beta, float eps, int frn, float2* out,
                               void* seg_ws, hipStream_t st);

@@ -146,6 +146,21 @@ __global__ __launch_bounds__(1024) void in_stats_kernel(const float* __restrict_
 
 int in_finalize_segments(int tiles) { return max(1, min(IN_MAX_SEGMENTS, tiles / 64)); }
 
+// range check (nst_set_range_check): any non-finite value among n floats raises *flag.  An activation outside the
+// fp16 range turns into inf in the 16-bit and split modes' operand conversions and then into a non-finite InstanceNorm
+// statistic, so the layers' IN tables and the raw output are what is checked
+__global__ __launch_bounds__(256) void check_finite_kernel(const float* __restrict__ v, size_t n, int* __restrict__ flag) {
+  bool bad = false;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    bad |= !__builtin_isfinite(v[i]);
+  if (bad) atomicOr(flag, 1);
+}
+hipError_t launch_check_finite(const float* v, size_t n, int* flag, hipStream_t st) {
+  const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(check_finite_kernel, dim3(std::max(1u, blocks)), dim3(256), 0, st, v, n, flag);
+  return hipGetLastError();
+}
+
 hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstride, double count,
                               const float* gamma, const float* beta, float eps, int frn, float2* out,
                               void* seg_ws, hipStream_t st) {

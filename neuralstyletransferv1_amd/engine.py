@@ -9,6 +9,7 @@ runs the whole network as hand-written HIP kernels on the caller's stream.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -48,6 +49,13 @@ class Engine:
         self._h = h
         self._keep = None
         self._ws: Optional[torch.Tensor] = None
+        # NST_RANGE_CHECK=1: every forward checks for values that left the compute dtype's range (NST_E_RANGE; a
+        # synchronising debug aid for the fp16 / split modes, off by default)
+        if os.environ.get("NST_RANGE_CHECK", "0") == "1":
+            self.set_range_check(True)
+
+    def set_range_check(self, enable: bool) -> None:
+        check(lib().nst_set_range_check(self._h, 1 if enable else 0), "nst_set_range_check")
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -548,3 +548,29 @@ def test_output_independent_of_stale_workspace(path, dtype):
             ws.copy_(torch.randint(0, 256, ws.shape, device="cuda", dtype=torch.uint8, generator=gen))
         outs.append(eng.stylize_u8(fr, preset).cpu())
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("dtype", ["fp16", "fp32s", "fp16m"])
+def test_range_check_flags_fp16_overflow(dtype):
+    """nst_set_range_check: a checkpoint whose first conv is scaled so its outputs leave the fp16
+    range (|v| > 65504) makes the 16-bit / split modes' forward return NST_E_RANGE instead of silently producing
+    frames from inf / NaN; the same net unscaled passes the check, and fp32 (no fp16 operands) passes either way."""
+    from neuralstyletransferv1_amd._lib import NstError
+    frames = torch.from_numpy(synthetic.make_frames(1, 64, 96, seed=3)).cuda()
+    for scale, expect_bad in ((1.0, False), (2e6, True)):
+        sd = synthetic.make_state_dict("johnson", 0)
+        sd["conv1.conv2d.weight"] = sd["conv1.conv2d.weight"] * scale
+        sd["conv1.conv2d.bias"] = sd["conv1.conv2d.bias"] * scale
+        m = synthetic.build_module("johnson")
+        m.load_state_dict(sd)
+        m = m.cuda().eval()
+        for dt, bad in ((dtype, expect_bad), ("fp32", False)):
+            m.compute_dtype = dt
+            eng = m.engine(frames.device)
+            eng.set_range_check(True)
+            if bad:
+                with pytest.raises(NstError, match=r"\(-6\)"):
+                    eng.stylize_u8(frames, "imagenet_255")
+            else:
+                eng.stylize_u8(frames, "imagenet_255")
+            eng.set_range_check(False)

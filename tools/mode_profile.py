@@ -19,6 +19,7 @@ m = synthetic.build_module(arch)
 m.load_state_dict(synthetic.make_state_dict(arch, 0))
 m = m.to(dev).eval()
 m.compute_dtype = dt
+m.kernel_select = frozenset(k for k in os.environ.get("MODE_KSEL", "").split(",") if k)  # e.g. no_wstat,no_ws2
 eng = m.engine(dev)
 for _ in range(2):
     eng.stylize_u8(frames, "imagenet_255")
@@ -34,6 +35,7 @@ for _ in range(3):
     eng.stylize_u8(frames, "imagenet_255")
 torch.cuda.synchronize()
 prof = eng.profile_end()
-print(json.dumps({"arch": arch, "dtype": dt, "lib": os.environ.get("NST_HIP_LIB", "default"), "frames_per_s": round(8 / step, 1),
+print(json.dumps({"arch": arch, "dtype": dt, "lib": os.environ.get("NST_HIP_LIB", "default"),
+                  "ksel": sorted(m.kernel_select), "frames_per_s": round(8 / step, 1),
                   "ms_per_step": round(step * 1e3, 3),
                   "per_layer_ms": {n: round(ms / max(c, 1), 3) for n, ms, c in prof}}), flush=True)
