@@ -423,6 +423,14 @@ class FrameSource:
             return pil
         # the round trip goes through an anonymous in-memory file with a real descriptor: Pillow encodes to a
         # descriptor with the GIL released (to a BytesIO it holds the GIL, so a thread pool would serialise)
+        if not hasattr(os, "memfd_create"):  # (not Linux: same bytes through a BytesIO)
+            import io
+            buf = io.BytesIO()
+            pil.save(buf, format="JPEG", quality=q)
+            buf.seek(0)
+            im = Image.open(buf)
+            im.load()
+            return im if im.mode == "RGB" else im.convert("RGB")
         with os.fdopen(os.memfd_create("nst_stage"), "w+b") as f:
             pil.save(f, format="JPEG", quality=q)
             f.seek(0)
