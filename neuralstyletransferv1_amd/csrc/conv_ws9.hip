@@ -58,10 +58,16 @@ constexpr int WS9_RING = NST_WS9_RING;  // input-row operands in flight ahead of
 // kernel spends on the two 16-channel M tiles go to Wh and Wl of ONE M tile, into separate accumulators added in
 // the epilogue, so a wave covers 16 output channels (wave w: channel half w / (NW/2), 16-column strip w % (NW/2))
 // and a tile is half as wide.  O32: fp32 output (the next layer reads it as a split hi / lo operand).
-template <int NW_, bool SW = false, bool O32 = false>
+// CO (plain weights only): output channels, 32 or 64.  64 (ReCoNet's 48 -> 64 padded first layer): two channel
+// halves of 32 (each wave: one half's two M tiles and weight set, the same registers as 32 channels), so a tile
+// has half as many 16-column strips.
+template <int NW_, bool SW = false, bool O32 = false, int CO = 32>
 struct W9Cfg {
-  static constexpr int NW = NW_, NT = 64 * NW, TH = WS9_TH, COUT = 32;
-  static constexpr int NSTRIP = SW ? NW / 2 : NW;  // 16-column strips per tile
+  static constexpr int NW = NW_, NT = 64 * NW, TH = WS9_TH, COUT = CO;
+  static constexpr int MH = SW ? 2 : CO / 32;      // channel halves (SW: hi / lo weight halves of 16 channels)
+  static constexpr int NSTRIP = NW / MH;           // 16-column strips per tile
+  static_assert(!SW || CO == 32, "split weights: 32 channels");
+  static_assert(CO == 32 || CO == 64, "32 or 64 output channels");
   static constexpr int TW = 16 * NSTRIP;
   static constexpr int HR = TH + 8;                 // halo rows
   // 16-B chunks per halo row: TW + 8 px used, rounded up so the row stride is == 32 mod 64 dwords
@@ -82,7 +88,7 @@ struct W9Cfg {
   static constexpr int NWM = 9 * 2;                 // 16x16x32 weight fragments (ky, m)
   static constexpr int NWK = 3 * 2;                 // 16x16x16 weight fragments (j, m)
   static constexpr int WHALF = NWM * 64 * 16 + NWK * 64 * 8;  // one weight set (SW: one channel half)
-  static constexpr int WBYTES = (SW ? 2 : 1) * WHALF;
+  static constexpr int WBYTES = MH * WHALF;
   static_assert(NCHK % 64 == 0, "whole-wave DMA requests");
   static_assert(2 * RCH >= TW + 8 && (RS / 4) % 64 == 32, "halo row");
   static_assert(NST * NT * 16 == TH * TW * PIXB, "whole 16-B stores per thread");
@@ -93,16 +99,16 @@ struct W9Cfg {
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 
-template <typename T, int NW, bool SW, bool O32>
+template <typename T, int NW, bool SW, bool O32, int CO>
 __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
-  using C = W9Cfg<NW, SW, O32>;
+  using C = W9Cfg<NW, SW, O32, CO>;
   static_assert(!SW || IS_F16<T>, "split weights are fp16 pairs");
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, px = lane & 15;
-  const int strip = SW ? wv % C::NSTRIP : wv;  // the wave's 16 output columns
-  const int mh = SW ? wv / C::NSTRIP : 0;      // SW: the wave's 16 output channels 16 mh ..
+  const int strip = wv % C::NSTRIP;  // the wave's 16 output columns
+  const int mh = wv / C::NSTRIP;     // SW: the wave's 16 output channels 16 mh ..; CO = 64: its 32 channels 32 mh ..
 
   struct Work {
     int n, tile, oy0, ox0;
@@ -241,12 +247,12 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   // ---- epilogue: bias, 16-bit values into the LDS output tile, IN partials from the fp32 values ----
   auto epilogue = [&](const Work& wk_, Acc& acc) {
     if constexpr (!SW) {
-      const f32x4_t bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (4 * g) * 4);
-      const f32x4_t bias1 = *(const f32x4_t*)(smem + C::BIAS_OFF + (16 + 4 * g) * 4);
+      const f32x4_t bias0 = *(const f32x4_t*)(smem + C::BIAS_OFF + (32 * mh + 4 * g) * 4);
+      const f32x4_t bias1 = *(const f32x4_t*)(smem + C::BIAS_OFF + (32 * mh + 16 + 4 * g) * 4);
       const int e = 2 * ((px >> 2) & 3);  // slot swizzle of this lane's pixel
-      int obase = C::OUT_OFF + (16 * wv + px) * C::PIXB;
+      int obase = C::OUT_OFF + (16 * strip + px) * C::PIXB;
       asm volatile("" : "+v"(obase));
-      const int o0 = ((0 + g) ^ e) * 8, o1 = ((4 + g) ^ e) * 8;
+      const int o0 = ((8 * mh + 0 + g) ^ e) * 8, o1 = ((8 * mh + 4 + g) ^ e) * 8;
       f32x4_t s1a = {0.f, 0.f, 0.f, 0.f}, s2a = s1a, s1b = s1a, s2b = s1a;
       // interior tiles (all but the frame's last row / column of tiles) take the select-free copy
       auto rows = [&](auto masked) {
@@ -259,7 +265,7 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
           *(u32x2_t*)(smem + obase + y * C::TW * C::PIXB + o1) = pb;
           f32x4_t xa = va, xb = vb;
           if constexpr (decltype(masked)::value) {
-            const bool valid = wk_.oy0 + y < p.oh && wk_.ox0 + 16 * wv + px < p.ow;
+            const bool valid = wk_.oy0 + y < p.oh && wk_.ox0 + 16 * strip + px < p.ow;
             const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
             xa = valid ? va : z;
             xb = valid ? vb : z;
@@ -342,7 +348,18 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
     if (wv == 0) {
       const float* pp = (const float*)(smem + C::PART_OFF);
       float t;
-      if constexpr (!SW) {
+      if constexpr (!SW && CO == 64) {
+        // 64 channels x 2 statistics: lane l sums value l of half 0 and of half 1 over the half's strips
+        const __amdgpu_buffer_rsrc_t prs2 = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * (2 * CO)), (short)0, 2 * CO * 4, 0x00020000);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float u = pp[(h * C::NSTRIP) * 64 + lane];
+#pragma unroll
+          for (int s2 = 1; s2 < C::NSTRIP; ++s2) u += pp[(h * C::NSTRIP + s2) * 64 + lane];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(u), prs2, (uint32_t)((64 * h + lane) * 4), 0, 0);
+        }
+      } else if constexpr (!SW) {
         t = pp[lane];
 #pragma unroll
         for (int w = 1; w < C::NW; ++w) t += pp[w * 64 + lane];
@@ -352,9 +369,11 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
 #pragma unroll
         for (int s2 = 1; s2 < C::NSTRIP; ++s2) t += pp[(h * C::NSTRIP + s2) * 64 + e];
       }
-      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * 64), (short)0, 256, 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (uint32_t)(lane * 4), 0, 0);
+      if constexpr (SW || CO == 32) {
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * 64), (short)0, 256, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (uint32_t)(lane * 4), 0, 0);
+      }
     }
     const size_t obytes = (size_t)p.oh * p.ow * C::PIXB;
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
@@ -397,9 +416,9 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   vm_wait<0>();
 }
 
-template <typename T, int NW, bool SW = false, bool O32 = false>
+template <typename T, int NW, bool SW = false, bool O32 = false, int CO = 32>
 struct Ws9Inst {
-  using C = W9Cfg<NW, SW, O32>;
+  using C = W9Cfg<NW, SW, O32, CO>;
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;
@@ -414,7 +433,7 @@ struct Ws9Inst {
     ConvParams p = p0;
     p.n_work = (int)grid.x * (int)grid.y;
     const int nb = std::min(p.n_work, cus() * (8 / NW));  // 8 waves per CU (VGPRs)
-    hipLaunchKernelGGL((ws9_kernel<T, NW, SW, O32>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((ws9_kernel<T, NW, SW, O32, CO>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
@@ -439,7 +458,10 @@ struct Ws9Inst {
 const ConvKernelInfo* conv_table_ws9(int* count) {
   static const ConvKernelInfo table[] = {Ws9Inst<__bf16, WS9_NW>::info(), Ws9Inst<_Float16, WS9_NW>::info(),
                                          Ws9Inst<_Float16, WS9_NW, true, true>::info(),
-                                         Ws9Inst<_Float16, WS9_NW, true, false>::info()};
+                                         Ws9Inst<_Float16, WS9_NW, true, false>::info(),
+                                         // ReCoNet's 9x9 first layer (48 channels padded to 64)
+                                         Ws9Inst<__bf16, WS9_NW, false, false, 64>::info(),
+                                         Ws9Inst<_Float16, WS9_NW, false, false, 64>::info()};
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;
 }

@@ -483,7 +483,21 @@ std::vector<float> pack_ws2_weights(const ConvKernelInfo& k, const LayerDef& d, 
 // fragments [j][m][lane][8 bf16], j = 0: kernel row 2 (l >> 4) + (i >> 2); j = 1: kernel row 8 in
 // lane group 0, elements 0..3 only; input channel i & 3.  (k.korder == 0: 6 16x16x16 fragments
 // [j][m][lane][4 bf16], kernel row 4 j + (l >> 4), input channel i.)
+// 64-channel kernels (k.bn == 64, ReCoNet): one such 32-channel set per channel half, half h = channels 32 h ..
 std::vector<float> pack_ws9_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
+  if (k.bn > 32) {
+    std::vector<float> all;
+    for (int h = 0; h < k.bn / 32; ++h) {
+      ConvKernelInfo kh = k;
+      kh.bn = 32;
+      LayerDef dh = d;
+      dh.cout = std::max(0, std::min(32, d.cout - 32 * h));
+      const std::vector<float> part =
+          dh.cout > 0 ? pack_ws9_weights(kh, dh, W + (size_t)32 * h * d.cin * 81) : pack_ws9_weights(kh, dh, W);
+      all.insert(all.end(), part.begin(), part.end());
+    }
+    return all;
+  }
   const bool pair = k.korder == 1;
   std::vector<float> out((size_t)18 * 64 * 8 + (pair ? 4 * 64 * 8 : 6 * 64 * 4), 0.f);
   auto w = [&](int co, int ci, int ky, int kx) -> float {
