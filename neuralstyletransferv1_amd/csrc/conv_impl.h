@@ -621,7 +621,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
     return (ro >= 0 && co >= 0) ? ro + co + c * 16 : -1;
   };
   // residual join fused into the fill (p.res_r): second source, optional residual-stream write of
-  // the tile's own pixels (plain stride-1 convs: those halo entries are the pixels themselves)
+  // the tile's own pixels (plain stride-1 convs: those halo entries are the pixels themselves); without a
+  // join, p.res_out receives the normalised input of those pixels (x_0 = ReLU(IN(C)) of block 1's conv1)
   constexpr bool CAN_RESOUT = MODE == MODE_STD && S == 1 && INK == IN_ACT;
   constexpr bool resf = INK == IN_ACT && (VAR & VAR_RES) != 0;
   const bool has_rn = p.res_rnorm != nullptr;
@@ -688,6 +689,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
             }
           } else {
             v = norm_chunk<T>(v, nmv);
+            if constexpr (CAN_RESOUT) {  // x_0 export (block 1's conv1): the normalised input of its own pixels
+              int ly, lx;
+              if (p.res_out != nullptr && entry_xy(e, ly, lx) && interior(wk, ly, lx))
+                *(uint4*)(rout + (unsigned)srcs[k]) = v;
+            }
           }
         }
         *(uint4*)(smem + e * EB + 16 * c) = lds_form<T>(v);
@@ -768,6 +774,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
               *(uint4*)(rout + (unsigned)(psrc[k] + 64 * q)) = v;
           } else {
             v = p.in_norm != nullptr ? norm_chunk<T>(praw[k], nm) : praw[k];
+            if (CAN_RESOUT && ((pint >> k) & 1u) && p.res_out != nullptr)  // x_0 export, as above
+              *(uint4*)(rout + (unsigned)(psrc[k] + 64 * q)) = v;
           }
         }
         *(uint4*)(smem + (it >> 2) * EB + (it & 3) * 16 + 64 * q) = lds_form<T>(v);

@@ -293,18 +293,26 @@ struct Out9Inst {
   }
 };
 
+// ReCoNet's 48 (64-padded) -> 3 output conv: strip groups G and waves NW (build-time, for sweeps)
+// (r04 sweep, 8 x 1080p: G 3 / NW 4 0.869 ms, G 2 / NW 4 0.800, G 2 / NW 6 0.686, G 1 / NW 8 0.643)
+#ifndef NST_OUT9_R_G
+#define NST_OUT9_R_G 1
+#endif
+#ifndef NST_OUT9_R_NW
+#define NST_OUT9_R_NW 8
+#endif
 #define E(...) Out9Inst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_out9(int* count) {
   static const ConvKernelInfo table[] = {
       //  T     CINP G NW OUT          TANH
       E(__bf16, 32, 3, 8, OUT_U8_NHWC, false),    // Johnson deconv3 / NST final (frames)
       E(__bf16, 32, 3, 8, OUT_F32_NCHW, false),   // tensor API
-      E(__bf16, 64, 3, 4, OUT_U8_NHWC, true),     // ReCoNet (48 channels, bf16 padded to 64; tanh output)
-      E(__bf16, 64, 3, 4, OUT_F32_NCHW, true),
+      E(__bf16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_U8_NHWC, true),   // ReCoNet (48 channels, padded to 64; tanh)
+      E(__bf16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_F32_NCHW, true),
       E(_Float16, 32, 3, 8, OUT_U8_NHWC, false),  // fp16 mode
       E(_Float16, 32, 3, 8, OUT_F32_NCHW, false),
-      E(_Float16, 64, 3, 4, OUT_U8_NHWC, true),
-      E(_Float16, 64, 3, 4, OUT_F32_NCHW, true),
+      E(_Float16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_U8_NHWC, true),
+      E(_Float16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_F32_NCHW, true),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

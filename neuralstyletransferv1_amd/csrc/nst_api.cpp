@@ -1086,7 +1086,9 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
   }
   // x_0 export needs block 1's conv1 on the weight-stationary kernel; otherwise block 2's join
   // normalises conv3's output itself (the same layers and residual layers either way)
-  if (fuse_res && !f16m && h->layers[3].mode != MODE_WSTAT) build_program(arch, true, false, defs, h->prog);
+  // x_0 export: the weight-stationary trunk kernel and the generic stride-1 kernel write it from their fill
+  if (fuse_res && !f16m && h->layers[3].mode != MODE_WSTAT && h->layers[3].mode != MODE_STD)
+    build_program(arch, true, false, defs, h->prog);
   *out = h;
   return NST_OK;
 }
@@ -1272,8 +1274,10 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     p.cout_stride = Ly.coutp;
     tile_grid(*k, p.hs, p.ws, p.oh, p.ow, &p.tiles_x, &p.tiles_y);
     p.n_cblk = Ly.coutp / k->bn;
-    if (p.res_out != nullptr && p.res_r == nullptr && (Ly.mode != MODE_WSTAT || p.in_norm == nullptr)) {
-      set_error("conv " + Ly.d.conv + ": only the weight-stationary trunk kernel writes its normalised input");
+    if (p.res_out != nullptr && p.res_r == nullptr &&
+        ((Ly.mode != MODE_WSTAT && Ly.mode != MODE_STD) || p.in_norm == nullptr || Ly.d.stride != 1)) {
+      set_error("conv " + Ly.d.conv + ": only the trunk kernels (weight-stationary / generic stride-1) write their "
+                "normalised input");
       return NST_E_SHAPE;
     }
     if (Ly.mode == MODE_WSTAT && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out == nullptr || p.res_relu)) {

@@ -195,7 +195,8 @@ def check_layers(net, frames_u8: np.ndarray, preset: str, bands: Optional[Sequen
                     for q in bad[:6].tolist():
                         b_, c_, y_, x_ = q
                         ex.append({"at": q, "got": float(got[b_, c_, y_, x_]), "want": float(joined[b_, c_, y_, x_]),
-                                   "y": float(ysrc[b_, c_, y_, x_]), "r": float(r[b_, c_, y_, x_]),
+                                   "y": float(ysrc[b_, c_, y_, x_]),
+                                   "r": None if r is None else float(r[b_, c_, y_, x_]),
                                    "ys": ys[b_, c_].tolist(), "rs": None if rs is None else rs[b_, c_].tolist()})
                     raise AssertionError(f"op {i} ({conv}): joined residual stream differs at {bad.shape[0]} of "
                                          f"{got.numel()} values (nan got {int(got.isnan().sum())} want "
