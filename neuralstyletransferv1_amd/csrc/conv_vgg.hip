@@ -18,6 +18,22 @@
 #define NST_VGG_TB1 8, 32, 4, 1  // conv1_1 backward (-> the image gradient)
 #endif
 
+#ifndef NST_VGG_T21
+#define NST_VGG_T21 8, 16, 2, 2  // conv2_1 forward (64 -> 128)
+#endif
+#ifndef NST_VGG_T22
+#define NST_VGG_T22 8, 16, 2, 2  // 128 -> 128
+#endif
+#ifndef NST_VGG_T3
+#define NST_VGG_T3 8, 16, 2, 2  // 256 input channels
+#endif
+#ifndef NST_VGG_T4
+#define NST_VGG_T4 4, 16, 2, 2  // 512 input channels
+#endif
+#ifndef NST_VGG_TB2
+#define NST_VGG_TB2 8, 16, 2, 2  // conv2_1 backward (128 -> 64)
+#endif
+
 namespace nst {
 typedef __bf16 B;
 #define E(...) ConvInst<__VA_ARGS__>::info()
@@ -28,12 +44,12 @@ const ConvKernelInfo* conv_table_vgg(int* count) {
       // forward
       E(B, SD, 3, 1, 4, 64, NST_VGG_T11, IN_F32_NCHW, OUT_ACT),   // conv1_1 (normalised image)
       E(B, SD, 3, 1, 64, 64, NST_VGG_T12, IN_ACT, OUT_ACT),       // conv1_2
-      E(B, SD, 3, 1, 64, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),      // conv2_1
-      E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // conv2_2, conv3_1 (2 channel blocks); backward 2_2
-      E(B, SD, 3, 1, 256, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT),     // conv3_2..3_4, conv4_1; backward 3_1..3_4
-      E(B, SD, 3, 1, 512, 128, 4, 16, 2, 2, IN_ACT, OUT_ACT),     // conv4_2..5_1; backward 4_1..5_1
+      E(B, SD, 3, 1, 64, 128, NST_VGG_T21, IN_ACT, OUT_ACT),      // conv2_1
+      E(B, SD, 3, 1, 128, 128, NST_VGG_T22, IN_ACT, OUT_ACT),     // conv2_2, conv3_1 (2 channel blocks); backward 2_2
+      E(B, SD, 3, 1, 256, 128, NST_VGG_T3, IN_ACT, OUT_ACT),     // conv3_2..3_4, conv4_1; backward 3_1..3_4
+      E(B, SD, 3, 1, 512, 128, NST_VGG_T4, IN_ACT, OUT_ACT),     // conv4_2..5_1; backward 4_1..5_1
       // backward
-      E(B, SD, 3, 1, 128, 64, 8, 16, 2, 2, IN_ACT, OUT_ACT),      // conv2_1 -> 64 input channels
+      E(B, SD, 3, 1, 128, 64, NST_VGG_TB2, IN_ACT, OUT_ACT),      // conv2_1 -> 64 input channels
       E(B, SD, 3, 1, 64, 16, NST_VGG_TB1, IN_ACT, OUT_F32_NCHW),  // conv1_1 -> the image gradient (3 of 16)
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));

@@ -219,6 +219,7 @@ size_t gram_workspace_bytes(int n, int c, int hw);
 // The Gatys style term fused into the Gram's reduce pass: Mb = bf16(k (G - A)) and loss_out = sum (G - A)^2
 // (per-block partials in `parts`, <= GRAM_DELTA_MAX_PARTS = c*c/64 of them, summed in block order)
 constexpr int GRAM_DELTA_MAX_PARTS = 512 * 512 / 64;
+int gram_delta_parts(int n, int c, int hw);  // how many `parts` launch_gram's reduce writes
 struct GramDelta {
   const float* A;
   float k;

@@ -3,6 +3,7 @@
 // All fp32 elementwise arithmetic is written op-by-op in the reference's order and the
 // library is built with -ffp-contract=off, so no FMA contraction changes a rounding.
 #include <algorithm>
+#include <cstdlib>
 
 #include "nst_internal.h"
 #include "seg_internal.h"
@@ -1025,11 +1026,91 @@ __global__ __launch_bounds__(1024) void gram_reduce_kernel(const float* __restri
   }
 }
 
+// The float4 form (n c^2 % 4 == 0 and 16-byte aligned buffers: every VGG style layer).  A 256-thread block is
+// G slice groups x L = 256 / G lanes, each lane owning 4 consecutive entries; group g sums its contiguous share of
+// the slices with four interleaved accumulators, the G group sums are added in group order.  The host sizes G so
+// that a thread reads at most 8 (16 at G = 32) slices: the 1024-thread, 64-entry blocks of gram_reduce_kernel
+// left 12 of 16 groups idle at 4 slices and launched 4,096 blocks for a c = 512 Gram (11.7-13.9 us for 4-16 MiB)
+template <int G, bool DELTA>
+__global__ __launch_bounds__(256) void gram_reduce4_kernel(const float4* part, int slices, size_t n4,
+                                                           float denom, float4* Gout, GramDelta gd) {
+  constexpr int L = 256 / G;
+  __shared__ float4 red[G > 1 ? G : 1][L];
+  __shared__ float wsum[4];
+  const int lane = threadIdx.x % L, grp = threadIdx.x / L;
+  const size_t e = (size_t)blockIdx.x * L + lane;
+  const int per = (slices + G - 1) / G;
+  const int s0 = grp * per, s1 = min(slices, s0 + per);
+  float4 a[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n4) {
+    int s = s0;
+#pragma unroll 2
+    for (; s + 4 <= s1; s += 4) {
+      float4 x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = part[(size_t)(s + j) * n4 + e];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += x[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j)  // the tail (static indices: a dynamic a[j] would live in scratch)
+      if (s + j < s1) a[j] += part[(size_t)(s + j) * n4 + e];
+  }
+  float4 t = (a[0] + a[1]) + (a[2] + a[3]);
+  if constexpr (G > 1) {
+    red[grp][lane] = t;
+    __syncthreads();
+    if (grp == 0) {
+      t = red[0][lane];
+#pragma unroll 4
+      for (int g = 1; g < G; ++g) t += red[g][lane];
+    }
+  }
+  float d2 = 0.f;
+  if (grp == 0 && e < n4) {
+    const float4 gv = make_float4(t.x / denom, t.y / denom, t.z / denom, t.w / denom);
+    Gout[e] = gv;
+    if constexpr (DELTA) {
+      const float4 av = ((const float4*)gd.A)[e];
+      const float d[4] = {gv.x - av.x, gv.y - av.y, gv.z - av.z, gv.w - av.w};
+      __bf16 m[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        m[j] = (__bf16)(gd.k * d[j]);
+        d2 += d[j] * d[j];
+      }
+      *(uint2*)(gd.Mb + 4 * e) = __builtin_bit_cast(uint2, m);
+    }
+  }
+  if constexpr (DELTA) {
+    // fixed-order tree: xor within each wave, then the 4 wave sums in wave order
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) d2 = d2 + __shfl_xor(d2, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = d2;
+    __syncthreads();
+    if (threadIdx.x == 0) gd.parts[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+  }
+}
+
 namespace {
 struct GramPlan {
   int ti, tt, slices, kslice;
   size_t ws_bytes;
 };
+// the float4 reduce's slice groups per block (0: the scalar gram_reduce_kernel)
+int gram_reduce_groups(size_t slice, int slices) {
+  if (slice % 4) return 0;
+  int G = 1;
+  while (G < 32 && (slices + G - 1) / G > 8) G *= 2;
+  while (G > 1 && (slice / 4 + 256 / G - 1) / (256 / G) > (size_t)GRAM_DELTA_MAX_PARTS) G /= 2;
+  return G;
+}
+size_t gram_reduce_blocks(size_t slice, int slices) {
+  const int G = gram_reduce_groups(slice, slices);
+  return G ? (slice / 4 + 256 / G - 1) / (256 / G) : (slice + 63) / 64;
+}
 GramPlan gram_plan(int n, int c, int hw) {
   GramPlan g;
   // 128-channel tiles above 64 channels: the 256 tile left a c = 512 Gram with 4 output tiles, so all of its
@@ -1040,7 +1121,11 @@ GramPlan gram_plan(int n, int c, int hw) {
   const int fills = (hw + 63) / 64;
   // enough K slices to fill the chip (~512 workgroups), but their fp32 partials (c*c*4 B each) no more than
   // four times the bytes of F (bf16) itself: beyond that the split-K traffic costs more than it buys
-  const int cap = std::max(1, (int)(((size_t)4 * 2 * hw) / ((size_t)4 * c)));
+  static const int capx = [] {
+    const char* e = std::getenv("NST_GRAM_CAP");  // tuning sweeps only
+    return e ? std::max(1, std::atoi(e)) : 4;
+  }();
+  const int cap = std::max(1, (int)(((size_t)capx * 2 * hw) / ((size_t)4 * c)));
   g.slices = std::max(1, std::min(std::min(fills, cap), (512 + blocks - 1) / blocks));
   g.kslice = ((fills + g.slices - 1) / g.slices) * 64;
   g.slices = (hw + g.kslice - 1) / g.kslice;
@@ -1050,6 +1135,10 @@ GramPlan gram_plan(int n, int c, int hw) {
 }  // namespace
 
 size_t gram_workspace_bytes(int n, int c, int hw) { return gram_plan(n, c, hw).ws_bytes; }
+
+int gram_delta_parts(int n, int c, int hw) {
+  return (int)gram_reduce_blocks((size_t)n * c * c, gram_plan(n, c, hw).slices);
+}
 
 hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, int hw, float* G, void* ws,
                        hipStream_t st, int relu, const GramDelta* delta) {
@@ -1086,9 +1175,31 @@ hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, i
 #undef NST_GRAM_GO
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const unsigned nb = (unsigned)((slice + 63) / 64);
+  auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  const int rg = (al16(dst) && al16(G) && (!delta || (al16(delta->A) && ((uintptr_t)delta->Mb & 7) == 0)))
+                     ? gram_reduce_groups(slice, g.slices) : 0;
+  const unsigned nb = (unsigned)(rg ? gram_reduce_blocks(slice, g.slices) : (slice + 63) / 64);
+  if (delta && nb > (unsigned)GRAM_DELTA_MAX_PARTS) return hipErrorInvalidValue;
+  if (rg) {
+#define NST_GRED4(GG)                                                                                          \
+  case GG:                                                                                                     \
+    if (delta)                                                                                                 \
+      hipLaunchKernelGGL((gram_reduce4_kernel<GG, true>), dim3(nb), dim3(256), 0, st, (const float4*)dst,     \
+                         g.slices, slice / 4, denom, (float4*)G, *delta);                                      \
+    else                                                                                                       \
+      hipLaunchKernelGGL((gram_reduce4_kernel<GG, false>), dim3(nb), dim3(256), 0, st, (const float4*)dst,    \
+                         g.slices, slice / 4, denom, (float4*)G, GramDelta{});                                 \
+    break;
+    switch (rg) {
+      NST_GRED4(1) NST_GRED4(2) NST_GRED4(4) NST_GRED4(8) NST_GRED4(16) NST_GRED4(32)
+      default: return hipErrorInvalidValue;
+    }
+#undef NST_GRED4
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return delta && delta->loss_out ? launch_vgg_sum_parts(delta->parts, (int)nb, delta->loss_out, st) : hipSuccess;
+  }
   if (delta) {
-    if (nb > (unsigned)GRAM_DELTA_MAX_PARTS) return hipErrorInvalidValue;
     hipLaunchKernelGGL(gram_reduce_kernel<true>, dim3(nb), dim3(1024), 0, st, dst, g.slices, slice, denom, G, *delta);
     e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -438,7 +438,7 @@ int gatys_grad_impl(nst_vgg* v, const float* image, int h, int w, const float* s
     // partials per layer, summed by the loss kernel below (one launch for the five layers)
     const GramDelta gd{(const float*)(sp + P.sA[l]), (float)k, (__bf16*)(ws + P.M[l]),
                        (float*)(ws + P.spart) + (size_t)l * GRAM_DELTA_MAX_PARTS, nullptr};
-    snparts[l] = (int)(((size_t)c * c + 63) / 64);  // launch_gram's reduce blocks
+    snparts[l] = gram_delta_parts(1, c, hw);  // launch_gram's reduce blocks
     VGG_CHECK(launch_gram(ws + P.z[i], NST_DT_BF16, 1, 1, c, hw, (float*)(ws + P.gram[l]), ws + P.gram_ws, st, 1, &gd));
     sscale[l] = (float)(style_weight * wl / ((double)c * c));
   }

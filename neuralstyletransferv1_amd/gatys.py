@@ -148,15 +148,27 @@ class Gatys:
              style_layer_weights: Sequence[float] = (1.0,) * 5) -> Tuple[torch.Tensor, torch.Tensor]:
         """-> (dL/d normalised image [1,3,h,w] fp32, losses [total, content, style] fp32 on device)."""
         image = self._image(image)
+        g = torch.empty_like(image)
+        self._grad_into(image, g, self.losses_for(image), content_weight, style_weight, style_layer_weights)
+        return g, self.losses[:3].clone()
+
+    def losses_for(self, image: torch.Tensor) -> torch.Tensor:
+        self._workspace(image.shape[2], image.shape[3])
+        return self.losses
+
+    def _grad_into(self, image: torch.Tensor, g: torch.Tensor, losses: torch.Tensor, content_weight: float,
+                   style_weight: float, style_layer_weights: Sequence[float]) -> None:
+        """nst_gatys_grad into caller-owned buffers: g ([1,3,h,w] fp32) and losses (3 contiguous fp32 on the
+        device), so the optimisation loop writes each step's losses straight into its trajectory row."""
         _, _, hgt, wid = image.shape
         stt = self._targets(hgt, wid)
         ws = self._workspace(hgt, wid)
-        g = torch.empty_like(image)
+        if losses.dtype != torch.float32 or losses.numel() < 3 or not losses.is_contiguous():
+            raise NstError("losses: 3 contiguous fp32 values")
         wl = (ctypes.c_float * 5)(*[float(v) for v in style_layer_weights])
         check(lib().nst_gatys_grad(self._h, image.data_ptr(), hgt, wid, wl, float(content_weight), float(style_weight),
-                                   stt.data_ptr(), g.data_ptr(), self.losses.data_ptr(), ws.data_ptr(), ws.numel(),
+                                   stt.data_ptr(), g.data_ptr(), losses.data_ptr(), ws.data_ptr(), ws.numel(),
                                    _lib.stream_ptr(self.device)), "nst_gatys_grad")
-        return g, self.losses[:3].clone()
 
     def grad_capture(self, image: torch.Tensor, content_weight: float = 1.0, style_weight: float = 1e6,
                      style_layer_weights: Sequence[float] = (1.0,) * 5):
@@ -199,15 +211,16 @@ class Gatys:
         x = (content if init is None else init).detach().to(self.device, torch.float32).clone().contiguous()
         m, v = torch.zeros_like(x), torch.zeros_like(x)
         hist = []
-        traj = None
+        g = torch.empty_like(x)
+        losses = self.losses_for(x)
+        traj = torch.empty((steps, 3), dtype=torch.float32, device=self.device) if trajectory else None
+        sw = (1.0,) * 5
         for t in range(1, steps + 1):
-            g, losses = self.grad(x, content_weight, style_weight)
-            if trajectory:
-                if traj is None:
-                    traj = torch.empty((steps, losses.numel()), dtype=losses.dtype, device=losses.device)
-                traj[t - 1].copy_(losses)
-            elif record_every and (t == 1 or t % record_every == 0):
-                hist.append((t - 1,) + tuple(float(z) for z in losses.cpu()))
+            # the trajectory row is the losses buffer itself: no copy launch per step
+            out = traj[t - 1] if trajectory else losses
+            self._grad_into(x, g, out, content_weight, style_weight, sw)
+            if not trajectory and record_every and (t == 1 or t % record_every == 0):
+                hist.append((t - 1,) + tuple(float(z) for z in out[:3].cpu()))
             self.adam(x, g, m, v, t, lr)
         if traj is not None:
             hist = [(i,) + tuple(float(z) for z in row) for i, row in enumerate(traj.cpu())]
