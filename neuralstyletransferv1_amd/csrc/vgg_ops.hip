@@ -7,6 +7,7 @@
 // The reference has no VGG / Gatys loop; the pieces follow the usual definitions:
 // torchvision VGG-19 features (conv3x3 + ReLU, MaxPool2d(2)), Gram = utils.py:80-83, MSE losses,
 // torch.optim.Adam's update rule.
+#include <cstdlib>
 #include <algorithm>
 
 #include "nst_internal.h"
@@ -173,6 +174,86 @@ __global__ __launch_bounds__(256) void vgg_gram_bwd_kernel(const __bf16* __restr
   }
 }
 
+// The same product with ReLU(z) staged once per workgroup in LDS: wave w owns channels i0 + 16w .. +15 for all 64
+// pixels (4 pixel subtiles), reading its 16 rows of M straight from memory and the 64 pixels from LDS.  The form
+// above reads the workgroup's 64 rows of M in every wave (4x the M traffic: 64 KiB per wave at C = 512) and leaves
+// each lane one dependent load chain per K step; here each M row is read once per workgroup.  Same products, same
+// K order per output: bit-identical results
+template <int C>
+__global__ __launch_bounds__(256) void vgg_gram_bwd_lds_kernel(const __bf16* __restrict__ z, const __bf16* __restrict__ ga,
+                                                               const __bf16* __restrict__ P, float cw,
+                                                               const __bf16* __restrict__ Mb, int hw,
+                                                               __bf16* __restrict__ gz) {
+  constexpr int ZS = C * 2 + 16;  // bytes per staged pixel row (16-B pad: a 16-lane group's rows spread over banks)
+  constexpr int TP = 64 + 4;      // floats per pixel row of the product tile (aliases the staged rows)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int i0 = blockIdx.y * 64;
+  constexpr int CQ = C / 8;  // 16-B chunks per pixel
+#pragma unroll
+  for (int it = 0; it < 64 * CQ / 256; ++it) {
+    const int q = it * 256 + threadIdx.x;
+    const int pl = q / CQ, cq = q - pl * CQ;
+    const int p = blockIdx.x * 64 + pl;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (p < hw) {
+      float f[8];
+      unpack8(*(const uint4*)(z + (size_t)p * C + 8 * cq), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+      v = pack8(f);
+    }
+    *(uint4*)(smem + pl * ZS + 16 * cq) = v;
+  }
+  __syncthreads();
+  f32x4_t acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const __bf16* mrow = Mb + (size_t)(i0 + 16 * wv + col) * C + 8 * g;
+#pragma unroll
+  for (int k = 0; k < C; k += 32) {
+    const uint4 a = *(const uint4*)(mrow + k);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint4 b = *(const uint4*)(smem + (16 * t + col) * ZS + (k + 8 * g) * 2);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                       acc[t], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // the staged rows are dead: the product tile reuses the space
+  float* tile = (float*)smem;
+  // D[4g + r][col] of subtile t: channel i0 + 16 wv + 4g + r of pixel 16t + col
+#pragma unroll
+  for (int t = 0; t < 4; ++t) *(f32x4_t*)(tile + (16 * t + col) * TP + 16 * wv + 4 * g) = acc[t];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = k * 256 + threadIdx.x;  // 64 pixels x 8 chunks of 8 channels
+    const int pl = q >> 3, cq = q & 7;
+    const int p = blockIdx.x * 64 + pl;
+    if (p >= hw) continue;
+    const size_t o = (size_t)p * C + i0 + 8 * cq;
+    float zv[8], gv[8], pv[8], o8[8];
+    unpack8(*(const uint4*)(z + o), zv);
+    if (ga) unpack8(*(const uint4*)(ga + o), gv);
+    if (P) unpack8(*(const uint4*)(P + o), pv);
+    const f32x4_t m0 = *(const f32x4_t*)(tile + pl * TP + 8 * cq), m1 = *(const f32x4_t*)(tile + pl * TP + 8 * cq + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = j < 4 ? m0[j] : m1[j - 4];
+      if (ga) v = v + gv[j];
+      if (P) v = v + cw * (fmaxf(zv[j], 0.f) - pv[j]);
+      o8[j] = zv[j] > 0.f ? v : 0.f;
+    }
+    *(uint4*)(gz + o) = pack8(o8);
+  }
+}
+template <int C>
+constexpr size_t gram_bwd_lds_bytes() {
+  return std::max((size_t)64 * (C * 2 + 16), (size_t)64 * 68 * 4);
+}
+
 // ---- block partials summed in block order (deterministic): the style loss (gram_reduce_kernel<true>) and the
 // content loss ----
 __global__ __launch_bounds__(256) void vgg_sum_parts_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
@@ -301,6 +382,26 @@ hipError_t launch_vgg_gram_bwd(const void* z, const void* ga, const void* P, flo
   const dim3 grid((unsigned)((hw + 63) / 64), (unsigned)(c / 64));
   const __bf16 *zz = (const __bf16*)z, *gg = (const __bf16*)ga, *pp = (const __bf16*)P, *mm = (const __bf16*)Mb;
   __bf16* out = (__bf16*)gz;
+  static const bool lds = [] {
+    const char* e = std::getenv("NST_GRAM_BWD_LDS");  // A/B switch: 0 = the register form
+    return !e || std::atoi(e) != 0;
+  }();
+#define NST_GBWD_LDS(CC)                                                                                        \
+  case CC: {                                                                                                    \
+    static const hipError_t attr = hipFuncSetAttribute((const void*)vgg_gram_bwd_lds_kernel<CC>,               \
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+    (void)attr;                                                                                                 \
+    hipLaunchKernelGGL(vgg_gram_bwd_lds_kernel<CC>, grid, dim3(256), gram_bwd_lds_bytes<CC>(), st, zz, gg, pp, cw, \
+                       mm, hw, out);                                                                            \
+    return hipGetLastError();                                                                                   \
+  }
+  if (lds) {
+    switch (c) {
+      NST_GBWD_LDS(64) NST_GBWD_LDS(128) NST_GBWD_LDS(256) NST_GBWD_LDS(512)
+      default: return hipErrorInvalidValue;
+    }
+  }
+#undef NST_GBWD_LDS
   switch (c) {
     case 64: hipLaunchKernelGGL(vgg_gram_bwd_kernel<64>, grid, dim3(256), 0, st, zz, gg, pp, cw, mm, hw, out); break;
     case 128: hipLaunchKernelGGL(vgg_gram_bwd_kernel<128>, grid, dim3(256), 0, st, zz, gg, pp, cw, mm, hw, out); break;
