@@ -109,6 +109,26 @@ def main():
                 "mask_share": round(res[MASK_DT] / ms, 3),
                 # the step with each mask dtype: its mask time / (that + the rest of the step)
                 "mask_share_by_dtype": {d: round(t / (ms - res[MASK_DT] + t), 3) for d, t in res.items()}})
+    # the same step with the mask program on a second HIP stream beside the stylization (independent until the
+    # composite): DeepLab's small GEMMs leave most CUs idle, and the stylization's kernels fill them
+    side = torch.cuda.Stream(dev)
+
+    def step_overlap():
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            m = me.masks(frames, ids, feather_px=3)
+        st = eng.stylize_u8(frames, "imagenet_255")
+        torch.cuda.current_stream(dev).wait_stream(side)
+        m.record_stream(torch.cuda.current_stream(dev))
+        return blend_frames(st, frames, 1.0, m, "keep")
+    ref_out = step()
+    ov_out = step_overlap()
+    torch.cuda.synchronize(dev)
+    ov_ms = timed(step_overlap, STEPS)
+    out.update({"step_ms_overlap": round(ov_ms, 3), "frames_per_s_overlap": round(N / ov_ms * 1e3, 1),
+                # the part of the overlapped step the mask adds beyond the stylization alone
+                "mask_exposed_share_overlap": round(max(0.0, ov_ms - styl_ms) / ov_ms, 3),
+                "overlap_identical": bool(torch.equal(ref_out, ov_out))})
     if os.environ.get("SEG_GRAPH", "0") == "1":
         # launch-overhead probe: the mask program (MASK_DT) replayed from a captured HIP graph (static input / output
         # buffers); the captured kernels are the same launches on the same stream
