@@ -12,7 +12,7 @@
 #define NST_D1_TILE 4, 16, 1, 4
 #define NST_D2_TILE 4, 16, 1, 4
 #ifndef NST_R_UP1_TILE
-#define NST_R_UP1_TILE 4, 32, 1, 4  // ReCoNet 192 -> 96 up-conv (phases): 2.24 -> 1.61 ms per batch of 8 vs 2 x 16
+#define NST_R_UP1_TILE 8, 16, 1, 4  // ReCoNet 192 -> 96 up-conv (phases): 8 x 16 tiles 1 % ahead of 4 x 32 after the keep-live change (r04); 2.24 -> 1.61 ms per batch of 8 vs 2 x 16 (r03)
 #endif
 #ifndef NST_R_TRUNK_TILE
 #define NST_R_TRUNK_TILE 16, 16, 2, 4  // ReCoNet 192-channel trunk: 8 waves (2 x 4: 8 x 3 accumulator sub-tiles each,

@@ -14,7 +14,7 @@ Restated per stage (per pyramid level, coarsest -> finest):
                    16, Sobel 3x3 gradients of I0 (spatialGradient, int16, BORDER_REFLECT_101)
   structure tensor separable running box sums of Ix^2, Iy^2, IxIy, Ix, Iy over every 8x8 patch (fp32, cv2's
                    running-sum order)
-  inverse search   8 stripes of patch rows, each a forward and a backward sweep (4 + 4 inner iterations); per
+  inverse search   8 stripes of patch rows, each a forward and a backward sweep (8 + 8 inner iterations); per
                    patch: the flow at the patch centre (first sweep), the left / upper neighbour candidates
                    by mean-normalised SSD, then inverse-compositional Gauss-Newton steps with the inverted
                    structure tensor, stopping when the SSD stops falling; a result farther than 8 px from the
