@@ -7,17 +7,19 @@
 // Tile shapes (TH, TW, WM, WN) of the Johnson/NST layers; overridable at build time for tile sweeps.
 // Trunk 8x16 tiles on 8 waves (2x4) and 8-row up-conv / output tiles: r03 sweep of the split-fp16 mode
 // (tools/mode_profile.py), 221 -> 297 frames/s over the 4x16-tile shapes the fp32 mode started with
+// r04: the down-convs and the trunk on waves of 16 output channels over the whole tile (WM = 1; the Gatys VGG
+// finding): split-fp16 conv2 2.37 -> 1.01 ms, conv3 1.15 -> 0.72, trunk 1.05 -> 1.02 per batch of 8
 #ifndef NST_T32_C1
 #define NST_T32_C1 8, 32, 4, 1
 #endif
 #ifndef NST_T32_C2
-#define NST_T32_C2 4, 16, 4, 1
+#define NST_T32_C2 4, 16, 1, 4
 #endif
 #ifndef NST_T32_C3
-#define NST_T32_C3 4, 16, 2, 2
+#define NST_T32_C3 8, 16, 1, 8
 #endif
 #ifndef NST_T32_RES
-#define NST_T32_RES 8, 16, 2, 4
+#define NST_T32_RES 8, 16, 1, 8
 #endif
 #ifndef NST_T32_D1
 #define NST_T32_D1 8, 16, 1, 4
