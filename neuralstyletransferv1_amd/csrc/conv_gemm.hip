@@ -658,6 +658,20 @@ int gemm_t256() {
   }();
   return v;
 }
+// register-staged 64 x 64 tiles: split K while there are fewer than reg_tiles() tiles, to about reg_target()
+// workgroups (sweep overrides NST_GEMM_REG_TILES / NST_GEMM_REG_TARGET; defaults 240 / 480)
+int gemm_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+int reg_tiles() {
+  static const int v = gemm_env("NST_GEMM_REG_TILES", 240);
+  return v;
+}
+int reg_target() {
+  static const int v = gemm_env("NST_GEMM_REG_TARGET", 480);
+  return v;
+}
 struct GemmShape {
   int kind;
   int ksplit;
@@ -701,8 +715,8 @@ GemmShape gemm_shape(int dtype, const GemmConvParams& p) {
   }
   // fewer 64x64 tiles than a wave of the chip and a long K loop: split K (at most 8 slices)
   const long tiles = (long)((p.npix + 63) / 64) * ((p.cout_store + 63) / 64);
-  if (tiles < 240 && nstage >= 16) {
-    long k = (480 + tiles - 1) / tiles;
+  if (tiles < reg_tiles() && nstage >= 16) {
+    long k = (reg_target() + tiles - 1) / tiles;
     k = std::min<long>(k, std::min<long>(8, nstage / 8));
     g.ksplit = (int)std::max<long>(k, 1);
   }
