@@ -301,11 +301,17 @@ struct Out9Inst {
 #ifndef NST_OUT9_R_NW
 #define NST_OUT9_R_NW 8
 #endif
+#ifndef NST_OUT9_J_G
+#define NST_OUT9_J_G 3
+#endif
+#ifndef NST_OUT9_J_NW
+#define NST_OUT9_J_NW 8
+#endif
 #define E(...) Out9Inst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_out9(int* count) {
   static const ConvKernelInfo table[] = {
       //  T     CINP G NW OUT          TANH
-      E(__bf16, 32, 3, 8, OUT_U8_NHWC, false),    // Johnson deconv3 / NST final (frames)
+      E(__bf16, 32, NST_OUT9_J_G, NST_OUT9_J_NW, OUT_U8_NHWC, false),    // Johnson deconv3 / NST final (frames)
       E(__bf16, 32, 3, 8, OUT_F32_NCHW, false),   // tensor API
       E(__bf16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_U8_NHWC, true),   // ReCoNet (48 channels, padded to 64; tanh)
       E(__bf16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_F32_NCHW, true),
