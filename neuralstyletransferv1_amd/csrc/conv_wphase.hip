@@ -478,7 +478,10 @@ struct WphaseInst {
   }
 };
 
-constexpr int WP1_TH = 4;  // 128 -> 64: 8 rows spill (128 weight + 64 accumulator VGPRs); 4 leaves LDS room for the staged output tile
+#ifndef NST_WP1_TH
+#define NST_WP1_TH 4
+#endif
+constexpr int WP1_TH = NST_WP1_TH;  // 128 -> 64: 8 rows spill (6 rows too: 40-52 B of scratch per lane, r04) (128 weight + 64 accumulator VGPRs); 4 leaves LDS room for the staged output tile
 constexpr int WP1_NF = 8;  // frames per launch (IN tables in LDS)
 #define E(...) WphaseInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wphase(int* count) {
