@@ -24,6 +24,9 @@
 namespace nst {
 
 constexpr int WP_RING = 3;  // operand reads in flight ahead of the MFMAs
+#ifndef NST_WP_PAIR
+#define NST_WP_PAIR 1
+#endif
 
 template <int CINP, int COUT, int TH, int NF, int SW = 2>
 struct WpCfg {  // SW: staged tensors per unit (2: the residual join's y and r, 1: y)
@@ -147,7 +150,12 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
       }
     }
   };
-  const int ebase = (wv & 3) * C::QENT + lane;
+  // paired units (four parts, at most 32 halo entries per wave and unit): lanes 0-31 stage / consume unit 2p and
+  // lanes 32-63 unit 2p + 1, i.e. both 16-channel halves of part p in one request and one consume pass (54 of
+  // 64 lanes busy at QENT = 27 instead of 27 of 64: deconv1's fill was VALU-issue-bound on the idle lanes)
+  constexpr bool PR = NST_WP_PAIR && C::NPART == 4 && C::QENT <= 32;
+  const int plane = PR ? (lane & 31) : lane, phalf = PR ? (lane >> 5) : 0;
+  const int ebase = (wv & 3) * C::QENT + plane;
   struct Item {
     int src;
     bool valid;
@@ -156,7 +164,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     const int* rowmap = (const int*)(smem + C::MAP_OFF + slot * C::MAPB);
     const int* colmap = rowmap + C::LH;
     Item it;
-    it.valid = lane < C::QENT;
+    it.valid = plane < C::QENT;
     const int e = it.valid ? ebase : 0;
     const int ly = e / C::LW, lx = e - ly * C::LW;
     const int ro = rowmap[ly], co = colmap[lx];
@@ -171,9 +179,19 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     dma16(rs_in, voff, lds, soff);
     if constexpr (RES) dma16(rs_r, voff, lds + C::NW * 1024, soff);
   };
-  auto consume = [&](const Work& wk, int u, const Item& it) {
+  // part pp of the paired form: units 2pp (lanes 0-31) and 2pp + 1 (lanes 32-63), staging slot pp % 2
+  auto request_p = [&](int n, int pp, const Item& it) {
+    const uint32_t voff =
+        (it.valid && it.src >= 0) ? (uint32_t)it.src + (uint32_t)n * fb + 32u * (uint32_t)phalf : 0x80000000u;
+    const int soff = (4 * pp + team) * 16;
+    const uint32_t lds = stg + (pp % 2) * C::SLOTB;
+    dma16(rs_in, voff, lds, soff);
+    if constexpr (RES) dma16(rs_r, voff, lds + C::NW * 1024, soff);
+  };
+  // unit u (this lane's; chunk 2u + team) from staging slot `slot`
+  auto consume_s = [&](const Work& wk, int u, int slot, const Item& it) {
     const int ch = 2 * u + team;
-    const char* sp = smem + C::STG_OFF + (u % C::NSLOT) * C::SLOTB + (wv * 64 + lane) * 16;
+    const char* sp = smem + C::STG_OFF + slot * C::SLOTB + (wv * 64 + lane) * 16;
     const uint4 y = *(const uint4*)sp;
     const uint4 rr = RES ? *(const uint4*)(sp + C::NW * 1024) : make_uint4(0u, 0u, 0u, 0u);
     const float* ny = norm_y + (wk.n * C::NCH + ch) * 16;
@@ -214,10 +232,13 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     asm volatile("" : "+v"(eb));
     *(u32x4_t*)(smem + (it.valid ? eb : C::DUMMY_OFF + lane * 16)) = v;
   };
+  auto consume = [&](const Work& wk, int u, const Item& it) { consume_s(wk, u, u % C::NSLOT, it); };
+  auto consume_p = [&](const Work& wk, int pp, const Item& it) { consume_s(wk, 2 * pp + phalf, pp % 2, it); };
   // vmcnt accounting as in conv_wstat.hip: 3 units' requests after unit g's, plus the epilogue's
   // TH * NS output stores and NS partial stores when one lies in between
   constexpr int DPU = RES ? 2 : 1;
-  constexpr int KIN = 3 * DPU;
+  // paired: one part's requests (DPU) after the consumed part's, two parts in flight
+  constexpr int KIN = (PR ? 1 : 3) * DPU;
   constexpr int KEP = KIN + (C::OST ? C::NST : TH * NS) + NS;
 
   // ---- K loop ----
@@ -342,9 +363,25 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   __syncthreads();
   Item xx = items(0);
   Item xd = xx;
+  if constexpr (PR) {
+    // parts 0 and 1 in flight; consume parts 0..2, each freeing its slot for the part after next
+    request_p(cur.n, 0, xd);
+    request_p(cur.n, 1, xd);
+    const Work n1 = decode(min(wn, last));
 #pragma unroll
-  for (int u = 0; u < C::NSLOT; ++u) request(cur.n, u, xd);
-  {
+    for (int pp = 0; pp < C::NPART - 1; ++pp) {
+      vm_wait<0>();
+      consume_p(cur, pp, xx);
+      if (pp + 2 < C::NPART) {
+        request_p(cur.n, pp + 2, xd);
+      } else {
+        if (pp + 2 == C::NPART) xd = items(1);
+        request_p(n1.n, pp + 2 - C::NPART, xd);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < C::NSLOT; ++u) request(cur.n, u, xd);
     const Work n1 = decode(min(wn, last));
 #pragma unroll
     for (int u = 0; u < U - 2; ++u) {
@@ -376,6 +413,28 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
         acc,
         [&](int q, int rem) {
           const int pa = POS_A + (team ? DT : 0), pb = POS_B + (team ? DT : 0);
+          if constexpr (PR) {
+            // one pass per part: the current tile's last part at part 0 (requesting the next tile's part 1), else
+            // the next tile's part q - 1 (requesting part q + 1, or the tile after next's part q - 3)
+            if (rem != pa) return;
+            if (q == 0) {
+              vm_wait<KEP>();
+              consume_p(cur, C::NPART - 1, xx);
+              request_p(nxt.n, 1, xd);
+            } else {
+              const int pp = q - 1;
+              if (pp == 0) xx = items(ns);
+              if (q == 1) vm_wait<KEP>(); else vm_wait<KIN>();
+              consume_p(nxt, pp, xx);
+              if (pp + 2 < C::NPART) {
+                request_p(nxt.n, pp + 2, xd);
+              } else {
+                if (pp + 2 == C::NPART) xd = items(cs);
+                request_p(nxt2.n, pp + 2 - C::NPART, xd);
+              }
+            }
+            return;
+          }
           if (rem != pa && rem != pb) return;
           const int half = rem == pa ? 0 : 1;
           if (q == 0) {  // the current tile's last region: units U-2, U-1; request 2, 3 of nxt
