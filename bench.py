@@ -13,8 +13,9 @@ ToPILImage truncation -> uint8 frames in HBM.
 Frames shard round-robin across ranks (each rank its own batch, no data-path collective:
 scaling "weak"); timing = barrier + synchronize around exactly K steps, max over ranks.
 --gather adds the video pipeline's exchange to the timed step (configs[3]): every rank's stylized
-frames go to rank 0 in frame order (point-to-point, RCCL over xGMI) and rank 0 runs the LAB
-lightness EMA (pipeline.py:1942-1978) over all of them in order.
+frames' LAB L planes go to rank 0 in frame order (point-to-point, RCCL over xGMI), rank 0 runs the
+LAB lightness EMA (pipeline.py:1942-1978) over all of them in order and returns each smoothed plane
+to the frame's owner, which rebuilds RGB, blends 0.9 with the original and D2Hs its own frames.
 
 Rank 0 prints ONE JSON line.  The headline K steps run without instrumentation; a separate
 profiled pass (HIP events around every conv launch, on the forward's stream) gives the per-layer
@@ -57,7 +58,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frame", type=str, default="1920x1080", help="WxH of the synthetic frames")
     ap.add_argument("--gather", action="store_true",
-                    help="time the ordered gather to rank 0 + rank-0 LAB EMA with the forward (configs[3])")
+                    help="time the video pipeline's exchange with the forward (configs[3]): L planes to rank 0, ordered "
+                         "LAB EMA there, planes back to the owners, merge + blend + D2H on the owner")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode timing (profiling runs)")
     ap.add_argument("--cpu-frames", type=int, default=3, help="timed 1080p frames per CPU configuration")
@@ -184,10 +186,21 @@ F16M_IO_BYTES = {"conv1.conv2d": (2, 4), "conv2.conv2d": (4, 4), "conv3.conv2d":
                  "res1.conv2.conv2d": (4, 4)}
 
 
+def _pmc_res() -> dict:
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_res_conv.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
 def mode_roofline(eng, frames, H: int, W: int, nloc: int) -> dict:
-    """The dominant kernel of a precision mode (largest share of a profiled step): its algorithmic FLOP per launch /
-    its average launch time (HIP events on the forward's stream) against the fp16 MFMA peak divided by the MFMA
-    issues per product of its arithmetic, and its algorithmic HBM bytes per launch."""
+    """The dominant kernel of a precision mode (largest share of a profiled step) against the roofline that bounds
+    it: its algorithmic FLOP per launch over the fp16 MFMA peak divided by the MFMA issues per product of its
+    arithmetic, and its algorithmic HBM bytes per launch over the HBM peak; `bound` is whichever floor is longer,
+    and `achieved` / `frac` are in that roofline's unit.  Launch time: HIP events on the forward's stream.  `traffic`
+    = the kernel's HBM bytes per launch from the rocprofv3 PMC pass of this kernel build (profiles/pmc_res_conv.json
+    `fp16m_conv2`, keyed by the hash of conv_ws2.hip's sources and flags), or None."""
     eng.profile_begin()
     torch.cuda.synchronize(frames.device)
     for _ in range(3):
@@ -198,17 +211,36 @@ def mode_roofline(eng, frames, H: int, W: int, nloc: int) -> dict:
     avg_ms = ms / max(cnt, 1)
     fl = layer_flops(H, W)[name] * nloc
     mpp = F16M_MFMA_PER_PRODUCT.get(name, 1)
-    peak = MFMA_BF16_PEAK_TFLOPS / mpp
-    ach = fl / (avg_ms * 1e-3) / 1e12
+    mfma_peak = MFMA_BF16_PEAK_TFLOPS / mpp
+    tflops = fl / (avg_ms * 1e-3) / 1e12
     cin, cout = {"conv1.conv2d": (3, 32), "conv2.conv2d": (32, 64), "conv3.conv2d": (64, 128),
                  "deconv1.conv2d": (128, 64), "deconv2.conv2d": (64, 32), "deconv3.conv2d": (32, 3)}.get(name, (128, 128))
     ib, ob = F16M_IO_BYTES.get(name, (2, 2))
     stride_in = {"conv2.conv2d": 2, "conv3.conv2d": 2, "deconv1.conv2d": 0.5, "deconv2.conv2d": 0.5}.get(name, 1)
     opix = fl / nloc / (2 * cin * cout * (81 if name in ("conv1.conv2d", "deconv3.conv2d") else 9))
     byts = nloc * opix * (cin * ib * stride_in * stride_in + cout * ob)
-    return {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "traffic": None, "avg_launch_ms": round(avg_ms, 4),
-            "flop_per_launch": fl, "mfma_issues_per_product": mpp, "algorithmic_bytes_per_launch": int(byts),
+    gbs = byts / (avg_ms * 1e-3) / 1e9
+    mfma_floor_ms = fl / (mfma_peak * 1e12) * 1e3
+    hbm_floor_ms = byts / (HBM_PEAK_GBS * 1e9) * 1e3
+    hbm = hbm_floor_ms >= mfma_floor_ms
+    traffic, tsrc = None, "no PMC summary for this kernel build"
+    pm = _pmc_res().get("fp16m_conv2") if name == "conv2.conv2d" else None
+    if pm:
+        from neuralstyletransferv1_amd import _lib
+        if pm.get("kernel_src_sha16") == _lib.ws2_kernel_sha() and pm.get("hbm_bytes_per_launch"):
+            # the PMC pass profiles the bench's 8-frame batch; scale to this launch's frames
+            traffic, tsrc = int(pm["hbm_bytes_per_launch"] * nloc / BATCH), f"profiles/pmc_res_conv.json {pm['kernel']}"
+        else:
+            tsrc = f"PMC summary is of conv_ws2 sources {pm.get('kernel_src_sha16')}, not this build"
+    return {"bound": "hbm" if hbm else "mfma", "kernel": name,
+            "achieved": round(gbs if hbm else tflops, 2), "peak": HBM_PEAK_GBS if hbm else round(mfma_peak, 1),
+            "unit": "GB/s" if hbm else "TFLOP/s", "frac": round((gbs / HBM_PEAK_GBS) if hbm else (tflops / mfma_peak), 4),
+            "traffic": traffic, "traffic_source": tsrc, "avg_launch_ms": round(avg_ms, 4),
+            "algorithmic_bytes_per_launch": int(byts), "flop_per_launch": fl, "mfma_issues_per_product": mpp,
+            "floors_ms": {"mfma": round(mfma_floor_ms, 4), "hbm": round(hbm_floor_ms, 4)},
+            "mfma": {"achieved_tflops": round(tflops, 2), "peak_tflops": round(mfma_peak, 1),
+                     "frac": round(tflops / mfma_peak, 4)},
+            "hbm": {"achieved_gbs": round(gbs, 1), "peak_gbs": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4)},
             "per_layer_avg_ms": {n: round(t / max(c, 1), 4) for n, t, c in prof}}
 
 
@@ -234,7 +266,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from neuralstyletransferv1_amd import synthetic
-    from neuralstyletransferv1_amd.frames import gather_finish, gather_start, owners, rank0_share
+    from neuralstyletransferv1_amd.frames import owners, run_pipeline
     from neuralstyletransferv1_amd.postproc import LabSmoother
     from neuralstyletransferv1_amd.transformer_net import TransformerNet
 
@@ -245,32 +277,35 @@ def main():
     net.compute_dtype = "bf16"
     eng = net.engine(dev)
 
-    # round-robin shard: rank r owns frames r, r+N, ... (distinct seeded content per rank).  With --gather rank 0,
-    # which also runs the ordered post chain, stylizes a lighter share (frames.rank0_share)
-    caps = [rank0_share(world, BATCH) if args.gather else BATCH] + [BATCH] * (world - 1)
+    # round-robin shard: rank r owns frames r, r+N, ... (distinct seeded content per rank)
+    caps = [BATCH] * world
     nloc = caps[rank]
     frames_np = synthetic.make_frames(nloc, H, W, seed=1000 + rank)
     frames = torch.from_numpy(frames_np).to(dev)
     group = list(range(sum(caps)))
     assert sum(1 for o in owners(len(group), world, caps) if o == rank) == nloc
-    ema = LabSmoother(dev, True, 0.65) if args.gather else None
-    inflight = [None]
-
-    def drain():  # complete the previous step's exchange; rank 0 runs its LAB EMA in frame order
-        ex, inflight[0] = inflight[0], None
-        if ex is not None:
-            full = gather_finish(ex)
-            if full is not None:
-                return ema(full)
-        return None
+    from neuralstyletransferv1_amd.postproc import blend_frames
 
     def step():
-        out = eng.stylize_u8(frames, PRESET)
-        if args.gather:  # the exchange of step k overlaps the forward of step k+1 (frames.run_sharded's schedule)
-            prev = drain()
-            inflight[0] = gather_start(out, group, world, rank, caps)
-            return prev
-        return out
+        return eng.stylize_u8(frames, PRESET)
+
+    def run_gather(k):
+        """--gather: k groups through the video pipeline's schedule (frames.run_pipeline): each rank stylizes its
+        shard, extracts the LAB L plane, rank 0 runs the ordered EMA (alpha 0.65) over the whole group's planes and
+        returns each frame's smoothed plane to its owner, which merges it, blends 0.9 with the original and D2Hs
+        its own frames into page-locked memory (the per-rank PCIe leg; the encode is host work, tools/cli_bench.py)"""
+        ema = LabSmoother(dev, True, 0.65)
+        host = torch.empty((nloc, H, W, 3), dtype=torch.uint8, pin_memory=True)
+
+        def stylize(idx):
+            out = eng.stylize_u8(frames, PRESET)
+            return ema.planes(out), out
+
+        def emit(idx, rows, out):
+            host.copy_(blend_frames(ema.merge(out, rows), frames, 0.9), non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+        run_pipeline([group] * k, world, rank, stylize, lambda g, full: ema.smooth_planes(full, (H, W)), emit,
+                     lambda g: ((1, H * W), torch.uint8), dev, caps)
 
     def timed(k):
         torch.cuda.synchronize(dev)
@@ -278,10 +313,12 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for _ in range(k):
-            out = step()
+        out = None
         if args.gather:
-            out = drain()  # the last step's exchange and EMA belong to the timed work
+            run_gather(k)  # the last group's exchange, EMA, return and D2H belong to the timed work
+        else:
+            for _ in range(k):
+                out = step()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -292,10 +329,11 @@ def main():
             el = float(t.item())
         return el, out
 
-    for _ in range(args.warmup):
-        step()
     if args.gather:
-        drain()
+        run_gather(max(1, args.warmup))
+    else:
+        for _ in range(args.warmup):
+            step()
     elapsed, out = timed(args.steps)           # the headline: no instrumentation
     total_frames = sum(caps) * args.steps
     fps = total_frames / elapsed
@@ -412,12 +450,14 @@ def main():
         "config": {
             "workload": (f"configs[1]: TransformerNet (Johnson) forward, {W}x{H}, batch {BATCH} per GPU, bf16 MFMA / "
                          f"fp32 accumulate, io_preset {PRESET}, uint8 frames in/out resident in HBM"
-                         + ("; + ordered gather to rank 0 and rank-0 LAB EMA (configs[3] exchange)" if args.gather
-                            else "")),
+                         + ("; + the video pipeline's exchange (configs[3]): L planes to rank 0, ordered LAB EMA, "
+                            "smoothed planes back to each frame's owner, merge + blend 0.9 + D2H on the owner"
+                            if args.gather else "")),
             "global_batch": sum(caps),
             "frame_hw": [H, W],
             "parallelism": f"frames round-robin over {world} GPU(s), " +
-                           ("point-to-point gather to rank 0" if args.gather else "no data-path collective"),
+                           ("point-to-point L-plane gather to rank 0 and return to the owners" if args.gather
+                            else "no data-path collective"),
             "dist_backend": args.dist_backend if world > 1 else None,
             "ranks_per_gpu": (world if args.device is not None else 1) if world > 1 else 1,
         },

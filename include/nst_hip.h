@@ -125,6 +125,13 @@ void nst_destroy(nst_handle* h);
  * (Johnson/ReCoNet: 4*ceil(ceil(h/2)/2); NST: centre-cropped back to h x w). */
 int nst_output_hw(const nst_handle* h, int in_h, int in_w, int* out_h, int* out_w);
 
+/* Whether nst_forward feeds the first layer the reference's encoded input without any extra rounding for this
+ * input format and io_preset (*exact = 1): always in the fp32-activation modes; in the 16-bit modes only for uint8
+ * frames whose preset encode folds into the first layer's weights (reflection-padded first layers: every preset;
+ * zero-padded ones, the NST net: presets without an offset).  NST_DT_F16M's +-1 LSB bar needs it (the Python
+ * engine runs the other combinations on an NST_DT_F32S twin).  Replaces no reference call: a property query. */
+int nst_input_exact(const nst_handle* h, int x_fmt, int preset, int* exact);
+
 /* Device workspace nst_forward needs for a batch of n frames of h x w. */
 int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* out);
 
@@ -222,6 +229,25 @@ int nst_lab_ema_u8(const nst_lab* lab, const uint8_t* rgb_in, uint8_t* rgb_out, 
                    int smooth_lightness, float alpha, float one_minus_alpha, int smooth_chroma,
                    float chroma_alpha, float one_minus_chroma_alpha, float* state, int first,
                    void* stream);
+
+/*
+ * nst_lab_ema_u8 split in three stages for the sharded video pipeline (pipeline.py:1942-1978 with the
+ * frames of one sequence stylized on several GPUs): the EMA's only cross-frame dependency is the fp32
+ * state of the planes it smooths, so each frame's owner extracts those planes, one rank runs the ordered
+ * EMA over the planes alone, and the owner rebuilds RGB from its own frame with the smoothed planes put
+ * back.  The three calls give bytes identical to nst_lab_ema_u8 on the same frames in the same order.
+ * planes: uint8 [n][np][h*w], np = smooth_lightness + 2*smooth_chroma, planes in the order L, a, b.
+ *   nst_lab_planes_u8: rgb [n,h,w,3] -> planes (rgb2lab bytes of the smoothed channels);
+ *   nst_lab_ema_planes: planes_in -> planes_out in frame order (may alias), state / first as nst_lab_ema_u8;
+ *   nst_lab_merge_u8: rgb + smoothed planes -> rgb_out = lab2rgb(rgb2lab(rgb) with those planes replaced).
+ */
+int nst_lab_planes_u8(const nst_lab* lab, const uint8_t* rgb_in, int n, int h, int w, int smooth_lightness,
+                      int smooth_chroma, uint8_t* planes, void* stream);
+int nst_lab_ema_planes(const uint8_t* planes_in, uint8_t* planes_out, int n, int h, int w, int smooth_lightness,
+                       float alpha, float one_minus_alpha, int smooth_chroma, float chroma_alpha,
+                       float one_minus_chroma_alpha, float* state, int first, void* stream);
+int nst_lab_merge_u8(const nst_lab* lab, const uint8_t* rgb_in, const uint8_t* planes, int n, int h, int w,
+                     int smooth_lightness, int smooth_chroma, uint8_t* rgb_out, void* stream);
 
 /*
  * Multi-model LAB blend (pipeline.py:1841-1870, --blend_models_lab): L from model A; per pixel

@@ -47,7 +47,8 @@ EXPORTED_SYMBOLS = (
     "nst_region_composite_u8", "nst_region_crop_input", "nst_region_resize", "nst_region_morph",
     "nst_region_morph_scratch_floats", "nst_gray_u8", "nst_flow_scratch_floats", "nst_flow_farneback",
     "nst_flow_fuse", "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale", "nst_resize_area_u8",
-    "nst_flow_dis_scratch_bytes", "nst_flow_dis", "nst_set_range_check",
+    "nst_flow_dis_scratch_bytes", "nst_flow_dis", "nst_set_range_check", "nst_input_exact",
+    "nst_lab_planes_u8", "nst_lab_ema_planes", "nst_lab_merge_u8",
 )
 # region compositor limits / geometry kinds (include/nst_hip.h NST_REGION_*, NST_RG_*)
 NST_REGION_MAX, NST_REGION_TERMS, NST_REGION_MAX_SRC = 32, 9, 16
@@ -90,20 +91,34 @@ class NstError(RuntimeError):
 TRUNK_KERNEL_SOURCES = ("csrc/conv_wstat.hip", "csrc/conv_ws_common.h", "csrc/conv_impl.h")
 
 
-def trunk_kernel_sha() -> str:
+def kernel_sha(sources=TRUNK_KERNEL_SOURCES, obj: str = "conv_wstat") -> str:
+    """sha256[:16] of a kernel's sources and the build flags of its translation unit `obj` (the key of its PMC
+    summary under profiles/)."""
     import hashlib
     import re
     h = hashlib.sha256()
-    for rel in TRUNK_KERNEL_SOURCES:
+    for rel in sources:
         with open(os.path.join(_HERE, rel), "rb") as f:
             h.update(f.read())
-    # the compiler and the code-generation flags of conv_wstat.hip's own translation unit: the global
+    # the compiler and the code-generation flags of the object's own translation unit: the global
     # HIPCC / ARCH / SLP / CXXFLAGS definitions and target-specific CXXFLAGS / SLP assignments naming that
     # object alone (diagnostic-only rules such as the multi-target NOSCRATCH remark pass do not change code)
-    pat = r"(HIPCC|ARCH|SLP|CXXFLAGS) |\$\(BUILD\)/conv_wstat\.hip\.o: *(CXXFLAGS|SLP) "
+    pat = r"(HIPCC|ARCH|SLP|CXXFLAGS) |\$\(BUILD\)/" + re.escape(obj) + r"\.hip\.o: *(CXXFLAGS|SLP) "
     with open(os.path.join(_HERE, "..", "Makefile")) as f:
         h.update("".join(l for l in f if re.match(pat, l)).encode())
     return h.hexdigest()[:16]
+
+
+def trunk_kernel_sha() -> str:
+    return kernel_sha(TRUNK_KERNEL_SOURCES, "conv_wstat")
+
+
+# the NST_DT_F16M mode's dominant kernel (the split-operand down-conv conv2, conv_ws2.hip)
+WS2_KERNEL_SOURCES = ("csrc/conv_ws2.hip", "csrc/conv_ws_common.h", "csrc/conv_impl.h")
+
+
+def ws2_kernel_sha() -> str:
+    return kernel_sha(WS2_KERNEL_SOURCES, "conv_ws2")
 
 
 def lib() -> ctypes.CDLL:
@@ -197,6 +212,12 @@ def lib() -> ctypes.CDLL:
         L.nst_lab_destroy.argtypes = [vp]
         L.nst_lab_destroy.restype = None
         L.nst_lab_ema_u8.argtypes = [vp, vp, vp, i, i, i, i, f, f, i, f, f, vp, i, vp]
+        L.nst_lab_planes_u8.argtypes = [vp, vp, i, i, i, i, i, vp, vp]
+        L.nst_lab_ema_planes.argtypes = [vp, vp, i, i, i, i, f, f, i, f, f, vp, i, vp]
+        L.nst_lab_merge_u8.argtypes = [vp, vp, vp, i, i, i, i, i, vp, vp]
+        L.nst_input_exact.argtypes = [vp, i, i, ctypes.POINTER(i)]
+        for name in ("nst_lab_planes_u8", "nst_lab_ema_planes", "nst_lab_merge_u8", "nst_input_exact"):
+            getattr(L, name).restype = i
         L.nst_blend_u8.argtypes = [vp, vp, vp, i, f, f, vp, i, i, i, vp]
         L.nst_blend_mask8_u8.argtypes = [vp, vp, vp, i, f, f, vp, i, i, i, vp]
         L.nst_blend_mask8_u8.restype = i

@@ -1121,6 +1121,18 @@ int nst_output_hw(const nst_handle* h, int in_h, int in_w, int* out_h, int* out_
   return NST_OK;
 }
 
+int nst_input_exact(const nst_handle* h, int x_fmt, int preset, int* exact) {
+  if (!h || !exact || (x_fmt != NST_IO_U8_NHWC && x_fmt != NST_IO_F32_NCHW) || preset < 0 || preset >= 8) {
+    set_error("nst_input_exact: invalid arguments");
+    return NST_E_INVALID;
+  }
+  if (f32_storage(h->dtype)) { *exact = 1; return NST_OK; }  // the operand keeps the encoded fp32 value
+  *exact = 0;
+  for (const Layer& Ly : h->layers)
+    if (Ly.prepad) *exact = (x_fmt == NST_IO_U8_NHWC && Ly.wpk_fold[preset] != nullptr) ? 1 : 0;
+  return NST_OK;
+}
+
 int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* out) {
   if (!h || !out || n <= 0 || in_h <= 0 || in_w <= 0) { set_error("nst_workspace_bytes: invalid arguments"); return NST_E_INVALID; }
   Plan P = make_plan(h, n, in_h, in_w);
@@ -1557,6 +1569,45 @@ int nst_lab_ema_u8(const nst_lab* lab, const uint8_t* rgb_in, uint8_t* rgb_out, 
                                 one_minus_alpha, smooth_chroma, chroma_alpha, one_minus_chroma_alpha, state, first,
                                 (hipStream_t)stream);
   if (e != hipSuccess) { set_error(std::string("lab_ema launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+int nst_lab_planes_u8(const nst_lab* lab, const uint8_t* rgb_in, int n, int h, int w, int smooth_lightness,
+                      int smooth_chroma, uint8_t* planes, void* stream) {
+  const int sl = smooth_lightness ? 1 : 0, sc = smooth_chroma ? 1 : 0;
+  if (!lab || !rgb_in || !planes || n <= 0 || h <= 0 || w <= 0 || !(sl || sc)) {
+    set_error("nst_lab_planes_u8: invalid arguments");
+    return NST_E_INVALID;
+  }
+  hipError_t e = launch_lab_planes(lab->rgb2lab, rgb_in, planes, n, h * w, sl, sc, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("lab_planes launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+int nst_lab_ema_planes(const uint8_t* planes_in, uint8_t* planes_out, int n, int h, int w, int smooth_lightness,
+                       float alpha, float one_minus_alpha, int smooth_chroma, float chroma_alpha,
+                       float one_minus_chroma_alpha, float* state, int first, void* stream) {
+  const int sl = smooth_lightness ? 1 : 0, sc = smooth_chroma ? 1 : 0;
+  if (!planes_in || !planes_out || !state || n <= 0 || h <= 0 || w <= 0 || !(sl || sc)) {
+    set_error("nst_lab_ema_planes: invalid arguments");
+    return NST_E_INVALID;
+  }
+  hipError_t e = launch_lab_ema_planes(planes_in, planes_out, n, h * w, sl, alpha, one_minus_alpha, sc, chroma_alpha,
+                                       one_minus_chroma_alpha, state, first, (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("lab_ema_planes launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
+  return NST_OK;
+}
+
+int nst_lab_merge_u8(const nst_lab* lab, const uint8_t* rgb_in, const uint8_t* planes, int n, int h, int w,
+                     int smooth_lightness, int smooth_chroma, uint8_t* rgb_out, void* stream) {
+  const int sl = smooth_lightness ? 1 : 0, sc = smooth_chroma ? 1 : 0;
+  if (!lab || !rgb_in || !planes || !rgb_out || n <= 0 || h <= 0 || w <= 0 || !(sl || sc)) {
+    set_error("nst_lab_merge_u8: invalid arguments");
+    return NST_E_INVALID;
+  }
+  hipError_t e = launch_lab_merge(lab->rgb2lab, lab->lab2rgb, rgb_in, planes, rgb_out, n, h * w, sl, sc,
+                                  (hipStream_t)stream);
+  if (e != hipSuccess) { set_error(std::string("lab_merge launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
   return NST_OK;
 }
 

@@ -201,6 +201,13 @@ hipError_t launch_blend_models_u8(const float* const* ys, const float (*dp)[3], 
 hipError_t launch_lab_ema(const uint32_t* rgb2lab, const uint32_t* lab2rgb, const uint8_t* in,
                           uint8_t* out, int n, int hw, int sl, float a, float oma, int sc, float ca,
                           float coma, float* state, int first, hipStream_t st);
+// the EMA split for the sharded pipeline: owner extracts planes, rank 0 runs the ordered EMA on them, owner merges
+hipError_t launch_lab_planes(const uint32_t* rgb2lab, const uint8_t* in, uint8_t* planes, int n, int hw, int sl, int sc,
+                             hipStream_t st);
+hipError_t launch_lab_ema_planes(const uint8_t* in, uint8_t* out, int n, int hw, int sl, float a, float oma, int sc,
+                                 float ca, float coma, float* state, int first, hipStream_t st);
+hipError_t launch_lab_merge(const uint32_t* rgb2lab, const uint32_t* lab2rgb, const uint8_t* in, const uint8_t* planes,
+                            uint8_t* out, int n, int hw, int sl, int sc, hipStream_t st);
 hipError_t launch_lab_blend(const uint32_t* rgb2lab, const uint32_t* lab2rgb, const uint8_t* const* frames,
                             const float* wrest, int nrest, float wL, float wab, size_t npix, uint8_t* out,
                             hipStream_t st);

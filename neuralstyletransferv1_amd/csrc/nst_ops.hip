@@ -608,6 +608,170 @@ hipError_t launch_lab_ema(const uint32_t* rgb2lab, const uint32_t* lab2rgb, cons
 }
 
 // ---------------------------------------------------------------------------------------
+// The same EMA split in three stages for the --gpus N video pipeline (frames.py): the frame's owner
+// extracts the LAB planes the EMA reads (lab_planes_kernel: L, and a / b with chroma smoothing), rank 0
+// runs the ordered EMA over those planes alone (lab_ema_planes_kernel: 1-3 bytes per pixel cross xGMI
+// instead of the RGB frame), and the owner rebuilds RGB from its own frame with the smoothed planes
+// substituted (lab_merge_kernel).  Same tables, same LabEma::step arithmetic: bit-identical to
+// lab_ema_kernel.  Planes: uint8 [n][np][hw], np = sl + 2 sc, in the order L, a, b.
+__global__ __launch_bounds__(256) void lab_planes_kernel(const uint32_t* __restrict__ rgb2lab, const uint8_t* in,
+                                                         uint8_t* __restrict__ planes, int n, int hw, int sl, int sc) {
+  const int np = sl + 2 * sc;
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // (frame, 4-pixel group)
+  const int groups = (hw + 3) / 4;
+  if (q >= (size_t)n * groups) return;
+  const int f = (int)(q / groups), p0 = (int)(q % groups) * 4;
+  const int cnt = min(4, hw - p0);
+  const uint8_t* src = in + ((size_t)f * hw + p0) * 3;
+  uint32_t lab[4];
+  if (cnt == 4 && (hw & 3) == 0) {
+    const uint32_t* s = (const uint32_t*)src;
+    const uint32_t w[3] = {s[0], s[1], s[2]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      lab[k] = rgb2lab[(byte_of(w, 3 * k) << 16) | (byte_of(w, 3 * k + 1) << 8) | byte_of(w, 3 * k + 2)];
+  } else {
+    const volatile uint8_t* v = src;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      lab[k] = k < cnt ? rgb2lab[((uint32_t)v[3 * k] << 16) | ((uint32_t)v[3 * k + 1] << 8) | (uint32_t)v[3 * k + 2]] : 0u;
+  }
+  uint8_t* dst = planes + (size_t)f * np * hw + p0;
+  int pl = 0;
+  for (int c = 0; c < 3; ++c) {
+    if (c == 0 ? !sl : !sc) continue;
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o |= ((lab[k] >> (8 * c)) & 0xffu) << (8 * k);
+    uint8_t* d = dst + (size_t)pl * hw;
+    if (cnt == 4 && (hw & 3) == 0) {
+      *(uint32_t*)d = o;
+    } else {
+      for (int k = 0; k < cnt; ++k) d[k] = (uint8_t)(o >> (8 * k));
+    }
+    ++pl;
+  }
+}
+
+__global__ __launch_bounds__(256) void lab_ema_planes_kernel(const uint8_t* in, uint8_t* out, int n, int hw, LabEma e,
+                                                             float* __restrict__ state, int first) {
+  const int np = e.sl + 2 * e.sc;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= hw) return;
+  float pL = e.sl ? state[p] : 0.f;
+  float pa = e.sc ? state[hw + p] : 0.f;
+  float pb = e.sc ? state[2 * hw + p] : 0.f;
+  for (int f = 0; f < n; ++f) {
+    const uint8_t* s = in + (size_t)f * np * hw + p;
+    uint32_t lab = 0;
+    int pl = 0;
+    if (e.sl) lab |= (uint32_t)s[(size_t)(pl++) * hw];
+    if (e.sc) {
+      lab |= (uint32_t)s[(size_t)(pl++) * hw] << 8;
+      lab |= (uint32_t)s[(size_t)(pl++) * hw] << 16;
+    }
+    const uint32_t li = e.step(lab, first && f == 0, pL, pa, pb);  // (L << 16) | (a << 8) | b
+    uint8_t* d = out + (size_t)f * np * hw + p;
+    pl = 0;
+    if (e.sl) d[(size_t)(pl++) * hw] = (uint8_t)(li >> 16);
+    if (e.sc) {
+      d[(size_t)(pl++) * hw] = (uint8_t)(li >> 8);
+      d[(size_t)(pl++) * hw] = (uint8_t)li;
+    }
+  }
+  if (e.sl) state[p] = pL;
+  if (e.sc) { state[hw + p] = pa; state[2 * hw + p] = pb; }
+}
+
+__global__ __launch_bounds__(256) void lab_merge_kernel(const uint32_t* __restrict__ rgb2lab,
+                                                        const uint32_t* __restrict__ lab2rgb, const uint8_t* in,
+                                                        const uint8_t* __restrict__ planes, uint8_t* out, int n,
+                                                        int hw, int sl, int sc) {
+  const int np = sl + 2 * sc;
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int groups = (hw + 3) / 4;
+  if (q >= (size_t)n * groups) return;
+  const int f = (int)(q / groups), p0 = (int)(q % groups) * 4;
+  const int cnt = min(4, hw - p0);
+  const bool vec = cnt == 4 && (hw & 3) == 0;
+  const uint8_t* src = in + ((size_t)f * hw + p0) * 3;
+  uint32_t lab[4];
+  if (vec) {
+    const uint32_t* s = (const uint32_t*)src;
+    const uint32_t w[3] = {s[0], s[1], s[2]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      lab[k] = rgb2lab[(byte_of(w, 3 * k) << 16) | (byte_of(w, 3 * k + 1) << 8) | byte_of(w, 3 * k + 2)];
+  } else {
+    const volatile uint8_t* v = src;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      lab[k] = k < cnt ? rgb2lab[((uint32_t)v[3 * k] << 16) | ((uint32_t)v[3 * k + 1] << 8) | (uint32_t)v[3 * k + 2]] : 0u;
+  }
+  const uint8_t* pp = planes + (size_t)f * np * hw + p0;
+  uint32_t pw[3] = {0u, 0u, 0u};
+  for (int pl = 0; pl < np; ++pl) {
+    if (vec) {
+      pw[pl] = *(const uint32_t*)(pp + (size_t)pl * hw);
+    } else {
+      for (int k = 0; k < cnt; ++k) pw[pl] |= (uint32_t)pp[(size_t)pl * hw + k] << (8 * k);
+    }
+  }
+  uint32_t rgb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t L = lab[k] & 0xffu, A = (lab[k] >> 8) & 0xffu, B = (lab[k] >> 16) & 0xffu;
+    int pl = 0;
+    if (sl) L = (pw[pl++] >> (8 * k)) & 0xffu;
+    if (sc) {
+      A = (pw[pl++] >> (8 * k)) & 0xffu;
+      B = (pw[pl++] >> (8 * k)) & 0xffu;
+    }
+    rgb[k] = lab2rgb[(L << 16) | (A << 8) | B];
+  }
+  uint8_t* dst = out + ((size_t)f * hw + p0) * 3;
+  if (vec) {
+    uint32_t o[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int i = 3 * k + c;
+        o[i >> 2] |= ((rgb[k] >> (8 * c)) & 0xffu) << (8 * (i & 3));
+      }
+    uint32_t* d = (uint32_t*)dst;
+    d[0] = o[0]; d[1] = o[1]; d[2] = o[2];
+  } else {
+    for (int k = 0; k < cnt; ++k)
+      for (int c = 0; c < 3; ++c) dst[3 * k + c] = (uint8_t)((rgb[k] >> (8 * c)) & 0xffu);
+  }
+}
+
+hipError_t launch_lab_planes(const uint32_t* rgb2lab, const uint8_t* in, uint8_t* planes, int n, int hw, int sl, int sc,
+                             hipStream_t st) {
+  const size_t threads = (size_t)n * ((hw + 3) / 4);
+  hipLaunchKernelGGL(lab_planes_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, rgb2lab, in, planes,
+                     n, hw, sl, sc);
+  return hipGetLastError();
+}
+
+hipError_t launch_lab_ema_planes(const uint8_t* in, uint8_t* out, int n, int hw, int sl, float a, float oma, int sc,
+                                 float ca, float coma, float* state, int first, hipStream_t st) {
+  const LabEma e{sl, sc, a, oma, ca, coma};
+  hipLaunchKernelGGL(lab_ema_planes_kernel, dim3((unsigned)((hw + 255) / 256)), dim3(256), 0, st, in, out, n, hw, e,
+                     state, first);
+  return hipGetLastError();
+}
+
+hipError_t launch_lab_merge(const uint32_t* rgb2lab, const uint32_t* lab2rgb, const uint8_t* in, const uint8_t* planes,
+                            uint8_t* out, int n, int hw, int sl, int sc, hipStream_t st) {
+  const size_t threads = (size_t)n * ((hw + 3) / 4);
+  hipLaunchKernelGGL(lab_merge_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, rgb2lab, lab2rgb, in,
+                     planes, out, n, hw, sl, sc);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // Multi-model LAB blend (pipeline.py:1841-1870): L from model A; a/b = clip(wL*a_A + wab*mix, 0, 255)
 // with mix = sum_i w_i * a_i over models B.. in order (float32 accumulation starting from 0), all on
 // the raw LAB bytes (Pillow keeps the signed a/b as uint8, so the reference mixes the wrapped
@@ -1179,6 +1343,9 @@ hipError_t launch_gram(const void* F, int dtype, int layout_hwc, int n, int c, i
   const int rg = (al16(dst) && al16(G) && (!delta || (al16(delta->A) && ((uintptr_t)delta->Mb & 7) == 0)))
                      ? gram_reduce_groups(slice, g.slices) : 0;
   const unsigned nb = (unsigned)(rg ? gram_reduce_blocks(slice, g.slices) : (slice + 63) / 64);
+  // the delta mode's loss partials are counted by gram_delta_parts (the float4 reduce): the scalar reduce writes
+  // a different number of them, so a caller summing gram_delta_parts() partials would undercount -- refuse it
+  if (delta && (!rg || nb != (unsigned)gram_delta_parts(n, c, hw))) return hipErrorInvalidValue;
   if (delta && nb > (unsigned)GRAM_DELTA_MAX_PARTS) return hipErrorInvalidValue;
   if (rg) {
 #define NST_GRED4(GG)                                                                                          \

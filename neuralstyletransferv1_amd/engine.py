@@ -49,6 +49,37 @@ class Engine:
         self._h = h
         self._keep = None
         self._ws: Optional[torch.Tensor] = None
+        # NST_DT_F16M's +-1 LSB bar rests on an exact first-layer operand (the io_preset encode folded into the
+        # first layer's weights over raw bytes); inputs where that fold does not hold (float32 tensors, a
+        # zero-padded first layer with an offset preset, no_fold) run on an NST_DT_F32S twin of the same weights
+        self._f16m_src = (host, kernel_flags) if self.dtype == _lib.NST_DT_F16M else None
+        self._twin: Optional["Engine"] = None
+        self._exact: Dict[Tuple[int, int], bool] = {}
+
+    def _for_input(self, x_fmt: int, pid: int) -> "Engine":
+        """The engine that runs this input format and preset: self, or the fp32s twin (see __init__)."""
+        if self._f16m_src is None:
+            return self
+        key = (x_fmt, pid)
+        if key not in self._exact:
+            ex = ctypes.c_int()
+            check(lib().nst_input_exact(self._h, x_fmt, pid, ctypes.byref(ex)), "nst_input_exact")
+            self._exact[key] = bool(ex.value)
+        if self._exact[key]:
+            return self
+        if self._twin is None:
+            host, flags = self._f16m_src
+            self._twin = Engine(self.arch, host, "fp32s", self.device, flags & ~_lib.KSEL["f16m_two_blocks"])
+        return self._twin
+
+    def forward_into(self, x: torch.Tensor, x_fmt: int, n: int, h: int, w: int, pid: int, y: torch.Tensor,
+                     y_fmt: int) -> None:
+        """nst_forward of a device batch into y on the current stream (workspace managed here), on the engine
+        that holds this mode's bar for the input (_for_input)."""
+        e = self._for_input(x_fmt, pid)
+        ws = e.workspace(n, h, w)
+        check(lib().nst_forward(e._h, x.data_ptr(), x_fmt, n, h, w, pid, y.data_ptr(), y_fmt, ws.data_ptr(),
+                                ws.numel(), _lib.stream_ptr(self.device)), "nst_forward")
         # NST_RANGE_CHECK=1: every forward checks for values that left the compute dtype's range (NST_E_RANGE; a
         # synchronising debug aid for the fp16 / split modes, off by default)
         if os.environ.get("NST_RANGE_CHECK", "0") == "1":
@@ -162,10 +193,7 @@ class Engine:
         n, _, h, w = x.shape
         oh, ow = self.output_hw(h, w)
         y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=self.device)
-        ws = self.workspace(n, h, w)
-        check(lib().nst_forward(self._h, x.data_ptr(), _lib.NST_IO_F32_NCHW, n, h, w, 0, y.data_ptr(),
-                                _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(), _lib.stream_ptr(self.device)),
-              "nst_forward")
+        self.forward_into(x, _lib.NST_IO_F32_NCHW, n, h, w, 0, y, _lib.NST_IO_F32_NCHW)
         return y
 
     def stylize_u8(self, frames: torch.Tensor, preset: str) -> torch.Tensor:
@@ -183,17 +211,14 @@ class Engine:
         frames = frames.contiguous()
         n, h, w, _ = frames.shape
         oh, ow = self.output_hw(h, w)
-        ws = self.workspace(n, h, w)
         out = torch.empty((n, h, w, 3), dtype=torch.uint8, device=self.device)
         st = _lib.stream_ptr(self.device)
         pid = _lib.PRESETS[preset]
         if (oh, ow) == (h, w):
-            check(lib().nst_forward(self._h, frames.data_ptr(), _lib.NST_IO_U8_NHWC, n, h, w, pid, out.data_ptr(),
-                                    _lib.NST_IO_U8_NHWC, ws.data_ptr(), ws.numel(), st), "nst_forward")
+            self.forward_into(frames, _lib.NST_IO_U8_NHWC, n, h, w, pid, out, _lib.NST_IO_U8_NHWC)
             return out
         y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=self.device)
-        check(lib().nst_forward(self._h, frames.data_ptr(), _lib.NST_IO_U8_NHWC, n, h, w, pid, y.data_ptr(),
-                                _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(), st), "nst_forward")
+        self.forward_into(frames, _lib.NST_IO_U8_NHWC, n, h, w, pid, y, _lib.NST_IO_F32_NCHW)
         check(lib().nst_decode_resize_u8(y.data_ptr(), n, oh, ow, pid, out.data_ptr(), h, w, st),
               "nst_decode_resize_u8")
         return out

@@ -170,10 +170,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--keep_staged", action="store_true",
                     help="--input_dir: also write the staged frame copies (the reference's work_dir/frames files); the "
                          "frames are staged in memory either way, with the same pixels")
-    ap.add_argument("--png_writer", choices=["fast", "pil"], default="fast",
-                    help="PNG outputs: 'fast' = Up filter + zlib RLE deflate (pngio.py: ~6x faster than Pillow's "
-                         "default encoder, files within a few percent of its size), 'pil' = Pillow's encoder at its "
-                         "defaults, byte-identical to the reference's files.  The pixels are identical either way")
+    ap.add_argument("--png_writer", choices=["fast", "pil"], default="pil",
+                    help="PNG outputs: 'pil' (default) = Pillow's encoder at its defaults, byte-identical to the "
+                         "reference's files; 'fast' = Up filter + zlib RLE deflate (pngio.py: ~6x faster than Pillow's "
+                         "default encoder, files within a few percent of its size, opt-in).  The pixels are "
+                         "identical either way")
     ap.add_argument("--png_compress_level", type=int, default=None, choices=range(10), metavar="0-9",
                     help="Pillow's PNG encoder at this zlib level (overrides --png_writer); the pixels are the same "
                          "at every level, only the file size and the encode time change")
@@ -403,7 +404,10 @@ class FrameSource:
         with Image.open(self.files[i]) as im:
             w, h = im.size
             if self.staged is not None:  # the staged copy is EXIF-upright: orientations 6 / 8 swap the sides
-                tags = getattr(im, "_getexif", lambda: None)() or {}
+                try:
+                    tags = getattr(im, "_getexif", lambda: None)() or {}
+                except Exception:  # noqa: BLE001 -- unreadable EXIF: the raw copy is staged (_open_rgb)
+                    tags = {}
                 if _EXIF_UPRIGHT.get(tags.get(0x0112)) in (90, 270):
                     w, h = h, w
         return (h, w)
@@ -418,7 +422,13 @@ class FrameSource:
         # frame -- PNG (lossless: the decoded frame is that RGB image itself) or JPEG at --jpeg_quality, whose
         # encode -> decode round trip runs here in memory (the same bytes PIL writes, so the same pixels)
         src, q = self.staged[i]
-        pil = _get_image_with_exif_pil(str(src))
+        try:
+            pil = _get_image_with_exif_pil(str(src))
+        except Exception as e:  # noqa: BLE001 -- pipeline.py:2587-2589: the raw file is copied instead
+            _log(f"[stage][WARN] EXIF-normalize failed for {src} ({e}); copying instead")
+            im = Image.open(src)
+            im.load()
+            return im if im.mode == "RGB" else im.convert("RGB")
         if q is None:
             return pil
         # the round trip goes through an anonymous in-memory file with a real descriptor: Pillow encodes to a
@@ -466,7 +476,7 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     import torch
     from PIL import Image
 
-    from .frames import plan_groups, rank0_share, run_sharded
+    from .frames import plan_groups, rank0_share, run_pipeline
     t_setup = time.perf_counter()
     from .postproc import LabSmoother, blend_frames
 
@@ -525,8 +535,10 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         names = [f"frame_{i + 1:04d}" for i in range(n_syn)]
     else:
         staged = getattr(args, "_staged_sources", None)
-        if staged is not None:  # --input_dir: frame_{i:04d} staged in memory (prepare)
-            entries = [(f"frame_{i:04d}", s) for i, s in enumerate(staged, start=1)]
+        if staged is not None:  # --input_dir: frame_{i:04d} staged in memory (prepare); only .png/.jpg/.jpeg
+            # staged frames are styled (pipeline.py:1019-1021 filters frames_dir by suffix)
+            entries = [(f"frame_{i:04d}", s) for i, s in enumerate(staged, start=1)
+                       if Path(s[0]).suffix.lower() in {".png", ".jpg", ".jpeg"}]
         else:
             files = sorted(p for p in frames_dir.iterdir() if p.is_file() and p.name.startswith("frame_")
                            and p.suffix.lower() in {".png", ".jpg", ".jpeg"})
@@ -557,12 +569,14 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     prof = _PipeProf()
     with prof("size_scan"):  # header reads (a PNG's EXIF lookup decodes it): on the pool
         sizes = list(pool.map(src.size, range(len(src))))
-    # rank 0 also runs every frame's ordered post chain: a lighter share of each group (frames.rank0_share)
+    # with --flow_ema rank 0 runs every frame's temporal stage (flow + fused EMA + LAB EMA + blend): a lighter share
+    # of each group (frames.rank0_share).  Otherwise its ordered stage is the LAB EMA over 1-3 byte planes per
+    # pixel (negligible), and every rank takes a full share.
     bsz = max(1, args.batch)
-    r0 = rank0_share(world, bsz)
+    flow_mode = bool(getattr(args, "flow_ema", False))
+    r0 = rank0_share(world, bsz) if flow_mode else bsz
     caps = [r0] + [bsz] * (world - 1)
     groups = plan_groups(sizes, world, bsz, r0)
-    flow_mode = bool(getattr(args, "flow_ema", False))
     need_orig = blend < 1.0 or bool(args.mask or args.mask_dir) or (flow_mode and bool(getattr(args, "motion_blend", False)))
 
     # host decode runs ahead of the GPU: this rank's next group(s) are loading on the pool while a group is
@@ -670,48 +684,83 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     t_start = time.perf_counter()
     done = [0]
 
-    def consume(g: List[int], full):
-        motion = None
-        if flow_mode:  # unpack [out01 f32 | orig u8] and run the temporal stage in frame order
-            from .temporal import motion_alpha, planar_to_u8
-            h0, w0 = sizes[g[0]]
-            nb = 3 * h0 * w0 * 4
-            out01 = full[:, :nb].contiguous().view(torch.float32).reshape(len(g), 3, h0, w0)
-            orig = full[:, nb:].contiguous().reshape(len(g), h0, w0, 3)
-            if lab.hw is not None and lab.hw != (h0, w0):
-                flow.reset()
-            # None for the first frame of a run (no previous frame); the batch's flows come in one call
-            fused, flows = flow.batch(out01, orig)
-            if getattr(args, "motion_blend", False):  # pipeline.py:2072-2080 alpha from this frame's flow
-                motion = [None if fl is None else motion_alpha(fl, blend) for fl in flows]
-            styled = planar_to_u8(torch.stack(fused))
-            full = torch.cat([styled, orig], dim=3) if need_orig else styled
-        styled = full[..., :3].contiguous() if need_orig else full
-        h0, w0 = styled.shape[1], styled.shape[2]
+    # Output stages (frames.run_pipeline).  The frame's owner stylizes it and, at the end, D2Hs and encodes it on its
+    # own PCIe link and host pool; the only ordered work is the LAB EMA (pipeline.py:1942-1978), which rank 0 runs
+    # over the planes it smooths (1 byte per pixel by default) -- or, with --flow_ema, the whole temporal chain over
+    # [out01 | orig], returning finished frames.  Mask composite and blend (pipeline.py:1984-2092) run on the owner.
+    ordered_lab = (lab.sl or lab.sc) and not flow_mode
+
+    def stylize_send(idx: List[int]):
+        full = stylize(idx)
+        if flow_mode:
+            return full, None
+        if ordered_lab:
+            return lab.planes(full[..., :3] if need_orig else full), full
+        return None, full
+
+    def root_post(g: List[int], full):
+        h0, w0 = sizes[g[0]]
         if lab.hw is not None and lab.hw != (h0, w0):
             _log(f"[size][reset] frame dims changed {lab.hw} -> {(h0, w0)}; resetting EMA caches")
             lab.reset()
-        styled = lab(styled)  # frame order within and across groups
+            if flow is not None:
+                flow.reset()
+        if not flow_mode:
+            return lab.smooth_planes(full, (h0, w0)) if ordered_lab else None
+        # unpack [out01 f32 | orig u8] and run the temporal stage in frame order
+        from .temporal import motion_alpha, planar_to_u8
+        nb = 3 * h0 * w0 * 4
+        out01 = full[:, :nb].contiguous().view(torch.float32).reshape(len(g), 3, h0, w0)
+        orig = full[:, nb:].contiguous().reshape(len(g), h0, w0, 3)
+        # None for the first frame of a run (no previous frame); the batch's flows come in one call
+        fused, flows = flow.batch(out01, orig)
+        motion = None
+        if getattr(args, "motion_blend", False):  # pipeline.py:2072-2080 alpha from this frame's flow
+            motion = [None if fl is None else motion_alpha(fl, blend) for fl in flows]
+        styled = lab(planar_to_u8(torch.stack(fused)))
+        lab.hw = (h0, w0)
         if need_orig:
-            orig = full[..., 3:].contiguous()
-            alpha = _masks_for(g, h0, w0)
             styled_in = styled
-            styled = blend_frames(styled, orig, blend, alpha, args.composite_mode)
+            styled = blend_frames(styled, orig, blend, _masks_for(g, h0, w0), args.composite_mode)
             if motion is not None:  # frames with a flow and no mask: the motion-adaptive blend replaces it
                 for j, f in enumerate(g):
                     if motion[j] is not None and not _has_mask(f):
                         styled[j:j + 1] = blend_frames(styled_in[j:j + 1], orig[j:j + 1], 1.0, motion[j][None], "keep")
+        return styled
+
+    def ret_spec(g: List[int]):
+        h0, w0 = sizes[g[0]]
+        if flow_mode:
+            return (h0, w0, 3), torch.uint8
+        return ((lab.nplanes, h0 * w0), torch.uint8) if ordered_lab else None
+
+    def emit(idx: List[int], rows, full):
+        if not idx:
+            return
+        if flow_mode:
+            styled = rows
+        else:
+            styled = full[..., :3].contiguous() if need_orig else full
+            if ordered_lab:
+                styled = lab.merge(styled, rows)
+            if need_orig:
+                h0, w0 = styled.shape[1], styled.shape[2]
+                styled = blend_frames(styled, full[..., 3:].contiguous(), blend, _masks_for(idx, h0, w0),
+                                      args.composite_mode)
         with prof("d2h"):  # page-locked: the saves read it after one stream sync
             host_t = torch.empty(styled.shape, dtype=torch.uint8, pin_memory=True)
             host_t.copy_(styled, non_blocking=True)
             torch.cuda.current_stream(dev).synchronize()
             host = host_t.numpy()
         if not args.no_save:
-            for j, f in enumerate(g):
+            for j, f in enumerate(idx):
                 pending.append(pool.submit(_save, host[j], f))
-        done[0] += len(g)
+                written.append(f)
+        done[0] += len(idx)
         el = time.perf_counter() - t_start
-        _log(f"[frame] {done[0]}/{len(src)} styled  ({done[0] / max(el, 1e-9):.2f} frames/s)")
+        who = f" rank {rank}" if world > 1 else ""
+        _log(f"[frame]{who} {done[0]}/{len(src) if world == 1 else sum(len(sh) for sh in my_shards)} styled  "
+             f"({done[0] / max(el, 1e-9):.2f} frames/s)")
 
     def _has_mask(f):  # pipeline.py:1985-1993 mask_used: a --mask, or this frame's --mask_dir file exists
         if getattr(args, "mask", None):
@@ -773,21 +822,33 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
             out_img.save(out_path, format="JPEG", quality=int(jpeg_quality))
         elif getattr(args, "png_compress_level", None) is not None:
             out_img.save(out_path, compress_level=int(args.png_compress_level))
-        elif getattr(args, "png_writer", "fast") == "fast":  # same pixels as Pillow's file (pngio docstring)
+        elif getattr(args, "png_writer", "pil") == "fast":  # same pixels as Pillow's file (pngio docstring)
             from .pngio import write_png
             write_png(out_path, img)
         else:
             out_img.save(out_path)
         return str(out_path)
 
-    run_sharded(groups, world, rank, stylize, consume, dev, caps)
+    written: List[int] = []
+    if ordered_lab or flow_mode:
+        run_pipeline(groups, world, rank, stylize_send, root_post, emit, ret_spec, dev, caps)
+    else:  # no ordered stage: every rank runs its frames start to finish, no exchange
+        for sh in my_shards:
+            if sh:
+                _, full = stylize_send(sh)
+                emit(sh, None, full)
     with prof("drain_saves"):
         for p in pending:
             p.result()
     pool.shutdown()
     prof.report(rank)
     el = time.perf_counter() - t_start
-    LAST_RUN_STATS.update(frames=len(src), seconds=el, setup_seconds=t_start - t_setup)
+    LAST_RUN_STATS.update(frames=len(src), seconds=el, setup_seconds=t_start - t_setup, rank=rank,
+                          written=[names[f] for f in written])
+    if os.environ.get("NST_PIPE_WRITTEN"):  # diagnostics: the frames this rank encoded and wrote (tests)
+        import json
+        with open(os.path.join(os.environ["NST_PIPE_WRITTEN"], f"rank{rank}.json"), "w") as fh:
+            json.dump({"rank": rank, "world": world, "written": [names[f] for f in written]}, fh)
     if rank == 0:
         _log(f"Styled {len(src)}/{len(src)} frames in {el:.2f}s ({len(src) / max(el, 1e-9):.2f} frames/s)")
 
@@ -833,10 +894,7 @@ def _slot_u8(model, preset, xin, h0, w0):
     if (oh, ow) == (h, w) == (h0, w0):
         return model.stylize_frames(xin, preset)
     y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=dev)
-    ws = eng.workspace(n, h, w)
-    check(lib().nst_forward(eng._h, xin.data_ptr(), _lib.NST_IO_U8_NHWC, n, h, w, _lib.PRESETS[preset],
-                            y.data_ptr(), _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(),
-                            _lib.stream_ptr(dev)), "nst_forward")
+    eng.forward_into(xin, _lib.NST_IO_U8_NHWC, n, h, w, _lib.PRESETS[preset], y, _lib.NST_IO_F32_NCHW)
     out = torch.empty((n, h0, w0, 3), dtype=torch.uint8, device=dev)
     check(lib().nst_decode_resize_u8(y.data_ptr(), n, oh, ow, _lib.PRESETS[preset], out.data_ptr(), h0, w0,
                                      _lib.stream_ptr(dev)), "nst_decode_resize_u8")
@@ -858,10 +916,7 @@ def _blend_slots(slots, weights, xin, h0, w0):
         n, h, w, _ = xin.shape
         oh, ow = eng.output_hw(h, w)
         y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=dev)
-        ws = eng.workspace(n, h, w)
-        check(lib().nst_forward(eng._h, xin.data_ptr(), _lib.NST_IO_U8_NHWC, n, h, w, _lib.PRESETS[preset],
-                                y.data_ptr(), _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(),
-                                _lib.stream_ptr(dev)), "nst_forward")
+        eng.forward_into(xin, _lib.NST_IO_U8_NHWC, n, h, w, _lib.PRESETS[preset], y, _lib.NST_IO_F32_NCHW)
         ys.append(y)
         presets.append(_lib.PRESETS[preset])
     shapes = {tuple(y.shape) for y in ys}

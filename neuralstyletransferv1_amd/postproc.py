@@ -105,6 +105,59 @@ class LabSmoother:
                                    self.state.data_ptr(), first, _lib.stream_ptr(self.device)), "nst_lab_ema_u8")
         return out
 
+    # ---- the same EMA in three stages for the sharded pipeline (nst_lab_planes_u8 / _ema_planes / _merge_u8):
+    # the owner of a frame extracts the planes the EMA reads, the ordered stage smooths them in frame order, the
+    # owner puts them back; bytes identical to __call__ on the same frames in the same order
+    @property
+    def nplanes(self) -> int:
+        return int(self.sl) + 2 * int(self.sc)
+
+    def planes(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        """[n,h,w,3] uint8 -> [n, nplanes, h*w] uint8 LAB planes (L, then a, b) of the smoothed channels."""
+        _lib.require_gpu_tensor(frames_u8, "frames")
+        frames_u8 = frames_u8.contiguous()
+        n, h, w, _ = frames_u8.shape
+        out = torch.empty((n, self.nplanes, h * w), dtype=torch.uint8, device=frames_u8.device)
+        if n:
+            t = lab_tables(frames_u8.device)
+            check(lib().nst_lab_planes_u8(t._h, frames_u8.data_ptr(), n, h, w, int(self.sl), int(self.sc),
+                                          out.data_ptr(), _lib.stream_ptr(frames_u8.device)), "nst_lab_planes_u8")
+        return out
+
+    def smooth_planes(self, planes: torch.Tensor, hw: tuple) -> torch.Tensor:
+        """The ordered stage: [n, nplanes, h*w] planes of consecutive frames of size hw -> smoothed planes (state
+        carried across calls, reset on a size change like __call__)."""
+        _lib.require_gpu_tensor(planes, "planes")
+        planes = planes.contiguous()
+        n = planes.shape[0]
+        h, w = hw
+        first = 0
+        if self.state is None or self.hw != (h, w):
+            self.state = torch.zeros(3 * h * w, dtype=torch.float32, device=self.device)
+            self.hw = (h, w)
+            first = 1
+        out = torch.empty_like(planes)
+        check(lib().nst_lab_ema_planes(planes.data_ptr(), out.data_ptr(), n, h, w, int(self.sl), float(self.a),
+                                       float(self.oma), int(self.sc), float(self.ca), float(self.coma),
+                                       self.state.data_ptr(), first, _lib.stream_ptr(self.device)),
+              "nst_lab_ema_planes")
+        return out
+
+    def merge(self, frames_u8: torch.Tensor, planes: torch.Tensor) -> torch.Tensor:
+        """The owner's last stage: frames with their smoothed planes put back (LAB -> RGB)."""
+        _lib.require_gpu_tensor(frames_u8, "frames")
+        frames_u8, planes = frames_u8.contiguous(), planes.to(frames_u8.device).contiguous()
+        n, h, w, _ = frames_u8.shape
+        if planes.shape != (n, self.nplanes, h * w):
+            raise _lib.NstError(f"planes {tuple(planes.shape)} do not match frames {tuple(frames_u8.shape)}")
+        out = torch.empty_like(frames_u8)
+        if n:
+            t = lab_tables(frames_u8.device)
+            check(lib().nst_lab_merge_u8(t._h, frames_u8.data_ptr(), planes.data_ptr(), n, h, w, int(self.sl),
+                                         int(self.sc), out.data_ptr(), _lib.stream_ptr(frames_u8.device)),
+                  "nst_lab_merge_u8")
+        return out
+
 
 def blend_frames(styled_u8: torch.Tensor, orig_u8: torch.Tensor, blend: float = 1.0,
                  mask: Optional[torch.Tensor] = None, composite_mode: str = "keep") -> torch.Tensor:

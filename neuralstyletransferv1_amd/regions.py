@@ -662,9 +662,7 @@ def forward_raw(model, x: torch.Tensor, preset: str) -> torch.Tensor:
         fmt = _lib.NST_IO_F32_NCHW
     oh, ow = eng.output_hw(h, w)
     y = torch.empty((n, 3, oh, ow), dtype=torch.float32, device=dev)
-    ws = eng.workspace(n, h, w)
-    check(lib().nst_forward(eng._h, x.data_ptr(), fmt, n, h, w, _lib.PRESETS[preset], y.data_ptr(),
-                            _lib.NST_IO_F32_NCHW, ws.data_ptr(), ws.numel(), _stream(dev)), "nst_forward")
+    eng.forward_into(x.contiguous(), fmt, n, h, w, _lib.PRESETS[preset], y, _lib.NST_IO_F32_NCHW)
     return y
 
 

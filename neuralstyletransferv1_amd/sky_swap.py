@@ -188,12 +188,12 @@ def main(argv=None) -> int:
     ap.add_argument("--morph_close_ks", type=int, default=5,
                     help="accepted for compatibility: the reference never passes it on (infer_mask always closes 5x5)")
     # build additions
-    ap.add_argument("--dtype", choices=["fp32s", "fp32", "fp16", "bf16"], default="fp32s",
-                    help="DeepLab compute dtype on the MI355X: fp32s (default) = fp32 activations with every GEMM "
-                         "operand an fp16 hi/lo pair: the fp32 mode's bars against the reference logits (same "
-                         "argmax wherever the top-2 margin exceeds 1e-4, 1080p masks within 1 LSB of the reference "
-                         "chain's), ~15 %% faster; fp32 = exact-f32 MFMAs; fp16 / bf16 = faster still, 98.9 %% / "
-                         "95.3 %% of 1080p mask pixels within 1 LSB")
+    ap.add_argument("--dtype", choices=["fp32", "fp32s", "fp16", "bf16"], default="fp32",
+                    help="DeepLab compute dtype on the MI355X: fp32 (default) = exact-f32 MFMAs, the reference's "
+                         "arithmetic; fp32s (opt-in) = fp32 activations with every GEMM operand an fp16 hi/lo pair: "
+                         "the fp32 mode's bars against the reference logits (same argmax wherever the top-2 margin "
+                         "exceeds 1e-4, 1080p masks within 1 LSB of the reference chain's), ~15 %% faster; fp16 / "
+                         "bf16 = faster still, 98.9 %% / 95.3 %% of 1080p mask pixels within 1 LSB")
     args = ap.parse_args(argv)
     if not args.batch_frames and not args.image:
         ap.error("either --image or --batch_frames must be provided")

@@ -179,6 +179,27 @@ def test_1080p_fp16m_vs_oracle_8_frames(ksel):
     assert d.max() <= 1 and (d > 0).mean() < 0.08
 
 
+@pytest.mark.parametrize("preset", ["raw_01", "imagenet_255"])
+def test_1080p_fp16m_nst_net_within_1lsb(preset):
+    """NST_DT_F16M on the NST net (zero-padded first layer after ReflectionPad2d(40)) at 1080p vs the CPU reference
+    (ADVICE r04): raw_01 -- the pipeline's io_preset for NST checkpoints (pipeline.py:610-614) -- folds into the first
+    layer (exact operand) and runs the split-head program; imagenet_255 has an offset the zero padding does not
+    carry, so the engine runs it on its fp32s twin (nst_input_exact).  Both: every value within +-1 LSB."""
+    sd = synthetic.make_state_dict("nst", 0)
+    frames = synthetic.make_frames(2, 1080, 1920, seed=1000)
+    ref = np.concatenate([O.stylize_u8("nst", sd, frames[i:i + 1], preset) for i in range(2)])
+    net = _net("nst", 0, "fp16m")
+    eng = net.engine(torch.device("cuda", 0))
+    from neuralstyletransferv1_amd import _lib
+    routed = eng._for_input(_lib.NST_IO_U8_NHWC, _lib.PRESETS[preset])
+    assert (routed is eng) == (preset == "raw_01")
+    assert eng._for_input(_lib.NST_IO_F32_NCHW, 0) is not eng  # float tensors: no exact operand in 16 bits
+    out = net.stylize_frames(torch.from_numpy(frames).cuda(), preset).cpu().numpy()
+    d = np.abs(out.astype(int) - ref.astype(int))
+    print(f"1080p x2 NST fp16m {preset}: max {d.max()} LSB, values off by one {(d > 0).mean():.6f}")
+    assert d.max() <= 1 and (d > 0).mean() < 0.08
+
+
 def test_1080p_fp16_vs_oracle():
     """fp16 mode on the bench's 8 1080p frames (the frames the bench's fp16_mode compares) vs the CPU reference
     (pre-LAB uint8): within 1 LSB on >= 99.97 % of values, max F16_MAX_LSB (3); per pixel (any channel) reported."""
@@ -252,6 +273,26 @@ def test_lab_ema_bit_exact_sequence():
     out = gpu(torch.from_numpy(frames).cuda()).cpu().numpy()
     for i in range(11):
         assert np.array_equal(out[i], ref(frames[i])), ("chunks", i)
+
+
+@pytest.mark.parametrize("shape", [(96, 128), (37, 61)])
+def test_lab_ema_split_stages_bit_exact(shape):
+    """The sharded pipeline's LAB EMA (planes on the owner, ordered EMA over planes, merge on the owner) gives the
+    bytes of the one-kernel EMA and of Pillow's chain, over batches, in every smoothing mode, aligned and ragged."""
+    from neuralstyletransferv1_amd.postproc import LabSmoother
+    frames = synthetic.make_frames(7, *shape, seed=31)
+    for sl, a, sc, ca in ((True, 0.65, False, 0.85), (True, 0.7, True, 0.85), (False, 0.7, True, 0.5)):
+        split = LabSmoother("cuda", sl, a, sc, ca)
+        ref = O.LabEMA(sl, a, sc, ca)
+        outs = []
+        for lo, hi in ((0, 3), (3, 4), (4, 7)):
+            f = torch.from_numpy(frames[lo:hi]).cuda()
+            pl = split.planes(f)
+            assert pl.shape == (hi - lo, int(sl) + 2 * int(sc), shape[0] * shape[1])
+            outs.append(split.merge(f, split.smooth_planes(pl, shape)).cpu().numpy())
+        out = np.concatenate(outs)
+        for i in range(7):
+            assert np.array_equal(out[i], ref(frames[i])), (shape, sl, a, sc, ca, i)
 
 
 def test_blend_and_mask_bit_exact():

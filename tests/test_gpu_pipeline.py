@@ -276,35 +276,52 @@ def test_inference_res_lanczos_cli(tmp_path):
     assert got.shape == (120, 162, 3) and within2 >= 0.999, (within2, dmax)
 
 
-def test_multi_gpu_orchestration_gloo_matches_single(tmp_path):
-    """The --gpus N orchestration (pipeline.py main -> one spawned process per rank, round-robin
-    frames, ordered gather to rank 0, rank-0 LAB EMA + mask/blend + save) with the gloo backend and
-    both ranks on this box's one GPU: outputs byte-identical to --gpus 1 (frame order and the EMA's
-    sequential state survive the sharding)."""
+@pytest.mark.parametrize("gpus,extra", [(2, []), (3, ["--mask", "MASK", "--smooth_chroma"]),
+                                        (2, ["--no-smooth_lightness"])])
+def test_multi_gpu_orchestration_gloo_matches_single(tmp_path, monkeypatch, gpus, extra):
+    """The --gpus N orchestration (pipeline.py main -> one spawned process per rank, round-robin frames; the LAB
+    planes of every frame to rank 0, the ordered EMA there, the smoothed planes back to each frame's owner, which
+    merges them, composites the mask, blends and encodes its own frames) with the gloo backend and every rank on
+    this box's one GPU: outputs byte-identical to --gpus 1 (frame order and the EMA's sequential state survive the
+    sharding), and each rank wrote exactly the frames it stylized."""
+    import json
+    from neuralstyletransferv1_amd import frames as F
     ck, _ = _ckpt(tmp_path, "johnson", 2)
     frames = synthetic.make_frames(7, 48, 64, seed=90)
     d_in = tmp_path / "in"
     d_in.mkdir()
     for i, f in enumerate(frames):
         Image.fromarray(f).save(d_in / f"frame_{i + 1:04d}.png")
+    mask = tmp_path / "mask.png"
+    Image.fromarray(((np.indices((48, 64)).sum(0) % 17) * 15).astype(np.uint8)).save(mask)
+    extra = [str(mask) if a == "MASK" else a for a in extra]
     outs = {}
-    for gpus in (1, 2):
-        d_out = tmp_path / f"out{gpus}"
+    for n in (1, gpus):
+        d_out = tmp_path / f"out{n}"
         argv = ["--input_dir", str(d_in), "--output_dir", str(d_out), "--model", ck, "--io_preset", "imagenet_255",
                 "--blend", "0.9", "--smooth_alpha", "0.65", "--batch", "2", "--dtype", "bf16",
-                "--work_dir", str(tmp_path / f"w{gpus}")]
-        if gpus > 1:
-            argv += ["--gpus", "2", "--dist_backend", "gloo", "--dist_timeout", "120"]
+                "--work_dir", str(tmp_path / f"w{n}")] + extra
+        if n > 1:
+            wdir = tmp_path / f"written{n}"
+            wdir.mkdir()
+            monkeypatch.setenv("NST_PIPE_WRITTEN", str(wdir))
+            argv += ["--gpus", str(n), "--dist_backend", "gloo", "--dist_timeout", "120"]
         assert P.main(argv) == 0
-        outs[gpus] = [np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png")) for i in range(7)]
+        outs[n] = [np.array(Image.open(d_out / f"styled_frame_{i + 1:04d}.png")) for i in range(7)]
     for i in range(7):
-        assert np.array_equal(outs[1][i], outs[2][i]), i
+        assert np.array_equal(outs[1][i], outs[gpus][i]), i
+    # each rank encoded exactly its own round-robin shard (groups of `batch` frames per rank)
+    groups = F.plan_groups([(48, 64)] * 7, gpus, 2)
+    for r in range(gpus):
+        got = json.load(open(tmp_path / f"written{gpus}" / f"rank{r}.json"))["written"]
+        want = [f"frame_{f + 1:04d}" for g in groups for f in F.shard(g, gpus, r)]
+        assert got == want, (r, got, want)
 
 
 def test_bench_two_ranks_under_torchrun_gloo(tmp_path):
     """The driver's multi-GPU bench command (python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N),
     rehearsed on this one-GPU box: 2 ranks, both on GPU 0 (--device 0), gloo (exchange through host memory), with
-    the ordered gather to rank 0 (--gather).  torchrun is started as a child process (no exec from this process);
+    the video pipeline's exchange (--gather: L planes to rank 0, smoothed planes back to the owners).  torchrun is started as a child process (no exec from this process);
     rank 0 prints ONE JSON line with n_gpus 2 and the whole-job frame count.  Scaling itself is not measured here."""
     import json
     import socket
@@ -325,8 +342,7 @@ def test_bench_two_ranks_under_torchrun_gloo(tmp_path):
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["dist_backend"] == "gloo"
-    from neuralstyletransferv1_amd.frames import rank0_share
-    assert d["config"]["global_batch"] == rank0_share(2, 8) + 8
+    assert d["config"]["global_batch"] == 16
     assert d["value"] > 0 and abs(d["value"] - d["config"]["global_batch"] * 3 / (d["ms_per_step"] * 3e-3)) < 1e-3 * d["value"]
 
 

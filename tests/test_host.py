@@ -116,6 +116,95 @@ def test_ordered_gather_gloo(world, caps):
         assert vals == g  # frame j of each group is the frame itself, in order
 
 
+def _pipeline_worker(rank, world, port, q, caps=None, fail_emit=None):
+    """run_pipeline with an ordered stage on rank 0 (a running sum over the frames in order, like the LAB EMA's
+    state) and the output stage on each frame's owner."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    sizes = [(2, 3)] * 7 + [(5, 1)] * 4
+    groups = F.plan_groups(sizes, world, batch=2 if caps is None else caps[1],
+                           rank0_batch=None if caps is None else caps[0])
+    emitted, state = [], [0]
+
+    def stylize(idx):
+        h, w = sizes[idx[0]] if idx else sizes[0]
+        send = torch.stack([torch.full((h * w,), f + 1, dtype=torch.int64) for f in idx]) if idx else \
+            torch.empty((0, h * w), dtype=torch.int64)
+        return send, [f * 10 for f in idx]
+
+    def root_post(g, full):
+        out = []
+        for j in range(full.shape[0]):  # sequential: frame j's value depends on every earlier frame
+            state[0] += int(full[j, 0])
+            out.append(torch.full_like(full[j], state[0]))
+        return torch.stack(out)
+
+    def emit(idx, rows, keep):
+        if fail_emit is not None and rank == fail_emit and idx and idx[0] >= 4:
+            raise OSError("encode failed")
+        assert keep == [f * 10 for f in idx] and rows.shape[0] == len(idx)
+        emitted.extend((f, int(rows[j, 0]), rows.shape[1]) for j, f in enumerate(idx))
+
+    outcome = "ok"
+    try:
+        F.run_pipeline(groups, world, rank, stylize, root_post, emit,
+                       lambda g: ((sizes[g[0]][0] * sizes[g[0]][1],), torch.int64), caps=caps)
+    except F.RankFailed:
+        outcome = "RankFailed"
+    except OSError:
+        outcome = "OSError"
+    dist.destroy_process_group()
+    q.put((rank, outcome, emitted, [F.shard(g, world, rank, caps) for g in groups]))
+
+
+@pytest.mark.parametrize("world,caps", [(2, None), (3, None), (3, [1, 2, 2])])
+def test_pipeline_returns_each_frame_to_its_owner(world, caps):
+    """Multi-GPU output leg: rank 0 runs the ordered stage over the group's frames in order and
+    sends each frame's result back to the rank that stylized it; each rank emits (D2H + encode) exactly its own
+    frames, with the values the single-rank sequential order gives; a frame-size change mid-stream."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, q, caps)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (o, e, sh) for r, o, e, sh in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+    expect = np.cumsum(np.arange(1, 12))
+    sizes = [6] * 7 + [5] * 4
+    seen = set()
+    for r in range(world):
+        outcome, emitted, shards = res[r]
+        assert outcome == "ok"
+        assert [f for f, _, _ in emitted] == [f for sh in shards for f in sh]  # only its own frames, in order
+        for f, v, n in emitted:
+            assert v == expect[f] and n == sizes[f], (r, f, v)
+            seen.add(f)
+    assert seen == set(range(11))
+
+
+def test_pipeline_emit_failure_reaches_every_rank():
+    """An owner whose output stage raises (disk full) stops every rank."""
+    import torch.multiprocessing as mp
+    world = 3
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, q, None, 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: o for r, o, _, _ in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "RankFailed", 1: "OSError", 2: "RankFailed"}
+
+
 def _failing_worker(rank, world, port, fail_rank, fail_in, q, caps=None):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)

@@ -62,6 +62,51 @@ __global__ __launch_bounds__(256) void read_kernel(const uint4* __restrict__ in,
   if (x == 0x9e3779b9u) out[0] = x;  // practically never: keeps the loads live
 }
 
+// Contiguous-chunk forms (each workgroup streams one contiguous slice, U float4 loads in flight per thread before
+// the first store), with plain or non-temporal (nt) stores: the grid-stride form above interleaves the whole grid's
+// accesses and measured 4.65-5.08 TB/s, below the guide's 6.29 TB/s float4 copy.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_chunk_kernel(const uint4* __restrict__ in_, uint4* __restrict__ out_,
+                                                         size_t n) {
+  const u32x4_t* in = (const u32x4_t*)in_;
+  u32x4_t* out = (u32x4_t*)out_;
+  const size_t per = (size_t)256 * U;
+  for (size_t base = (size_t)blockIdx.x * per; base < n; base += (size_t)gridDim.x * per) {
+    u32x4_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + (size_t)u * 256 + threadIdx.x;
+      if (i < n) v[u] = NT ? __builtin_nontemporal_load(in + i) : in[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + (size_t)u * 256 + threadIdx.x;
+      if (i < n) {
+        if (NT) __builtin_nontemporal_store(v[u], out + i);
+        else out[i] = v[u];
+      }
+    }
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void read_chunk_kernel(const uint4* __restrict__ in, size_t n,
+                                                         unsigned* __restrict__ out) {
+  const size_t per = (size_t)256 * U;
+  unsigned x = 0;
+  for (size_t base = (size_t)blockIdx.x * per; base < n; base += (size_t)gridDim.x * per) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + (size_t)u * 256 + threadIdx.x;
+      v[u] = i < n ? in[i] : uint4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  if (x == 0x9e3779b9u) out[0] = x;
+}
+
 static uint16_t bf16_of(float f) {
   uint32_t u;
   std::memcpy(&u, &f, 4);
@@ -133,12 +178,53 @@ int main() {
     copy_gbs = std::fmax(copy_gbs, 2.0 * bytes / (copy_ms * 1e-3) / 1e9);
     read_gbs = std::fmax(read_gbs, bytes / (read_ms * 1e-3) / 1e9);
   }
+  // contiguous-chunk forms: best over unroll depth, nt, and grid size (1-8 workgroups per CU, or one slice each)
+  double chunk_copy_gbs = 0.0, chunk_read_gbs = 0.0;
+  char chunk_copy_cfg[64] = "", chunk_read_cfg[64] = "";
+  for (int wpc : {1, 2, 4, 8, 0}) {
+    auto go = [&](auto kern, int u, bool nt) -> int {
+      const size_t per = (size_t)256 * u;
+      const int gb = wpc ? cus * wpc : (int)((n + per - 1) / per);
+      const float ms = time_ms([&] { hipLaunchKernelGGL(kern, dim3(gb), dim3(256), 0, 0, a, b, n); }, 10);
+      CK(hipGetLastError());
+      const double g = 2.0 * bytes / (ms * 1e-3) / 1e9;
+      if (g > chunk_copy_gbs) {
+        chunk_copy_gbs = g;
+        std::snprintf(chunk_copy_cfg, sizeof(chunk_copy_cfg), "U%d%s wg/cu %d", u, nt ? " nt" : "", wpc);
+      }
+      return 0;
+    };
+    go(copy_chunk_kernel<4, false>, 4, false);
+    go(copy_chunk_kernel<8, false>, 8, false);
+    go(copy_chunk_kernel<4, true>, 4, true);
+    go(copy_chunk_kernel<8, true>, 8, true);
+    go(copy_chunk_kernel<16, true>, 16, true);
+    auto rd = [&](auto kern, int u) -> int {
+      const size_t per = (size_t)256 * u;
+      const int gb = wpc ? cus * wpc : (int)((n + per - 1) / per);
+      const float ms = time_ms([&] { hipLaunchKernelGGL(kern, dim3(gb), dim3(256), 0, 0, a, n, sink); }, 10);
+      CK(hipGetLastError());
+      const double g = bytes / (ms * 1e-3) / 1e9;
+      if (g > chunk_read_gbs) {
+        chunk_read_gbs = g;
+        std::snprintf(chunk_read_cfg, sizeof(chunk_read_cfg), "U%d wg/cu %d", u, wpc);
+      }
+      return 0;
+    };
+    rd(read_chunk_kernel<4>, 4);
+    rd(read_chunk_kernel<8>, 8);
+    rd(read_chunk_kernel<16>, 16);
+  }
 
   std::printf(
       "{\"device\": \"%s\", \"cus\": %d, \"mfma_bf16_16x16x32_tflops\": {\"random_2w\": %.1f, \"random_4w\": %.1f, "
       "\"zeros_2w\": %.1f, \"zeros_4w\": %.1f}, \"hbm_copy_gbs\": %.1f, \"hbm_read_gbs\": %.1f, "
-      "\"spec\": {\"mfma_bf16_tflops\": 2500, \"hbm_gbs\": 8000}}\n",
-      prop.gcnArchName, cus, mfma_tf[0][0], mfma_tf[0][1], mfma_tf[1][0], mfma_tf[1][1], copy_gbs, read_gbs);
+      "\"hbm_copy_grid_stride_gbs\": %.1f, \"hbm_read_grid_stride_gbs\": %.1f, "
+      "\"hbm_copy_chunk_gbs\": %.1f, \"hbm_copy_chunk_cfg\": \"%s\", \"hbm_read_chunk_gbs\": %.1f, "
+      "\"hbm_read_chunk_cfg\": \"%s\", \"spec\": {\"mfma_bf16_tflops\": 2500, \"hbm_gbs\": 8000}}\n",
+      prop.gcnArchName, cus, mfma_tf[0][0], mfma_tf[0][1], mfma_tf[1][0], mfma_tf[1][1],
+      std::fmax(copy_gbs, chunk_copy_gbs), std::fmax(read_gbs, chunk_read_gbs), copy_gbs, read_gbs, chunk_copy_gbs,
+      chunk_copy_cfg, chunk_read_gbs, chunk_read_cfg);
   CK(hipFree(a));
   CK(hipFree(b));
   CK(hipFree(sink));

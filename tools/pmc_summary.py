@@ -108,6 +108,13 @@ def main():
             j = out[jk]
             res["joined"] = {"kernel": jk, "avg_us_profiled": j.get("avg_us"), "hbm_bytes_per_launch": j.get("hbm_bytes"),
                              "eff_clock_ghz": j.get("eff_clock_ghz"), "algorithmic_bytes_per_launch": 2 * 530841600}
+        # NST_DT_F16M's dominant kernel (the split-operand conv2, fp32 operand and output), same passes
+        from neuralstyletransferv1_amd._lib import ws2_kernel_sha
+        mk = next((k for k in out if re.search(r"ws2_kernel<fp16, 32, 64, \d+, false, \d, true, true", k)), None)
+        if mk is not None:
+            m = out[mk]
+            res["fp16m_conv2"] = {"kernel": mk, "kernel_src_sha16": ws2_kernel_sha(), "avg_us_profiled": m.get("avg_us"),
+                                  "hbm_bytes_per_launch": m.get("hbm_bytes"), "eff_clock_ghz": m.get("eff_clock_ghz")}
         with open(sys.argv[sys.argv.index("--res-json") + 1], "w") as f:
             json.dump(res, f, indent=1)
 

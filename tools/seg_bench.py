@@ -60,7 +60,8 @@ def timed(fn, steps):
     return (time.perf_counter() - t0) / steps * 1e3
 
 
-# the mask program's dtype in the configs[4] step: sky_swap.py's default
+# the mask program's dtype in the configs[4] step: fp32s, the fastest mode holding the fp32 bars against the reference
+# logits (sky_swap.py --dtype fp32s; the CLI's default is exact fp32)
 MASK_DT = os.environ.get("SEG_MASK_DT", "fp32s")
 
 
