@@ -44,6 +44,15 @@ constexpr uint32_t OOB = 0xFFFFFF00u;  // buffer offset past every launch's reco
 #ifndef NST_WS_PK_STATS
 #define NST_WS_PK_STATS 1
 #endif
+// experiment switches (tools/build_variants.sh): the join's IN apply as one fma per value (NOT the unfused residual
+// kernel's product-then-sum arithmetic: off in the product), and s_setprio 1 for team 1 (waves 4-7, the second
+// half of the workgroup: MI355X_MICROARCH.md 'Two waves per SIMD' item 4)
+#ifndef NST_WS_JOIN_FMA
+#define NST_WS_JOIN_FMA 0
+#endif
+#ifndef NST_WS_PRIO
+#define NST_WS_PRIO 0
+#endif
 
 template <int TH, int FILL>
 struct WsCfg {
@@ -222,8 +231,8 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
       for (int j = 0; j < 4; ++j) {
         float r0 = lo16<T>(w2[j]), r1 = hi16<T>(w2[j]);
         const float4 n = ny[j];
-        const float a = lo16<T>(w[j]) * n.x + n.z;
-        const float bb = hi16<T>(w[j]) * n.y + n.w;
+        const float a = NST_WS_JOIN_FMA ? __builtin_fmaf(lo16<T>(w[j]), n.x, n.z) : lo16<T>(w[j]) * n.x + n.z;
+        const float bb = NST_WS_JOIN_FMA ? __builtin_fmaf(hi16<T>(w[j]), n.y, n.w) : hi16<T>(w[j]) * n.y + n.w;
         o[j] = pack16<T>(r0 + a, r1 + bb);
       }
     } else if constexpr (FILL == WF_RAW) {
@@ -425,6 +434,7 @@ __global__ __launch_bounds__(512) void wstat_kernel(ConvParams p) {
   }
   vm_wait<0>();
   __syncthreads();
+  if (NST_WS_PRIO && team) __builtin_amdgcn_s_setprio(1);
   // Unit schedule (u = 2q + half; region q is free once the barrier ending part q has passed):
   //   part 0: A: unit 6 of cur, request 2 of nxt    | B: unit 7 of cur, request 3 of nxt
   //   part 1: A: unit 0 of nxt, request 4 of nxt    | B: unit 1, request 5
@@ -563,14 +573,18 @@ struct WstatInst {
 #ifndef NST_WSTAT_TH
 #define NST_WSTAT_TH 8
 #endif
-constexpr int WSTAT_TH = NST_WSTAT_TH;  // tile rows
+#ifndef NST_WSTAT_TH_RES
+#define NST_WSTAT_TH_RES NST_WSTAT_TH
+#endif
+constexpr int WSTAT_TH = NST_WSTAT_TH;          // tile rows (plain trunk conv)
+constexpr int WSTAT_TH_RES = NST_WSTAT_TH_RES;  // ... of the joined variant (its staging ring takes twice the LDS)
 #define E(...) WstatInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wstat(int* count) {
   static const ConvKernelInfo table[] = {
       E(__bf16, WSTAT_TH, false),    // residual trunk
-      E(__bf16, WSTAT_TH, true),     // + residual join in the fill
+      E(__bf16, WSTAT_TH_RES, true),     // + residual join in the fill
       E(_Float16, WSTAT_TH, false),  // fp16 mode
-      E(_Float16, WSTAT_TH, true),
+      E(_Float16, WSTAT_TH_RES, true),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

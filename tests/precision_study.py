@@ -38,10 +38,58 @@ def _r(t: torch.Tensor, f: str, fmt: str) -> torch.Tensor:
     return B.rnd16(t, fmt) if f == "16" else t
 
 
+def predicted_centres(arch: str, sd, in_mean: float = 0.45):
+    """Per-layer, per-channel constant c the stored conv output is centred on ('P' storage): the conv's bias plus
+    sum W * m over its operand's predicted channel means m -- for an operand ReLU(IN(y)) the mean of ReLU over a
+    normal with IN's mean beta and std |gamma|; for the residual stream x_k the stream's mean m(x_0) + sum of
+    the joined blocks' betas; for the image, in_mean (raw byte / 256 operand of the folded first layer, in
+    encoded units here)."""
+    from math import erf, exp, pi, sqrt
+    Ls = B.LAYERS[arch]
+
+    def relu_mean(beta, gamma):
+        out = []
+        for b, g in zip(beta.tolist(), gamma.tolist()):
+            g = abs(g)
+            if g < 1e-12:
+                out.append(max(b, 0.0))
+                continue
+            t = b / g
+            out.append(g * exp(-t * t / 2) / sqrt(2 * pi) + b * 0.5 * (1 + erf(t / sqrt(2))))
+        return torch.tensor(out, dtype=torch.float64)
+
+    def centre(i, m):
+        conv = Ls[i][0]
+        W, b = sd[conv + ".weight"].double(), sd[conv + ".bias"].double()
+        if Ls[i][6] == B.ZINSERT:  # ConvTranspose: [cin, cout, k, k]
+            return (b + (W.sum(dim=(2, 3)) * m[:, None]).sum(dim=0)).float()[None, :, None, None]
+        return (b + (W.sum(dim=(2, 3)) * m[None, :]).sum(dim=1)).float()[None, :, None, None]
+
+    def norm_mean(i):
+        nm = Ls[i][1]
+        return relu_mean(sd[nm + ".bias"].double(), sd[nm + ".weight"].double())
+
+    c = [None] * len(Ls)
+    c[0] = None  # the image operand's mean depends on the frame
+    c[1], c[2] = centre(1, norm_mean(0)), centre(2, norm_mean(1))
+    nres = 4 if arch == "reconet" else 5
+    mx = norm_mean(2)
+    for r in range(nres):
+        l1, l2 = 3 + 2 * r, 4 + 2 * r
+        c[l1] = centre(l1, mx)
+        c[l2] = centre(l2, norm_mean(l1))
+        mx = mx + sd[Ls[l2][1] + ".bias"].double()
+    u1 = 3 + 2 * nres
+    c[u1] = centre(u1, mx)
+    c[u1 + 1] = centre(u1 + 1, norm_mean(u1))
+    return c
+
+
 def forward_mixed(arch: str, sd, x: torch.Tensor, spec: Spec, fmt: str = "fp16") -> torch.Tensor:
     """bf16_layers.forward_layers with per-layer rounding points (stats from the fp32 values)."""
     Ls = B.LAYERS[arch]
     n = x.shape[0]
+    centre = predicted_centres(arch, sd)
 
     def run(i, operand):
         conv, norm, cin, cout, ks, st, axis, pad, pre = Ls[i]
@@ -61,6 +109,12 @@ def forward_mixed(arch: str, sd, x: torch.Tensor, spec: Spec, fmt: str = "fp16")
         return _r(v, spec[i][1], fmt).clamp_min(0.0)
 
     def store(i, z):
+        if spec[i][2] == "C":  # fp16 of the value minus its per-(frame, channel) mean (IN is shift-invariant)
+            c = z.double().mean(dim=(2, 3), keepdim=True).float()
+            return B.rnd16(z - c, fmt) + c
+        if spec[i][2] == "P":  # ... minus a per-channel constant predicted from the weights (centre[i])
+            c = centre[i]
+            return B.rnd16(z - c, fmt) + c if c is not None else _r(z, "16", fmt)
         return _r(z, spec[i][2], fmt)
 
     z = run(0, _r(x, spec[0][1], fmt))
@@ -138,7 +192,7 @@ def main():
 
         if a.mix:
             flags = a.mix.split(",")
-            spec = [tuple("16" if c == "1" else "32" for c in f) for f in flags]
+            spec = [tuple({"1": "16", "3": "32"}.get(c, c) for c in f) for f in flags]
             print(a.mix, "rms %.4f live-max %.3f u8max %d within1 %.7f n(live>0.8) %d n(u8>1) %d" % err(spec), flush=True)
             return
         t0 = time.time()

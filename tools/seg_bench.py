@@ -130,6 +130,27 @@ def main():
                 # the part of the overlapped step the mask adds beyond the stylization alone
                 "mask_exposed_share_overlap": round(max(0.0, ov_ms - styl_ms) / ov_ms, 3),
                 "overlap_identical": bool(torch.equal(ref_out, ov_out))})
+    # a larger mask batch: one DeepLab run per `mb` frames (the masks of mb / 8 stylization steps), which amortises
+    # the latency-bound ResNet layer3 GEMMs (1,152 output pixels per 8 frames); the step below runs one mask call
+    # and mb / 8 stylize + composite steps, reported per 8 frames
+    mbs = [int(v) for v in os.environ.get("SEG_MASK_BATCHES", "16,32").split(",") if v]
+    for mb in mbs:
+        big = torch.cat([frames] * (mb // N)).contiguous()
+        mb_ms = timed(lambda: me.masks(big, ids, feather_px=3), max(3, STEPS // 2))
+        k = mb // N
+
+        def step_mb():
+            m = me.masks(big, ids, feather_px=3)
+            outs = []
+            for j in range(k):
+                st = eng.stylize_u8(frames, "imagenet_255")
+                outs.append(blend_frames(st, frames, 1.0, m[j * N:(j + 1) * N], "keep"))
+            return outs
+        ms_mb = timed(step_mb, max(3, STEPS // 2)) / k
+        same = torch.equal(step_mb()[0], ref_out)
+        out[f"mask_batch_{mb}"] = {"mask_ms_per_8_frames": round(mb_ms * N / mb, 3), "step_ms_per_8_frames": round(ms_mb, 3),
+                                   "frames_per_s": round(N / ms_mb * 1e3, 1),
+                                   "mask_share": round(mb_ms * N / mb / ms_mb, 3), "outputs_identical": bool(same)}
     if os.environ.get("SEG_GRAPH", "0") == "1":
         # launch-overhead probe: the mask program (MASK_DT) replayed from a captured HIP graph (static input / output
         # buffers); the captured kernels are the same launches on the same stream
