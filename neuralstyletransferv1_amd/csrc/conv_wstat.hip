@@ -32,7 +32,10 @@
 
 namespace nst {
 
-constexpr int WS_RING = 3;  // operand reads in flight ahead of the MFMAs
+#ifndef NST_WS_RING
+#define NST_WS_RING 3
+#endif
+constexpr int WS_RING = NST_WS_RING;  // operand reads in flight ahead of the MFMAs
 constexpr int WS_SPLIT = 1;  // read steps between a unit's staging read and its transform (0: back to back)
 constexpr uint32_t OOB = 0xFFFFFF00u;  // buffer offset past every launch's records: loads 0, stores dropped
 // the conv bias enters as the C operand of each tile row's first MFMA (bias + the K sum in the accumulator, one

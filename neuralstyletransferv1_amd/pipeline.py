@@ -747,15 +747,22 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
                 h0, w0 = styled.shape[1], styled.shape[2]
                 styled = blend_frames(styled, full[..., 3:].contiguous(), blend, _masks_for(idx, h0, w0),
                                       args.composite_mode)
-        with prof("d2h"):  # page-locked: the saves read it after one stream sync
+        with prof("d2h"):
+            # page-locked D2H on a copy stream behind the frames' last kernel; the encoders wait for its event, so
+            # this thread goes on queueing the next group's forward instead of waiting for the GPU
             host_t = torch.empty(styled.shape, dtype=torch.uint8, pin_memory=True)
-            host_t.copy_(styled, non_blocking=True)
-            torch.cuda.current_stream(dev).synchronize()
-            host = host_t.numpy()
+            copy_stream.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(copy_stream):
+                host_t.copy_(styled, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(copy_stream)
+            styled.record_stream(copy_stream)
         if not args.no_save:
             for j, f in enumerate(idx):
-                pending.append(pool.submit(_save, host[j], f))
+                pending.append(pool.submit(_save_after, ev, host_t, j, f))
                 written.append(f)
+        else:
+            pending.append(pool.submit(ev.synchronize))
         done[0] += len(idx)
         el = time.perf_counter() - t_start
         who = f" rank {rank}" if world > 1 else ""
@@ -805,6 +812,12 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         if not any_mask:
             return None
         return torch.stack(ms)
+
+    copy_stream = torch.cuda.Stream(dev)
+
+    def _save_after(ev, host_t, j: int, f: int):
+        ev.synchronize()
+        return _save(host_t[j].numpy(), f)
 
     def _save(img: np.ndarray, f: int):
         out_img = Image.fromarray(img)
