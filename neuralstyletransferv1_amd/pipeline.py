@@ -861,7 +861,8 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     if os.environ.get("NST_PIPE_WRITTEN"):  # diagnostics: the frames this rank encoded and wrote (tests)
         import json
         with open(os.path.join(os.environ["NST_PIPE_WRITTEN"], f"rank{rank}.json"), "w") as fh:
-            json.dump({"rank": rank, "world": world, "written": [names[f] for f in written]}, fh)
+            json.dump({"rank": rank, "world": world, "written": [names[f] for f in written], "loop_seconds": el,
+                       "setup_seconds": t_start - t_setup}, fh)
     if rank == 0:
         _log(f"Styled {len(src)}/{len(src)} frames in {el:.2f}s ({len(src) / max(el, 1e-9):.2f} frames/s)")
 

@@ -35,6 +35,45 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+def _run_ranks(P, args, vargv, fd, ck, ext, tmp):
+    """The frames_dir loop as `--gpus N --dist_backend gloo` (pipeline._worker per rank, as pipeline.main spawns
+    them): every rank decodes, stylizes and encodes its own round-robin shard; rank 0 runs the ordered LAB EMA
+    over the L planes.  -> (frames written, wall seconds, per-rank record)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    wdir = os.path.join(tmp, f"written_{ext}")
+    os.makedirs(wdir, exist_ok=True)
+    os.environ["NST_PIPE_WRITTEN"] = wdir
+    thr = max(1, args.threads // args.gpus)
+    argv = [a for a in vargv] + ["--dist_backend", "gloo", "--dist_timeout", "300", "--model_type", "transformer"]
+    i = argv.index("--threads")
+    argv[i + 1] = str(thr)
+    prep = (fd, Path(ck), {}, False, True)
+    out = None
+    for rep in range(2):  # warm-up, then timed
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        t0 = time.perf_counter()
+        mp.start_processes(P._worker, args=(args.gpus, argv, port, prep, None), nprocs=args.gpus, start_method="spawn")
+        t_cli = time.perf_counter() - t0
+        out = t_cli
+    del os.environ["NST_PIPE_WRITTEN"]
+    ranks = {}
+    n = 0
+    for r in range(args.gpus):
+        d = json.load(open(os.path.join(wdir, f"rank{r}.json")))
+        n += len(d["written"])
+        ranks[f"rank{r}"] = {"frames": len(d["written"]), "loop_s": round(d["loop_seconds"], 3),
+                             "loop_frames_per_s": round(len(d["written"]) / d["loop_seconds"], 2),
+                             "setup_s": round(d["setup_seconds"], 3)}
+    ranks.update({"ranks": args.gpus, "threads_per_rank": thr, "wall_s_incl_spawn": round(out, 3),
+                  "job_loop_frames_per_s": round(n / max(v["loop_s"] for k, v in ranks.items() if k.startswith("rank")), 2),
+                  "note": "gloo, every rank on GPU 0 of one box (a rehearsal of the orchestration, not a scaling run)"})
+    return n, out, ranks
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=240)
@@ -42,6 +81,10 @@ def main():
     ap.add_argument("--png_writer", default="fast", choices=["fast", "pil"])
     ap.add_argument("--formats", default="jpg,png")
     ap.add_argument("--paths", default="frames_dir,input_dir")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="frames_dir path only: N ranks (--dist_backend gloo, every rank on GPU 0 of this box, "
+                         "--threads split between them): the multi-GPU orchestration with each rank encoding its "
+                         "own frames; per-rank frames/s reported")
     args = ap.parse_args()
     from neuralstyletransferv1_amd import pipeline as P
     from neuralstyletransferv1_amd import pngio, synthetic
@@ -105,8 +148,13 @@ def main():
                 fd.mkdir(parents=True)
                 for p in paths:
                     os.link(p, fd / os.path.basename(p))
-                a = P.build_parser().parse_args(["--input_video", "x", "--output_video", "y", "--work_dir", str(wd)]
-                                                + common)
+                vargv = ["--input_video", "x", "--output_video", "y", "--work_dir", str(wd)] + common
+                if args.gpus > 1:
+                    n_out, t_cli, ranks = _run_ranks(P, args, vargv, fd, ck, ext, tmp)
+                    res[ext][path + f"_gpus{args.gpus}"] = ranks
+                    print(ext, path, args.gpus, json.dumps(ranks), flush=True)
+                    continue
+                a = P.build_parser().parse_args(vargv)
                 a.model_type = "transformer"
                 P._run_style(a, fd, Path(ck), {}, False)  # warm-up (writes the outputs once)
                 t0 = time.perf_counter()
