@@ -45,7 +45,7 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md chip ta
 HBM_PEAK_GBS = 8000.0
 # measured ceilings beside the spec: back-to-back v_mfma_f32_16x16x32_bf16 on random operands
 # at the trunk kernel's occupancy (two waves per SIMD), and a streaming copy, tools/peak_bench.hip
-PEAKS_JSON = "profiles/r05_c_peaks.json"
+PEAKS_JSON = "profiles/r05_peaks.json"
 # Algorithmic work: 307,584 FLOP and 822 B (bf16 activations) per output pixel.
 FLOP_PER_PIXEL = 307584
 BYTES_PER_PIXEL = 822

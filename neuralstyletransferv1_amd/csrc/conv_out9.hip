@@ -28,19 +28,23 @@ namespace nst {
 
 typedef __attribute__((address_space(3))) uint64_t lds_u64;  // volatile LDS loads: never merged
 
-template <int CINP, int G, int NW>
+// ESZ: LDS bytes per channel, 2 for the 16-bit modes, 4 for the split-fp16 mode (NST_DT_F32S: each 16-B chunk is
+// [hi0..3, lo0..3] of 4 fp32 channels, conv_impl.h F32Split; one 32x32x16 K step = 8 channels)
+template <int CINP, int G, int NW, int ESZ = 2>
 struct Out9Cfg {
-  static constexpr int KC = CINP / 16;            // 16-channel K blocks per tap
-  static constexpr int NCH = CINP / 8;            // 16-B chunks per pixel
+  static constexpr int KC = CINP * ESZ / 32;      // 32-byte K blocks per tap (16 channels, 8 split)
+  static constexpr int NCH = CINP * ESZ / 16;     // 16-B chunks per pixel
+  static constexpr int CPCH = 16 / ESZ;           // channels per chunk
   // LDS bytes per pixel: one 16-B pad makes the stride an odd number of 16-B slots, so the 16
   // lanes of every ds_read_b128 lane group hit 16 distinct slots (consecutive columns)
-  static constexpr int EB = CINP * 2 + 16;
+  static constexpr int EB = CINP * ESZ + 16;
   static constexpr int SW = 32 * G;               // output columns per strip
   static constexpr int LWS = SW + 8;              // input columns per strip row
   static constexpr int ROWB = LWS * EB;
   static constexpr int WAVE_LDS = 2 * ROWB;
   // weight table: [part p][block (kx, kc)][K half h][row i = 3*ky + c] x 8 bytes (4 x 16 bit); a lane's
-  // 16-B A fragment is two ds_read_b64 (parts 0 and 1, PART_BYTES apart).  The 32 lanes of one
+  // 16-B A fragment is two ds_read_b64 (parts 0 and 1, PART_BYTES apart).  Split mode: part 0 = Wh, part 1 = Wl
+  // of the same 4 channels (the two MFMAs' fragments [Wh Wh] x [xh xl] and [Wl 0] x [xh xl]).  The 32 lanes of one
   // half read 27 different rows (the rotation permutes them), i.e. 27 consecutive 8-B slots: no
   // bank conflict for any rotation (ds_read_b64 banks 32-lane groups mod 64 dwords); the 5 unused
   // rows re-read row 0's address (broadcast).  The two reads stay separate instructions: hipcc
@@ -64,7 +68,9 @@ struct Out9Cfg {
 
 template <typename T, int CINP, int G, int NW, int OUTK, bool TANH>
 __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
-  using C = Out9Cfg<CINP, G, NW>;
+  constexpr bool SPLIT = IS_SPLIT<T>;
+  using TM = std::conditional_t<SPLIT, _Float16, T>;  // the MFMA operand type
+  using C = Out9Cfg<CINP, G, NW, SPLIT ? 4 : 2>;
   constexpr int KC = C::KC, EB = C::EB;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   const int b_lane = rho * EB + 16 * h;
   // fill: item lane + 64*j -> strip column PPJ*j + lane % PPJ, chunk lane / PPJ (fixed per lane)
   const int chunk = lane / C::PPJ;
-  const int pix_bytes = p.cs * 2;
+  const int pix_bytes = p.cs * (SPLIT ? 4 : 2);  // HBM activations: fp32 in the split mode
   const int row_bytes = p.ws * pix_bytes;
   int coloff[C::IPL];
 #pragma unroll
@@ -119,9 +125,9 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
     const int sx = map_axis(x0 + p.crop_x - p.pad + col, p.ws, p.axis_mode, p.pre);
     coloff[j] = (col < C::LWS && sx >= 0) ? sx * pix_bytes + chunk * 16 : -1;
   }
-  float2 nm[8];
+  float2 nm[C::CPCH];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) nm[j] = p.in_norm[(size_t)n * p.cs + chunk * 8 + j];
+  for (int j = 0; j < C::CPCH; ++j) nm[j] = p.in_norm[(size_t)n * p.cs + chunk * C::CPCH + j];
   const char* img = (const char*)p.in + (size_t)n * p.hs * row_bytes;
   const int vy0 = o0 + p.crop_y - p.pad;
 
@@ -147,7 +153,7 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
     for (int j = 0; j < C::IPL; ++j) {
       if (C::PPJ * j + lane % C::PPJ < C::LWS) {
         const bool ok = ro >= 0 && coloff[j] >= 0;
-        const uint4 v4 = norm_chunk<T>(raw[j], nm);
+        const uint4 v4 = lds_form<T>(norm_chunk<T>(raw[j], nm));  // split: IN + ReLU in fp32, then hi / lo
         *(uint4*)(dst + j * C::PPJ * EB) = ok ? v4 : make_uint4(0u, 0u, 0u, 0u);
       }
     }
@@ -211,13 +217,19 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
       const char* ab = smem + a_off[t];
       // operands of tap column kx, double-buffered: tap kx+1's reads are issued before tap kx's
       // MFMAs, one scheduling region per tap (keeps the live operand set at two taps)
-      uint4 av[2][KC], bv[2][KC][G];
-      auto ld = [&](int kx, uint4 (&a)[KC], uint4 (&b)[KC][G]) {
+      constexpr int AF = SPLIT ? 2 : 1;  // A fragments per K block
+      uint4 av[2][KC][AF], bv[2][KC][G];
+      auto ld = [&](int kx, uint4 (&a)[KC][AF], uint4 (&b)[KC][G]) {
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
           const uint64_t a0 = *(const volatile lds_u64*)(ab + (kx * KC + kc) * C::BLK_BYTES);
           const uint64_t a1 = *(const volatile lds_u64*)(ab + (kx * KC + kc) * C::BLK_BYTES + C::PART_BYTES);
-          a[kc] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
+          if constexpr (SPLIT) {  // [Wh Wh] and [Wl 0] for the lane's chunk [xh0..3 xl0..3]
+            a[kc][0] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a0, (uint32_t)(a0 >> 32));
+            a[kc][AF - 1] = make_uint4((uint32_t)a1, (uint32_t)(a1 >> 32), 0u, 0u);
+          } else {
+            a[kc][0] = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
+          }
 #pragma unroll
           for (int gi = 0; gi < G; ++gi) b[kc][gi] = *(const uint4*)(rb + (gi * 32 + kx) * EB + kc * 32);
         }
@@ -230,7 +242,9 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
         for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
           for (int gi = 0; gi < G; ++gi)
-            acc[gi] = mfma32x32x16<T>(av[kx & 1][kc], bv[kx & 1][kc][gi], acc[gi]);
+#pragma unroll
+            for (int f = 0; f < AF; ++f)  // split: Wh * (xh + xl) + Wl * xh (~22-bit products, fp32 sums)
+              acc[gi] = mfma32x32x16<TM>(av[kx & 1][kc][f], bv[kx & 1][kc][gi], acc[gi]);
         __builtin_amdgcn_sched_barrier(0);
       }
       // slot (t+1) % 9 now holds output row v - 8: store it, then clear it for output row v + 1
@@ -250,7 +264,7 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
 
 template <typename T, int CINP, int G, int NW, int OUTK, bool TANH>
 struct Out9Inst {
-  using C = Out9Cfg<CINP, G, NW>;
+  using C = Out9Cfg<CINP, G, NW, IS_SPLIT<T> ? 4 : 2>;
   static constexpr auto kernel = out9_kernel<T, CINP, G, NW, OUTK, TANH>;
   static int cus() {
     static const int v = [] {
@@ -284,7 +298,8 @@ struct Out9Inst {
     k.mode = MODE_KYROT;
     k.ks = 9; k.stride = 1; k.cinp = CINP; k.bn = 16; k.th = 1; k.tw = C::SW; k.wm = NW; k.wn = 1;
     k.in_kind = IN_ACT; k.out_kind = OUTK;
-    k.cpc = 8; k.nch = C::NCH; k.lds_bytes = C::LDS;
+    k.cpc = C::CPCH; k.nch = C::NCH; k.lds_bytes = C::LDS;
+    k.in_esz = IS_SPLIT<T> ? 4 : 0;
     k.wbytes = C::W_BYTES;
     k.part_rows = 1;
     k.tanh_out = TANH ? 1 : 0;
@@ -307,6 +322,12 @@ struct Out9Inst {
 #ifndef NST_OUT9_J_NW
 #define NST_OUT9_J_NW 8
 #endif
+#ifndef NST_OUT9_S_G
+#define NST_OUT9_S_G 1
+#endif
+#ifndef NST_OUT9_S_NW
+#define NST_OUT9_S_NW 8
+#endif
 #define E(...) Out9Inst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_out9(int* count) {
   static const ConvKernelInfo table[] = {
@@ -319,6 +340,10 @@ const ConvKernelInfo* conv_table_out9(int* count) {
       E(_Float16, 32, 3, 8, OUT_F32_NCHW, false),
       E(_Float16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_U8_NHWC, true),
       E(_Float16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_F32_NCHW, true),
+      // split-fp16 mode (NST_DT_F32S): fp32 activations, two f16 MFMAs per K step (the x-shift generic kernel's
+      // 9-chunk LDS entries were 2-way bank-conflicted on most operand reads: 5.2 ms per batch of 8)
+      E(F32Split, 32, NST_OUT9_S_G, NST_OUT9_S_NW, OUT_U8_NHWC, false),
+      E(F32Split, 32, NST_OUT9_S_G, NST_OUT9_S_NW, OUT_F32_NCHW, false),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

@@ -398,8 +398,11 @@ std::vector<float> split_weight_frags(const ConvKernelInfo& k, const std::vector
 // MODE_KYROT weight table (conv_out9.hip): [part p][block (kx, kc)][K half h][row 3*ky + c][4],
 // element j of a row = input channel kc*16 + 8h + 4p + j (kc = 16-channel block of the padded
 // input channels), c = model output channel 0..2.
+// Split mode (NST_DT_F32S, kc = 8-channel block): element j of a row = input channel kc*8 + 4h + j, part 0 its
+// Wh = RNE16(w) (exact fp32 value here) and part 1 w - Wh, which the fp16 upload rounds to Wl = RNE16(w - Wh).
 std::vector<float> pack_kyrot_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
-  const int kc_n = k.cinp / 16, nblk = 9 * kc_n;
+  const bool split = k.dtype == NST_DT_F32S;
+  const int cpb = split ? 8 : 16, kc_n = k.cinp / cpb, nblk = 9 * kc_n;
   std::vector<float> out((size_t)k.wbytes / 2, 0.f);
   for (int pp = 0; pp < 2; ++pp)
     for (int ky = 0; ky < 9; ++ky)
@@ -408,10 +411,12 @@ std::vector<float> pack_kyrot_weights(const ConvKernelInfo& k, const LayerDef& d
           for (int hh = 0; hh < 2; ++hh)
             for (int c = 0; c < 3; ++c)
               for (int j = 0; j < 4; ++j) {
-                const int ci = kc * 16 + 8 * hh + 4 * pp + j;
+                const int ci = split ? kc * 8 + 4 * hh + j : kc * 16 + 8 * hh + 4 * pp + j;
                 if (ci >= d.cin) continue;
                 const size_t row = (((size_t)pp * nblk + kx * kc_n + kc) * 2 + hh) * 27 + 3 * ky + c;
-                out[row * 4 + j] = W[(((size_t)c * d.cin + ci) * d.ks + ky) * d.ks + kx];
+                const float w = W[(((size_t)c * d.cin + ci) * d.ks + ky) * d.ks + kx];
+                const float hi = f16_to_f32(f32_to_f16_rne(w));
+                out[row * 4 + j] = split ? (pp == 0 ? hi : w - hi) : w;
               }
   return out;
 }
@@ -1036,7 +1041,10 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     Ly.in_esz = Ly.k_main->in_esz ? Ly.k_main->in_esz : (int)act_elem_bytes(kdt);
     Ly.out_esz = Ly.k_main->out_esz ? Ly.k_main->out_esz : (int)act_elem_bytes(kdt);
     if (Ly.mode == MODE_KYROT) {
-      if ((rc = upload_packed(pack_kyrot_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;
+      const std::vector<float> pk = pack_kyrot_weights(*Ly.k_main, d, W);
+      // the split table holds its Wh / Wl parts itself: plain fp16 upload
+      if ((rc = Ly.k_main->dtype == NST_DT_F32S ? upload_weights(NST_DT_F16, pk, &Ly.wpk) : upload_packed(pk, &Ly.wpk)) != NST_OK)
+        break;
     } else if (Ly.mode == MODE_WSTAT) {
       if ((rc = upload_packed(pack_wstat_weights(d, W), &Ly.wpk)) != NST_OK) break;
     } else if (Ly.mode == MODE_WPHASE) {

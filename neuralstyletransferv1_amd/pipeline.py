@@ -757,12 +757,11 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
                 ev = torch.cuda.Event()
                 ev.record(copy_stream)
             styled.record_stream(copy_stream)
+        # one waiter thread per run waits for the copy's event and then hands the frames to the encoder pool, so no
+        # pool thread sits blocked on the GPU (the pool also decodes the next groups)
+        pending.append(waiter.submit(_hand_off, ev, host_t, list(idx) if not args.no_save else []))
         if not args.no_save:
-            for j, f in enumerate(idx):
-                pending.append(pool.submit(_save_after, ev, host_t, j, f))
-                written.append(f)
-        else:
-            pending.append(pool.submit(ev.synchronize))
+            written.extend(idx)
         done[0] += len(idx)
         el = time.perf_counter() - t_start
         who = f" rank {rank}" if world > 1 else ""
@@ -814,10 +813,12 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         return torch.stack(ms)
 
     copy_stream = torch.cuda.Stream(dev)
+    waiter = ThreadPoolExecutor(max_workers=1)
 
-    def _save_after(ev, host_t, j: int, f: int):
+    def _hand_off(ev, host_t, idx):
         ev.synchronize()
-        return _save(host_t[j].numpy(), f)
+        host = host_t.numpy()
+        return [pool.submit(_save, host[j], f) for j, f in enumerate(idx)], host_t
 
     def _save(img: np.ndarray, f: int):
         out_img = Image.fromarray(img)
@@ -852,7 +853,10 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
                 emit(sh, None, full)
     with prof("drain_saves"):
         for p in pending:
-            p.result()
+            futs, _keep = p.result()
+            for q in futs:
+                q.result()
+    waiter.shutdown()
     pool.shutdown()
     prof.report(rank)
     el = time.perf_counter() - t_start

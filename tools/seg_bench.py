@@ -133,7 +133,7 @@ def main():
     # a larger mask batch: one DeepLab run per `mb` frames (the masks of mb / 8 stylization steps), which amortises
     # the latency-bound ResNet layer3 GEMMs (1,152 output pixels per 8 frames); the step below runs one mask call
     # and mb / 8 stylize + composite steps, reported per 8 frames
-    mbs = [int(v) for v in os.environ.get("SEG_MASK_BATCHES", "16,32,64").split(",") if v]
+    mbs = [int(v) for v in os.environ.get("SEG_MASK_BATCHES", "32,64,128").split(",") if v]
     for mb in mbs:
         big = torch.cat([frames] * (mb // N)).contiguous()
         mb_ms = timed(lambda: me.masks(big, ids, feather_px=3), max(3, STEPS // 2))
