@@ -43,11 +43,11 @@ const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, 
   // 16-bit formats (bf16, fp16) share the specialised tables; an entry matches only its own dtype
   const TableFn tables_16[] = {conv_table_bf16_wl, conv_table_wstat, conv_table_wphase, conv_table_ws2, conv_table_ws9,
                                conv_table_out9, conv_table_bf16, conv_table_f16, conv_table_ws1s};
-  // 4-byte activation formats (fp32, split-fp16): the generic kernels only
-  const TableFn tables_f32[] = {conv_table_f32, conv_table_f32s};
+  // 4-byte activation formats (fp32, split-fp16): the generic kernels, and the split-fp16 row-streaming output conv
+  const TableFn tables_f32[] = {conv_table_out9, conv_table_f32, conv_table_f32s};
   const bool h16 = !f32_storage(dtype);
   const TableFn* tables = h16 ? tables_16 : tables_f32;
-  const int ntables = h16 ? 9 : 2;
+  const int ntables = h16 ? 9 : 3;
   for (int ti = (h16 && no_persistent) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
     const ConvKernelInfo* t = tables[ti](&count);

@@ -103,8 +103,8 @@ def _mask_kwargs(args):
 
 def batch_masks(args, model, used_nc: int, dev: torch.device) -> None:
     """sky_swap.py:271-366 batch_masks_from_frames, frames grouped into same-size batches of --mask_batch on the GPU
-    (the DeepLab program's ResNet layer3 GEMMs are latency-bound at the 256-px working size: 32 frames per run cost
-    0.63x the per-frame mask time of 8, profiles/r05_c_seg_bench.json)."""
+    (the DeepLab program's ResNet layer3 GEMMs are latency-bound at the 256-px working size: per frame, a run over 32
+    / 64 / 128 frames costs 0.62 / 0.56 / 0.53 of one over 8, identical masks; profiles/r05_e_seg_bench.json)."""
     fdir = Path(args.batch_frames)
     odir = Path(args.batch_out_dir or str(fdir.parent / "masks"))
     odir.mkdir(parents=True, exist_ok=True)
@@ -187,7 +187,7 @@ def main(argv=None) -> int:
     ap.add_argument("--debug_pred", action="store_true")
     ap.add_argument("--debug_overlay", action="store_true")
     ap.add_argument("--transpose", choices=["none", "rot90", "rot270", "flip_h", "flip_v"], default="none")
-    ap.add_argument("--mask_batch", type=int, default=32,
+    ap.add_argument("--mask_batch", type=int, default=128,
                     help="frames per DeepLab run (build addition; masks are identical for any value)")
     ap.add_argument("--morph_close_ks", type=int, default=5,
                     help="accepted for compatibility: the reference never passes it on (infer_mask always closes 5x5)")
