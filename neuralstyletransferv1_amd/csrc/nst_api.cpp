@@ -93,6 +93,9 @@ struct Layer {
   // (fold_first_layer; nullptr where the fold does not hold), used with the raw-byte staging (ConvParams::enc_raw)
   void* wpk_fold[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   float* bias_fold[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // NST_DT_F32S image layer: the kernel that runs uint8 frames of a folded preset (the split-weight 9x9 kernel over
+  // the pre-padded raw bytes, wpk_fold / bias_fold); float frames and unfolded presets keep k_main / k_alt
+  const ConvKernelInfo* k_u8fold = nullptr;
 };
 
 // Program steps
@@ -664,7 +667,7 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
                 " needs " + std::to_string(std::max(fin, fout)) + " bytes per frame (limit 2^31)";
         return P;
       }
-      if (op.src == B_IMG && Ly.prepad) {  // bf16 x4 per pixel over the conv's padded input extent
+      if (op.src == B_IMG && (Ly.prepad || Ly.k_u8fold)) {  // 16-bit x4 per pixel over the conv's padded input extent
         // + zeroed tail slack (prepad_slack_rows): the 9x9 kernel's last tile row reads up to 16 halo rows
         // (and a pixel of column wrap) from its tile origin, which may lie past the last frame's padded extent
         const int wpad = cw + Ly.d.ks - 1;
@@ -691,11 +694,13 @@ Plan make_plan(const nst_handle* h, int n, int H, int W) {
         bh[op.dst] = ch; bw[op.dst] = cw; be[op.dst] = Ly.out_esz;
         const size_t bytes = (size_t)n * ch * cw * Ly.coutp * Ly.out_esz;
         if (bytes > P.buf_bytes[op.dst]) P.buf_bytes[op.dst] = bytes;
-        int ttx, tty;
-        tile_grid(*Ly.k_main, sh, sw, ch, cw, &ttx, &tty);
-        const int tiles = ttx * tty;
-        const size_t pf = (size_t)n * tiles * Ly.k_main->part_rows * Ly.coutp * 2;
-        if (pf > P.partial_floats) P.partial_floats = pf;
+        for (const ConvKernelInfo* kk : {Ly.k_main, Ly.k_u8fold}) {
+          if (!kk) continue;
+          int ttx, tty;
+          tile_grid(*kk, sh, sw, ch, cw, &ttx, &tty);
+          const size_t pf = (size_t)n * ttx * tty * kk->part_rows * Ly.coutp * 2;
+          if (pf > P.partial_floats) P.partial_floats = pf;
+        }
         const size_t sb = (size_t)n * IN_MAX_SEGMENTS * Ly.coutp * 16;
         if (sb > P.seg_bytes) P.seg_bytes = sb;
       }
@@ -1069,6 +1074,26 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       }
       if (rc != NST_OK) break;
     }
+    // NST_DT_F32S over uint8 frames: raw byte / 256 is exact in fp16, so NST_DT_F16M's split-weight 9x9 kernel (fp16
+    // hi / lo weight pairs, fp32 accumulate and output) over the folded encode computes what the split-operand
+    // generic kernel computes for those frames (its lo operand half is zero) at conv_ws9.hip's rate
+    if (image_in && compute_dtype == NST_DT_F32S && d.stride == 1 &&
+        !(flags & (NST_KSEL_NO_FOLD | NST_KSEL_NO_WS9 | NST_KSEL_NO_PREPAD))) {
+      const ConvKernelInfo* kf = find_conv_kernel(NST_KDT_SW_O32, MODE_WS9, d.ks, d.stride, 4, Ly.coutp, IN_ACT, OUT_ACT, 0, no_pers);
+      if (kf && kf->out_esz == Ly.out_esz && kf->bn == Ly.coutp) {
+        for (int pr = 1; pr < 8 && rc == NST_OK; ++pr) {
+          std::vector<float> Wf, bfo;
+          if (!fold_first_layer(d, W, b, pr, Wf, bfo)) continue;
+          if ((rc = upload_weights(NST_DT_F16, split_weight_frags(*kf, pack_ws9_weights(*kf, d, Wf.data())), &Ly.wpk_fold[pr])) != NST_OK)
+            break;
+          std::vector<float> bpad(Ly.coutp, 0.f);
+          std::copy(bfo.begin(), bfo.end(), bpad.begin());
+          rc = upload(bpad.data(), bpad.size() * 4, (void**)&Ly.bias_fold[pr]);
+        }
+        if (rc != NST_OK) break;
+        Ly.k_u8fold = kf;
+      }
+    }
     std::vector<float> bp(Ly.coutp, 0.f), gp(Ly.coutp, 0.f), btp(Ly.coutp, 0.f);
     for (int c = 0; c < d.cout; ++c) {
       bp[c] = b[c];
@@ -1223,6 +1248,13 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     const ConvKernelInfo* k = Ly.k_main;
     if (image_in && x_fmt == NST_IO_F32_NCHW) k = Ly.k_alt;
     if (final_out && y_fmt == NST_IO_F32_NCHW) k = Ly.k_alt;
+    // uint8 frames through a first layer with this preset folded in: stage the raw bytes (exact operand)
+    const bool fold = image_in && x_fmt == NST_IO_U8_NHWC && preset >= 0 && preset < 8 && Ly.wpk_fold[preset] != nullptr &&
+                      (Ly.prepad || Ly.k_u8fold);
+    if (fold && Ly.k_u8fold) k = Ly.k_u8fold;
+    const bool prepad = Ly.prepad || (fold && Ly.k_u8fold);
+    const int mode = fold && Ly.k_u8fold ? MODE_WS9 : Ly.mode;
+    const int kdt = fold && Ly.k_u8fold ? NST_KDT_SW_O32 : Ly.kdt;
     ConvParams p;
     std::memset(&p, 0, sizeof(p));
     p.in = image_in ? x : bufs[op.src];
@@ -1231,7 +1263,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     p.cs = image_in ? 3 : Ly.cinp;
     p.axis_mode = Ly.d.axis_mode;
     p.pad = Ly.d.axis_mode == AX_ZINSERT ? 1 : Ly.d.pad;
-    if (Ly.mode == MODE_PHASE || Ly.mode == MODE_WPHASE) {
+    if (mode == MODE_PHASE || mode == MODE_WPHASE) {
       // source-grid halo of one pixel; nearest-x2 reflect(1) == clamp on the source grid,
       // ConvTranspose reads zeros past the edge
       p.axis_mode = Ly.d.axis_mode == AX_ZINSERT ? AX_ZERO : AX_CLAMP;
@@ -1255,17 +1287,14 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     if (image_in && x_fmt == NST_IO_F32_NCHW && preset == NST_PRESET_NONE) {
       for (int c = 0; c < 3; ++c) { p.enc_a[c] = 1.f; p.enc_b[c] = 0.f; p.enc_d[c] = 1.f; p.enc_perm[c] = c; }
     }
-    // uint8 frames through a first layer with this preset folded in: stage the raw bytes (exact operand)
-    const bool fold = image_in && Ly.prepad && x_fmt == NST_IO_U8_NHWC && preset >= 0 && preset < 8 &&
-                      Ly.wpk_fold[preset] != nullptr;
     p.enc_raw = fold ? 1 : 0;
-    if (image_in && Ly.prepad) {
+    if (image_in && prepad) {
       // resolve padding + encode once into the workspace, then run the conv over it with an
       // identity coordinate map (pad 0, no reflection)
       const int hp = P.ch[i] + Ly.d.ks - 1, wp = P.cw[i] + Ly.d.ks - 1;
       void* pre = ws + P.off_pre;
       // the staged operand's format: bf16, or fp16 (the fp16 mode and NST_DT_F16M's split-weight first layer)
-      const int pdt = (Ly.kdt == NST_DT_F16 || Ly.kdt == NST_KDT_SW_O32 || Ly.kdt == NST_KDT_SW_O16) ? NST_DT_F16 : NST_DT_BF16;
+      const int pdt = (kdt == NST_DT_F16 || kdt == NST_KDT_SW_O32 || kdt == NST_KDT_SW_O16) ? NST_DT_F16 : NST_DT_BF16;
       hipError_t e = launch_prepad_encode(pdt, p, x_fmt == NST_IO_U8_NHWC ? IN_U8_NHWC : IN_F32_NCHW, n, hp, wp, pre, st);
       if (e != hipSuccess) { set_error(std::string("prepad launch: ") + hipGetErrorString(e)); return NST_E_HIP; }
       p.in = pre;
@@ -1279,7 +1308,7 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     p.dec_tanh = (is_reconet(h->arch) && final_out) ? 1 : 0;
     p.wpk = fold ? Ly.wpk_fold[preset] : Ly.wpk;
     p.bias = fold ? Ly.bias_fold[preset] : Ly.bias;
-    if (Ly.mode == MODE_XSHIFT && final_out && y_fmt == NST_IO_U8_NHWC && pc.dperm[0] == 2) {
+    if (mode == MODE_XSHIFT && final_out && y_fmt == NST_IO_U8_NHWC && pc.dperm[0] == 2) {
       p.wpk = Ly.wpk_rev;  // decode channel c from model channel 2-c (caffe_bgr)
       p.bias = Ly.bias_rev;
     }
@@ -1295,33 +1324,33 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     tile_grid(*k, p.hs, p.ws, p.oh, p.ow, &p.tiles_x, &p.tiles_y);
     p.n_cblk = Ly.coutp / k->bn;
     if (p.res_out != nullptr && p.res_r == nullptr &&
-        ((Ly.mode != MODE_WSTAT && Ly.mode != MODE_STD) || p.in_norm == nullptr || Ly.d.stride != 1)) {
+        ((mode != MODE_WSTAT && mode != MODE_STD) || p.in_norm == nullptr || Ly.d.stride != 1)) {
       set_error("conv " + Ly.d.conv + ": only the trunk kernels (weight-stationary / generic stride-1) write their "
                 "normalised input");
       return NST_E_SHAPE;
     }
-    if (Ly.mode == MODE_WSTAT && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out == nullptr || p.res_relu)) {
+    if (mode == MODE_WSTAT && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out == nullptr || p.res_relu)) {
       set_error("conv " + Ly.d.conv + ": weight-stationary kernel joins IN(y) + r into a residual-stream buffer");
       return NST_E_SHAPE;
     }
-    if (Ly.mode == MODE_WS2 && (p.in_norm == nullptr || p.res_r != nullptr || p.crop_x || p.crop_y)) {
+    if (mode == MODE_WS2 && (p.in_norm == nullptr || p.res_r != nullptr || p.crop_x || p.crop_y)) {
       set_error("conv " + Ly.d.conv + ": weight-stationary down-conv reads a normalized activation, uncropped");
       return NST_E_SHAPE;
     }
-    if (Ly.mode == MODE_WS9 && (!Ly.prepad || p.in_norm != nullptr || p.res_r != nullptr || p.crop_x || p.crop_y || final_out)) {
+    if (mode == MODE_WS9 && (!prepad || p.in_norm != nullptr || p.res_r != nullptr || p.crop_x || p.crop_y || final_out)) {
       set_error("conv " + Ly.d.conv + ": weight-stationary 9x9 kernel reads the pre-padded frame, uncropped");
       return NST_E_SHAPE;
     }
-    if (Ly.mode == MODE_WS1S && (p.res_r != nullptr || p.res_out != nullptr || p.crop_x || p.crop_y)) {
+    if (mode == MODE_WS1S && (p.res_r != nullptr || p.res_out != nullptr || p.crop_x || p.crop_y)) {
       set_error("conv " + Ly.d.conv + ": split-operand trunk kernel runs plain convs, uncropped");
       return NST_E_SHAPE;
     }
-    if ((Ly.mode == MODE_WPHASE || Ly.mode == MODE_WSTAT || Ly.mode == MODE_WS2 || Ly.mode == MODE_WS9 ||
-         Ly.mode == MODE_WS1S) && p.cout_stride != k->bn) {
+    if ((mode == MODE_WPHASE || mode == MODE_WSTAT || mode == MODE_WS2 || mode == MODE_WS9 ||
+         mode == MODE_WS1S) && p.cout_stride != k->bn) {
       set_error("conv " + Ly.d.conv + ": weight-stationary kernels store whole pixels of bn channels");
       return NST_E_SHAPE;
     }
-    if (Ly.mode == MODE_WPHASE && p.res_r != nullptr &&
+    if (mode == MODE_WPHASE && p.res_r != nullptr &&
         (p.in_norm == nullptr || p.res_out != nullptr || p.res_relu || p.res_rnorm != nullptr)) {
       set_error("conv " + Ly.d.conv + ": weight-stationary phase kernel joins IN(y) + r without writing the stream");
       return NST_E_SHAPE;

@@ -148,6 +148,27 @@ def test_1080p_fp32s_vs_oracle():
     assert d.max() <= 1 and (d > 0).mean() < 0.01
 
 
+@pytest.mark.parametrize("arch,preset", [("johnson", "imagenet_255"), ("johnson", "caffe_bgr"), ("nst", "raw_01")])
+def test_fp32s_u8_first_layer_fold(arch, preset):
+    """NST_DT_F32S runs uint8 frames of a foldable preset on the split-weight 9x9 kernel (conv_ws9.hip SW, NST_DT_F16M's
+    first layer): raw byte / 256 is exact in fp16 and the io_preset encode is folded into the weights.  Its raw
+    output from the uint8 frames stays within the fp32 bar (1e-4 of the magnitude) of the oracle's fp32 forward of the
+    encoded frames, and as close as the split-operand kernel's output from the same frames given as float input."""
+    sd = synthetic.make_state_dict(arch, 0)
+    frames = synthetic.make_frames(2, 72, 100, seed=7)
+    x = O.encode(O.to_tensor01(frames), preset)
+    ref = O.forward(arch, sd, x).numpy()
+    eng = _net(arch, 0, "fp32s").engine(torch.device("cuda", 0))
+    y_u8, ops, _ = eng.forward_capture(torch.from_numpy(frames).cuda(), "u8", preset, "f32")
+    y_f = eng.forward_tensor(x.cuda())
+    scale = np.abs(ref).max()
+    rel_u8 = np.abs(y_u8.cpu().numpy() - ref).max() / scale
+    rel_f = np.abs(y_f.cpu().numpy() - ref).max() / scale
+    print(f"{arch} {preset} fp32s: raw rel from u8 (folded) {rel_u8:.3e}, from float {rel_f:.3e}")
+    assert rel_u8 <= FP32_REL_TOL and rel_f <= FP32_REL_TOL
+    assert rel_u8 <= 4 * rel_f + 1e-6
+
+
 _BENCH8 = {}
 
 
