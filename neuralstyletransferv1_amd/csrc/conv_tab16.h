@@ -19,6 +19,9 @@
                                        // two waves per SIMD): 0.968 -> 0.735 ms per conv and batch of 8 (r04 sweep;
                                        // 2 x 2 waves 0.968, 4 x 2 0.792, 4 x 1 0.978; r03: 8 x 16 tiles 1.12)
 #endif
+#ifndef NST_R_TRUNK_RES_TILE
+#define NST_R_TRUNK_RES_TILE NST_R_TRUNK_TILE  // ... its joined form (the residual join in the fill)
+#endif
 #ifndef NST_R_C1_TILE
 #define NST_R_C1_TILE 16, 16, 4, 2  // ReCoNet 9x9 first layer (48 -> 64 channels): 8 waves on 16 x 16 tiles, 1.064 ->
                                     // 0.93 ms (r04 sweeps: 16 x 32 1.008, 8 x 64 1.345)
@@ -55,8 +58,12 @@ const ConvKernelInfo* conv_table_16(int* count) {
       // consumers of the residual stream (residual join fused into the fill)
       E(B, SD, 3, 1, 128, 128, 8, 16, 2, 2, IN_ACT, OUT_ACT, VAR_RES),
       E(B, PH, 3, 1, 128, 64, NST_D1_TILE, IN_ACT, OUT_ACT, VAR_RES),
-      E(B, SD, 3, 1, 192, 192, NST_R_TRUNK_TILE, IN_ACT, OUT_ACT, VAR_RES),
+      E(B, SD, 3, 1, 192, 192, NST_R_TRUNK_RES_TILE, IN_ACT, OUT_ACT, VAR_RES),
       E(B, PH, 3, 1, 192, 128, NST_R_UP1_TILE, IN_ACT, OUT_ACT, VAR_RES),
+      // the decoder's 96-channel stream unpadded (nst_api.cpp: ReCoNet layers 11 / 12)
+      E(B, PH, 3, 1, 192, 96, NST_R_UP1_TILE, IN_ACT, OUT_ACT),
+      E(B, PH, 3, 1, 192, 96, NST_R_UP1_TILE, IN_ACT, OUT_ACT, VAR_RES),
+      E(B, PH, 3, 1, 96, 64, NST_D1_TILE, IN_ACT, OUT_ACT),
       E(B, SD, 9, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_U8_NHWC),
       E(B, SD, 9, 1, 64, 16, 8, 32, 4, 1, IN_ACT, OUT_F32_NCHW),
   };

@@ -14,7 +14,7 @@
 //     y - ty for both y-taps, so each read feeds two MFMAs per 16-channel subtile.
 //   * K order part-major (part q = input channels 32q..32q+31 = one K step per tap); the next tile's
 //     halo streams in by LDS-DMA into a 4-slot staging ring (conv_wstat.hip's schedule, generalised
-//     to 2 or 4 parts) and is consumed (IN + ReLU / residual join) into each region once freed.
+//     to 2, 3 or 4 parts) and is consumed (IN + ReLU / residual join) into each region once freed.
 //   * one InstanceNorm partial row per phase and tile (part_rows = 4).
 #include <algorithm>
 #include <cstring>
@@ -42,7 +42,9 @@ struct WpCfg {  // SW: staged tensors per unit (2: the residual join's y and r, 
   static constexpr int EB = (NCH + 2) * 16;       // 2 x odd chunks
   static constexpr int QENT = NENT / 4;           // entries per wave and unit (four waves per chunk)
   static constexpr int NFMAX = NF;                // frames per launch (IN tables resident in LDS)
-  static constexpr int NSLOT = 4;
+  // staging slots: unit u lands in slot u % NSLOT and unit u + 4 is requested once u is consumed, so the ring must
+  // divide a tile's units (three parts: one slot per unit)
+  static constexpr int NSLOT = NUNIT % 4 == 0 ? 4 : NUNIT;
   static constexpr int SLOTB = SW * NW * 1024;    // [y | r] x wave x lane x 16 B
   static constexpr int MAPB = ((LH + LW) * 4 + 15) / 16 * 16;
   static constexpr int MAP_OFF = NENT * EB;
@@ -66,7 +68,7 @@ struct WpCfg {  // SW: staged tensors per unit (2: the residual join's y and r, 
   static constexpr int LDS = OST ? OUT_OFF + OUTB : OUT_OFF;
   static_assert(!OST || NST * NT * 16 == 2 * TH * ROWB, "whole 16-B stores per thread");
   static constexpr int WBYTES = NW * NSTEP * NSUBW * 64 * 16;
-  static_assert(CINP % 32 == 0 && COUT % 32 == 0 && (NPART == 2 || NPART == 4), "channel shapes");
+  static_assert(CINP % 32 == 0 && COUT % 32 == 0 && NPART >= 2 && NPART <= 4, "channel shapes");
   static_assert(NENT % 4 == 0 && QENT <= 64, "four waves per unit chunk, one item per lane");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     }
   } else {
 #pragma unroll
-    for (int u = 0; u < C::NSLOT; ++u) request(cur.n, u, xd);
+    for (int u = 0; u < 4; ++u) request(cur.n, u, xd);
     const Work n1 = decode(min(wn, last));
 #pragma unroll
     for (int u = 0; u < U - 2; ++u) {
@@ -455,8 +457,8 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
           }
         },
         [&](int q) {
-          if constexpr (C::NPART == 4) {
-            if (q == 0) build_maps(nxt2, cs);  // published by the barriers ending parts 1 and 2
+          if constexpr (C::NPART >= 3) {
+            if (q == 0) build_maps(nxt2, cs);  // published by the barrier ending part 1 (read in part 2)
           } else {
             // two parts: the tile after nxt2 into nxt's slot (nxt's sources were resolved in
             // part 1); published by the next iteration's first barrier
@@ -542,6 +544,10 @@ struct WphaseInst {
 #endif
 constexpr int WP1_TH = NST_WP1_TH;  // 128 -> 64: 8 rows spill (6 rows too: 40-52 B of scratch per lane, r04) (128 weight + 64 accumulator VGPRs); 4 leaves LDS room for the staged output tile
 constexpr int WP1_NF = 8;  // frames per launch (IN tables in LDS)
+#ifndef NST_WPR_TH
+#define NST_WPR_TH 6
+#endif
+constexpr int WPR_TH = NST_WPR_TH;  // ReCoNet 96 -> 64 tile rows: 6 (0.81-0.87 ms per batch of 8) over 4 (0.92-0.97) and 2 (1.38); 8 leaves no LDS for the staged output tile (2.9)
 #define E(...) WphaseInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wphase(int* count) {
   static const ConvKernelInfo table[] = {
@@ -549,9 +555,11 @@ const ConvKernelInfo* conv_table_wphase(int* count) {
       E(__bf16, 128, 64, WP1_TH, WP1_NF, false),    // deconv1 / up1
       E(__bf16, 128, 64, WP1_TH, WP1_NF, true),     // deconv1 joining the last residual block (fused join)
       E(__bf16, 64, 32, 12, 8, false),              // deconv2 / up2: 12 rows (540 = 45 tiles) fit with one-tensor slots
+      E(__bf16, 96, 64, WPR_TH, 8, false),          // ReCoNet decoder 96 -> 48 (padded to 64; three parts)
       E(_Float16, 128, 64, WP1_TH, WP1_NF, false),  // fp16 mode
       E(_Float16, 128, 64, WP1_TH, WP1_NF, true),
       E(_Float16, 64, 32, 12, 8, false),
+      E(_Float16, 96, 64, WPR_TH, 8, false),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

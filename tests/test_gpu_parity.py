@@ -473,7 +473,7 @@ def test_weight_stationary_trunk_batch_chunks():
 @pytest.mark.parametrize("arch,h,w", [
     ("johnson", 70, 90),      # nearest-x2 up-convs over 18x23 / 35x45 sources: ragged tiles, fused join
     ("nst", 72, 100),         # ConvTranspose2d phases (zeros past the edge), pre-reflect 40
-    ("reconet", 61, 90),      # 96 -> 48 up-conv padded to 128 -> 64 (the 192-channel one stays generic)
+    ("reconet", 61, 90),      # 96 -> 48 up-conv (three 32-channel parts; 48 padded to 64; the 192 -> 96 one stays generic)
     ("johnson", 1080, 1920),  # the bench shape (270x480 and 540x960 sources), one frame
 ])
 def test_weight_stationary_upconv_vs_generic(arch, h, w):
@@ -492,6 +492,25 @@ def test_weight_stationary_upconv_vs_generic(arch, h, w):
     d = np.abs(a.astype(int) - b.astype(int))
     assert d.mean() < 0.5 and (d > 2).mean() < 0.01, (d.mean(), (d > 2).mean(), d.max())
     assert np.abs(ya - yb).max() <= 3e-2 * np.abs(yb).max(), np.abs(ya - yb).max() / np.abs(yb).max()
+
+
+@pytest.mark.parametrize("arch,h,w", [("reconet", 61, 90), ("reconet_frn", 72, 100), ("reconet", 1080, 1920)])
+def test_reconet_unpadded_decoder_vs_padded(arch, h, w):
+    """ReCoNet's decoder stream (decoder.layers.1 -> .3, 96 channels) runs unpadded in the 16-bit modes: the 192 -> 96
+    up-conv computes 96 output channels and the 96 -> 48 one three 32-channel K parts.  The padded program
+    (NST_KSEL_PAD_DECODER: 128-channel stride) adds zero weights times zero-valued channels only, so the two agree to
+    the fp32 rounding of the same sums (measured: identical)."""
+    frames = torch.from_numpy(synthetic.make_frames(2 if h < 512 else 1, h, w, seed=25)).cuda()
+    x = torch.randn(frames.shape[0], 3, h, w, generator=torch.Generator().manual_seed(7)).cuda()
+    fast = _net(arch, 11, "bf16")
+    a, ya = fast.stylize_frames(frames, "imagenet_255").cpu().numpy(), fast(x).cpu().numpy()
+    ref = _net(arch, 11, "bf16", {"pad_decoder"})
+    b, yb = ref.stylize_frames(frames, "imagenet_255").cpu().numpy(), ref(x).cpu().numpy()
+    d = np.abs(a.astype(int) - b.astype(int))
+    print(f"{arch} {h}x{w}: frames identical {bool((d == 0).all())}, max {d.max()}; raw max rel "
+          f"{np.abs(ya - yb).max() / np.abs(yb).max():.3e}")
+    assert d.max() <= 1 and (d > 0).mean() < 1e-3
+    assert np.abs(ya - yb).max() <= 1e-3 * np.abs(yb).max()
 
 
 @pytest.mark.parametrize("arch,h,w", [
