@@ -74,7 +74,39 @@ __global__ __launch_bounds__(256) void prepad_encode_u8_kernel(ConvParams p, int
   for (int j = 0; j < PREP_PX; ++j) sxs[j] = x0 + j < wp ? map_axis(x0 + j - p.pad, p.ws, p.axis_mode, p.pre) : -1;
   const bool run = sxs[0] >= 0 && sxs[PREP_PX - 1] == sxs[0] + PREP_PX - 1;
   const int pr0 = p.enc_perm[0], pr1 = p.enc_perm[1], pr2 = p.enc_perm[2];
-  for (int y = blockIdx.y * PREP_ROWS; y < min(hp, (int)(blockIdx.y + 1) * PREP_ROWS); ++y) {
+  const int ybeg = blockIdx.y * PREP_ROWS;
+  // interior column run of a whole block of rows with dword-aligned rows: every row's 3 dwords are requested before
+  // the first is used (one HBM latency per block of rows instead of one per row: the pass ran at ~2.6 TB/s)
+  if (run && ybeg + PREP_ROWS <= hp && (p.ws * 3) % 4 == 0 && ((uintptr_t)p.in & 3) == 0 && (sxs[0] * 3) % 4 == 0 &&
+      x0 + PREP_PX <= wp && ((((size_t)n * hp + ybeg) * wp + x0) & 1) == 0 && (wp & 1) == 0) {
+    uint32_t dw[PREP_ROWS][3];
+    bool live[PREP_ROWS];
+#pragma unroll
+    for (int r = 0; r < PREP_ROWS; ++r) {
+      const int sy = map_axis(ybeg + r - p.pad, p.hs, p.axis_mode, p.pre);
+      live[r] = sy >= 0;
+      const uint32_t* d = (const uint32_t*)((const uint8_t*)p.in + ((size_t)n * p.hs + (sy < 0 ? 0 : sy)) * p.ws * 3 +
+                                            (size_t)sxs[0] * 3);
+      dw[r][0] = d[0];
+      dw[r][1] = d[1];
+      dw[r][2] = d[2];
+    }
+#pragma unroll
+    for (int r = 0; r < PREP_ROWS; ++r) {
+      auto byte = [&](int k) { return (dw[r][k >> 2] >> (8 * (k & 3))) & 255u; };
+      uint32_t w[2 * PREP_PX];
+#pragma unroll
+      for (int j = 0; j < PREP_PX; ++j) {
+        w[2 * j] = live[r] ? ((uint32_t)lut[0][byte(3 * j + pr0)] | ((uint32_t)lut[1][byte(3 * j + pr1)] << 16)) : 0u;
+        w[2 * j + 1] = live[r] ? ((uint32_t)lut[2][byte(3 * j + pr2)] | ((uint32_t)pack16<T>(0.f, 0.f) & 0xffff0000u)) : 0u;
+      }
+      uint4* o = (uint4*)((uint2*)out + ((size_t)n * hp + ybeg + r) * wp + x0);
+      o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+    return;
+  }
+  for (int y = ybeg; y < min(hp, ybeg + PREP_ROWS); ++y) {
     const int sy = map_axis(y - p.pad, p.hs, p.axis_mode, p.pre);
     const uint8_t* row = (const uint8_t*)p.in + ((size_t)n * p.hs + (sy < 0 ? 0 : sy)) * p.ws * 3;
     uint32_t w[2 * PREP_PX];

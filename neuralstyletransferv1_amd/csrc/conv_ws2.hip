@@ -33,6 +33,10 @@
 namespace nst {
 
 constexpr int W2_RING = 3;  // operand reads in flight ahead of the MFMAs
+// !PF fill: halo slots loaded per round (each round's HBM latency is exposed: the K loop is over)
+#ifndef NST_W2_FD_B
+#define NST_W2_FD_B 16  // all of them (NPF <= 16): conv3 SPL 0.64 -> 0.56 ms over 4 per round (r05_k)
+#endif
 
 // SPL (the split-precision modes' down-convs): fp32 input; the fill stages each normalised value v as an fp16
 // pair xh = RNE(v), xl = RNE(v - xh) in two planes of the LDS entry ([xh: CINP x 2 B][xl: CINP x 2 B]); the
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) nsp[j] = p.in_norm[(size_t)wk.n * p.cs + 4 * fc + j];
     }
-    constexpr int B = 4;  // slots in flight
+    constexpr int B = NST_W2_FD_B < C::NPF ? NST_W2_FD_B : C::NPF;  // slots in flight
 #pragma unroll
     for (int k0 = 0; k0 < C::NPF; k0 += B) {
       uint4 v[B];

@@ -7,7 +7,7 @@ TAG=$1; shift
 for r in 1 2; do
   for v in default "$@"; do
     if [ "$v" = default ]; then unset NST_HIP_LIB; else export NST_HIP_LIB="sweep/libnst_hip_$v.so"; fi
-    timeout -k 10 200 python -u tools/mode_profile.py bf16 reconet > gpurun_out/ab_${TAG}_${v}_$r.json 2> gpurun_out/ab_${TAG}_${v}_$r.err || { echo "variant $v failed"; tail -5 gpurun_out/ab_${TAG}_${v}_$r.err; exit 1; }
+    timeout -k 10 200 python -u tools/mode_profile.py ${AB_ARGS:-bf16 reconet} > gpurun_out/ab_${TAG}_${v}_$r.json 2> gpurun_out/ab_${TAG}_${v}_$r.err || { echo "variant $v failed"; tail -5 gpurun_out/ab_${TAG}_${v}_$r.err; exit 1; }
     python3 tools/ab_line.py "$v" gpurun_out/ab_${TAG}_${v}_$r.json
   done
 done
