@@ -118,7 +118,9 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
                                             precision margin: live max 0.920 instead of 0.958 LSB; ~10 % slower) */
 #define NST_KSEL_PAD_DECODER 0x400       /* ReCoNet, 16-bit modes: the decoder's 96-channel stream padded to 128
                                             channels, as the encoder's (default: unpadded) */
-#define NST_KSEL_ALL 0x7ff
+#define NST_KSEL_PAD_ENCODER 0x800       /* ReCoNet, 16-bit modes: the encoder's 96-channel map padded to 128 (default:
+                                            unpadded) */
+#define NST_KSEL_ALL 0xfff
 int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                   unsigned flags, nst_handle** out);
 void nst_destroy(nst_handle* h);

@@ -22,6 +22,9 @@
 #ifndef NST_R_TRUNK_RES_TILE
 #define NST_R_TRUNK_RES_TILE NST_R_TRUNK_TILE  // ... its joined form (the residual join in the fill)
 #endif
+#ifndef NST_R_DOWN2_96_TILE
+#define NST_R_DOWN2_96_TILE NST_R_DOWN2_TILE  // ... with its input unpadded (96 channels)
+#endif
 #ifndef NST_R_C1_TILE
 #define NST_R_C1_TILE 16, 16, 4, 2  // ReCoNet 9x9 first layer (48 -> 64 channels): 8 waves on 16 x 16 tiles, 1.064 ->
                                     // 0.93 ms (r04 sweeps: 16 x 32 1.008, 8 x 64 1.345)
@@ -53,6 +56,9 @@ const ConvKernelInfo* conv_table_16(int* count) {
       E(B, SD, 9, 1, 4, 64, NST_R_C1_TILE, IN_U8_NHWC, OUT_ACT),
       E(B, SD, 9, 1, 4, 64, NST_R_C1_TILE, IN_F32_NCHW, OUT_ACT),
       E(B, SD, 3, 2, 128, 192, NST_R_DOWN2_TILE, IN_ACT, OUT_ACT),
+      // the encoder's 96-channel map unpadded (nst_api.cpp: ReCoNet layers 1 / 2)
+      E(B, SD, 3, 2, 64, 96, NST_C3_TILE, IN_ACT, OUT_ACT),
+      E(B, SD, 3, 2, 96, 192, NST_R_DOWN2_96_TILE, IN_ACT, OUT_ACT),
       E(B, SD, 3, 1, 192, 192, NST_R_TRUNK_TILE, IN_ACT, OUT_ACT),
       E(B, PH, 3, 1, 192, 128, NST_R_UP1_TILE, IN_ACT, OUT_ACT),
       // consumers of the residual stream (residual join fused into the fill)

@@ -44,10 +44,12 @@ constexpr int W2_RING = 3;  // operand reads in flight ahead of the MFMAs
 // and Wh xl + Wl xh into a second (Wl xl, ~2^-22 of the product, is dropped): ~22-bit products, fp32 sums.
 // O32: fp32 output.  PF: prefetch the next tile's halo into registers during the MFMAs (off: loaded after
 // the epilogue, for the shapes whose split weights leave no registers for it).
+// 8 waves; 12 (three per SIMD) for 96 output channels (ReCoNet's unpadded encoder.layers.1): 6 groups x 2 row groups
+constexpr int w2_threads(int cout) { return cout == 96 ? 768 : 512; }
 template <int CINP, int COUT, int TH, bool SPL = false, bool O32 = false>
 struct W2Cfg {
-  static constexpr int NW = 8, NT = 512, TW = 16;
   static constexpr int NCG = COUT / 16;             // 16-channel groups
+  static constexpr int NW = w2_threads(COUT) / 64, NT = NW * 64, TW = 16;
   static constexpr int NRG = NW / NCG;              // output row groups
   static constexpr int THW = TH / NRG;              // output rows per wave
   static constexpr int IESZ = SPL ? 4 : 2;          // input element bytes
@@ -63,6 +65,13 @@ struct W2Cfg {
   static constexpr int NCHK = LH * LW * NCH;        // 16-B chunks per halo
   static constexpr int NPF = (NCHK + NT - 1) / NT;  // fill slots per thread
   static constexpr int PIXB = COUT * (O32 ? 4 : 2);
+  // 16-bit output staging: 8-byte slot s of pixel px at slot s ^ 2 (px & 7), or (s + 2 (px & 7)) mod NSL when the
+  // pixel's slot count is not a power of two (96 channels: 24 slots), so a slot never leaves its pixel
+  static constexpr int NSL = PIXB / 8;
+  static constexpr bool SWZ_XOR = (NSL & (NSL - 1)) == 0;
+  static __device__ __forceinline__ int oslot(int s, int px) {
+    return SWZ_XOR ? (s ^ (2 * (px & 7))) : (s + 2 * (px & 7)) % NSL;
+  }
   static constexpr int OUT_OFF = HALO;
   static constexpr int OUTB = TH * TW * PIXB;
   static constexpr int NST = OUTB / (NT * 16);      // 16-B output stores per thread
@@ -77,12 +86,14 @@ struct W2Cfg {
   static_assert(NW % NCG == 0 && TH % NRG == 0, "waves split channel groups x row groups");
   static_assert(NST * NT * 16 == OUTB, "whole 16-B stores per thread");
   static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(!O32 || (PIXB & (PIXB - 1)) == 0, "fp32 staging: XOR swizzle over a power-of-two pixel");
 };
 
-// OCC = waves per SIMD the register allocation must allow: 4 = two workgroups per CU (conv2's
+// OCC = waves per SIMD the register allocation must allow (12-wave form: 3 = one workgroup per CU): 4 = two
+// workgroups per CU (conv2's
 // 8-row tiles fit 126 VGPRs and 72 KB of LDS), 2 = one
 template <typename T, int CINP, int COUT, int TH, bool ZPAD, int OCC, bool SPL, bool O32, bool PF>
-__global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
+__global__ __launch_bounds__(w2_threads(COUT), OCC) void ws2_kernel(ConvParams p) {
   using C = W2Cfg<CINP, COUT, TH, SPL, O32>;
   static_assert(!SPL || IS_F16<T>, "split operands / weights are fp16 pairs");
   static_assert(PF || SPL, "the 16-bit kernels always prefetch");
@@ -319,7 +330,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
     const int c0 = 16 * cg + 4 * g;
     const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
     // 16-bit: 8-B slots swizzled by pixel; O32: 16-B chunk 4 cg + g of the pixel, XOR (px & 15): conflict-free
-    int obase = C::OUT_OFF + px * C::PIXB + (O32 ? (((4 * cg + g) ^ (px & 15)) * 16) : (((4 * cg + g) ^ (2 * (px & 7))) * 8));
+    int obase = C::OUT_OFF + px * C::PIXB + (O32 ? (((4 * cg + g) ^ (px & 15)) * 16) : (C::oslot(4 * cg + g, px) * 8));
     asm volatile("" : "+v"(obase));
     f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
     const bool full = wk.oy0 + TH <= p.oh && wk.ox0 + C::TW <= p.ow;
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(512, OCC) void ws2_kernel(ConvParams p) {
       const int off = (k * C::NT + t0) * 16;
       const int pp = off / C::PIXB, cb = off - pp * C::PIXB;
       const int x = pp % C::TW, oy = wk.oy0 + pp / C::TW, ox = wk.ox0 + x;
-      const int la = O32 ? (((cb >> 4) ^ (x & 15)) << 4) : (((cb >> 3) ^ (2 * (x & 7))) << 3);
+      const int la = O32 ? (((cb >> 4) ^ (x & 15)) << 4) : (C::oslot(cb >> 3, x) << 3);
       const u32x4_t v = *(const u32x4_t*)(smem + C::OUT_OFF + pp * C::PIXB + la);
       const bool ok = oy < p.oh && ox < p.ow;
       __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, ST_AUX);
@@ -424,7 +435,7 @@ struct Ws2Inst {
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
     ConvParams p = p0;
     p.n_work = (int)grid.x * (int)grid.y;
-    const int nb = std::min(p.n_work, cus() * (OCC / 2));  // workgroups resident per CU
+    const int nb = std::min(p.n_work, cus() * (OCC * 4 / C::NW));  // workgroups resident per CU
     if (p.axis_mode == AX_ZERO || p.axis_mode == AX_ZERO_PREREFLECT)
       hipLaunchKernelGGL((ws2_kernel<T, CINP, COUT, TH, true, OCC, SPL, O32, PF>), dim3(nb), dim3(C::NT), 0, st, p);
     else
@@ -459,6 +470,9 @@ const ConvKernelInfo* conv_table_ws2(int* count) {
       E(__bf16, 64, 128, W2_C3_TH, W2_C3_TH <= 4 ? 4 : 2),   // conv3 / down3 / ReCoNet 48 -> 96 (padded 64 -> 128)
       E(_Float16, 32, 64, W2_C2_TH, W2_C2_TH <= 8 ? 4 : 2),  // fp16 mode
       E(_Float16, 64, 128, W2_C3_TH, W2_C3_TH <= 4 ? 4 : 2),
+      // ReCoNet encoder.layers.1 48 -> 96 with its 96 output channels unpadded (48 in, padded to 64): 12 waves
+      E(__bf16, 64, 96, 8, 3),
+      E(_Float16, 64, 96, 8, 3),
       // split-precision head (NST_DT_F16M): conv2 with fp32 output, conv3 with fp32 or fp16 output
       //  T        CINP COUT TH OCC SPL   O32    PF
       E(_Float16, 32, 64, 8, 2, true, true, true),

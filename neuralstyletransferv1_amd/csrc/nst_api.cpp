@@ -975,6 +975,11 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       if (li == 11) Ly.coutp = 96;
       if (li == 12) Ly.cinp = 96;
     }
+    // ... and the encoder's (encoder.layers.1 -> .2): 96 output channels on 12-wave down-conv tiles, K of 96
+    if (is_reconet(arch) && !f32_storage(compute_dtype) && !(flags & NST_KSEL_PAD_ENCODER)) {
+      if (li == 1) Ly.coutp = 96;
+      if (li == 2) Ly.cinp = 96;
+    }
     const int ink = image_in ? IN_U8_NHWC : IN_ACT;
     const int outk = final_layer ? OUT_U8_NHWC : OUT_ACT;
     // preferred mapping: sub-pixel phases for x2 up-convs, x-shift rows for the 3-channel output

@@ -494,17 +494,20 @@ def test_weight_stationary_upconv_vs_generic(arch, h, w):
     assert np.abs(ya - yb).max() <= 3e-2 * np.abs(yb).max(), np.abs(ya - yb).max() / np.abs(yb).max()
 
 
+@pytest.mark.parametrize("pad", ["pad_decoder", "pad_encoder"])
 @pytest.mark.parametrize("arch,h,w", [("reconet", 61, 90), ("reconet_frn", 72, 100), ("reconet", 1080, 1920)])
-def test_reconet_unpadded_decoder_vs_padded(arch, h, w):
-    """ReCoNet's decoder stream (decoder.layers.1 -> .3, 96 channels) runs unpadded in the 16-bit modes: the 192 -> 96
-    up-conv computes 96 output channels and the 96 -> 48 one three 32-channel K parts.  The padded program
-    (NST_KSEL_PAD_DECODER: 128-channel stride) adds zero weights times zero-valued channels only, so the two agree to
-    the fp32 rounding of the same sums (measured: identical)."""
+def test_reconet_unpadded_96_channel_maps_vs_padded(arch, h, w, pad):
+    """ReCoNet's 96-channel maps run unpadded in the 16-bit modes.  Decoder (decoder.layers.1 -> .3): the 192 -> 96
+    up-conv computes 96 output channels and the 96 -> 48 one three 32-channel K parts.  Encoder (encoder.layers.1 ->
+    .2): the 48 -> 96 down-conv on 12-wave weight-stationary tiles (6 channel groups x 2 row groups), the 96 -> 192 one
+    with a K of 96.  The padded programs (NST_KSEL_PAD_DECODER / _ENCODER: 128-channel strides) add zero weights times
+    zero-valued channels only; the encoder's InstanceNorm partials come in two row groups per tile instead of one, so
+    its statistics may round differently in the last bit (decoder: measured identical)."""
     frames = torch.from_numpy(synthetic.make_frames(2 if h < 512 else 1, h, w, seed=25)).cuda()
     x = torch.randn(frames.shape[0], 3, h, w, generator=torch.Generator().manual_seed(7)).cuda()
     fast = _net(arch, 11, "bf16")
     a, ya = fast.stylize_frames(frames, "imagenet_255").cpu().numpy(), fast(x).cpu().numpy()
-    ref = _net(arch, 11, "bf16", {"pad_decoder"})
+    ref = _net(arch, 11, "bf16", {pad})
     b, yb = ref.stylize_frames(frames, "imagenet_255").cpu().numpy(), ref(x).cpu().numpy()
     d = np.abs(a.astype(int) - b.astype(int))
     print(f"{arch} {h}x{w}: frames identical {bool((d == 0).all())}, max {d.max()}; raw max rel "
