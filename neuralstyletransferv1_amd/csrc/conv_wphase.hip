@@ -24,6 +24,14 @@
 namespace nst {
 
 constexpr int WP_RING = 3;  // operand reads in flight ahead of the MFMAs
+// the conv bias as the C operand of each (row, subtile)'s first MFMA and the epilogue's InstanceNorm sums as packed
+// f32 pairs (after the MFMA drain): conv_wstat.hip's epilogue, for the phase kernels whose epilogue is half their VALU
+#ifndef NST_WP_BIAS_C
+#define NST_WP_BIAS_C 1
+#endif
+#ifndef NST_WP_PK_STATS
+#define NST_WP_PK_STATS 1
+#endif
 #ifndef NST_WP_PAIR
 #define NST_WP_PAIR 1
 #endif
@@ -254,9 +262,17 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
     const int tx = rem / NRD, y = rem % NRD;
     return *(const uint4*)(smem + lbase + (y * C::LW + tx) * C::EB + 64 * q);
   };
-  auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first) { mfma_tied<T>(c, a, bop, first); };
   auto kloop = [&](Acc& acc, auto&& hook, auto&& bound) {
     constexpr int NI = C::NPART * PRD, D = WP_RING;
+    f32x4_t bias0[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+      bias0[t] = NST_WP_BIAS_C ? *(const f32x4_t*)(smem + C::BIAS_OFF + (team * (COUT / 2) + t * 16 + 4 * g) * 4)
+                               : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    auto mfma = [&](f32x4_t& c, const uint4& a, const uint4& bop, bool first, int t) {
+      if constexpr (NST_WP_BIAS_C) mfma_tied_c<T>(c, a, bop, first, bias0[t]);
+      else mfma_tied<T>(c, a, bop, first);
+    };
     uint4 ring[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) ring[i] = bread(i);
@@ -273,7 +289,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
         const int r = y - ty;
         if (r < 0 || r >= TH) continue;
 #pragma unroll
-        for (int t = 0; t < NS; ++t) mfma(acc[r][t], wr[q * 4 + 2 * ty + tx][t], bcur, q == 0 && tx == 0 && ty == 0);
+        for (int t = 0; t < NS; ++t) mfma(acc[r][t], wr[q * 4 + 2 * ty + tx][t], bcur, q == 0 && tx == 0 && ty == 0, t);
       }
       hook(q, rem);
       if (rem == PRD - 1) {
@@ -304,14 +320,14 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
       const int c0 = team * (COUT / 2) + t * 16 + 4 * g;
-      const f32x4_t bias = *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
+      const f32x4_t bias = NST_WP_BIAS_C ? (f32x4_t){0.f, 0.f, 0.f, 0.f} : *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
       const uint32_t off0 = (uint32_t)(((oy0 * p.ow + ox) * p.cout_stride + c0) * 2);
       f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
       auto rows = [&](auto all_valid) {
 #pragma unroll
         for (int r = 0; r < TH; ++r) {
           const bool valid = decltype(all_valid)::value || (oy0 + 2 * r < p.oh && ox < p.ow);
-          const f32x4_t v = add4(acc[r][t], bias);
+          const f32x4_t v = NST_WP_BIAS_C ? acc[r][t] : add4(acc[r][t], bias);
           const u32x2_t pk = {pack16<T>(v[0], v[1]), pack16<T>(v[2], v[3])};
           if constexpr (C::OST) {  // into the LDS output tile: row 2r + a, pixel 2 px + b
             *(u32x2_t*)(smem + C::OUT_OFF + ((2 * r + (ph >> 1)) * 2 * C::TW + 2 * px + (ph & 1)) * C::PIXP +
@@ -320,7 +336,17 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
             __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, ST_AUX);
           }
           const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
-          stat4(s1, s2, x);
+          if constexpr (NST_WP_PK_STATS) {
+            if (r == 0) {
+              s1 = x;
+              s2 = x * x;
+            } else {
+              s1 = s1 + x;
+              s2 = __builtin_elementwise_fma(x, x, s2);
+            }
+          } else {
+            stat4(s1, s2, x);
+          }
         }
       };
       if (full)
