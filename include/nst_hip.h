@@ -136,8 +136,16 @@ int nst_output_hw(const nst_handle* h, int in_h, int in_w, int* out_h, int* out_
  * engine runs the other combinations on an NST_DT_F32S twin).  Replaces no reference call: a property query. */
 int nst_input_exact(const nst_handle* h, int x_fmt, int preset, int* exact);
 
-/* Device workspace nst_forward needs for a batch of n frames of h x w. */
+/* Device workspace nst_forward needs for a batch of n frames of h x w (with the handle's stream split: one slice
+ * per sub-batch). */
 int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* out);
+
+/* Run each nst_forward batch as k sub-batches (1 <= k <= 4) on internal streams forked from and joined back to the
+ * caller's stream (events only: the caller's stream order is kept, frames are independent, outputs identical).
+ * Default: 2 for the ReCoNet nets in the 16-bit modes (their generic kernels' launch gaps and tails are filled by
+ * the other sub-batches), 1 otherwise.  Profiling and the range check run a batch whole.  Replaces no reference
+ * call: scheduling only. */
+int nst_set_stream_split(nst_handle* h, int k);
 
 /*
  * Stylize a batch.  Replaces `model(x_in)` with its io_preset pre/post arithmetic

@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "nst_region_composite_u8", "nst_region_crop_input", "nst_region_resize", "nst_region_morph",
     "nst_region_morph_scratch_floats", "nst_gray_u8", "nst_flow_scratch_floats", "nst_flow_farneback",
     "nst_flow_fuse", "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale", "nst_resize_area_u8",
-    "nst_flow_dis_scratch_bytes", "nst_flow_dis", "nst_set_range_check", "nst_input_exact",
+    "nst_flow_dis_scratch_bytes", "nst_flow_dis", "nst_set_range_check", "nst_input_exact", "nst_set_stream_split",
     "nst_lab_planes_u8", "nst_lab_ema_planes", "nst_lab_merge_u8",
 )
 # region compositor limits / geometry kinds (include/nst_hip.h NST_REGION_*, NST_RG_*)
@@ -143,6 +143,8 @@ def lib() -> ctypes.CDLL:
         L.nst_num_ops.restype = i
         L.nst_set_range_check.argtypes = [vp, i]
         L.nst_set_range_check.restype = i
+        L.nst_set_stream_split.argtypes = [vp, i]
+        L.nst_set_stream_split.restype = i
         L.nst_op_describe.argtypes = [vp, i, i, i, i, ctypes.POINTER(NstOpDesc)]
         L.nst_forward_capture.argtypes = [vp, vp, i, i, i, i, i, vp, i, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(vp),
                                           ctypes.POINTER(vp), vp]

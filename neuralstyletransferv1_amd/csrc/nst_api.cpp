@@ -257,6 +257,11 @@ struct nst_handle {
   bool profiling = false;
   struct Rec { int layer; hipEvent_t a, b; };
   std::vector<Rec> recs;
+  // nst_set_stream_split: a batch runs as `split` sub-batches on internal streams forked from / joined to the
+  // caller's, so one sub-batch's launch gaps and kernel tails are filled by another's kernels
+  int split = 1;
+  hipStream_t sub[NST_MAX_STREAM_SPLIT] = {};
+  hipEvent_t fork = nullptr, join[NST_MAX_STREAM_SPLIT] = {};
 };
 
 struct nst_lab {
@@ -1133,6 +1138,11 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
   // x_0 export: the weight-stationary trunk kernel and the generic stride-1 kernel write it from their fill
   if (fuse_res && !f16m && h->layers[3].mode != MODE_WSTAT && h->layers[3].mode != MODE_STD)
     build_program(arch, true, false, defs, h->prog);
+  // ReCoNet's 16-bit programs (generic kernels with launch tails) run a batch as 2 sub-batches on 2 streams: 10.66-10.75
+  // -> 10.38-10.45 ms per 8 1080p frames (4 sub-batches: 11.1, more streams than the 4 hardware queues;
+  // tools/stream_split_bench.py, profiles/r05_x_stream_split.txt); the Johnson / NST programs (persistent kernels
+  // filling every CU) measured slower split (5.17 -> 5.27 / 5.44 ms), fp16m neutral
+  h->split = is_reconet(arch) && !f32_storage(compute_dtype) ? 2 : 1;
   *out = h;
   return NST_OK;
 }
@@ -1140,6 +1150,11 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
 void nst_destroy(nst_handle* h) {
   if (!h) return;
   DeviceGuard guard(h->device);
+  for (int i = 0; i < NST_MAX_STREAM_SPLIT; ++i) {
+    if (h->sub[i]) (void)hipStreamDestroy(h->sub[i]);
+    if (h->join[i]) (void)hipEventDestroy(h->join[i]);
+  }
+  if (h->fork) (void)hipEventDestroy(h->fork);
   if (h->range_flag) (void)hipFree(h->range_flag);
   for (Layer& Ly : h->layers) {
     if (Ly.wpk) (void)hipFree(Ly.wpk);
@@ -1181,7 +1196,22 @@ int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* 
   if (!h || !out || n <= 0 || in_h <= 0 || in_w <= 0) { set_error("nst_workspace_bytes: invalid arguments"); return NST_E_INVALID; }
   Plan P = make_plan(h, n, in_h, in_w);
   if (!P.ok) { set_error(P.err); return NST_E_SHAPE; }
-  *out = P.ws_bytes;
+  // a split batch takes one workspace slice per sub-batch; enough for the unsplit run too (profiling, range check)
+  const int k = std::min(h->split, n);
+  size_t bytes = P.ws_bytes;
+  if (k > 1) {
+    const int nb = (n + k - 1) / k;
+    const Plan Q = make_plan(h, nb, in_h, in_w);
+    if (!Q.ok) { set_error(Q.err); return NST_E_SHAPE; }
+    bytes = std::max(bytes, (size_t)((n + nb - 1) / nb) * align256(Q.ws_bytes));
+  }
+  *out = bytes;
+  return NST_OK;
+}
+
+int nst_set_stream_split(nst_handle* h, int k) {
+  if (!h || k < 1 || k > NST_MAX_STREAM_SPLIT) { set_error("nst_set_stream_split: invalid arguments"); return NST_E_INVALID; }
+  h->split = k;
   return NST_OK;
 }
 
@@ -1427,7 +1457,42 @@ extern "C" {
 
 int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset, void* y,
                 int y_fmt, void* workspace, size_t workspace_bytes, void* stream) {
-  return forward_impl(h, x, x_fmt, n, in_h, in_w, preset, y, y_fmt, workspace, workspace_bytes, stream, nullptr);
+  // one stream: profiling (per-layer event pairs) and the range check (a synchronous verdict) keep the batch whole
+  const int k = (!h || h->profiling || h->range_flag || n <= 1) ? 1 : std::min(h->split, n);
+  if (k == 1 || !x || !y || in_h <= 0 || in_w <= 0 || (x_fmt != NST_IO_F32_NCHW && x_fmt != NST_IO_U8_NHWC) ||
+      (y_fmt != NST_IO_F32_NCHW && y_fmt != NST_IO_U8_NHWC))
+    return forward_impl(h, x, x_fmt, n, in_h, in_w, preset, y, y_fmt, workspace, workspace_bytes, stream, nullptr);
+  const int nb = (n + k - 1) / k, parts = (n + nb - 1) / nb;
+  const Plan Q = make_plan(h, nb, in_h, in_w);
+  if (!Q.ok) { set_error(Q.err); return NST_E_SHAPE; }
+  const size_t per = align256(Q.ws_bytes);
+  if (!workspace || workspace_bytes < per * parts) {
+    set_error("nst_forward: workspace too small (" + std::to_string(workspace_bytes) + " < " + std::to_string(per * parts) +
+              "; nst_workspace_bytes sizes the split batch)");
+    return NST_E_WORKSPACE;
+  }
+  DeviceGuard guard(h->device);
+  if (!h->fork) NST_HIP_CHECK(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
+  for (int i = 0; i < parts; ++i) {
+    if (!h->sub[i]) NST_HIP_CHECK(hipStreamCreateWithFlags(&h->sub[i], hipStreamNonBlocking));
+    if (!h->join[i]) NST_HIP_CHECK(hipEventCreateWithFlags(&h->join[i], hipEventDisableTiming));
+  }
+  const hipStream_t st = (hipStream_t)stream;
+  const size_t fx = x_fmt == NST_IO_U8_NHWC ? (size_t)in_h * in_w * 3 : (size_t)3 * in_h * in_w * 4;
+  const size_t fy = y_fmt == NST_IO_U8_NHWC ? (size_t)Q.out_h * Q.out_w * 3 : (size_t)3 * Q.out_h * Q.out_w * 4;
+  NST_HIP_CHECK(hipEventRecord(h->fork, st));
+  int rc = NST_OK;
+  for (int i = 0; i < parts; ++i) {
+    NST_HIP_CHECK(hipStreamWaitEvent(h->sub[i], h->fork, 0));
+    const int f0 = i * nb, m = std::min(nb, n - f0);
+    if (rc == NST_OK)
+      rc = forward_impl(h, (const char*)x + f0 * fx, x_fmt, m, in_h, in_w, preset, (char*)y + f0 * fy, y_fmt,
+                        (char*)workspace + i * per, per, h->sub[i], nullptr);
+    // joined even after a failed launch: nothing queued on a sub-stream outlives the caller's stream order
+    NST_HIP_CHECK(hipEventRecord(h->join[i], h->sub[i]));
+    NST_HIP_CHECK(hipStreamWaitEvent(st, h->join[i], 0));
+  }
+  return rc;
 }
 
 int nst_forward_capture(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in_w, int preset, void* y,

@@ -128,6 +128,7 @@ struct ConvParams {
 //   SPLIT: fp32 input staged as an fp16 hi / lo operand pair x fp16 hi / lo weight pairs (Wh xh + Wh xl + Wl xh)
 //   O32 / O16: fp32 / fp16 output storage
 //   SPLITO: fp32 input staged as an fp16 hi / lo operand pair x fp16 weights (Wh xh + Wh xl), fp32 output
+constexpr int NST_MAX_STREAM_SPLIT = 4;  // nst_set_stream_split
 enum KernelDtype { NST_KDT_SW_O32 = 16, NST_KDT_SW_O16 = 17, NST_KDT_SPLIT_O32 = 18, NST_KDT_SPLIT_O16 = 19,
                    NST_KDT_SPLITO_O32 = 20 };
 

@@ -88,6 +88,10 @@ class Engine:
     def set_range_check(self, enable: bool) -> None:
         check(lib().nst_set_range_check(self._h, 1 if enable else 0), "nst_set_range_check")
 
+    def set_stream_split(self, k: int) -> None:
+        """nst_set_stream_split: run each batch as k sub-batches on the library's internal streams (1 = whole)."""
+        check(lib().nst_set_stream_split(self._h, int(k)), "nst_set_stream_split")
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:

@@ -494,6 +494,22 @@ def test_weight_stationary_upconv_vs_generic(arch, h, w):
     assert np.abs(ya - yb).max() <= 3e-2 * np.abs(yb).max(), np.abs(ya - yb).max() / np.abs(yb).max()
 
 
+@pytest.mark.parametrize("arch,n,split", [("reconet", 8, 4), ("reconet", 5, 4), ("reconet_frn", 3, 2), ("johnson", 6, 4)])
+def test_stream_split_identical(arch, n, split):
+    """nst_set_stream_split: the batch as sub-batches on the library's internal streams (forked from / joined to the
+    caller's stream by events) gives the same frames and raw outputs as the whole batch, ragged splits included
+    (5 frames over 4 streams: 2 + 2 + 1)."""
+    frames = torch.from_numpy(synthetic.make_frames(n, 61, 90, seed=26)).cuda()
+    x = torch.randn(n, 3, 61, 90, generator=torch.Generator().manual_seed(8)).cuda()
+    net = _net(arch, 12, "bf16")
+    eng = net.engine(torch.device("cuda", 0))
+    eng.set_stream_split(split)
+    a, ya = net.stylize_frames(frames, "imagenet_255").cpu(), net(x).cpu()
+    eng.set_stream_split(1)
+    b, yb = net.stylize_frames(frames, "imagenet_255").cpu(), net(x).cpu()
+    assert torch.equal(a, b) and torch.equal(ya, yb)
+
+
 @pytest.mark.parametrize("pad", ["pad_decoder", "pad_encoder"])
 @pytest.mark.parametrize("arch,h,w", [("reconet", 61, 90), ("reconet_frn", 72, 100), ("reconet", 1080, 1920)])
 def test_reconet_unpadded_96_channel_maps_vs_padded(arch, h, w, pad):
