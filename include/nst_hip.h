@@ -120,7 +120,9 @@ int nst_create(int arch, const nst_param* params, int n_params, int compute_dtyp
                                             channels, as the encoder's (default: unpadded) */
 #define NST_KSEL_PAD_ENCODER 0x800       /* ReCoNet, 16-bit modes: the encoder's 96-channel map padded to 128 (default:
                                             unpadded) */
-#define NST_KSEL_ALL 0xfff
+#define NST_KSEL_PAD_48 0x1000         /* ReCoNet, 16-bit modes: the decoder's 48-channel output padded to 64 (default:
+                                            unpadded) */
+#define NST_KSEL_ALL 0x1fff
 int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_dtype, int device,
                   unsigned flags, nst_handle** out);
 void nst_destroy(nst_handle* h);

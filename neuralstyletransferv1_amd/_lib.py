@@ -59,7 +59,7 @@ NST_GRAM_CHW, NST_GRAM_HWC = 0, 1
 KSEL = {
     "no_wstat": 0x1, "no_wphase": 0x2, "no_ws2": 0x4, "no_ws9": 0x8, "no_kyrot": 0x10, "no_prepad": 0x20,
     "no_persistent": 0x40, "unfused_residual": 0x80, "no_fold": 0x100, "f16m_two_blocks": 0x200,
-    "pad_decoder": 0x400, "pad_encoder": 0x800,
+    "pad_decoder": 0x400, "pad_encoder": 0x800, "pad_48": 0x1000,
 }
 NST_BUF_INPUT, NST_BUF_OUTPUT = -1, -2
 

@@ -66,7 +66,8 @@ struct Out9Cfg {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <typename T, int CINP, int G, int NW, int OUTK, bool TANH>
+// CLD: input channels stored (<= CINP; ReCoNet's unpadded 48-channel decoder output): the chunks past them stage zeros
+template <typename T, int CINP, int G, int NW, int OUTK, bool TANH, int CLD = CINP>
 __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   constexpr bool SPLIT = IS_SPLIT<T>;
   using TM = std::conditional_t<SPLIT, _Float16, T>;  // the MFMA operand type
@@ -123,11 +124,12 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   for (int j = 0; j < C::IPL; ++j) {
     const int col = C::PPJ * j + lane % C::PPJ;
     const int sx = map_axis(x0 + p.crop_x - p.pad + col, p.ws, p.axis_mode, p.pre);
-    coloff[j] = (col < C::LWS && sx >= 0) ? sx * pix_bytes + chunk * 16 : -1;
+    coloff[j] = (col < C::LWS && sx >= 0 && chunk * C::CPCH < CLD) ? sx * pix_bytes + chunk * 16 : -1;
   }
   float2 nm[C::CPCH];
 #pragma unroll
-  for (int j = 0; j < C::CPCH; ++j) nm[j] = p.in_norm[(size_t)n * p.cs + chunk * C::CPCH + j];
+  for (int j = 0; j < C::CPCH; ++j)
+    nm[j] = chunk * C::CPCH < CLD ? p.in_norm[(size_t)n * p.cs + chunk * C::CPCH + j] : make_float2(0.f, 0.f);
   const char* img = (const char*)p.in + (size_t)n * p.hs * row_bytes;
   const int vy0 = o0 + p.crop_y - p.pad;
 
@@ -262,10 +264,10 @@ __global__ __launch_bounds__(64 * NW) void out9_kernel(ConvParams p) {
   }
 }
 
-template <typename T, int CINP, int G, int NW, int OUTK, bool TANH>
+template <typename T, int CINP, int G, int NW, int OUTK, bool TANH, int CLD = CINP>
 struct Out9Inst {
   using C = Out9Cfg<CINP, G, NW, IS_SPLIT<T> ? 4 : 2>;
-  static constexpr auto kernel = out9_kernel<T, CINP, G, NW, OUTK, TANH>;
+  static constexpr auto kernel = out9_kernel<T, CINP, G, NW, OUTK, TANH, CLD>;
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;
@@ -296,7 +298,8 @@ struct Out9Inst {
     std::memset(&k, 0, sizeof(k));
     k.dtype = dtype_code<T>();
     k.mode = MODE_KYROT;
-    k.ks = 9; k.stride = 1; k.cinp = CINP; k.bn = 16; k.th = 1; k.tw = C::SW; k.wm = NW; k.wn = 1;
+    k.ks = 9; k.stride = 1; k.cinp = CLD; k.bn = 16;
+    k.cinp_k = CLD != CINP ? CINP : 0; k.th = 1; k.tw = C::SW; k.wm = NW; k.wn = 1;
     k.in_kind = IN_ACT; k.out_kind = OUTK;
     k.cpc = C::CPCH; k.nch = C::NCH; k.lds_bytes = C::LDS;
     k.in_esz = IS_SPLIT<T> ? 4 : 0;
@@ -336,10 +339,14 @@ const ConvKernelInfo* conv_table_out9(int* count) {
       E(__bf16, 32, 3, 8, OUT_F32_NCHW, false),   // tensor API
       E(__bf16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_U8_NHWC, true),   // ReCoNet (48 channels, padded to 64; tanh)
       E(__bf16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_F32_NCHW, true),
+      E(__bf16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_U8_NHWC, true, 48),  // ... reading 48 unpadded channels
+      E(__bf16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_F32_NCHW, true, 48),
       E(_Float16, 32, 3, 8, OUT_U8_NHWC, false),  // fp16 mode
       E(_Float16, 32, 3, 8, OUT_F32_NCHW, false),
       E(_Float16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_U8_NHWC, true),
       E(_Float16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_F32_NCHW, true),
+      E(_Float16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_U8_NHWC, true, 48),
+      E(_Float16, 64, NST_OUT9_R_G, NST_OUT9_R_NW, OUT_F32_NCHW, true, 48),
       // split-fp16 mode (NST_DT_F32S): fp32 activations, two f16 MFMAs per K step (the x-shift generic kernel's
       // 9-chunk LDS entries were 2-way bank-conflicted on most operand reads: 5.2 ms per batch of 8)
       E(F32Split, 32, NST_OUT9_S_G, NST_OUT9_S_NW, OUT_U8_NHWC, false),

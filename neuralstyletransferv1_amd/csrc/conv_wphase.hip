@@ -81,7 +81,8 @@ struct WpCfg {  // SW: staged tensors per unit (2: the residual join's y and r, 
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <typename T, int CINP, int COUT, int TH, int NF, int FILL, bool ZPAD>
+// CST: output channels stored (<= COUT; ReCoNet's 96 -> 48 up-conv computes 64 and stores its 48 unpadded)
+template <typename T, int CINP, int COUT, int TH, int NF, int FILL, bool ZPAD, int CST = COUT>
 __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   using C = WpCfg<CINP, COUT, TH, NF, (FILL >= WF_RES) ? 2 : 1>;
   constexpr bool RES = FILL >= WF_RES, RN = FILL == WF_RESRN;
@@ -320,6 +321,9 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
       const int c0 = team * (COUT / 2) + t * 16 + 4 * g;
+      // a subtile of padding channels (c0 >= CST): its stores and statistics go to the out-of-range offset, still
+      // issued (the unit waits count this epilogue's vector-memory instructions)
+      const bool live = team * (COUT / 2) + t * 16 < CST;
       const f32x4_t bias = NST_WP_BIAS_C ? (f32x4_t){0.f, 0.f, 0.f, 0.f} : *(const f32x4_t*)(smem + C::BIAS_OFF + c0 * 4);
       const uint32_t off0 = (uint32_t)(((oy0 * p.ow + ox) * p.cout_stride + c0) * 2);
       f32x4_t s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
             *(u32x2_t*)(smem + C::OUT_OFF + ((2 * r + (ph >> 1)) * 2 * C::TW + 2 * px + (ph & 1)) * C::PIXP +
                         (((c0 >> 2) ^ C::swz(2 * px + (ph & 1))) << 3)) = pk;
           } else {
-            __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid ? off0 + r * row2 : 0x80000000u, 0, ST_AUX);
+            __builtin_amdgcn_raw_buffer_store_b64(pk, ors, valid && live ? off0 + r * row2 : 0x80000000u, 0, ST_AUX);
           }
           const f32x4_t x = valid ? v : (f32x4_t){0.f, 0.f, 0.f, 0.f};
           if constexpr (NST_WP_PK_STATS) {
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
       const float sv = a1[0] + dpp_f<0xb1>(a1[0]);
       const int idx = (px >= 8 ? 4 : 0) + ((px & 4) ? 2 : 0) + ((px & 2) ? 1 : 0);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv), prs,
-                                            (px & 1) ? 0x80000000u : (uint32_t)(((c0 + (idx >> 1)) * 2 + (idx & 1)) * 4), 0, 0);
+                                            ((px & 1) || !live) ? 0x80000000u : (uint32_t)(((c0 + (idx >> 1)) * 2 + (idx & 1)) * 4), 0, 0);
     }
     if constexpr (C::OST) {
       // the staged tile as whole rows: 2 TW pixels x COUT channels contiguous in HBM (NHWC,
@@ -376,8 +380,8 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
         const u32x4_t v =
             *(const u32x4_t*)(smem + C::OUT_OFF + (row * 2 * C::TW + pix) * C::PIXP + (((cb >> 3) ^ C::swz(pix)) << 3));
         const int oy = oyb + row, ox = ox0 + pix;
-        const bool ok = oy < p.oh && ox < p.ow;
-        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * C::PIXB + cb) : 0x80000000u, 0, ST_AUX);
+        const bool ok = oy < p.oh && ox < p.ow && cb < CST * 2;
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ok ? (uint32_t)((oy * p.ow + ox) * CST * 2 + cb) : 0x80000000u, 0, ST_AUX);
       }
     }
   };
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(512) void wphase_kernel(ConvParams p) {
   vm_wait<0>();  // no LDS-DMA may land after the workgroup has released its LDS
 }
 
-template <typename T, int CINP, int COUT, int TH, int NF, bool RES>
+template <typename T, int CINP, int COUT, int TH, int NF, bool RES, int CST = COUT>
 struct WphaseInst {
   using C = WpCfg<CINP, COUT, TH, NF, RES ? 2 : 1>;
   static int cus() {
@@ -513,7 +517,7 @@ struct WphaseInst {
   }
   template <int FILL, bool ZPAD>
   static void go(const ConvParams& p, int nb, hipStream_t st) {
-    hipLaunchKernelGGL((wphase_kernel<T, CINP, COUT, TH, NF, FILL, ZPAD>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((wphase_kernel<T, CINP, COUT, TH, NF, FILL, ZPAD, CST>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   // grid.x = source tiles per frame, grid.y = frames; chunks of <= NFMAX frames per launch
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
@@ -553,7 +557,8 @@ struct WphaseInst {
     std::memset(&k, 0, sizeof(k));
     k.dtype = dtype_code<T>();
     k.mode = MODE_WPHASE;
-    k.ks = 3; k.stride = 1; k.cinp = CINP; k.bn = COUT; k.th = TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
+    k.ks = 3; k.stride = 1; k.cinp = CINP; k.bn = CST; k.th = TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
+    k.bn_k = CST != COUT ? COUT : 0;
     k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
     k.cpc = 8; k.nch = C::NCH; k.lds_bytes = C::LDS;
     k.wbytes = C::WBYTES;
@@ -582,10 +587,12 @@ const ConvKernelInfo* conv_table_wphase(int* count) {
       E(__bf16, 128, 64, WP1_TH, WP1_NF, true),     // deconv1 joining the last residual block (fused join)
       E(__bf16, 64, 32, 12, 8, false),              // deconv2 / up2: 12 rows (540 = 45 tiles) fit with one-tensor slots
       E(__bf16, 96, 64, WPR_TH, 8, false),          // ReCoNet decoder 96 -> 48 (padded to 64; three parts)
+      E(__bf16, 96, 64, WPR_TH, 8, false, 48),      // ... storing its 48 channels unpadded
       E(_Float16, 128, 64, WP1_TH, WP1_NF, false),  // fp16 mode
       E(_Float16, 128, 64, WP1_TH, WP1_NF, true),
       E(_Float16, 64, 32, 12, 8, false),
       E(_Float16, 96, 64, WPR_TH, 8, false),
+      E(_Float16, 96, 64, WPR_TH, 8, false, 48),
   };
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;

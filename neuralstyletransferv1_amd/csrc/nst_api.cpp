@@ -410,7 +410,7 @@ std::vector<float> split_weight_frags(const ConvKernelInfo& k, const std::vector
 // Wh = RNE16(w) (exact fp32 value here) and part 1 w - Wh, which the fp16 upload rounds to Wl = RNE16(w - Wh).
 std::vector<float> pack_kyrot_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
   const bool split = k.dtype == NST_DT_F32S;
-  const int cpb = split ? 8 : 16, kc_n = k.cinp / cpb, nblk = 9 * kc_n;
+  const int cpb = split ? 8 : 16, kc_n = (k.cinp_k ? k.cinp_k : k.cinp) / cpb, nblk = 9 * kc_n;
   std::vector<float> out((size_t)k.wbytes / 2, 0.f);
   for (int pp = 0; pp < 2; ++pp)
     for (int ky = 0; ky < 9; ++ky)
@@ -453,14 +453,15 @@ std::vector<float> pack_wstat_weights(const LayerDef& d, const float* W) {
 // 32q..32q+31, tap = 2 ty + tx); lane l holds MFMA row l & 15 = output channel
 // (w >> 2) * coutp / 2 + 16 t + (l & 15), K elements = input channels 32 q + 8 (l >> 4) + i.
 std::vector<float> pack_wphase_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
-  const int nstep = 4 * (k.cinp / 32), ns = k.bn / 32;
+  const int bn = k.bn_k ? k.bn_k : k.bn;  // computed channels (the stored bn may be narrower)
+  const int nstep = 4 * (k.cinp / 32), ns = bn / 32;
   std::vector<float> out((size_t)8 * nstep * ns * 64 * 8, 0.f);
   for (int w = 0; w < 8; ++w)
     for (int s = 0; s < nstep; ++s)
       for (int t = 0; t < ns; ++t)
         for (int l = 0; l < 64; ++l) {
           const int q = s / 4, tap = s % 4;
-          const int co = (w >> 2) * (k.bn / 2) + 16 * t + (l & 15);
+          const int co = (w >> 2) * (bn / 2) + 16 * t + (l & 15);
           for (int i = 0; i < 8; ++i) {
             const int ci = 32 * q + 8 * (l >> 4) + i;
             if (co < d.cout && ci < d.cin)
@@ -979,6 +980,14 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
     if (is_reconet(arch) && !f32_storage(compute_dtype) && !(flags & NST_KSEL_PAD_DECODER)) {
       if (li == 11) Ly.coutp = 96;
       if (li == 12) Ly.cinp = 96;
+    }
+    // ... and its 48-channel output (decoder.layers.3 -> .4): the phase kernel stores 48 of its 64 computed channels,
+    // the output conv stages zeros for the missing 16 (the three-part phase kernel and the row-streaming output conv
+    // only: not with the padded 96-channel decoder stream or without those kernels)
+    if (is_reconet(arch) && !f32_storage(compute_dtype) &&
+        !(flags & (NST_KSEL_PAD_48 | NST_KSEL_PAD_DECODER | NST_KSEL_NO_WPHASE | NST_KSEL_NO_KYROT))) {
+      if (li == 12) Ly.coutp = 48;
+      if (li == 13) Ly.cinp = 48;
     }
     // ... and the encoder's (encoder.layers.1 -> .2): 96 output channels on 12-wave down-conv tiles, K of 96
     if (is_reconet(arch) && !f32_storage(compute_dtype) && !(flags & NST_KSEL_PAD_ENCODER)) {

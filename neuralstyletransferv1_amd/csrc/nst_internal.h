@@ -147,6 +147,8 @@ struct ConvKernelInfo {
   int tanh_out;    // MODE_KYROT: tanh compiled into the output (ReCoNet); other kernels: p.dec_tanh
   int in_esz, out_esz;  // activation element bytes read / written (0: the dtype's own, act_elem_bytes)
   int split_w;          // packed weights are fp16 hi / lo pairs (pack functions place w and w - RNE16(w))
+  int cinp_k, bn_k;     // compute widths where the stored channel stride (cinp / bn) is narrower (0: the same):
+                        // the kernel zero-pads the staged input / drops the extra output channels
   void (*launch)(const ConvParams&, dim3 grid, hipStream_t);
 };
 

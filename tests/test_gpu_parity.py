@@ -510,13 +510,15 @@ def test_stream_split_identical(arch, n, split):
     assert torch.equal(a, b) and torch.equal(ya, yb)
 
 
-@pytest.mark.parametrize("pad", ["pad_decoder", "pad_encoder"])
+@pytest.mark.parametrize("pad", ["pad_decoder", "pad_encoder", "pad_48"])
 @pytest.mark.parametrize("arch,h,w", [("reconet", 61, 90), ("reconet_frn", 72, 100), ("reconet", 1080, 1920)])
 def test_reconet_unpadded_96_channel_maps_vs_padded(arch, h, w, pad):
     """ReCoNet's 96-channel maps run unpadded in the 16-bit modes.  Decoder (decoder.layers.1 -> .3): the 192 -> 96
     up-conv computes 96 output channels and the 96 -> 48 one three 32-channel K parts.  Encoder (encoder.layers.1 ->
     .2): the 48 -> 96 down-conv on 12-wave weight-stationary tiles (6 channel groups x 2 row groups), the 96 -> 192 one
-    with a K of 96.  The padded programs (NST_KSEL_PAD_DECODER / _ENCODER: 128-channel strides) add zero weights times
+    with a K of 96.  And the decoder's 48-channel output (decoder.layers.3 -> .4): the phase kernel stores 48 of its 64
+    computed channels, the output conv stages zeros for the other 16 (NST_KSEL_PAD_48: the 64-channel stride).
+    The padded programs (NST_KSEL_PAD_DECODER / _ENCODER: 128-channel strides) add zero weights times
     zero-valued channels only; the encoder's InstanceNorm partials come in two row groups per tile instead of one, so
     its statistics may round differently in the last bit (decoder: measured identical)."""
     frames = torch.from_numpy(synthetic.make_frames(2 if h < 512 else 1, h, w, seed=25)).cuda()
