@@ -92,7 +92,9 @@ struct W2Cfg {
 // OCC = waves per SIMD the register allocation must allow (12-wave form: 3 = one workgroup per CU): 4 = two
 // workgroups per CU (conv2's
 // 8-row tiles fit 126 VGPRs and 72 KB of LDS), 2 = one
-template <typename T, int CINP, int COUT, int TH, bool ZPAD, int OCC, bool SPL, bool O32, bool PF>
+// CLD: input channels stored (<= CINP; ReCoNet's unpadded 48-channel first-layer output): the chunks past them stage
+// zeros (IN constants 0 -> ReLU(0))
+template <typename T, int CINP, int COUT, int TH, bool ZPAD, int OCC, bool SPL, bool O32, bool PF, int CLD = CINP>
 __global__ __launch_bounds__(w2_threads(COUT), OCC) void ws2_kernel(ConvParams p) {
   using C = W2Cfg<CINP, COUT, TH, SPL, O32>;
   static_assert(!SPL || IS_F16<T>, "split operands / weights are fp16 pairs");
@@ -172,14 +174,14 @@ __global__ __launch_bounds__(w2_threads(COUT), OCC) void ws2_kernel(ConvParams p
       const bool pad = ro < 0 || co < 0;
       padm |= pad ? 1u << k : 0u;
       const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(
-          rs, (ok && !pad) ? (uint32_t)(ro + co + fc * 16) : 0x80000000u, 0, 0);
+          rs, (ok && !pad && fc * (16 / C::IESZ) < CLD) ? (uint32_t)(ro + co + fc * 16) : 0x80000000u, 0, 0);
       pf[k] = __builtin_bit_cast(uint4, v);
     }
     if constexpr (SPL) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) nsp[j] = p.in_norm[(size_t)wk.n * p.cs + 4 * fc + j];
     } else if (tid < CINP) {
-      nv = p.in_norm[(size_t)wk.n * p.cs + tid];
+      nv = tid < CLD ? p.in_norm[(size_t)wk.n * p.cs + tid] : make_float2(0.f, 0.f);
     }
   };
   auto put_norm = [&]() {  // after the MFMAs: the landing tile's IN constants into LDS
@@ -419,7 +421,8 @@ __global__ __launch_bounds__(w2_threads(COUT), OCC) void ws2_kernel(ConvParams p
   }
 }
 
-template <typename T, int CINP, int COUT, int TH, int OCC, bool SPL = false, bool O32 = false, bool PF = true>
+template <typename T, int CINP, int COUT, int TH, int OCC, bool SPL = false, bool O32 = false, bool PF = true,
+          int CLD = CINP>
 struct Ws2Inst {
   using C = W2Cfg<CINP, COUT, TH, SPL, O32>;
   static int cus() {
@@ -436,10 +439,15 @@ struct Ws2Inst {
     ConvParams p = p0;
     p.n_work = (int)grid.x * (int)grid.y;
     const int nb = std::min(p.n_work, cus() * (OCC * 4 / C::NW));  // workgroups resident per CU
-    if (p.axis_mode == AX_ZERO || p.axis_mode == AX_ZERO_PREREFLECT)
-      hipLaunchKernelGGL((ws2_kernel<T, CINP, COUT, TH, true, OCC, SPL, O32, PF>), dim3(nb), dim3(C::NT), 0, st, p);
-    else
-      hipLaunchKernelGGL((ws2_kernel<T, CINP, COUT, TH, false, OCC, SPL, O32, PF>), dim3(nb), dim3(C::NT), 0, st, p);
+    // the narrow-input form serves ReCoNet's reflection-padded layer only (its zero-padded instantiation spills at
+    // three waves per SIMD): nst_api selects it for that net alone
+    if constexpr (CLD == CINP) {
+      if (p.axis_mode == AX_ZERO || p.axis_mode == AX_ZERO_PREREFLECT) {
+        hipLaunchKernelGGL((ws2_kernel<T, CINP, COUT, TH, true, OCC, SPL, O32, PF, CLD>), dim3(nb), dim3(C::NT), 0, st, p);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((ws2_kernel<T, CINP, COUT, TH, false, OCC, SPL, O32, PF, CLD>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
@@ -449,7 +457,8 @@ struct Ws2Inst {
     k.out_esz = O32 ? 4 : 2;
     k.split_w = SPL ? 1 : 0;
     k.mode = MODE_WS2;
-    k.ks = 3; k.stride = 2; k.cinp = CINP; k.bn = COUT; k.th = TH; k.tw = C::TW; k.wm = C::NRG; k.wn = C::NCG;
+    k.ks = 3; k.stride = 2; k.cinp = CLD; k.bn = COUT;
+    k.cinp_k = CLD != CINP ? CINP : 0; k.th = TH; k.tw = C::TW; k.wm = C::NRG; k.wn = C::NCG;
     k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
     k.cpc = SPL ? 4 : 8; k.nch = C::NCH; k.lds_bytes = C::LDS;
     k.wbytes = C::WBYTES;
@@ -473,6 +482,9 @@ const ConvKernelInfo* conv_table_ws2(int* count) {
       // ReCoNet encoder.layers.1 48 -> 96 with its 96 output channels unpadded (48 in, padded to 64): 12 waves
       E(__bf16, 64, 96, 8, 3),
       E(_Float16, 64, 96, 8, 3),
+      // ... reading the first layer's 48 channels unpadded
+      E(__bf16, 64, 96, 8, 3, false, false, true, 48),
+      E(_Float16, 64, 96, 8, 3, false, false, true, 48),
       // split-precision head (NST_DT_F16M): conv2 with fp32 output, conv3 with fp32 or fp16 output
       //  T        CINP COUT TH OCC SPL   O32    PF
       E(_Float16, 32, 64, 8, 2, true, true, true),

@@ -99,7 +99,9 @@ struct W9Cfg {
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 
-template <typename T, int NW, bool SW, bool O32, int CO>
+// CST: output channels stored (<= CO; ReCoNet's 48-channel first layer computes 64 and stores 48 unpadded).  Stores of
+// the padding chunks / statistics go to the out-of-range offset, still issued (the waits count store_out's stores)
+template <typename T, int NW, bool SW, bool O32, int CO, int CST = CO>
 __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   using C = W9Cfg<NW, SW, O32, CO>;
   static_assert(!SW || IS_F16<T>, "split weights are fp16 pairs");
@@ -351,13 +353,14 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
       if constexpr (!SW && CO == 64) {
         // 64 channels x 2 statistics: lane l sums value l of half 0 and of half 1 over the half's strips
         const __amdgpu_buffer_rsrc_t prs2 = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * (2 * CO)), (short)0, 2 * CO * 4, 0x00020000);
+            (void*)(p.partial + ((size_t)wk_.n * ntile + wk_.tile) * (2 * CST)), (short)0, 2 * CST * 4, 0x00020000);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           float u = pp[(h * C::NSTRIP) * 64 + lane];
 #pragma unroll
           for (int s2 = 1; s2 < C::NSTRIP; ++s2) u += pp[(h * C::NSTRIP + s2) * 64 + lane];
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(u), prs2, (uint32_t)((64 * h + lane) * 4), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(u), prs2,
+                                                64 * h + lane < 2 * CST ? (uint32_t)((64 * h + lane) * 4) : 0x80000000u, 0, 0);
         }
       } else if constexpr (!SW) {
         t = pp[lane];
@@ -375,16 +378,17 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (uint32_t)(lane * 4), 0, 0);
       }
     }
-    const size_t obytes = (size_t)p.oh * p.ow * C::PIXB;
+    constexpr int OPB = C::PIXB / CO * CST;  // stored bytes per output pixel
+    const size_t obytes = (size_t)p.oh * p.ow * OPB;
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((char*)p.out + (size_t)wk_.n * obytes), (short)0, (int)obytes, 0x00020000);
-    const uint32_t voff = (wk_.ox0 + sx < p.ow) ? (uint32_t)((wk_.ox0 + sx) * C::PIXB + scb) : 0x80000000u;
+    const uint32_t voff = (wk_.ox0 + sx < p.ow && scb < OPB) ? (uint32_t)((wk_.ox0 + sx) * OPB + scb) : 0x80000000u;
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {  // store k: tile rows (k PXS + sq) / TW
       const int row = (k * C::PXS + sq) / C::TW;
       const u32x4_t v = *(const u32x4_t*)(smem + srd + k * C::PXS * C::PIXB);
       if (wk_.oy0 + row < p.oh)
-        __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + row) * p.ow * C::PIXB, ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff, (wk_.oy0 + row) * p.ow * OPB, ST_AUX);
     }
   };
 
@@ -416,7 +420,7 @@ __global__ __launch_bounds__(64 * NW, WS9_OCC) void ws9_kernel(ConvParams p) {
   vm_wait<0>();
 }
 
-template <typename T, int NW, bool SW = false, bool O32 = false, int CO = 32>
+template <typename T, int NW, bool SW = false, bool O32 = false, int CO = 32, int CST = CO>
 struct Ws9Inst {
   using C = W9Cfg<NW, SW, O32, CO>;
   static int cus() {
@@ -433,14 +437,15 @@ struct Ws9Inst {
     ConvParams p = p0;
     p.n_work = (int)grid.x * (int)grid.y;
     const int nb = std::min(p.n_work, cus() * (8 / NW));  // 8 waves per CU (VGPRs)
-    hipLaunchKernelGGL((ws9_kernel<T, NW, SW, O32, CO>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((ws9_kernel<T, NW, SW, O32, CO, CST>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   static ConvKernelInfo info() {
     ConvKernelInfo k;
     std::memset(&k, 0, sizeof(k));
     k.dtype = SW ? (O32 ? NST_KDT_SW_O32 : NST_KDT_SW_O16) : dtype_code<T>();
     k.mode = MODE_WS9;
-    k.ks = 9; k.stride = 1; k.cinp = 4; k.bn = C::COUT; k.th = C::TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
+    k.ks = 9; k.stride = 1; k.cinp = 4; k.bn = CST; k.th = C::TH; k.tw = C::TW; k.wm = 1; k.wn = C::NW;
+    k.bn_k = CST != CO ? CO : 0;
     k.in_esz = 2;
     k.out_esz = O32 ? 4 : 2;
     k.split_w = SW ? 1 : 0;
@@ -461,7 +466,10 @@ const ConvKernelInfo* conv_table_ws9(int* count) {
                                          Ws9Inst<_Float16, WS9_NW, true, false>::info(),
                                          // ReCoNet's 9x9 first layer (48 channels padded to 64)
                                          Ws9Inst<__bf16, WS9_NW, false, false, 64>::info(),
-                                         Ws9Inst<_Float16, WS9_NW, false, false, 64>::info()};
+                                         Ws9Inst<_Float16, WS9_NW, false, false, 64>::info(),
+                                         // ... storing its 48 channels unpadded
+                                         Ws9Inst<__bf16, WS9_NW, false, false, 64, 48>::info(),
+                                         Ws9Inst<_Float16, WS9_NW, false, false, 64, 48>::info()};
   *count = (int)(sizeof(table) / sizeof(table[0]));
   return table;
 }

@@ -475,7 +475,7 @@ std::vector<float> pack_wphase_weights(const ConvKernelInfo& k, const LayerDef& 
 // tap, part q = input channels 32q..32q+31, tap = 3 dy + dx; lane l holds MFMA row l & 15 = output
 // channel 16 cg + (l & 15), K elements = input channels 32 q + 8 (l >> 4) + i.
 std::vector<float> pack_ws2_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
-  const int ncg = k.bn / 16, nstep = 9 * (k.cinp / 32);
+  const int ncg = k.bn / 16, nstep = 9 * ((k.cinp_k ? k.cinp_k : k.cinp) / 32);
   std::vector<float> out((size_t)ncg * nstep * 64 * 8, 0.f);
   for (int cg = 0; cg < ncg; ++cg)
     for (int s = 0; s < nstep; ++s)
@@ -499,11 +499,13 @@ std::vector<float> pack_ws2_weights(const ConvKernelInfo& k, const LayerDef& d, 
 // [j][m][lane][4 bf16], kernel row 4 j + (l >> 4), input channel i.)
 // 64-channel kernels (k.bn == 64, ReCoNet): one such 32-channel set per channel half, half h = channels 32 h ..
 std::vector<float> pack_ws9_weights(const ConvKernelInfo& k, const LayerDef& d, const float* W) {
-  if (k.bn > 32) {
+  const int bnk = k.bn_k ? k.bn_k : k.bn;  // computed channels (the stored bn may be narrower)
+  if (bnk > 32) {
     std::vector<float> all;
-    for (int h = 0; h < k.bn / 32; ++h) {
+    for (int h = 0; h < bnk / 32; ++h) {
       ConvKernelInfo kh = k;
       kh.bn = 32;
+      kh.bn_k = 0;
       LayerDef dh = d;
       dh.cout = std::max(0, std::min(32, d.cout - 32 * h));
       const std::vector<float> part =
@@ -981,6 +983,13 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       if (li == 11) Ly.coutp = 96;
       if (li == 12) Ly.cinp = 96;
     }
+    // the first layer's 48-channel output (encoder.layers.0 -> .1): the 9x9 kernel stores 48 of 64, the down-conv
+    // stages zeros for the rest (with the unpadded 96-channel encoder map only)
+    if (is_reconet(arch) && !f32_storage(compute_dtype) &&
+        !(flags & (NST_KSEL_PAD_48 | NST_KSEL_PAD_ENCODER | NST_KSEL_NO_WS9 | NST_KSEL_NO_WS2 | NST_KSEL_NO_PREPAD))) {
+      if (li == 0) Ly.coutp = 48;
+      if (li == 1) Ly.cinp = 48;
+    }
     // ... and its 48-channel output (decoder.layers.3 -> .4): the phase kernel stores 48 of its 64 computed channels,
     // the output conv stages zeros for the missing 16 (the three-part phase kernel and the row-streaming output conv
     // only: not with the padded 96-channel decoder stream or without those kernels)
@@ -1381,6 +1390,10 @@ int forward_impl(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int i
     }
     if (mode == MODE_WSTAT && p.res_r != nullptr && (p.in_norm == nullptr || p.res_out == nullptr || p.res_relu)) {
       set_error("conv " + Ly.d.conv + ": weight-stationary kernel joins IN(y) + r into a residual-stream buffer");
+      return NST_E_SHAPE;
+    }
+    if (mode == MODE_WS2 && k->cinp_k && (p.axis_mode != AX_REFLECT)) {
+      set_error("conv " + Ly.d.conv + ": the narrow-input down-conv is built for reflection padding");
       return NST_E_SHAPE;
     }
     if (mode == MODE_WS2 && (p.in_norm == nullptr || p.res_r != nullptr || p.crop_x || p.crop_y)) {

@@ -517,7 +517,8 @@ def test_reconet_unpadded_96_channel_maps_vs_padded(arch, h, w, pad):
     up-conv computes 96 output channels and the 96 -> 48 one three 32-channel K parts.  Encoder (encoder.layers.1 ->
     .2): the 48 -> 96 down-conv on 12-wave weight-stationary tiles (6 channel groups x 2 row groups), the 96 -> 192 one
     with a K of 96.  And the decoder's 48-channel output (decoder.layers.3 -> .4): the phase kernel stores 48 of its 64
-    computed channels, the output conv stages zeros for the other 16 (NST_KSEL_PAD_48: the 64-channel stride).
+    computed channels, the output conv stages zeros for the other 16; likewise the first layer's 48-channel output
+    (encoder.layers.0 -> .1) between the 9x9 kernel and the down-conv (NST_KSEL_PAD_48: 64-channel strides).
     The padded programs (NST_KSEL_PAD_DECODER / _ENCODER: 128-channel strides) add zero weights times
     zero-valued channels only; the encoder's InstanceNorm partials come in two row groups per tile instead of one, so
     its statistics may round differently in the last bit (decoder: measured identical)."""
