@@ -44,6 +44,9 @@
 #ifndef NST_GEN_NTAB
 #define NST_GEN_NTAB 1
 #endif
+#ifndef NST_GEN_NTAB_RES
+#define NST_GEN_NTAB_RES 1  // the residual-join fills too: ReCoNet 820 -> 828-835 frames/s (r05_ad)
+#endif
 
 namespace nst {
 
@@ -477,8 +480,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
   // non-persistent fill whose threads' chunks vary per item (NT % NCH != 0: ReCoNet's 96 / 192-channel layers): the
   // tile's frame's IN table {scale, shift} in LDS, read per item instead of from memory (e2 0.75 -> 0.61 ms, plain trunk
   // 0.64-0.73 -> 0.59-0.66 per batch of 8)
-  // (not for the residual-join fill: ReCoNet's joined trunk conv measured 0.03 ms slower with it)
-  constexpr bool NTAB = NST_GEN_NTAB && !PERS && INK == IN_ACT && (NT % NCH) != 0 && (VAR & VAR_RES) == 0;
+  constexpr bool NTAB = NST_GEN_NTAB && !PERS && INK == IN_ACT && (NT % NCH) != 0 && (NST_GEN_NTAB_RES || (VAR & VAR_RES) == 0);
   constexpr int NTAB_OFF = RING_END;
   constexpr int LDS_TOTAL0 = PERS ? RED_OFF + C::RED_BYTES : RING_END + (NTAB ? 2 * CINP * 8 : 0);
   constexpr int LDS_TOTAL = LDS_TOTAL0 > C::LDS_ALLOC ? LDS_TOTAL0 : C::LDS_ALLOC;
