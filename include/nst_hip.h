@@ -144,8 +144,8 @@ int nst_workspace_bytes(const nst_handle* h, int n, int in_h, int in_w, size_t* 
 
 /* Run each nst_forward batch as k sub-batches (1 <= k <= 4) on internal streams forked from and joined back to the
  * caller's stream (events only: the caller's stream order is kept, frames are independent, outputs identical).
- * Default: 2 for the ReCoNet nets in the 16-bit modes (their generic kernels' launch gaps and tails are filled by
- * the other sub-batches), 1 otherwise.  Profiling and the range check run a batch whole.  Replaces no reference
+ * Default: 2 for the ReCoNet nets in the 16-bit modes and for NST_DT_F32S (their generic kernels' launch gaps and
+ * tails are filled by the other sub-batches), 1 otherwise.  Profiling and the range check run a batch whole.  Replaces no reference
  * call: scheduling only. */
 int nst_set_stream_split(nst_handle* h, int k);
 

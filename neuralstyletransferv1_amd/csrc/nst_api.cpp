@@ -1160,7 +1160,8 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
   // -> 10.38-10.45 ms per 8 1080p frames (4 sub-batches: 11.1, more streams than the 4 hardware queues;
   // tools/stream_split_bench.py, profiles/r05_x_stream_split.txt); the Johnson / NST programs (persistent kernels
   // filling every CU) measured slower split (5.17 -> 5.27 / 5.44 ms), fp16m neutral
-  h->split = is_reconet(arch) && !f32_storage(compute_dtype) ? 2 : 1;
+  // The split-fp16 mode's generic kernels gain too: Johnson fp32s 478 -> 485 frames/s with 2 (profiles/r05_ag_*)
+  h->split = (is_reconet(arch) && !f32_storage(compute_dtype)) || compute_dtype == NST_DT_F32S ? 2 : 1;
   *out = h;
   return NST_OK;
 }

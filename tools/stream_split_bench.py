@@ -66,7 +66,7 @@ for S in (1, 2, 4):
         ref = y.clone()
     out[f"split_{S}"] = {"ms_per_step": round(ms, 3), "frames_per_s": round(N / ms * 1e3, 1),
                          "identical": bool(torch.equal(y, ref))}
-for k in (1, 2, 4):
+for k in (1, 2, 3, 4):
     eng.set_stream_split(k)
     for _ in range(3):
         y2 = eng.stylize_u8(frames, "imagenet_255")
