@@ -1489,9 +1489,12 @@ int nst_forward(nst_handle* h, const void* x, int x_fmt, int n, int in_h, int in
   const Plan Q = make_plan(h, nb, in_h, in_w);
   if (!Q.ok) { set_error(Q.err); return NST_E_SHAPE; }
   const size_t per = align256(Q.ws_bytes);
-  if (!workspace || workspace_bytes < per * parts) {
-    set_error("nst_forward: workspace too small (" + std::to_string(workspace_bytes) + " < " + std::to_string(per * parts) +
-              "; nst_workspace_bytes sizes the split batch)");
+  // the size nst_workspace_bytes reports (the split slices, or the whole batch's plan if larger): one contract
+  const Plan Pn = make_plan(h, n, in_h, in_w);
+  if (!Pn.ok) { set_error(Pn.err); return NST_E_SHAPE; }
+  const size_t need = std::max(Pn.ws_bytes, per * parts);
+  if (!workspace || workspace_bytes < need) {
+    set_error("nst_forward: workspace too small (" + std::to_string(workspace_bytes) + " < " + std::to_string(need) + ")");
     return NST_E_WORKSPACE;
   }
   DeviceGuard guard(h->device);

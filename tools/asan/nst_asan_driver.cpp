@@ -111,6 +111,21 @@ void run_arch(const Params& P) {
            "unknown preset is rejected");
     expect(nst_forward(nullptr, x, NST_IO_U8_NHWC, n, h, w, NST_PRESET_IMAGENET_255, yf, NST_IO_F32_NCHW, ws, ws_bytes,
                        nullptr) == NST_E_INVALID, "null handle is rejected");
+    // the batch as sub-batches on the library's internal streams (split 3: one sub-batch per frame here; after the
+    // error paths, which use the workspace size of the handle's default split)
+    expect(nst_set_stream_split(hd, 0) == NST_E_INVALID && nst_set_stream_split(hd, 5) == NST_E_INVALID &&
+               nst_set_stream_split(nullptr, 2) == NST_E_INVALID, "bad stream splits are rejected");
+    expect(nst_set_stream_split(hd, 3) == NST_OK, "nst_set_stream_split");
+    {
+      size_t wsb3 = 0;
+      expect(nst_workspace_bytes(hd, n, h, w, &wsb3) == NST_OK && wsb3 > 0, "nst_workspace_bytes (split)");
+      void* ws3 = nullptr;
+      HC(hipMalloc(&ws3, wsb3));
+      expect(nst_forward(hd, x, NST_IO_U8_NHWC, n, h, w, NST_PRESET_IMAGENET_255, yf, NST_IO_F32_NCHW, ws3, wsb3,
+                         nullptr) == NST_OK, "nst_forward split u8 -> f32");
+      expect(hipDeviceSynchronize() == hipSuccess, "device sync (split)");
+      HC(hipFree(ws3));
+    }
     expect(nst_num_layers(hd) > 0 && nst_layer_name(hd, 0) != nullptr, "layer names");
     expect(hipDeviceSynchronize() == hipSuccess, "device sync");
     HC(hipFree(ws));
