@@ -44,6 +44,9 @@
 #ifndef NST_GEN_NTAB
 #define NST_GEN_NTAB 1
 #endif
+#ifndef NST_GEN_RES_PASSES
+#define NST_GEN_RES_PASSES 2
+#endif
 #ifndef NST_GEN_NTAB_RES
 #define NST_GEN_NTAB_RES 1  // the residual-join fills too: ReCoNet 820 -> 828-835 frames/s (r05_ad)
 #endif
@@ -646,13 +649,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
            wk.tx0 + lx - p.pad < p.ow;
   };
   // srcs[k] keeps each item's source offset (-1 = zero padding) for the store pass
-  auto issue_loads = [&](const Work& wk, int slot, uint4 (&raw)[IPT], uint4 (&raw2)[IPT], int (&srcs)[IPT]) {
+  // items kbase .. kbase + N - 1 of this thread (N = the arrays' extent: the whole fill, or one pass of it)
+  auto issue_loads = [&](const Work& wk, int slot, auto& raw, auto& raw2, auto& srcs, int kbase) {
+    constexpr int N = std::extent_v<std::remove_reference_t<decltype(srcs)>>;
     const char* img = (const char*)p.in + (size_t)wk.n * frame_bytes;
     const char* img2 = (const char*)p.res_r + (size_t)wk.n * frame_bytes;
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
+    for (int k = 0; k < N; ++k) {
       int e, c;
-      const int src = item_src(slot, k, e, c);
+      const int src = item_src(slot, k + kbase, e, c);
       srcs[k] = src;
       raw[k] = make_uint4(0u, 0u, 0u, 0u);
       raw2[k] = make_uint4(0u, 0u, 0u, 0u);
@@ -672,12 +677,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
       for (int j = 0; j < C::CPC; ++j) rnmc[j] = p.res_rnorm[(size_t)n * p.cs + c_fixed * C::CPC + j];
     }
   };
-  auto stage = [&](const Work& wk, const uint4 (&raw)[IPT], const uint4 (&raw2)[IPT], const int (&srcs)[IPT],
-                   const float2 (&nmc)[C::CPC], const float2 (&rnmc)[C::CPC]) {
+  auto stage = [&](const Work& wk, const auto& raw, const auto& raw2, const auto& srcs, const float2 (&nmc)[C::CPC],
+                   const float2 (&rnmc)[C::CPC], int kbase) {
+    constexpr int N = std::extent_v<std::remove_reference_t<decltype(srcs)>>;
     char* rout = (char*)p.res_out + (size_t)wk.n * frame_bytes;
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const int it = tid + k * NT;
+    for (int k = 0; k < N; ++k) {
+      const int it = tid + (k + kbase) * NT;
       if (it < NITEMS) {
         const int e = it / NCH, c = FIXED_CHUNK ? c_fixed : it - e * NCH;
         uint4 v = raw[k];
@@ -1314,8 +1320,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
     }
   } else {
     if constexpr (INK == IN_ACT) {
-      uint4 raw[IPT], raw2[IPT];
-      int srcs[IPT];
+      // the residual join holds two staged tensors per item: with many items per thread (ReCoNet's 192-channel
+      // halos: 16-17) the fill runs in two passes, so its registers do not spill (the joined trunk conv: 92 B/lane of
+      // scratch in one pass, 0.89-0.94 -> 0.77-0.78 ms in two; the 192-channel phase up-conv keeps 12 B either way and
+      // measured slower in three)
+      constexpr int NPASS = (resf && IPT > 8) ? NST_GEN_RES_PASSES : 1;
+      constexpr int IPP = (IPT + NPASS - 1) / NPASS;
+      uint4 raw[IPP], raw2[IPP];
+      int srcs[IPP];
       float2 nmc[C::CPC], rnmc[C::CPC];
       build_maps(cur, 0);
       if constexpr (NTAB) {
@@ -1326,9 +1338,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(ConvParams p) {
         }
       }
       __syncthreads();
-      issue_loads(cur, 0, raw, raw2, srcs);
       load_norm(cur.n, nmc, rnmc);
-      stage(cur, raw, raw2, srcs, nmc, rnmc);
+#pragma unroll
+      for (int ps = 0; ps < NPASS; ++ps) {
+        issue_loads(cur, 0, raw, raw2, srcs, ps * IPP);
+        stage(cur, raw, raw2, srcs, nmc, rnmc, ps * IPP);
+      }
     } else {
       stage_image(cur);
     }
