@@ -46,6 +46,7 @@ HBM_PEAK_GBS = 8000.0
 # measured ceilings beside the spec: back-to-back v_mfma_f32_16x16x32_bf16 on random operands
 # at the trunk kernel's occupancy (two waves per SIMD), and a streaming copy, tools/peak_bench.hip
 PEAKS_JSON = "profiles/r05_peaks.json"
+POWER_JSON = "profiles/r05_at_power.json"
 # Algorithmic work: 307,584 FLOP and 822 B (bf16 activations) per output pixel.
 FLOP_PER_PIXEL = 307584
 BYTES_PER_PIXEL = 822
@@ -163,6 +164,22 @@ def _measured_peaks():
                 "what": "v_mfma_f32_16x16x32_bf16 back to back on random operands at two waves per SIMD; the best "
                         "streaming copy (read + write bytes) and read of tools/peak_bench.hip"}
     except (OSError, KeyError, ValueError):
+        return None
+
+
+def _sustained_power():
+    """The step's sustained socket power and compute clocks (profiles/r05_at_power.json, amd-smi beside a long
+    back-to-back run of this workload), or None: the MFMA ceiling at the clock the power cap leaves."""
+    try:
+        with open(os.path.join(REPO, POWER_JSON)) as f:
+            d = json.load(f)
+        mhz = [v for s in d["samples"] for v in s["gfx_mhz"]]
+        w = [s["socket_w"] for s in d["samples"]]
+        clk = float(np.mean(mhz)) / d["max_gfx_mhz"]
+        return {"socket_w": round(float(np.mean(w)), 1), "board_limit_w": d["board_limit_w"],
+                "gfx_mhz": round(float(np.mean(mhz)), 1), "max_gfx_mhz": d["max_gfx_mhz"], "clock_frac": round(clk, 4),
+                "mfma_peak_at_clock_tflops": round(MFMA_BF16_PEAK_TFLOPS * clk, 1), "source": POWER_JSON}
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -406,6 +423,7 @@ def main():
     # profiled pass: per-conv HIP events on the forward's stream
     kp = max(3, min(args.steps, 10))
     measured = _measured_peaks()
+    power = _sustained_power()
     eng.profile_begin()
     torch.cuda.synchronize(dev)
     for _ in range(kp):
@@ -493,6 +511,10 @@ def main():
             "measured_peak": measured,
             "frac_of_measured_peak": (round(achieved_tflops / measured["mfma_tflops"], 4)
                                       if (achieved_tflops and measured) else None),
+            # the step holds the board at its power limit: the spec MFMA rate scaled to the sustained clock
+            "sustained_power": power,
+            "frac_at_sustained_clock": (round(achieved_tflops / power["mfma_peak_at_clock_tflops"], 4)
+                                        if (achieved_tflops and power) else None),
             # the same kernel build's rocprofv3 --kernel-trace average (profiles/pmc_res_conv.json; profiled runs
             # clock a few % lower than this un-profiled pass), so the fraction reproduces from the kept summary
             "rocprof_avg_launch_ms": round(prof_us / 1e3, 4) if prof_us else None,
