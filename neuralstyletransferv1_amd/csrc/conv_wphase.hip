@@ -579,18 +579,22 @@ constexpr int WP1_NF = 8;  // frames per launch (IN tables in LDS)
 #define NST_WPR_TH 6
 #endif
 constexpr int WPR_TH = NST_WPR_TH;  // ReCoNet 96 -> 64 tile rows: 6 (0.81-0.87 ms per batch of 8) over 4 (0.92-0.97) and 2 (1.38); 8 leaves no LDS for the staged output tile (2.9)
+#ifndef NST_WP2_TH
+#define NST_WP2_TH 12
+#endif
+constexpr int WP2_TH = NST_WP2_TH;  // 64 -> 32 tile rows: 12 (540 = 45 tiles) fit with one-tensor slots
 #define E(...) WphaseInst<__VA_ARGS__>::info()
 const ConvKernelInfo* conv_table_wphase(int* count) {
   static const ConvKernelInfo table[] = {
       //  T     CINP COUT TH NF RES
       E(__bf16, 128, 64, WP1_TH, WP1_NF, false),    // deconv1 / up1
       E(__bf16, 128, 64, WP1_TH, WP1_NF, true),     // deconv1 joining the last residual block (fused join)
-      E(__bf16, 64, 32, 12, 8, false),              // deconv2 / up2: 12 rows (540 = 45 tiles) fit with one-tensor slots
+      E(__bf16, 64, 32, WP2_TH, 8, false),          // deconv2 / up2
       E(__bf16, 96, 64, WPR_TH, 8, false),          // ReCoNet decoder 96 -> 48 (padded to 64; three parts)
       E(__bf16, 96, 64, WPR_TH, 8, false, 48),      // ... storing its 48 channels unpadded
       E(_Float16, 128, 64, WP1_TH, WP1_NF, false),  // fp16 mode
       E(_Float16, 128, 64, WP1_TH, WP1_NF, true),
-      E(_Float16, 64, 32, 12, 8, false),
+      E(_Float16, 64, 32, WP2_TH, 8, false),
       E(_Float16, 96, 64, WPR_TH, 8, false),
       E(_Float16, 96, 64, WPR_TH, 8, false, 48),
   };
