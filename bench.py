@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="process-group backend for --gpus N > 1 (nccl = RCCL over xGMI; gloo stages the exchange "
                          "through host memory, so N ranks can rehearse the multi-GPU command on one GPU)")
+    ap.add_argument("--process-group", action="store_true",
+                    help="create the process group even for one rank (torch.distributed.run --nproc-per-node 1), so "
+                         "the barriers and the max-over-ranks all-reduce run on RCCL with the one GPU a box has")
     ap.add_argument("--device", type=int, default=None,
                     help="GPU index for this rank (default LOCAL_RANK); e.g. 0 to put every rank on one GPU")
     return ap.parse_args()
@@ -278,7 +281,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = args.device if args.device is not None else (local if world > 1 else 0)
-    if world > 1:
+    pg = world > 1 or args.process_group
+    if pg:
         torch.cuda.set_device(gpu)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -343,7 +347,7 @@ def main():
 
     def timed(k):
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if pg:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -354,10 +358,10 @@ def main():
             for _ in range(k):
                 out = step()
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if pg:
             dist.barrier()
         el = time.perf_counter() - t0
-        if world > 1:
+        if pg:
             t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -493,7 +497,7 @@ def main():
             "parallelism": f"frames round-robin over {world} GPU(s), " +
                            ("point-to-point L-plane gather to rank 0 and return to the owners" if args.gather
                             else "no data-path collective"),
-            "dist_backend": args.dist_backend if world > 1 else None,
+            "dist_backend": args.dist_backend if pg else None,
             "ranks_per_gpu": (world if args.device is not None else 1) if world > 1 else 1,
         },
         "roofline": {
@@ -590,7 +594,7 @@ def main():
             })
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if pg:
         dist.barrier()
         dist.destroy_process_group()
 
