@@ -55,6 +55,12 @@ class Engine:
         self._f16m_src = (host, kernel_flags) if self.dtype == _lib.NST_DT_F16M else None
         self._twin: Optional["Engine"] = None
         self._exact: Dict[Tuple[int, int], bool] = {}
+        # NST_RANGE_CHECK=1: every forward checks for values that left the compute dtype's range (NST_E_RANGE; a
+        # synchronising debug aid for the fp16 / split modes, off by default).  Set once here; set_range_check
+        # overrides it and carries over to the fp32s twin
+        self._range_check = False
+        if os.environ.get("NST_RANGE_CHECK", "0") == "1":
+            self.set_range_check(True)
 
     def _for_input(self, x_fmt: int, pid: int) -> "Engine":
         """The engine that runs this input format and preset: self, or the fp32s twin (see __init__)."""
@@ -70,6 +76,7 @@ class Engine:
         if self._twin is None:
             host, flags = self._f16m_src
             self._twin = Engine(self.arch, host, "fp32s", self.device, flags & ~_lib.KSEL["f16m_two_blocks"])
+            self._twin.set_range_check(self._range_check)  # the parent's current setting
         return self._twin
 
     def forward_into(self, x: torch.Tensor, x_fmt: int, n: int, h: int, w: int, pid: int, y: torch.Tensor,
@@ -80,13 +87,13 @@ class Engine:
         ws = e.workspace(n, h, w)
         check(lib().nst_forward(e._h, x.data_ptr(), x_fmt, n, h, w, pid, y.data_ptr(), y_fmt, ws.data_ptr(),
                                 ws.numel(), _lib.stream_ptr(self.device)), "nst_forward")
-        # NST_RANGE_CHECK=1: every forward checks for values that left the compute dtype's range (NST_E_RANGE; a
-        # synchronising debug aid for the fp16 / split modes, off by default)
-        if os.environ.get("NST_RANGE_CHECK", "0") == "1":
-            self.set_range_check(True)
 
     def set_range_check(self, enable: bool) -> None:
+        """nst_set_range_check on this engine and on its fp32s twin (inputs routed to the twin are checked too)."""
+        self._range_check = bool(enable)
         check(lib().nst_set_range_check(self._h, 1 if enable else 0), "nst_set_range_check")
+        if self._twin is not None:
+            self._twin.set_range_check(enable)
 
     def set_stream_split(self, k: int) -> None:
         """nst_set_stream_split: run each batch as k sub-batches on the library's internal streams (1 = whole)."""

@@ -760,6 +760,8 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
         # one waiter thread per run waits for the copy's event and then hands the frames to the encoder pool, so no
         # pool thread sits blocked on the GPU (the pool also decodes the next groups)
         pending.append(waiter.submit(_hand_off, ev, host_t, list(idx) if not args.no_save else []))
+        del host_t  # the waiter holds it until the copy is done; the savers' row views keep it alive after that
+        _reap_pending()
         if not args.no_save:
             written.extend(idx)
         done[0] += len(idx)
@@ -818,7 +820,27 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     def _hand_off(ev, host_t, idx):
         ev.synchronize()
         host = host_t.numpy()
-        return [pool.submit(_save, host[j], f) for j, f in enumerate(idx)], host_t
+        # each save holds a row view of the page-locked buffer (numpy keeps the tensor as the view's base), so the
+        # buffer is released when the group's last save ends -- not held for the whole run
+        return [pool.submit(_save, host[j], f) for j, f in enumerate(idx)]
+
+    saves = []  # save futures of handed-off groups, reaped as they finish (errors surface at the next reap)
+
+    def _reap_pending(final: bool = False):
+        keep = []
+        for p in pending:
+            if final or p.done():
+                saves.extend(p.result())
+            else:
+                keep.append(p)
+        pending[:] = keep
+        left = []
+        for q in saves:
+            if final or q.done():
+                q.result()
+            else:
+                left.append(q)
+        saves[:] = left
 
     def _save(img: np.ndarray, f: int):
         out_img = Image.fromarray(img)
@@ -847,15 +869,21 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     if ordered_lab or flow_mode:
         run_pipeline(groups, world, rank, stylize_send, root_post, emit, ret_spec, dev, caps)
     else:  # no ordered stage: every rank runs its frames start to finish, no exchange
-        for sh in my_shards:
+        from .frames import agree_ok
+        for sh in my_shards:  # one entry per group on every rank (empty where this rank has no frames of it)
+            err = None
             if sh:
-                _, full = stylize_send(sh)
-                emit(sh, None, full)
+                try:
+                    _, full = stylize_send(sh)
+                    emit(sh, None, full)
+                except Exception as e:  # noqa: BLE001 -- re-raised below, after the other ranks have heard of it
+                    err = e
+            if world > 1:  # keep the ranks in step on errors, as run_pipeline does (RankFailed on the healthy ones)
+                agree_ok(err is None, dev)
+            if err is not None:
+                raise err
     with prof("drain_saves"):
-        for p in pending:
-            futs, _keep = p.result()
-            for q in futs:
-                q.result()
+        _reap_pending(final=True)
     waiter.shutdown()
     pool.shutdown()
     prof.report(rank)
