@@ -10,7 +10,9 @@ SLP ?= -fno-slp-vectorize
 CXXFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off $(SLP) -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
 SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_ws1s.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_f32s.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/conv_gemm.hip $(CSRC)/seg_ops.hip $(CSRC)/region_ops.hip $(CSRC)/flow_ops.hip $(CSRC)/dis_ops.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp $(CSRC)/seg_deeplab.cpp $(CSRC)/region_api.cpp $(CSRC)/flow_api.cpp
-OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
+# conv_wst32.hip: four objects from one source, one (dtype, join) instantiation pair each (NST_W32_PART)
+W32_OBJS := $(BUILD)/conv_wst32_p0.hip.o $(BUILD)/conv_wst32_p1.hip.o $(BUILD)/conv_wst32_p2.hip.o $(BUILD)/conv_wst32_p3.hip.o
+OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS)) $(W32_OBJS)
 LIB := $(PKG)/libnst_hip.so
 
 all: $(LIB)
@@ -27,6 +29,9 @@ $(BUILD)/conv_wstat.hip.o $(BUILD)/conv_wphase.hip.o $(BUILD)/conv_ws9.hip.o $(B
 # pragma-unroll size cap for that translation unit only
 $(BUILD)/conv_bf16_wl.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=200000
 $(BUILD)/conv_wstat.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
+$(BUILD)/conv_wst32_p%.hip.o: $(CSRC)/conv_wst32.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h include/nst_hip.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(CXXFLAGS) -mllvm -pragma-unroll-threshold=5000000 -DNST_W32_PART=$* -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $@.rem && python3 tools/check_scratch.py $@.rem || { rm -f $@; exit 1; }
 $(BUILD)/conv_wphase.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
 $(BUILD)/conv_wphase.hip.o: SLP =
 $(BUILD)/conv_ws2.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
@@ -61,3 +66,15 @@ clean:
 	rm -rf $(BUILD) $(LIB) build/asan $(ASAN_BIN)
 
 .PHONY: all clean asan
+
+# diagnostic library with s_memtime stamps in the 32x32x16 trunk kernel (tools/w32_stamps.py; NST_HIP_LIB selects it)
+# (STAMP_TAG / STAMP_FLAGS: variant builds for A/B, e.g. make stamp STAMP_TAG=st2 STAMP_FLAGS=-DNST_W32_ST=2)
+STAMP_TAG ?= stamp
+STAMP_FLAGS ?=
+STAMP_LIB := $(PKG)/libnst_hip_$(STAMP_TAG).so
+build/$(STAMP_TAG)/conv_wst32.hip.o: $(CSRC)/conv_wst32.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h include/nst_hip.h
+	@mkdir -p build/$(STAMP_TAG)
+	$(HIPCC) $(CXXFLAGS) -mllvm -pragma-unroll-threshold=5000000 -DNST_WST32_STAMP=1 $(STAMP_FLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $@.rem && python3 tools/check_scratch.py $@.rem
+$(STAMP_LIB): build/$(STAMP_TAG)/conv_wst32.hip.o $(filter-out $(W32_OBJS),$(OBJS))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+stamp: $(STAMP_LIB)

@@ -435,7 +435,7 @@ def main():
     torch.cuda.synchronize(dev)
     prof = eng.profile_end()
 
-    # dominant kernel: the residual-trunk conv without a fused join (conv_wstat.hip, WF_NORM):
+    # dominant kernel: the residual-trunk conv without a fused join (conv_wst32.hip, WF_NORM):
     # res1.conv1 and every res*.conv2, 6 launches per step; res2..5.conv1 also join the residual
     # stream in their fill (reported separately in whole_path)
     def _plain(n):  # "res1.conv1.conv2d", "res3.conv2.conv2d", ...
@@ -502,7 +502,8 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": f"wstat_kernel<8, WF_NORM> (residual-trunk conv 3x3 128->128 @{hq}x{wq}x{BATCH}, 6 launches/step)",
+            "kernel": (f"wst32_kernel<bf16, 8, WF_NORM> (conv_wst32.hip: residual-trunk conv 3x3 128->128 on 32x32x16 MFMAs, "
+                       f"one wave per SIMD, @{hq}x{wq}x{BATCH}, 6 launches/step)"),
             "achieved": round(achieved_tflops, 2) if achieved_tflops else None,
             "peak": MFMA_BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s",
@@ -527,7 +528,7 @@ def main():
                 "rocprof_avg_launch_ms": round(prof_joined_us / 1e3, 4) if prof_joined_us else None,
                 "rocprof_frac": (round(res_flop / (prof_joined_us * 1e-6) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4)
                                  if prof_joined_us else None),
-                "kernel": "wstat_kernel<8, WF_RES> (the same conv with the residual join in its fill, 4 launches/step)",
+                "kernel": "wst32_kernel<bf16, 8, WF_RES> (the same conv with the residual join in its fill, 4 launches/step)",
                 "avg_launch_ms": round(joined_avg_ms, 4),
                 "achieved": round(res_flop / (joined_avg_ms * 1e-3) / 1e12, 2) if joined_avg_ms else None,
                 "frac": round(res_flop / (joined_avg_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4) if joined_avg_ms else None,

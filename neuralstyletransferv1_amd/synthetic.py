@@ -22,6 +22,14 @@ import torch
 
 ARCHS = ("johnson", "nst", "reconet", "reconet_frn")
 _OUTPUT_CAL = {"johnson": (127.5, 60.0), "nst": (0.5, 0.25), "reconet": (0.0, 1.0), "reconet_frn": (0.0, 1.0)}
+# raw-output calibration for a checkpoint trained with a given io_preset (pipeline.py:1445-1486 decodes): the raw
+# output whose decode is ~0.5 +- 0.235 (the 127.5 +- 60 of the 0..255 presets), so the stylized frame spans the
+# preset's range; channel means / stds of the ImageNet presets averaged over RGB
+_PRESET_CAL = {
+    "imagenet_255": (127.5, 60.0), "raw_255": (127.5, 60.0), "caffe_bgr": (127.5, 60.0),
+    "raw_01": (0.5, 0.235), "tanh": (0.0, 0.47),
+    "imagenet_01": ((0.5 - (0.485 + 0.456 + 0.406) / 3) / ((0.229 + 0.224 + 0.225) / 3), 0.235 / ((0.229 + 0.224 + 0.225) / 3)),
+}
 
 
 def build_module(arch: str):
@@ -42,12 +50,14 @@ def _final_conv_name(arch: str) -> str:
             "reconet_frn": "decoder.layers.4.layers.0.layers.1"}[arch]
 
 
-def make_state_dict(arch: str, seed: int = 0) -> Dict[str, torch.Tensor]:
-    """Ordered {name: fp32 tensor} with the reference's keys for `arch`."""
+def make_state_dict(arch: str, seed: int = 0, preset: str | None = None) -> Dict[str, torch.Tensor]:
+    """Ordered {name: fp32 tensor} with the reference's keys for `arch`.  `preset` (Johnson): calibrate the output
+    conv for a checkpoint trained with that io_preset (_PRESET_CAL); every other tensor is the same as without it
+    (the random stream is consumed identically, only the output conv's scale and offset differ)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     template = build_module(arch).state_dict()
     final = _final_conv_name(arch)
-    mean, std = _OUTPUT_CAL[arch]
+    mean, std = _OUTPUT_CAL[arch] if preset is None else _PRESET_CAL[preset]
     out: Dict[str, torch.Tensor] = {}
     for name, t in template.items():
         shape = tuple(t.shape)

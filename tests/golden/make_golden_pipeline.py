@@ -2,7 +2,7 @@
 on a 256x256 JPEG (configs[0]) -- build container only; /root/reference does not exist on the GPU box and nothing
 at test time reads it (pin the pipeline glue to the reference's own code).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_pipeline.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_pipeline.py [--calibrated]
 
 pipeline.py imports torchvision and cv2 at module level; neither is installed here.  The run puts a shim directory
 first on PYTHONPATH (where this exact shim was verified):
@@ -109,6 +109,42 @@ def run_ref(shim, argv, cwd):
     return r.stdout
 
 
+# --calibrated: the presets whose decode range differs from the default checkpoint's 0..255 raw output, each run
+# with a checkpoint calibrated for it (synthetic.make_state_dict(..., preset=...)), into pipeline_c0_cal.npz
+CALIBRATED = [
+    ("imagenet_01_cal", "imagenet_01", ["--io_preset", "imagenet_01"]),
+    ("tanh_cal", "tanh", ["--io_preset", "tanh"]),
+    ("raw_01_cal", "raw_01", ["--io_preset", "raw_01"]),
+    ("tanh_cal_nolab", "tanh", ["--io_preset", "tanh", "--no-smooth_lightness"]),
+]
+
+
+def main_calibrated():
+    from neuralstyletransferv1_amd import synthetic
+    ins = [os.path.join(HERE, f"pipeline_c0_in{i}.jpg") for i in range(2)]  # the committed inputs
+    arrays, cases = {}, []
+    with tempfile.TemporaryDirectory() as tmp:
+        shim = os.path.join(tmp, "shim")
+        write_shim(shim)
+        for name, preset, extra in CALIBRATED:
+            ck = os.path.join(tmp, f"johnson_0_{preset}.pth")
+            if not os.path.exists(ck):
+                torch.save(synthetic.make_state_dict("johnson", 0, preset=preset), ck)
+            out = os.path.join(tmp, f"out_{name}.png")
+            argv = ["--input_image", ins[0], "--output_image", out, "--model", ck, "--device", "cpu",
+                    "--work_dir", os.path.join(tmp, f"w_{name}")] + extra
+            run_ref(shim, argv, tmp)
+            arrays[f"out_{name}"] = np.array(Image.open(out).convert("RGB"))
+            cases.append({"name": name, "args": extra, "ckpt_preset": preset})
+            print(name, arrays[f"out_{name}"].mean(), arrays[f"out_{name}"].std())
+    import PIL
+    meta = {"cases": {"single": cases, "seq": []}, "torch": torch.__version__, "pillow": PIL.__version__,
+            "numpy": np.__version__, "model": "synthetic.make_state_dict('johnson', 0, preset=<ckpt_preset>)",
+            "inputs": [os.path.basename(ins[0])]}
+    np.savez_compressed(os.path.join(HERE, "pipeline_c0_cal.npz"), meta=np.array(json.dumps(meta)), **arrays)
+    print("wrote", os.path.join(HERE, "pipeline_c0_cal.npz"))
+
+
 def main():
     from neuralstyletransferv1_amd import synthetic
     frames = synthetic.make_frames(2, 256, 256, seed=77)
@@ -155,4 +191,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main_calibrated() if "--calibrated" in sys.argv else main()

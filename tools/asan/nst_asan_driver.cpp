@@ -15,6 +15,8 @@
 
 #include <cstdint>
 #include <cstdio>
+
+#include <sanitizer/allocator_interface.h>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -181,10 +183,18 @@ int main(int argc, char** argv) {
   }
   run_gram();
   std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "ok", g_fail);
-  // Every handle and buffer is released above, under ASan.  Leave without running the HIP runtime's static
-  // destructors: its exit-time teardown frees HSA objects after ASan's device allocator has been unloaded, which
-  // trips ASan's own "dev_runtime_unloaded_" CHECK on some runs (seen in r05_ao, outside any nst_* call).
+  // Every handle and buffer is released above, under ASan.  The cause of r05_ao's abort: ROCm's ASan runtime
+  // intercepts hsa_amd_memory_pool_allocate / _free, so each device buffer hipFree returns goes into ASan's
+  // quarantine like a host chunk (use-after-free detection), and is really released only when the quarantine
+  // recycles it.  At exit the HIP runtime's static destructors shut HSA down first (ASan marks the device runtime
+  // unloaded), then free host objects; one of those operator deletes tips the quarantine over its limit, the recycle
+  // reaches a parked DEVICE chunk, and ASan's CHECK(!dev_runtime_unloaded_) fires (the r05_ao stack:
+  // __cxa_finalize in libamdhip64 -> libhsa-runtime64 -> operator delete -> quarantine recycle).  No nst_* buffer
+  // is leaked or freed late: the chunks were freed correctly and only parked.  So drain the quarantine while the
+  // runtime is alive (__sanitizer_purge_allocator: Allocator::Purge recycles every parked chunk) and leave through
+  // the normal exit path, static destructors included.
+  __sanitizer_purge_allocator();
   std::fflush(stdout);
   std::fflush(stderr);
-  std::_Exit(g_fail ? 1 : 0);
+  return g_fail ? 1 : 0;
 }
