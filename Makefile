@@ -10,9 +10,12 @@ SLP ?= -fno-slp-vectorize
 CXXFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off $(SLP) -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
 SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_ws1s.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_f32s.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/conv_gemm.hip $(CSRC)/seg_ops.hip $(CSRC)/region_ops.hip $(CSRC)/flow_ops.hip $(CSRC)/dis_ops.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp $(CSRC)/seg_deeplab.cpp $(CSRC)/region_api.cpp $(CSRC)/flow_api.cpp
-# conv_wst32.hip: four objects from one source, one (dtype, join) instantiation pair each (NST_W32_PART)
+# conv_wst16.hip (the residual trunk): nine objects from one source (NST_W16_PART: 0..7 two explicitly instantiated
+# kernels each, ~2-3 min per kernel, compiled in parallel; 8 the launchers and the table).  conv_wst32.hip, its 32x32x16 variant, only for A/B
+# libraries (`make wst32`: libnst_hip_wst32.so, where NST_WST16=0 selects it)
+W16_OBJS := $(patsubst %,$(BUILD)/conv_wst16_p%.hip.o,0 1 2 3 4 5 6 7 8)
 W32_OBJS := $(BUILD)/conv_wst32_p0.hip.o $(BUILD)/conv_wst32_p1.hip.o $(BUILD)/conv_wst32_p2.hip.o $(BUILD)/conv_wst32_p3.hip.o
-OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS)) $(W32_OBJS)
+OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS)) $(W16_OBJS)
 LIB := $(PKG)/libnst_hip.so
 
 all: $(LIB)
@@ -29,6 +32,13 @@ $(BUILD)/conv_wstat.hip.o $(BUILD)/conv_wphase.hip.o $(BUILD)/conv_ws9.hip.o $(B
 # pragma-unroll size cap for that translation unit only
 $(BUILD)/conv_bf16_wl.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=200000
 $(BUILD)/conv_wstat.hip.o: CXXFLAGS += -mllvm -pragma-unroll-threshold=5000000
+$(BUILD)/conv_wst16_p%.hip.o: $(CSRC)/conv_wst16.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h include/nst_hip.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(CXXFLAGS) -mllvm -pragma-unroll-threshold=5000000 -DNST_W16_PART=$* -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $@.rem && python3 tools/check_scratch.py $@.rem || { rm -f $@; exit 1; }
+# part 8: launchers and table only (every kernel an extern template: no kernel, no resource remarks)
+$(BUILD)/conv_wst16_p8.hip.o: $(CSRC)/conv_wst16.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h include/nst_hip.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(CXXFLAGS) -DNST_W16_PART=8 -c $< -o $@
 $(BUILD)/conv_wst32_p%.hip.o: $(CSRC)/conv_wst32.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h include/nst_hip.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(CXXFLAGS) -mllvm -pragma-unroll-threshold=5000000 -DNST_W32_PART=$* -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $@.rem && python3 tools/check_scratch.py $@.rem || { rm -f $@; exit 1; }
@@ -65,16 +75,21 @@ asan: $(ASAN_BIN)
 clean:
 	rm -rf $(BUILD) $(LIB) build/asan $(ASAN_BIN)
 
-.PHONY: all clean asan
+.PHONY: all clean asan stamp wst32
 
 # diagnostic library with s_memtime stamps in the 32x32x16 trunk kernel (tools/w32_stamps.py; NST_HIP_LIB selects it)
 # (STAMP_TAG / STAMP_FLAGS: variant builds for A/B, e.g. make stamp STAMP_TAG=st2 STAMP_FLAGS=-DNST_W32_ST=2)
 STAMP_TAG ?= stamp
 STAMP_FLAGS ?=
 STAMP_LIB := $(PKG)/libnst_hip_$(STAMP_TAG).so
-build/$(STAMP_TAG)/conv_wst32.hip.o: $(CSRC)/conv_wst32.hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h include/nst_hip.h
+STAMP_SRC ?= conv_wst16
+build/$(STAMP_TAG)/conv_wst32.hip.o: $(CSRC)/$(STAMP_SRC).hip $(CSRC)/conv_impl.h $(CSRC)/conv_ws_common.h include/nst_hip.h
 	@mkdir -p build/$(STAMP_TAG)
 	$(HIPCC) $(CXXFLAGS) -mllvm -pragma-unroll-threshold=5000000 -DNST_WST32_STAMP=1 $(STAMP_FLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $@.rem && python3 tools/check_scratch.py $@.rem
-$(STAMP_LIB): build/$(STAMP_TAG)/conv_wst32.hip.o $(filter-out $(W32_OBJS),$(OBJS))
+$(STAMP_LIB): build/$(STAMP_TAG)/conv_wst32.hip.o $(filter-out $(BUILD)/$(STAMP_SRC)_p%.hip.o,$(OBJS))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 stamp: $(STAMP_LIB)
+
+$(PKG)/libnst_hip_wst32.so: $(OBJS) $(W32_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+wst32: $(PKG)/libnst_hip_wst32.so

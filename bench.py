@@ -345,6 +345,57 @@ def main():
         for ev in done[-2:]:
             ev.synchronize()
 
+    def verify_gather(k=2):
+        """--gather self-check, outside the timed region: k more groups through the same schedule with a fresh EMA
+        (the state crosses a group boundary; gather, ordered stage and return leg all run), then rank 0 recomputes
+        them single-rank from every rank's regenerated seeded frames and compares the ordered-EMA planes bytewise and
+        each owner's final frames (merge + blend 0.9) by their sha256 (gathered from the ranks)."""
+        import hashlib
+        ema = LabSmoother(dev, True, 0.65)
+        got_planes, got_fin = [], []
+
+        def stylize(idx):
+            out = eng.stylize_u8(frames, PRESET)
+            return ema.planes(out), out
+
+        def root_post(g, full):
+            sm = ema.smooth_planes(full, (H, W))
+            got_planes.append(sm.clone())
+            return sm
+
+        def emit(idx, rows, out):
+            got_fin.append(blend_frames(ema.merge(out, rows), frames, 0.9))
+        run_pipeline([group] * k, world, rank, stylize, root_post, emit, lambda g: ((1, H * W), torch.uint8), dev, caps)
+        torch.cuda.synchronize(dev)
+
+        def sha(ts):
+            return hashlib.sha256(b"".join(t.cpu().numpy().tobytes() for t in ts)).hexdigest()[:16]
+        shas = [sha(got_fin)]
+        if pg:
+            shas = [None] * world
+            dist.all_gather_object(shas, sha(got_fin))
+        if rank != 0:
+            return None
+        ref = LabSmoother(dev, True, 0.65)
+        fr = [torch.from_numpy(synthetic.make_frames(caps[r], H, W, seed=1000 + r)).to(dev) for r in range(world)]
+        outs = [eng.stylize_u8(f, PRESET) for f in fr]
+        own = owners(len(group), world, caps)
+        local = [sum(1 for o in own[:j] if o == own[j]) for j in range(len(group))]  # frame j's index on its owner
+        pl = [ref.planes(o) for o in outs]
+        planes_ok, fins = True, [[] for _ in range(world)]
+        for gi in range(k):
+            full = torch.stack([pl[own[j]][local[j]] for j in range(len(group))])
+            sm = ref.smooth_planes(full, (H, W))
+            planes_ok = planes_ok and gi < len(got_planes) and torch.equal(sm, got_planes[gi])
+            for r in range(world):
+                rows = torch.stack([sm[j] for j in range(len(group)) if own[j] == r])
+                fins[r].append(blend_frames(ref.merge(outs[r], rows), fr[r], 0.9))
+        want = [sha(fins[r]) for r in range(world)]
+        return {"groups": k, "ranks": world, "planes_match": bool(planes_ok and len(got_planes) == k),
+                "frames_match": want == shas, "frames_sha16_per_rank": shas,
+                "what": "ordered-EMA planes of every group and each owner's final frames equal a single-rank "
+                        "recomputation on rank 0 (every rank's seeded frames regenerated)"}
+
     def timed(k):
         torch.cuda.synchronize(dev)
         if pg:
@@ -435,7 +486,7 @@ def main():
     torch.cuda.synchronize(dev)
     prof = eng.profile_end()
 
-    # dominant kernel: the residual-trunk conv without a fused join (conv_wst32.hip, WF_NORM):
+    # dominant kernel: the residual-trunk conv without a fused join (conv_wst16.hip, WF_NORM):
     # res1.conv1 and every res*.conv2, 6 launches per step; res2..5.conv1 also join the residual
     # stream in their fill (reported separately in whole_path)
     def _plain(n):  # "res1.conv1.conv2d", "res3.conv2.conv2d", ...
@@ -502,7 +553,7 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": (f"wst32_kernel<bf16, 8, WF_NORM> (conv_wst32.hip: residual-trunk conv 3x3 128->128 on 32x32x16 MFMAs, "
+            "kernel": (f"wst16_kernel<bf16, 8, WF_NORM> (conv_wst16.hip: residual-trunk conv 3x3 128->128 on 16x16x32 MFMAs, "
                        f"one wave per SIMD, @{hq}x{wq}x{BATCH}, 6 launches/step)"),
             "achieved": round(achieved_tflops, 2) if achieved_tflops else None,
             "peak": MFMA_BF16_PEAK_TFLOPS,
@@ -528,7 +579,7 @@ def main():
                 "rocprof_avg_launch_ms": round(prof_joined_us / 1e3, 4) if prof_joined_us else None,
                 "rocprof_frac": (round(res_flop / (prof_joined_us * 1e-6) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4)
                                  if prof_joined_us else None),
-                "kernel": "wst32_kernel<bf16, 8, WF_RES> (the same conv with the residual join in its fill, 4 launches/step)",
+                "kernel": "wst16_kernel<bf16, 8, WF_RES> (the same conv with the residual join in its fill, 4 launches/step)",
                 "avg_launch_ms": round(joined_avg_ms, 4),
                 "achieved": round(res_flop / (joined_avg_ms * 1e-3) / 1e12, 2) if joined_avg_ms else None,
                 "frac": round(res_flop / (joined_avg_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4) if joined_avg_ms else None,
@@ -560,6 +611,10 @@ def main():
         }
     for key, (_, info) in alt_modes.items():
         result[key] = info
+    if args.gather:
+        vg = verify_gather()
+        if rank == 0:
+            result["gather_verify"] = vg
     if rank == 0 and world == 1 and not args.no_fp32:
         # the fp32 parity mode (exact-f32 MFMA), same frames
         net.compute_dtype = "fp32"

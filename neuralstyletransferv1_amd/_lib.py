@@ -89,7 +89,7 @@ class NstError(RuntimeError):
 # Sources (and build flags) that determine the residual-trunk kernel's machine code: the key under
 # which tools/pmc_summary.py files that kernel's PMC traffic and bench.py looks it up, so unrelated
 # library changes do not orphan the measurement (and any change to the kernel does).
-TRUNK_KERNEL_SOURCES = ("csrc/conv_wst32.hip", "csrc/conv_ws_common.h", "csrc/conv_impl.h")
+TRUNK_KERNEL_SOURCES = ("csrc/conv_wst16.hip", "csrc/conv_ws_common.h", "csrc/conv_impl.h")
 
 
 def kernel_sha(sources=TRUNK_KERNEL_SOURCES, obj: str = "conv_wstat") -> str:
@@ -111,7 +111,7 @@ def kernel_sha(sources=TRUNK_KERNEL_SOURCES, obj: str = "conv_wstat") -> str:
 
 
 def trunk_kernel_sha() -> str:
-    return kernel_sha(TRUNK_KERNEL_SOURCES, "conv_wst32")
+    return kernel_sha(TRUNK_KERNEL_SOURCES, "conv_wst16")
 
 
 # the NST_DT_F16M mode's dominant kernel (the split-operand down-conv conv2, conv_ws2.hip)

@@ -1,27 +1,21 @@
-// conv_wst32.hip — weight-stationary residual-trunk conv on 32x32x16 MFMAs, one wave per SIMD.
+// conv_wst16.hip — weight-stationary residual-trunk conv on 16x16x32 MFMAs, one wave per SIMD.
 //
-// Same layer and fusions as conv_wstat.hip (the residual blocks' ConvLayer(128, 128, 3, 1) of
-// transformer_net.py:57-76 / transformer_net_nst.py:28-43 with the producer's InstanceNorm apply + ReLU or the
-// residual join in the fill and this layer's InstanceNorm partial sums in the epilogue), re-tiled for the
-// measured bound of that kernel: vector-instruction issue, not MFMA (VALU/MFMA 2.37, MFMA busy 0.55;
-// ≈10.6k issue cycles per tile and SIMD against 9.2k of MFMA).
+// conv_wst32.hip's design (4 waves, each holding 32 output channels x 1152 K of weights for the whole launch in 256
+// AGPRs + 32 VGPRs; tiles of TH rows x 32 pixels; LDS-DMA staged fill cut into per-MFMA micro-steps) on the MFMA
+// shape that costs less energy per FLOP: the residual trunk runs at the board's power limit, and
+// bare bf16 loops deliver ~1.12-1.15x the FLOP/s on v_mfma_f32_16x16x32 than on 32x32x16 at equal cycles per FLOP
+// (MI355X_MICROARCH 'DVFS give-back' (7)).  Same layer and fusions (transformer_net.py:57-76 res1..res5,
+// transformer_net_nst.py:28-43): the producer's InstanceNorm apply + ReLU or the residual join in the fill, this
+// layer's InstanceNorm partial sums in the epilogue.
 //
-//   * 4 waves, one per SIMD, each holding 32 output channels x 1152 K of weights for the whole launch:
-//     288 registers per lane, 256 of them AGPRs (MFMA A operands may be AGPRs) and 32 VGPRs.
-//   * v_mfma_f32_32x32x16: one MFMA is 32 channels x 32 pixels x 16 K and holds the SIMD's issue for 8 of its
-//     32 cycles, where two 16x16x32 MFMAs hold it for 16 (MI355X_MICROARCH 'vector-instruction ISSUE cost');
-//     each B operand read (32 pixels x 16 K from LDS) feeds 32 output channels instead of 16, so LDS reads per
-//     MFMA cycle halve too.
-//   * tile = TH rows x 32 pixels (a tile row is one MFMA column block), TH accumulators of 16 fp32 per lane;
-//     halo (TH+2) x 34 entries x 128 channels in LDS, entry stride 272 B (17 x 16 B: the 32 pixels of a B read
-//     land on 16 distinct 4-bank slots in each ds_read_b128 lane group).
-//   * K order: part q (input channels 32q..32q+31), x-tap dx, halo row y, K half kk; LDS row y of x-tap dx is
-//     the B operand of tile row y - dy for every y-tap dy (up to three MFMAs per read).
-//   * fill: region q (chunks 4q..4q+3 of every halo entry) of the NEXT tile streams in while part q+1 of this
-//     tile computes (region 3 of this tile during its own part 0); wave w stages chunk 4q + w of every entry,
-//     NIT items of 64 entries, by LDS-DMA into a ring of NIT slots one region ahead.
-//   * epilogue: bias, bf16 / fp16 packing, v_permlane32_swap pairs into 16-byte stores straight to HBM (no LDS
-//     staging: the 32-pixel halo leaves no room for it), InstanceNorm partial sums reduced over the 32 pixel lanes.
+//   * each wave's 32 channels are two 16-row A blocks; a B read is 32 K x 16 pixels (half a tile row) and feeds both
+//     blocks for every y-tap (up to six MFMAs), so LDS reads per FLOP stay half of conv_wstat.hip's.
+//   * an MFMA holds the SIMD's issue for 8 of its 16 cycles: the fill's micro-steps are one to three instructions
+//     each, one after each MFMA (288 MFMAs per part).
+//   * halo entry stride 288 B (18 x 16 B): the 16 pixels x 4 K-groups of a B read land on 16 distinct 4-bank slots
+//     in each ds_read_b128 lane group (stride 2 slots per pixel, K-groups of a lane group on odd offsets).
+//   * epilogue: bias, packing, v_permlane16_swap pairs (pixel halves) into 16-byte stores, the IN partial sums
+//     reduced over each 16-lane row.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -40,7 +34,7 @@ constexpr uint32_t OOB = 0xFFFFFF00u;  // buffer offset past every launch's reco
 
 // diagnostic build (-DNST_WST32_STAMP=1, a separate library): s_memtime intervals summed per wave in scalar registers
 // (the loop's counted vmcnt waits see no extra memory instruction) and written once at the end into a buffer of its
-// own (nst_debug_w32_stamps): [0..3] parts, [4] epilogue, [5] loop head, [6] tiles
+// own (nst_debug_w16_stamps): [0..3] parts, [4] epilogue, [5] loop head, [6] tiles
 #ifndef NST_WST32_STAMP
 #define NST_WST32_STAMP 0
 #endif
@@ -50,19 +44,19 @@ constexpr uint32_t OOB = 0xFFFFFF00u;  // buffer offset past every launch's reco
 #endif
 #if NST_WST32_STAMP
 constexpr int STAMP_IT = 1, STAMP_PT = 16;
-__device__ long long g_w32_stamp[256 * 4 * STAMP_IT * STAMP_PT];
+__device__ long long g_w16_stamp[256 * 4 * STAMP_IT * STAMP_PT];
 #endif
 
 template <int TH, int FILL>
-struct W32Cfg {
+struct W16Cfg {
   static constexpr bool RES = FILL == WF_RES;
   static constexpr int NW = 4, NT = 256;            // one wave per SIMD, wave w: channels 32w..32w+31
-  static constexpr int TW = 32;                     // tile width = MFMA column block
+  static constexpr int TW = 32;                     // tile width = two MFMA column blocks
   static constexpr int CINP = 128;
   static constexpr int LH = TH + 2, LW = TW + 2;
   static constexpr int NENT = LH * LW;
-  static constexpr int EB = 272;                    // 16 chunks + 1 pad chunk
-  static constexpr int NKS = 72;                    // 4 parts x 9 taps x 2 K halves (K = 16 per MFMA)
+  static constexpr int EB = 288;                    // 16 chunks + 2 pad chunks
+  static constexpr int NKS = 72;                    // 4 parts x 9 taps x 2 channel blocks (K = 32 per MFMA)
   static constexpr int NA = 64;                     // weight steps held in AGPRs (all 256 of them)
   static constexpr int NV = NKS - NA;               // ... and in VGPRs
   static constexpr int NIT = (NENT + 63) / 64;      // items per wave and region (one chunk per wave)
@@ -79,42 +73,42 @@ struct W32Cfg {
   static constexpr int STG_OFF = DUMMY_OFF + 64 * 16;
   static constexpr int LDS = STG_OFF + NIT * NW * SLOTB;
   static constexpr int SST = TH * TW * 4 / NT;      // residual-stream stores per lane and part
-  static constexpr int EPI = 2 * TH + 2;            // epilogue vector-memory instructions per wave
+  static constexpr int EPI = 2 * TH + 1;            // epilogue vector-memory instructions per wave
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(TH * TW * 4 % NT == 0 && TW == 32, "pixel-quarter stores");
 };
 
 template <typename T>
-__device__ __forceinline__ void mfma32_a(f32x16_t& c, const u32x4_t& a, const u32x4_t& b, bool first) {
+__device__ __forceinline__ void mfma16_a(f32x4_t& c, const u32x4_t& a, const u32x4_t& b, bool first) {
   if constexpr (IS_F16<T>) {
-    if (first) asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "a"(a), "v"(b));
-    else asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "a"(a), "v"(b));
+    if (first) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(c) : "a"(a), "v"(b));
+    else asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "a"(a), "v"(b));
   } else {
-    if (first) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "a"(a), "v"(b));
-    else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "a"(a), "v"(b));
+    if (first) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "a"(a), "v"(b));
+    else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "a"(a), "v"(b));
   }
 }
 template <typename T>
-__device__ __forceinline__ void mfma32_v(f32x16_t& c, const u32x4_t& a, const u32x4_t& b, bool first) {
+__device__ __forceinline__ void mfma16_v(f32x4_t& c, const u32x4_t& a, const u32x4_t& b, bool first) {
   if constexpr (IS_F16<T>) {
-    if (first) asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
-    else asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+    if (first) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
+    else asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
   } else {
-    if (first) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
-    else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+    if (first) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
+    else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
   }
 }
 
 template <typename T, int TH, int FILL, bool ZPAD, bool XO>
-__global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
-  using C = W32Cfg<TH, FILL>;
+__global__ __launch_bounds__(256) void wst16_kernel(ConvParams p) {
+  using C = W16Cfg<TH, FILL>;
   constexpr bool RES = C::RES;
   static_assert(!XO || FILL == WF_NORM, "x_0 export is a normalising fill");
   constexpr bool SOUT = RES || XO;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, px = lane & 31;
+  const int g4 = lane >> 4, p16 = lane & 15;  // MFMA K-group / output-row group, pixel within a 16-pixel half
 
   struct Work {
     int n, tile, ty0, tx0;
@@ -136,7 +130,7 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
   if (w0 >= p.n_work) return;
 
   // ---- this wave's 32 output channels x 1152 K: steps 0..NA-1 in AGPRs, the rest in VGPRs ----
-  // packed [wave][step][lane][8 x 16 bit], step s = 2 (9 q + 3 dy + dx) + kk
+  // packed [wave][step][lane][8 x 16 bit], step s = 2 (9 q + 3 dy + dx) + block
   u32x4_t wa[C::NA];
   u32x4_t wvr[C::NV];
   {
@@ -274,18 +268,20 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
   constexpr int KEP = KIN + C::EPI;
 
   // ---- K loop ----
-  typedef f32x16_t Acc[TH];
-  const int lbase = px * C::EB + h * 16;
-  constexpr int NRD = 2 * C::LH;  // reads per dx (halo row, K half)
+  typedef f32x4_t Acc[TH][2][2];  // [tile row][channel block][pixel half]
+  const int lbase = p16 * C::EB + g4 * 16;
+  // K order inside part q: x-tap dx, halo row y, pixel half hx.  LDS row y of x-tap dx is the B operand of tile row
+  // y - dy for every y-tap dy and of both channel blocks: up to six MFMAs per ds_read_b128.
+  constexpr int NRD = 2 * C::LH;  // reads per dx (halo row, pixel half)
   constexpr int PRD = 3 * NRD;    // reads per part
   auto bread = [&](int i) -> u32x4_t {
     const int q = i / PRD, rem = i - q * PRD;
-    const int dx = rem / NRD, y = (rem % NRD) >> 1, kk = rem & 1;
-    return *(const u32x4_t*)(smem + lbase + (y * C::LW + dx) * C::EB + (4 * q + 2 * kk) * 16);
+    const int dx = rem / NRD, y = (rem % NRD) >> 1, hx = rem & 1;
+    return *(const u32x4_t*)(smem + lbase + (y * C::LW + dx + 16 * hx) * C::EB + 4 * q * 16);
   };
-  // One wave per SIMD: nothing hides this wave's non-MFMA work but its own MFMAs' shadow (an MFMA holds the issue
-  // for 8 of its 32 cycles), so the fill is cut into micro-steps of a few instructions, one after each MFMA
-  // (`slot`: the MFMA's index in its part), instead of lumps that leave the MFMA pipe idle.
+  // One wave per SIMD: nothing hides this wave's non-MFMA work but its own MFMAs' shadow (a 16x16x32 MFMA holds the
+  // issue for 8 of its 16 cycles), so the fill is cut into micro-steps of one to three instructions, one after each
+  // MFMA (`slot`: the MFMA's index in its part), instead of lumps that leave the MFMA pipe idle.
   auto kloop = [&](Acc& acc, auto&& filler, auto&& bound) {
     // B reads in flight ahead of their MFMAs: 3, or 2 where the residual-stream pieces need the registers
     constexpr int NI = 4 * PRD, D = SOUT ? 2 : 3;
@@ -296,7 +292,7 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int q = i / PRD, rem = i - q * PRD;
-      const int dx = rem / NRD, y = (rem % NRD) >> 1, kk = rem & 1;
+      const int dx = rem / NRD, y = (rem % NRD) >> 1, hx = rem & 1;
       if (rem == 0) slot = 0;
       const u32x4_t bcur = ring[i % D];
       if (i + D < NI) ring[i % D] = bread(i + D);
@@ -304,13 +300,16 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
       for (int dy = 0; dy < 3; ++dy) {
         const int r = y - dy;
         if (r < 0 || r >= TH) continue;
-        const int s = 2 * (q * 9 + 3 * dy + dx) + kk;
-        const bool first = q == 0 && dx == 0 && dy == 0 && kk == 0;
-        if (s < C::NA) mfma32_a<T>(acc[r], wa[s], bcur, first);
-        else mfma32_v<T>(acc[r], wvr[s - C::NA], bcur, first);
-        filler(q, slot);
-        ++slot;
-        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          const int s = 2 * (q * 9 + 3 * dy + dx) + bb;
+          const bool first = q == 0 && dx == 0 && dy == 0;
+          if (s < C::NA) mfma16_a<T>(acc[r][bb][hx], wa[s], bcur, first);
+          else mfma16_v<T>(acc[r][bb][hx], wvr[s - C::NA], bcur, first);
+          filler(q, slot);
+          ++slot;
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       if (rem == PRD - 1) {
         lds_barrier();
@@ -320,69 +319,62 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
     }
   };
 
-  // ---- epilogue: lane (h, px) holds channels 32 wv + 8 j + 4 h + i (reg 4 j + i) of pixel px of every row ----
-  const float* biasl = (const float*)(smem + C::BIAS_OFF) + 32 * wv + 4 * h;
+  // ---- epilogue: lane (g4, p16) holds channels 32 wv + 16 bb + 4 g4 + i of pixels p16 / 16 + p16 of every row ----
+  const float* biasl = (const float*)(smem + C::BIAS_OFF) + 32 * wv + 4 * g4;
   auto epilogue = [&](const Work& wk, Acc& acc) {
-    // the last MFMAs' results: 16-pass XDL write -> VALU read needs >= 18 wait states
+    // the last MFMAs' results: XDL write -> VALU read wait states
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     const __amdgpu_buffer_rsrc_t ors = launch_rsrc(p.out, ob);
-    const int ox = wk.tx0 + px;
     const uint32_t row_bytes = (uint32_t)p.ow * p.cout_stride * 2;
-    const uint32_t off0 = (uint32_t)wk.n * ob + (uint32_t)(((wk.ty0 * p.ow + ox) * p.cout_stride + 32 * wv) * 2) + 16 * h;
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.partial + ((size_t)wk.n * ntile + wk.tile) * p.cout_stride * 2), (short)0, p.cout_stride * 8, 0x00020000);
+    // after the swaps lane l stores 8 channels (32 wv + 16 bb + 8 (g4 >> 1) + 0..7) of pixel p16 (g4 even) or
+    // 16 + p16 (g4 odd): each store covers the 32 pixels x 32 bytes of one channel block
+    const int spx = wk.tx0 + ((g4 & 1) ? 16 : 0) + p16;
+    const uint32_t soff = (uint32_t)wk.n * ob + (uint32_t)(((wk.ty0 * p.ow + spx) * p.cout_stride + 32 * wv + 8 * (g4 >> 1)) * 2);
+    const bool sok = spx < p.ow;
+    const bool ok0 = wk.tx0 + p16 < p.ow, ok1 = wk.tx0 + 16 + p16 < p.ow;
+    const f32x4_t bias0 = *(const f32x4_t*)(biasl), bias1 = *(const f32x4_t*)(biasl + 16);
+    f32x4_t s1[2], s2[2];
+    auto rows = [&](auto all_valid) {
 #pragma unroll
-    for (int jp = 0; jp < 2; ++jp) {
-      // channel groups g = 2 jp + e (regs 4 g .. 4 g + 3): channels 32 wv + 8 g + 4 h + i
-      const f32x4_t b0 = *(const f32x4_t*)(biasl + 16 * jp), b1 = *(const f32x4_t*)(biasl + 16 * jp + 8);
-      f32x4_t s1a, s2a, s1b, s2b;
-      auto rows = [&](auto all_valid) {
+      for (int r = 0; r < TH; ++r) {
+        const bool rv = decltype(all_valid)::value || wk.ty0 + r < p.oh;
 #pragma unroll
-        for (int r = 0; r < TH; ++r) {
-          const bool valid = decltype(all_valid)::value || (wk.ty0 + r < p.oh && ox < p.ow);
-          const f32x4_t va = (f32x4_t){acc[r][8 * jp], acc[r][8 * jp + 1], acc[r][8 * jp + 2], acc[r][8 * jp + 3]} + b0;
-          const f32x4_t vb = (f32x4_t){acc[r][8 * jp + 4], acc[r][8 * jp + 5], acc[r][8 * jp + 6], acc[r][8 * jp + 7]} + b1;
-          // lanes 32-63 of group 2jp swap with lanes 0-31 of group 2jp+1: lanes 0-31 then hold channels
-          // 16 jp + 0..7 (16 contiguous bytes), lanes 32-63 channels 16 jp + 8..15
-          const auto sx = __builtin_amdgcn_permlane32_swap(pack16<T>(va[0], va[1]), pack16<T>(vb[0], vb[1]), false, false);
-          const auto sy = __builtin_amdgcn_permlane32_swap(pack16<T>(va[2], va[3]), pack16<T>(vb[2], vb[3]), false, false);
+        for (int bb = 0; bb < 2; ++bb) {
+          const f32x4_t v0 = acc[r][bb][0] + (bb ? bias1 : bias0), v1 = acc[r][bb][1] + (bb ? bias1 : bias0);
+          // rows of 16 lanes 1 / 3 of the pixel-half-0 pair swap with rows 0 / 2 of the half-1 pair: lanes of even
+          // rows then hold 8 channels of pixel p16, of odd rows 8 channels of pixel 16 + p16
+          const auto sx = __builtin_amdgcn_permlane16_swap(pack16<T>(v0[0], v0[1]), pack16<T>(v1[0], v1[1]), false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(pack16<T>(v0[2], v0[3]), pack16<T>(v1[2], v1[3]), false, false);
           const u32x4_t pk = {sx[0], sy[0], sx[1], sy[1]};
-          __builtin_amdgcn_raw_buffer_store_b128(pk, ors, valid ? off0 + r * row_bytes + 32 * jp : OOB, 0, NST_W32_ST);
-          const f32x4_t xa = valid ? va : (f32x4_t){0.f, 0.f, 0.f, 0.f};
-          const f32x4_t xb = valid ? vb : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+          __builtin_amdgcn_raw_buffer_store_b128(pk, ors, (rv && sok) ? soff + r * row_bytes + 32 * bb : OOB, 0, NST_W32_ST);
+          const f32x4_t x0 = (decltype(all_valid)::value || (rv && ok0)) ? v0 : (f32x4_t){0.f, 0.f, 0.f, 0.f};
+          const f32x4_t x1 = (decltype(all_valid)::value || (rv && ok1)) ? v1 : (f32x4_t){0.f, 0.f, 0.f, 0.f};
           if (r == 0) {
-            s1a = xa; s2a = xa * xa; s1b = xb; s2b = xb * xb;
+            s1[bb] = x0 + x1;
+            s2[bb] = __builtin_elementwise_fma(x1, x1, x0 * x0);
           } else {
-            s1a = s1a + xa; s2a = __builtin_elementwise_fma(xa, xa, s2a);
-            s1b = s1b + xb; s2b = __builtin_elementwise_fma(xb, xb, s2b);
+            s1[bb] = (s1[bb] + x0) + x1;
+            s2[bb] = __builtin_elementwise_fma(x1, x1, __builtin_elementwise_fma(x0, x0, s2[bb]));
           }
         }
-      };
-      if (wk.ty0 + TH <= p.oh && wk.tx0 + C::TW <= p.ow) rows(std::true_type{});
-      else rows(std::false_type{});
-      // 16 statistics {s1, s2} x 8 channels, summed over the 32 pixel lanes of each half: v[2 ci + st]
-      const float v[16] = {s1a[0], s2a[0], s1a[1], s2a[1], s1a[2], s2a[2], s1a[3], s2a[3],
-                           s1b[0], s2b[0], s1b[1], s2b[1], s1b[2], s2b[2], s1b[3], s2b[3]};
-      // rows of 16 lanes: the lower row keeps values 0..7, the upper 8..15, each summed over both rows
-      float a8[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
-        a8[i] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
       }
-      const int pr = px & 15, upper = (px >> 4) & 1;
-      float a4[4], a2[2], a1[1];
-      rs_step<4, 0x140>(a8, a4, pr >= 8);
-      rs_step<2, 0x141>(a4, a2, (pr & 4) != 0);
-      rs_step<1, 0x1b>(a2, a1, (pr & 2) != 0);
-      const float t = a1[0] + dpp_f<0xb1>(a1[0]);
-      // even lane pr of row `upper` holds value 8 upper + idx: channel ci = value >> 1, statistic value & 1
-      const int idx = 8 * upper + (pr >= 8 ? 4 : 0) + ((pr & 4) ? 2 : 0) + ((pr & 2) ? 1 : 0);
-      const int ci = idx >> 1;
-      const int co = 32 * wv + 16 * jp + (ci < 4 ? 4 * h + ci : 8 + 4 * h + ci - 4);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), prs, (pr & 1) ? 0x80000000u : (uint32_t)((co * 2 + (idx & 1)) * 4),
-                                            0, 0);
-    }
+    };
+    if (wk.ty0 + TH <= p.oh && wk.tx0 + C::TW <= p.ow) rows(std::true_type{});
+    else rows(std::false_type{});
+    // 16 statistics per lane, v[(4 bb + i) 2 + st], reduce-scattered over the 16 pixel lanes of the row: lane p16 ends
+    // with value 8 (p16 >= 8) + 4 (p16 & 4) + 2 (p16 & 2) + (p16 & 1)
+    const float v[16] = {s1[0][0], s2[0][0], s1[0][1], s2[0][1], s1[0][2], s2[0][2], s1[0][3], s2[0][3],
+                         s1[1][0], s2[1][0], s1[1][1], s2[1][1], s1[1][2], s2[1][2], s1[1][3], s2[1][3]};
+    float a8[8], a4[4], a2[2], a1[1];
+    rs_step<8, 0x140>(v, a8, p16 >= 8);
+    rs_step<4, 0x141>(a8, a4, (p16 & 4) != 0);
+    rs_step<2, 0x1b>(a4, a2, (p16 & 2) != 0);
+    rs_step<1, 0xb1>(a2, a1, (p16 & 1) != 0);
+    const int idx = (p16 >= 8 ? 8 : 0) + ((p16 & 4) ? 4 : 0) + ((p16 & 2) ? 2 : 0) + (p16 & 1);
+    const int co = 32 * wv + 16 * (idx >> 3) + 4 * g4 + ((idx >> 1) & 3);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.partial + ((size_t)wk.n * ntile + wk.tile) * p.cout_stride * 2), (short)0, p.cout_stride * 8, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a1[0]), prs, (uint32_t)((co * 2 + (idx & 1)) * 4), 0, 0);
   };
 
   // ---- persistent walk ----
@@ -414,21 +406,23 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
   }
   vm_wait<0>();
   __syncthreads();
-  // Micro-step schedule of item k (MFMA slots 24 k + o of a part; a part has 144 MFMAs):
-  //   o = 0: wait for the item's LDS-DMA, staging read | 2 + 5 j: IN constants of channel pair j (one pair's
-  //   registers at a time) | 5 + 5 j / 6 + 5 j: pair j's lo / hi value | 22: halo write, then the next region's
-  //   request of item k, whose source is resolved at 3 / 8 (map reads, offset; not held across parts: registers).
-  //   RES / XO store residual-stream piece k < SST (19: halo read, 23: store, after the part's k-th request: SST
+  // Micro-step schedule of item k (MFMA slots 48 k + o of a part; a part has 288 MFMAs), at most ~2 instructions
+  // each (the 8 free issue cycles of a 16x16x32 MFMA):
+  //   o = 0: wait for the item's LDS-DMA, staging read | 2: map reads of the next region's item k (the next tile's
+  //   entry) | 4 + 8 j: IN constants of channel pair j | 8 + 8 j .. 11 + 8 j: pair j's value steps | 36, 37: the
+  //   request's source offset | 38: halo write | 40: the next region's request of item k (not held across parts).
+  //   RES / XO store residual-stream piece k < SST (42: halo read, 47: store, after the part's k-th request: SST
   //   stores lie between any item's request and its wait).
-  constexpr int SLOTS_PER_ITEM = 24;
-  static_assert(SLOTS_PER_ITEM * C::NIT <= 9 * TH * 2 && C::SST <= C::NIT, "micro-step slots");
+  constexpr int SLOTS_PER_ITEM = 48;
+  static_assert(SLOTS_PER_ITEM * C::NIT <= 9 * TH * 4 && C::SST <= C::NIT, "micro-step slots");
   Acc acc;
   Staged sy;                 // the staged chunk(s) of the item in flight
   float4 n0;                 // IN constants of one channel pair
-  float tl;                  // a pair's lo value between its two micro-steps
+  float tl, th;              // a pair's lo / hi value between its micro-steps
   uint32_t o4[4];            // the item's packed output
   int mro = 0, mco = 0;      // map entries of the next tile's item k
   bool padk = false;         // ZPAD: the consumed item k is zero padding (parts 1..3)
+  bool mok = false;          // the next tile's item k has a source (not padding, an entry)
   uint32_t rvoff = OOB;      // ... its source offset
   u32x4_t sv;                // residual-stream piece between its halo read and its store
 #if NST_WST32_STAMP
@@ -459,24 +453,24 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
           const int n = q == 0 ? cur.n : nxt.n;
           const int ch = item_chunk(R);
           const float4* ny = (const float4*)(norm_y + (n * 16 + ch) * 16);
-          auto half = [&](int j, int hi) {  // pair j of the staged chunk, lo (hi = 0) or hi value
+          // pair j's value steps: NORM IN + ReLU (fma lo | fma hi | pack + max); RES join (lo: y scale | + shift,
+          // + r | hi: the same | pack; product then sum, one rounding per op, as the unfused residual kernel)
+          auto pair_step = [&](int j, int st) {
             const uint32_t wy = j == 0 ? sy.y.x : j == 1 ? sy.y.y : j == 2 ? sy.y.z : sy.y.w;
-            const float4 nn = n0;
             if constexpr (RES) {
               const uint32_t wr = j == 0 ? sy.r.x : j == 1 ? sy.r.y : j == 2 ? sy.r.z : sy.r.w;
-              // ResidualBlock join (transformer_net.py:71-76): IN_y(y) + r in fp32, product then sum, one rounding
-              if (!hi) {
-                tl = lo16<T>(wr) + (lo16<T>(wy) * nn.x + nn.z);
-              } else {
-                o4[j] = pack16<T>(tl, hi16<T>(wr) + (hi16<T>(wy) * nn.y + nn.w));
-              }
+              // ResidualBlock join (transformer_net.py:71-76): IN_y(y) + r in fp32
+              if (st == 0) tl = lo16<T>(wy) * n0.x;
+              else if (st == 1) tl = lo16<T>(wr) + (tl + n0.z);
+              else if (st == 2) th = hi16<T>(wy) * n0.y;
+              else o4[j] = pack16<T>(tl, hi16<T>(wr) + (th + n0.w));
             } else if constexpr (FILL == WF_RAW) {
-              if (hi) o4[j] = wy;
+              if (st == 3) o4[j] = wy;
             } else {
-              if (!hi) {
-                tl = __builtin_fmaf(lo16<T>(wy), nn.x, nn.z);
-              } else {
-                const i16x2_t r = __builtin_bit_cast(i16x2_t, pack16<T>(tl, __builtin_fmaf(hi16<T>(wy), nn.y, nn.w)));
+              if (st == 0) tl = __builtin_fmaf(lo16<T>(wy), n0.x, n0.z);
+              else if (st == 1) th = __builtin_fmaf(hi16<T>(wy), n0.y, n0.w);
+              else if (st == 3) {
+                const i16x2_t r = __builtin_bit_cast(i16x2_t, pack16<T>(tl, th));
                 o4[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(r, (i16x2_t){0, 0}));
               }
             }
@@ -484,47 +478,47 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
           if (o == 0) {
             if (q == 0) vm_wait<KEP>(); else vm_wait<KIN>();
             sy = stage_read(k);
-          } else if (o == 2 || o == 7 || o == 12 || o == 17) {
-            if (FILL != WF_RAW) n0 = ny[(o - 2) / 5];  // pair j's IN constants, read three MFMAs before its use
-          } else if (o == 5 || o == 10 || o == 15 || o == 20) {
-            half((o - 5) / 5, 0);
-          } else if (o == 6 || o == 11 || o == 16 || o == 21) {
-            half((o - 6) / 5, 1);
-          } else if (o == 22) {
-            const bool pad = ZPAD && (q == 0 ? ((pad3 >> k) & 1u) != 0 : padk);
-            const u32x4_t v = {pad ? 0u : o4[0], pad ? 0u : o4[1], pad ? 0u : o4[2], pad ? 0u : o4[3]};
-            const bool valid = k < C::NIT - 1 || lane < C::LASTN;
-            int eb = item_entry(0) * C::EB + ch * 16;
-            asm volatile("" : "+v"(eb));
-            *(u32x4_t*)(smem + (valid ? eb + k * IT_STRIDE * C::EB : C::DUMMY_OFF + lane * 16)) = v;
-            request(k, q, rvoff);  // region q of nxt
-          } else if (o == 3) {
+          } else if (o >= 4 && o < 36 && (o - 4) % 8 == 0) {
+            if (FILL != WF_RAW) n0 = ny[(o - 4) / 8];  // pair j's IN constants, four MFMAs before its first step
+          } else if (o >= 8 && o < 36 && (o - 4) % 8 >= 4) {
+            pair_step((o - 4) / 8, (o - 4) % 8 - 4);
+          } else if (o == 2) {
             const int* rowmap = (const int*)(smem + C::MAP_OFF + ns * C::MAPB);
             const bool valid = k < C::NIT - 1 || lane < C::LASTN;
             const int e = valid ? item_entry(k) : 0;
             const int ly = e / C::LW, lx = e - ly * C::LW;
             mro = rowmap[ly];
             mco = rowmap[C::LH + lx];
-          } else if (o == 8) {
+          } else if (o == 36) {
             const bool valid = k < C::NIT - 1 || lane < C::LASTN;
-            const bool in = valid && mro >= 0 && mco >= 0;
-            rvoff = in ? (uint32_t)(mro + mco) + (uint32_t)nxt.n * fb : OOB;
-            // ZPAD: a zero-padding entry.  Parts 1..3 consume the item they request (nxt's item k: !in); part 3
-            // keeps the flags for the next iteration's part 0, which consumes this tile's region 3
+            mok = valid && mro >= 0 && mco >= 0;
+            // ZPAD: a zero-padding entry.  Parts 1..3 consume the item they request (nxt's item k); part 3 keeps
+            // the flags for the next iteration's part 0, which consumes this tile's region 3
             if (ZPAD) {
-              padk = valid && !in;
+              padk = valid && !mok;
               if (q == 3) pad3 = (pad3 & ~(1u << k)) | (padk ? 1u << k : 0u);
             }
+          } else if (o == 37) {
+            rvoff = mok ? (uint32_t)(mro + mco) + (uint32_t)nxt.n * fb : OOB;
+          } else if (o == 38) {
+            const bool pad = ZPAD && (q == 0 ? ((pad3 >> k) & 1u) != 0 : padk);
+            const u32x4_t v = {pad ? 0u : o4[0], pad ? 0u : o4[1], pad ? 0u : o4[2], pad ? 0u : o4[3]};
+            const bool valid = k < C::NIT - 1 || lane < C::LASTN;
+            int eb = item_entry(0) * C::EB + ch * 16;
+            asm volatile("" : "+v"(eb));
+            *(u32x4_t*)(smem + (valid ? eb + k * IT_STRIDE * C::EB : C::DUMMY_OFF + lane * 16)) = v;
+          } else if (o == 40) {
+            request(k, q, rvoff);  // region q of nxt
           }
           // the tile after nxt into cur's map slot (cur's sources were resolved in the previous iteration; the
           // barriers ending parts 1..3 publish it before the next iteration's part 0 reads it)
-          if (q == 1 && k == 0 && o == 18) build_maps(nxt2, cs);
-          if (SOUT && k < C::SST && o == 19) {
+          if (q == 1 && k == 0 && o == 44) build_maps(nxt2, cs);
+          if (SOUT && k < C::SST && o == 42) {
             const int cl = lane >> 4, x16 = ((lane & 15) - cl) & 15;
             const int P = 16 * (C::SST * wv + k) + x16;
             sv = *(const u32x4_t*)(smem + (((P >> 5) + 1) * C::LW + (P & 31) + 1) * C::EB + (4 * q + cl) * 16);
           }
-          if (SOUT && k < C::SST && o == 23) {
+          if (SOUT && k < C::SST && o == 47) {
             const int cl = lane >> 4, x16 = ((lane & 15) - cl) & 15;
             const int P = 16 * (C::SST * wv + k) + x16;
             const int c = 4 * q + cl, oy = cur.ty0 + (P >> 5), ox = cur.tx0 + (P & 31);
@@ -544,13 +538,13 @@ __global__ __launch_bounds__(256) void wst32_kernel(ConvParams p) {
   vm_wait<0>();  // no LDS-DMA may land after the workgroup has released its LDS
 #if NST_WST32_STAMP
   if (lane == 0 && b < 256)
-    for (int i = 0; i < 7; ++i) g_w32_stamp[(b * 4 + wv) * STAMP_PT + i] = st_acc[i];
+    for (int i = 0; i < 7; ++i) g_w16_stamp[(b * 4 + wv) * STAMP_PT + i] = st_acc[i];
 #endif
 }
 
 template <typename T, int TH, bool RES>
-struct Wst32Inst {
-  using C = W32Cfg<TH, RES ? WF_RES : WF_NORM>;
+struct Wst16Inst {
+  using C = W16Cfg<TH, RES ? WF_RES : WF_NORM>;
   static int cus() {
     static const int v = [] {
       int dev = 0, c = 0;
@@ -562,7 +556,7 @@ struct Wst32Inst {
   }
   template <int FILL, bool ZPAD, bool XO = false>
   static void go(const ConvParams& p, int nb, hipStream_t st) {
-    hipLaunchKernelGGL((wst32_kernel<T, TH, FILL, ZPAD, XO>), dim3(nb), dim3(C::NT), 0, st, p);
+    hipLaunchKernelGGL((wst16_kernel<T, TH, FILL, ZPAD, XO>), dim3(nb), dim3(C::NT), 0, st, p);
   }
   static void launch(const ConvParams& p0, dim3 grid, hipStream_t st) {
     const int ntile = (int)grid.x, n = (int)grid.y;
@@ -606,7 +600,7 @@ struct Wst32Inst {
     std::memset(&k, 0, sizeof(k));
     k.dtype = dtype_code<T>();
     k.mode = MODE_WSTAT;
-    k.ks = 3; k.stride = 1; k.cinp = C::CINP; k.bn = 128; k.th = TH; k.tw = C::TW; k.wm = C::NW; k.wn = 1;
+    k.ks = 3; k.stride = 1; k.cinp = C::CINP; k.bn = 128; k.th = TH; k.tw = C::TW; k.wm = C::NW; k.wn = 2;  // wn = 2: two 16-channel blocks per wave (pack_wst16_weights)
     k.in_kind = IN_ACT; k.out_kind = OUT_ACT;
     k.cpc = 8; k.nch = 16; k.lds_bytes = C::LDS;
     k.wbytes = C::NW * C::NKS * 1024;
@@ -618,42 +612,57 @@ struct Wst32Inst {
   }
 };
 
-#ifndef NST_WST32_TH
-#define NST_WST32_TH 8
+#ifndef NST_WST16_TH
+#define NST_WST16_TH 8
 #endif
-// The four instantiations compile ~1.5 min each (fully unrolled 576-MFMA tiles), so the library builds this file
-// four times in parallel, NST_W32_PART = 0..3 one (dtype, join) pair each; -1 (experiment builds): all in one object.
-#ifndef NST_W32_PART
-#define NST_W32_PART -1
+// Build split: one kernel instantiation compiles for ~2-3 min (fully unrolled 1,152-MFMA tiles), so the library
+// compiles this file nine times in parallel.  NST_W16_PART = 0..7 explicitly instantiate two kernels each (dtype
+// bf16 for 0..3, fp16 for 4..7; p % 4 = 0: normalising fill without / with the x_0 export, 1: the same zero-padded,
+// 2: identity fill, reflect / zero-padded, 3: residual join, reflect / zero-padded); 8 holds the launchers, infos and
+// the table, with every kernel an extern template; -1 (experiment builds): all in one object, instantiated by use.
+#ifndef NST_W16_PART
+#define NST_W16_PART -1
 #endif
-ConvKernelInfo wst32_info_0();
-ConvKernelInfo wst32_info_1();
-ConvKernelInfo wst32_info_2();
-ConvKernelInfo wst32_info_3();
-#if NST_W32_PART < 0 || NST_W32_PART == 0
-ConvKernelInfo wst32_info_0() { return Wst32Inst<__bf16, NST_WST32_TH, false>::info(); }  // residual trunk
+#define W16_KERNELS(X, T)                                                                                     \
+  X(T, WF_NORM, false, false) X(T, WF_NORM, false, true) X(T, WF_NORM, true, false) X(T, WF_NORM, true, true) \
+  X(T, WF_RAW, false, false) X(T, WF_RAW, true, false) X(T, WF_RES, false, false) X(T, WF_RES, true, false)
+#define W16_EXTERN(T, F, Z, X_) extern template __global__ void wst16_kernel<T, NST_WST16_TH, F, Z, X_>(ConvParams);
+#define W16_INST(T, F, Z, X_) template __global__ void wst16_kernel<T, NST_WST16_TH, F, Z, X_>(ConvParams);
+#if NST_W16_PART >= 0 && NST_W16_PART < 8
+#define W16_T_ __bf16
+#if NST_W16_PART >= 4
+#undef W16_T_
+#define W16_T_ _Float16
 #endif
-#if NST_W32_PART < 0 || NST_W32_PART == 1
-ConvKernelInfo wst32_info_1() { return Wst32Inst<__bf16, NST_WST32_TH, true>::info(); }   // + residual join in the fill
+#if NST_W16_PART % 4 == 0
+W16_INST(W16_T_, WF_NORM, false, false)
+W16_INST(W16_T_, WF_NORM, false, true)
+#elif NST_W16_PART % 4 == 1
+W16_INST(W16_T_, WF_NORM, true, false)
+W16_INST(W16_T_, WF_NORM, true, true)
+#elif NST_W16_PART % 4 == 2
+W16_INST(W16_T_, WF_RAW, false, false)
+W16_INST(W16_T_, WF_RAW, true, false)
+#else
+W16_INST(W16_T_, WF_RES, false, false)
+W16_INST(W16_T_, WF_RES, true, false)
 #endif
-#if !NST_W32_MIN && (NST_W32_PART < 0 || NST_W32_PART == 2)
-ConvKernelInfo wst32_info_2() { return Wst32Inst<_Float16, NST_WST32_TH, false>::info(); }  // fp16 mode
+#else
+#if NST_W16_PART == 8
+W16_KERNELS(W16_EXTERN, __bf16)
+W16_KERNELS(W16_EXTERN, _Float16)
 #endif
-#if !NST_W32_MIN && (NST_W32_PART < 0 || NST_W32_PART == 3)
-ConvKernelInfo wst32_info_3() { return Wst32Inst<_Float16, NST_WST32_TH, true>::info(); }
-#endif
-#if NST_W32_PART <= 0
-// searched before conv_table_wstat (first match wins); NST_WST32=0 in the environment hides it (A/B runs)
-const ConvKernelInfo* conv_table_wst32(int* count) {
+// searched before conv_table_wstat (first match wins); NST_WST16=0 in the environment hides it (A/B runs)
+const ConvKernelInfo* conv_table_wst16(int* count) {
   static const ConvKernelInfo table[] = {
-      wst32_info_0(),
-      wst32_info_1(),
+      Wst16Inst<__bf16, NST_WST16_TH, false>::info(),  // residual trunk
+      Wst16Inst<__bf16, NST_WST16_TH, true>::info(),   // + residual join in the fill
 #if !NST_W32_MIN
-      wst32_info_2(),
-      wst32_info_3(),
+      Wst16Inst<_Float16, NST_WST16_TH, false>::info(),  // fp16 mode
+      Wst16Inst<_Float16, NST_WST16_TH, true>::info(),
 #endif
   };
-  const char* env = std::getenv("NST_WST32");
+  const char* env = std::getenv("NST_WST16");
   *count = (env != nullptr && env[0] == '0') ? 0 : (int)(sizeof(table) / sizeof(table[0]));
   return table;
 }
@@ -662,9 +671,9 @@ const ConvKernelInfo* conv_table_wst32(int* count) {
 }  // namespace nst
 
 #if NST_WST32_STAMP
-extern "C" int nst_debug_w32_stamps(long long* host, int n) {
+extern "C" int nst_debug_w16_stamps(long long* host, int n) {
   const int cap = 256 * 4 * nst::STAMP_IT * nst::STAMP_PT;
   if (n > cap) n = cap;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(nst::g_w32_stamp), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(nst::g_w16_stamp), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
 }
 #endif

@@ -31,7 +31,14 @@ const ConvKernelInfo* conv_table_f32(int* count);
 const ConvKernelInfo* conv_table_f32s(int* count);
 const ConvKernelInfo* conv_table_out9(int* count);
 const ConvKernelInfo* conv_table_wstat(int* count);
-const ConvKernelInfo* conv_table_wst32(int* count);
+const ConvKernelInfo* conv_table_wst16(int* count);
+// conv_wst32.hip (32x32x16 variant of the trunk kernel): built only by `make wst32` (A/B builds), so weak here
+const ConvKernelInfo* conv_table_wst32(int* count) __attribute__((weak));
+static const ConvKernelInfo* table_wst32_or_none(int* count) {
+  if (conv_table_wst32 != nullptr) return conv_table_wst32(count);
+  *count = 0;
+  return nullptr;
+}
 const ConvKernelInfo* conv_table_wphase(int* count);
 const ConvKernelInfo* conv_table_ws2(int* count);
 const ConvKernelInfo* conv_table_ws9(int* count);
@@ -42,13 +49,14 @@ const ConvKernelInfo* find_conv_kernel(int dtype, int mode, int ks, int stride, 
                                        int out_kind, int res, bool no_persistent) {
   typedef const ConvKernelInfo* (*TableFn)(int*);
   // 16-bit formats (bf16, fp16) share the specialised tables; an entry matches only its own dtype
-  const TableFn tables_16[] = {conv_table_bf16_wl, conv_table_wst32, conv_table_wstat, conv_table_wphase, conv_table_ws2,
-                               conv_table_ws9, conv_table_out9, conv_table_bf16, conv_table_f16, conv_table_ws1s};
+  const TableFn tables_16[] = {conv_table_bf16_wl, conv_table_wst16, table_wst32_or_none, conv_table_wstat, conv_table_wphase,
+                               conv_table_ws2, conv_table_ws9, conv_table_out9, conv_table_bf16, conv_table_f16,
+                               conv_table_ws1s};
   // 4-byte activation formats (fp32, split-fp16): the generic kernels, and the split-fp16 row-streaming output conv
   const TableFn tables_f32[] = {conv_table_out9, conv_table_f32, conv_table_f32s};
   const bool h16 = !f32_storage(dtype);
   const TableFn* tables = h16 ? tables_16 : tables_f32;
-  const int ntables = h16 ? 10 : 3;
+  const int ntables = h16 ? 11 : 3;
   for (int ti = (h16 && no_persistent) ? 1 : 0; ti < ntables; ++ti) {
     int count = 0;
     const ConvKernelInfo* t = tables[ti](&count);
@@ -461,6 +469,25 @@ std::vector<float> pack_wst32_weights(const LayerDef& d, const float* W) {
         const int co = 32 * w + (l & 31);
         for (int i = 0; i < 8; ++i) {
           const int ci = 32 * q + 16 * kk + 8 * (l >> 5) + i;
+          if (co < d.cout && ci < d.cin)
+            out[(((size_t)w * 72 + s) * 64 + l) * 8 + i] = W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
+        }
+      }
+  return out;
+}
+
+// MODE_WSTAT on 16x16x32 MFMAs (conv_wst16.hip, tw == 32, wn == 2): [wave w][step s][lane][8 x 16 bit].  Step
+// s = 2 (9 q + tap) + b: part q = input channels 32q..32q+31, tap = 3 dy + dx, channel block b; lane l holds MFMA row
+// l & 15 = output channel 32 w + 16 b + (l & 15), K elements = input channels 32 q + 8 (l >> 4) + i.
+std::vector<float> pack_wst16_weights(const LayerDef& d, const float* W) {
+  std::vector<float> out((size_t)4 * 72 * 64 * 8, 0.f);
+  for (int w = 0; w < 4; ++w)
+    for (int s = 0; s < 72; ++s)
+      for (int l = 0; l < 64; ++l) {
+        const int b = s & 1, t = (s >> 1) % 9, q = (s >> 1) / 9, dy = t / 3, dx = t % 3;
+        const int co = 32 * w + 16 * b + (l & 15);
+        for (int i = 0; i < 8; ++i) {
+          const int ci = 32 * q + 8 * (l >> 4) + i;
           if (co < d.cout && ci < d.cin)
             out[(((size_t)w * 72 + s) * 64 + l) * 8 + i] = W[(((size_t)co * d.cin + ci) * d.ks + dy) * d.ks + dx];
         }
@@ -1105,7 +1132,9 @@ int nst_create_ex(int arch, const nst_param* params, int n_params, int compute_d
       if ((rc = Ly.k_main->dtype == NST_DT_F32S ? upload_weights(NST_DT_F16, pk, &Ly.wpk) : upload_packed(pk, &Ly.wpk)) != NST_OK)
         break;
     } else if (Ly.mode == MODE_WSTAT) {
-      if ((rc = upload_packed(Ly.k_main->tw == 32 ? pack_wst32_weights(d, W) : pack_wstat_weights(d, W), &Ly.wpk)) != NST_OK)
+      if ((rc = upload_packed(Ly.k_main->tw != 32 ? pack_wstat_weights(d, W)
+                                                   : Ly.k_main->wn == 2 ? pack_wst16_weights(d, W) : pack_wst32_weights(d, W),
+                              &Ly.wpk)) != NST_OK)
         break;
     } else if (Ly.mode == MODE_WPHASE) {
       if ((rc = upload_packed(pack_wphase_weights(*Ly.k_main, d, W), &Ly.wpk)) != NST_OK) break;

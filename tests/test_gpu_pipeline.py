@@ -344,6 +344,26 @@ def test_bench_two_ranks_under_torchrun_gloo(tmp_path):
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["dist_backend"] == "gloo"
     assert d["config"]["global_batch"] == 16
     assert d["value"] > 0 and abs(d["value"] - d["config"]["global_batch"] * 3 / (d["ms_per_step"] * 3e-3)) < 1e-3 * d["value"]
+    # bench.py's own check of the exchange: the ordered EMA and each owner's final frames equal rank 0's
+    # single-rank recomputation (what the driver's N-GPU --gather run reports)
+    v = d["gather_verify"]
+    assert v["ranks"] == 2 and v["planes_match"] and v["frames_match"], v
+
+
+def test_bench_gather_self_check_one_rank(tmp_path):
+    """bench.py --gather on one rank (no process group): the self-check runs the same exchange schedule (world 1)
+    and matches its recomputation."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1", "--gather",
+                        "--frame", "960x540", "--no-cpu-baseline", "--no-fp32", "--no-fp16", "--no-fp16m", "--no-fp32s"],
+                       capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    v = d["gather_verify"]
+    assert v["ranks"] == 1 and v["planes_match"] and v["frames_match"], v
 
 
 def test_input_dir_staging_in_memory_jpeg_exif_png(tmp_path):

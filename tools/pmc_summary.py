@@ -86,7 +86,7 @@ def main():
     if "--res-json" in sys.argv:  # the dominant kernel's summary bench.py reads (keyed by the library build)
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from neuralstyletransferv1_amd._lib import trunk_kernel_sha
-        key = next(k for k in out if "wst32_kernel<bf16, 8, 0, false, false>" in k)
+        key = next(k for k in out if "wst16_kernel<bf16, 8, 0, false, false>" in k)
         r = out[key]
         res = {
             "source": f"tools/prof_pass.sh {os.path.basename(d.rstrip('/'))} (rocprofv3 --kernel-trace --stats, then "
@@ -103,7 +103,7 @@ def main():
             "mfma_insts_per_launch": r.get("SQ_INSTS_MFMA"),
             "algorithmic_bytes_per_launch": 530841600,
         }
-        jk = next((k for k in out if "wst32_kernel<bf16, 8, 2, false, false>" in k), None)
+        jk = next((k for k in out if "wst16_kernel<bf16, 8, 2, false, false>" in k), None)
         if jk is not None:  # the joined variant (residual join in the fill), same PMC passes
             j = out[jk]
             res["joined"] = {"kernel": jk, "avg_us_profiled": j.get("avg_us"), "hbm_bytes_per_launch": j.get("hbm_bytes"),
