@@ -62,6 +62,10 @@ def parse():
                     help="time the video pipeline's exchange with the forward (configs[3]): L planes to rank 0, ordered "
                          "LAB EMA there, planes back to the owners, merge + blend + D2H on the owner")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="time the step as one HIP-graph replay of the captured forward (engine.capture_u8); "
+                         "--no-graph: ~60 eager launches per step (profiles/r06_graph_ab.txt: with a process group "
+                         "the eager step runs 1.5 %% slower, the graph step not)")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode timing (profiling runs)")
     ap.add_argument("--cpu-frames", type=int, default=3, help="timed 1080p frames per CPU configuration")
     ap.add_argument("--no-fp16", action="store_true", help="skip the fp16-mode timing")
@@ -314,6 +318,15 @@ def main():
 
     def step():
         return eng.stylize_u8(frames, PRESET)
+    if args.graph and not args.gather:
+        # the whole forward as one HIP-graph launch per step (engine.capture_u8): the same kernels on the same
+        # HBM-resident frames, without the host launching ~60 kernels per step
+        from neuralstyletransferv1_amd.engine import capture_u8
+        replay, graph_out = capture_u8(eng, frames, PRESET)
+
+        def step():  # noqa: F811
+            replay()
+            return graph_out
 
     def run_gather(k):
         """--gather: k groups through the video pipeline's schedule (frames.run_pipeline): each rank stylizes its
@@ -396,6 +409,10 @@ def main():
                 "what": "ordered-EMA planes of every group and each owner's final frames equal a single-rank "
                         "recomputation on rank 0 (every rank's seeded frames regenerated)"}
 
+    # diagnostic only (profiles/r06_pg_ab.txt): NST_BENCH_NO_CLOSING_BARRIER=1 leaves the closing barrier out of
+    # the timed region, to separate its cost from the process group's other effects on a one-rank run
+    closing_barrier = os.environ.get("NST_BENCH_NO_CLOSING_BARRIER", "0") != "1"
+
     def timed(k):
         torch.cuda.synchronize(dev)
         if pg:
@@ -409,7 +426,7 @@ def main():
             for _ in range(k):
                 out = step()
         torch.cuda.synchronize(dev)
-        if pg:
+        if pg and closing_barrier:
             dist.barrier()
         el = time.perf_counter() - t0
         if pg:
@@ -550,6 +567,8 @@ def main():
                             else "no data-path collective"),
             "dist_backend": args.dist_backend if pg else None,
             "ranks_per_gpu": (world if args.device is not None else 1) if world > 1 else 1,
+            "step_launch": ("one HIP-graph replay of the captured forward per step" if (args.graph and not args.gather)
+                            else "eager kernel launches"),
         },
         "roofline": {
             "bound": "mfma",
@@ -611,6 +630,8 @@ def main():
         }
     for key, (_, info) in alt_modes.items():
         result[key] = info
+    if args.graph and not args.gather:  # the replayed graph's output is the eager forward's, bit for bit
+        result["graph_step_matches_eager"] = bool(torch.equal(out, eng.stylize_u8(frames, PRESET)))
     if args.gather:
         vg = verify_gather()
         if rank == 0:

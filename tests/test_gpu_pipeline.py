@@ -417,3 +417,26 @@ def test_input_dir_staging_in_memory_jpeg_exif_png(tmp_path):
     assert len(kept) == 3
     for i, p in enumerate(kept):
         assert np.array_equal(np.array(Image.open(p).convert("RGB")), staged[i])
+
+
+def test_capture_u8_graph_replay_matches_eager():
+    """engine.capture_u8 (the bench's HIP-graph step): a replay equals the eager forward bit for bit, and a replay
+    after the input buffer is refilled in place stylizes the new frames."""
+    from neuralstyletransferv1_amd.engine import capture_u8
+    from neuralstyletransferv1_amd.transformer_net import TransformerNet
+    net = TransformerNet()
+    net.load_state_dict(synthetic.make_state_dict("johnson", 0))
+    net = net.cuda().eval()
+    net.compute_dtype = "bf16"
+    eng = net.engine(torch.device("cuda", 0))
+    a = torch.from_numpy(synthetic.make_frames(2, 120, 200, seed=4)).cuda()
+    b = torch.from_numpy(synthetic.make_frames(2, 120, 200, seed=5)).cuda()
+    frames = a.clone()
+    replay, out = capture_u8(eng, frames, "imagenet_255")
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eng.stylize_u8(a, "imagenet_255"))
+    frames.copy_(b)
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eng.stylize_u8(b, "imagenet_255"))
