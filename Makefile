@@ -9,7 +9,7 @@ BUILD := build/obj
 SLP ?= -fno-slp-vectorize
 CXXFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off $(SLP) -Wall -Wno-unused-function \
             -Iinclude -I$(CSRC)
-SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_ws1s.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_f32s.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/conv_gemm.hip $(CSRC)/seg_ops.hip $(CSRC)/region_ops.hip $(CSRC)/flow_ops.hip $(CSRC)/dis_ops.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp $(CSRC)/seg_deeplab.cpp $(CSRC)/region_api.cpp $(CSRC)/flow_api.cpp
+SRCS := $(CSRC)/conv_bf16.hip $(CSRC)/conv_f16.hip $(CSRC)/conv_bf16_wl.hip $(CSRC)/conv_wstat.hip $(CSRC)/conv_wphase.hip $(CSRC)/conv_ws2.hip $(CSRC)/conv_ws9.hip $(CSRC)/conv_ws1s.hip $(CSRC)/conv_out9.hip $(CSRC)/conv_prep.hip $(CSRC)/conv_f32.hip $(CSRC)/conv_f32s.hip $(CSRC)/conv_vgg.hip $(CSRC)/nst_ops.hip $(CSRC)/vgg_ops.hip $(CSRC)/conv_gemm.hip $(CSRC)/seg_ops.hip $(CSRC)/region_ops.hip $(CSRC)/flow_ops.hip $(CSRC)/dis_ops.hip $(CSRC)/png_enc.hip $(CSRC)/nst_api.cpp $(CSRC)/vgg_gatys.cpp $(CSRC)/seg_deeplab.cpp $(CSRC)/region_api.cpp $(CSRC)/flow_api.cpp
 # conv_wst16.hip (the residual trunk): nine objects from one source (NST_W16_PART: 0..7 two explicitly instantiated
 # kernels each, ~2-3 min per kernel, compiled in parallel; 8 the launchers and the table).  conv_wst32.hip, its 32x32x16 variant, only for A/B
 # libraries (`make wst32`: libnst_hip_wst32.so, where NST_WST16=0 selects it)

@@ -529,6 +529,19 @@ int nst_flow_fuse(const float* curr, const float* prev, const float* flow, int h
 int nst_motion_alpha(const float* flow, int h, int w, float motion_norm, double sigma, float max_alpha, float span,
                      float* alpha, float* scratch, void* stream);
 
+/* ---- PNG encode on the owner rank (pipeline.py:2099-2119 `Image.fromarray(out).save(path)`, the reference's
+ * default --image_ext png at :2170) ----
+ * n u8 frames [n,h,w,c] (c = 1 grey, 3 RGB, 4 RGBA; device) -> n complete PNG files, file j at out + j*out_stride,
+ * its byte count in sizes[j] (int64, device).  Every scanline carries the Up filter; each scanline is one deflate
+ * block (dynamic Huffman codes built per frame from that frame's run-length tokens, or a stored block where that is
+ * smaller), the zlib stream's Adler-32 and the chunks' CRC-32 computed on the device.  Lossless: decoders return
+ * the frames' bytes exactly, as from Pillow's file.  out_stride >= nst_png_bound; workspace per
+ * nst_png_workspace_bytes; w*c + 1 <= 65535. */
+int nst_png_bound(int h, int w, int c, size_t* out_stride);
+int nst_png_workspace_bytes(int n, int h, int w, int c, size_t* out);
+int nst_png_encode_u8(const uint8_t* frames, int n, int h, int w, int c, uint8_t* out, size_t out_stride,
+                      int64_t* sizes, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "nst_flow_fuse", "nst_motion_alpha", "nst_flow_downscale_gray", "nst_flow_upscale", "nst_resize_area_u8",
     "nst_flow_dis_scratch_bytes", "nst_flow_dis", "nst_set_range_check", "nst_input_exact", "nst_set_stream_split",
     "nst_lab_planes_u8", "nst_lab_ema_planes", "nst_lab_merge_u8",
+    "nst_png_bound", "nst_png_workspace_bytes", "nst_png_encode_u8",
 )
 # region compositor limits / geometry kinds (include/nst_hip.h NST_REGION_*, NST_RG_*)
 NST_REGION_MAX, NST_REGION_TERMS, NST_REGION_MAX_SRC = 32, 9, 16
@@ -219,6 +220,11 @@ def lib() -> ctypes.CDLL:
         L.nst_lab_ema_planes.argtypes = [vp, vp, i, i, i, i, f, f, i, f, f, vp, i, vp]
         L.nst_lab_merge_u8.argtypes = [vp, vp, vp, i, i, i, i, i, vp, vp]
         L.nst_input_exact.argtypes = [vp, i, i, ctypes.POINTER(i)]
+        L.nst_png_bound.argtypes = [i, i, i, ctypes.POINTER(sz)]
+        L.nst_png_workspace_bytes.argtypes = [i, i, i, i, ctypes.POINTER(sz)]
+        L.nst_png_encode_u8.argtypes = [vp, i, i, i, i, vp, sz, vp, vp, sz, vp]
+        for name in ("nst_png_bound", "nst_png_workspace_bytes", "nst_png_encode_u8"):
+            getattr(L, name).restype = i
         for name in ("nst_lab_planes_u8", "nst_lab_ema_planes", "nst_lab_merge_u8", "nst_input_exact"):
             getattr(L, name).restype = i
         L.nst_blend_u8.argtypes = [vp, vp, vp, i, f, f, vp, i, i, i, vp]

@@ -170,10 +170,12 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--keep_staged", action="store_true",
                     help="--input_dir: also write the staged frame copies (the reference's work_dir/frames files); the "
                          "frames are staged in memory either way, with the same pixels")
-    ap.add_argument("--png_writer", choices=["fast", "pil"], default="pil",
+    ap.add_argument("--png_writer", choices=["fast", "pil", "gpu"], default="pil",
                     help="PNG outputs: 'pil' (default) = Pillow's encoder at its defaults, byte-identical to the "
                          "reference's files; 'fast' = Up filter + zlib RLE deflate (pngio.py: ~6x faster than Pillow's "
-                         "default encoder, files within a few percent of its size, opt-in).  The pixels are "
+                         "default encoder, files within a few percent of its size, opt-in); 'gpu' = the whole file "
+                         "built on the GPU that styled the frame (csrc/png_enc.hip: Up filter, per-scanline dynamic "
+                         "Huffman blocks, CRC and Adler-32 on the device), the host only writes bytes.  The pixels are "
                          "identical either way")
     ap.add_argument("--png_compress_level", type=int, default=None, choices=range(10), metavar="0-9",
                     help="Pillow's PNG encoder at this zlib level (overrides --png_writer); the pixels are the same "
@@ -747,19 +749,32 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
                 h0, w0 = styled.shape[1], styled.shape[2]
                 styled = blend_frames(styled, full[..., 3:].contiguous(), blend, _masks_for(idx, h0, w0),
                                       args.composite_mode)
+        gpu_png = (getattr(args, "png_writer", "pil") == "gpu" and not args.no_save
+                   and getattr(args, "png_compress_level", None) is None and not any(_out_path(f)[1] for f in idx))
         with prof("d2h"):
             # page-locked D2H on a copy stream behind the frames' last kernel; the encoders wait for its event, so
-            # this thread goes on queueing the next group's forward instead of waiting for the GPU
-            host_t = torch.empty(styled.shape, dtype=torch.uint8, pin_memory=True)
+            # this thread goes on queueing the next group's forward instead of waiting for the GPU.  --png_writer gpu:
+            # the group's finished PNG files (and their sizes) instead of the pixels
+            if gpu_png:
+                from .pngio import encode_png_gpu
+                src, sizes_d = encode_png_gpu(styled)
+            else:
+                src, sizes_d = styled, None
+            host_t = torch.empty(src.shape, dtype=torch.uint8, pin_memory=True)
+            host_sz = torch.empty(src.shape[0], dtype=torch.int64, pin_memory=True) if gpu_png else None
             copy_stream.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(copy_stream):
-                host_t.copy_(styled, non_blocking=True)
+                host_t.copy_(src, non_blocking=True)
+                if gpu_png:
+                    host_sz.copy_(sizes_d, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(copy_stream)
-            styled.record_stream(copy_stream)
+            src.record_stream(copy_stream)
+            if gpu_png:
+                sizes_d.record_stream(copy_stream)
         # one waiter thread per run waits for the copy's event and then hands the frames to the encoder pool, so no
         # pool thread sits blocked on the GPU (the pool also decodes the next groups)
-        pending.append(waiter.submit(_hand_off, ev, host_t, list(idx) if not args.no_save else []))
+        pending.append(waiter.submit(_hand_off, ev, host_t, list(idx) if not args.no_save else [], host_sz))
         del host_t  # the waiter holds it until the copy is done; the savers' row views keep it alive after that
         _reap_pending()
         if not args.no_save:
@@ -817,11 +832,14 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
     copy_stream = torch.cuda.Stream(dev)
     waiter = ThreadPoolExecutor(max_workers=1)
 
-    def _hand_off(ev, host_t, idx):
+    def _hand_off(ev, host_t, idx, host_sz=None):
         ev.synchronize()
         host = host_t.numpy()
         # each save holds a row view of the page-locked buffer (numpy keeps the tensor as the view's base), so the
         # buffer is released when the group's last save ends -- not held for the whole run
+        if host_sz is not None:  # finished PNG files from the GPU: write their bytes
+            sz = host_sz.tolist()
+            return [pool.submit(_write_file, host[j, :sz[j]], f) for j, f in enumerate(idx)]
         return [pool.submit(_save, host[j], f) for j, f in enumerate(idx)]
 
     saves = []  # save futures of handed-off groups, reaped as they finish (errors surface at the next reap)
@@ -842,18 +860,29 @@ def style_frames(args, frames_dir: Optional[Path], model_path, output_prefix: st
                 left.append(q)
         saves[:] = left
 
-    def _save(img: np.ndarray, f: int):
-        out_img = Image.fromarray(img)
+    def _out_path(f: int):
+        """frame f's output file and whether it is a JPEG (pipeline.py:2099-2119)"""
         save_as_jpg = image_ext_out.lower() == "jpg"
         if image_mode and (f + 1) in save_map:
             out_path = Path(save_map[f + 1])
-            out_path.parent.mkdir(parents=True, exist_ok=True)
             save_as_jpg = out_path.suffix.lower() in (".jpg", ".jpeg")
         else:
             idx_str = names[f].split("_")[-1]
             base = frames_dir if frames_dir is not None else Path(args.work_dir)
-            base.mkdir(parents=True, exist_ok=True)
             out_path = (base / f"{output_prefix}_{idx_str}").with_suffix(".jpg" if save_as_jpg else ".png")
+        return out_path, save_as_jpg
+
+    def _write_file(data: np.ndarray, f: int):
+        out_path, _ = _out_path(f)
+        out_path.parent.mkdir(parents=True, exist_ok=True)
+        with open(out_path, "wb") as fh:
+            fh.write(memoryview(data))
+        return str(out_path)
+
+    def _save(img: np.ndarray, f: int):
+        out_img = Image.fromarray(img)
+        out_path, save_as_jpg = _out_path(f)
+        out_path.parent.mkdir(parents=True, exist_ok=True)
         if save_as_jpg:
             out_img.save(out_path, format="JPEG", quality=int(jpeg_quality))
         elif getattr(args, "png_compress_level", None) is not None:

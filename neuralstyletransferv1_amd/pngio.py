@@ -12,6 +12,11 @@ valid encoder yields the same pixels; this one writes
 
 File sizes land within a few percent of Pillow's level-6 files; decoding returns the identical uint8 array
 (tests/test_host.py checks with Pillow).  zlib releases the GIL while it deflates, so a thread pool scales.
+
+`encode_png_gpu` builds the same kind of file on the GPU (csrc/png_enc.hip, nst_png_encode_u8): Up filter, one
+deflate block per scanline with dynamic Huffman codes built per frame from its run-length tokens (a stored block
+where that is smaller), Adler-32 and CRC-32 on the device.  The owner rank copies finished files to the host and
+only writes bytes (`--png_writer gpu`).
 """
 from __future__ import annotations
 
@@ -50,3 +55,46 @@ def write_png(path, rgb: np.ndarray, level: int = 1) -> None:
     data = encode_png(rgb, level)
     with open(path, "wb") as f:
         f.write(data)
+
+
+_png_ws = {}  # (device, n, h, w, c) -> workspace tensor, reused across groups
+
+
+def encode_png_gpu(frames_u8):
+    """uint8 frames [n,h,w,c] (c in 1, 3, 4) on an MI355X -> (files [n, stride] uint8, sizes [n] int64), both on
+    the device, on the current stream: file j is files[j, :sizes[j]].  No CPU path: the library must be loaded."""
+    import ctypes
+
+    import torch
+
+    from . import _lib
+    _lib.require_gpu_tensor(frames_u8, "encode_png_gpu frames")
+    x = frames_u8 if frames_u8.dim() == 4 else frames_u8[..., None]
+    if x.dtype != torch.uint8 or x.dim() != 4:
+        raise ValueError(f"encode_png_gpu: need uint8 [n,h,w,c], got {frames_u8.dtype} {tuple(frames_u8.shape)}")
+    x = x.contiguous()
+    n, h, w, c = x.shape
+    L = _lib.lib()
+    bound, wsb = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.check(L.nst_png_bound(h, w, c, ctypes.byref(bound)), "nst_png_bound")
+    _lib.check(L.nst_png_workspace_bytes(n, h, w, c, ctypes.byref(wsb)), "nst_png_workspace_bytes")
+    key = (x.device, n, h, w, c)
+    ws = _png_ws.get(key)
+    if ws is None:
+        if len(_png_ws) > 4:
+            _png_ws.clear()
+        ws = _png_ws[key] = torch.empty(wsb.value, dtype=torch.uint8, device=x.device)
+    files = torch.empty((n, bound.value), dtype=torch.uint8, device=x.device)
+    sizes = torch.empty(n, dtype=torch.int64, device=x.device)
+    _lib.check(L.nst_png_encode_u8(x.data_ptr(), n, h, w, c, files.data_ptr(), bound.value, sizes.data_ptr(),
+                                   ws.data_ptr(), wsb.value, _lib.stream_ptr(x.device)), "nst_png_encode_u8")
+    ws.record_stream(torch.cuda.current_stream(x.device))
+    return files, sizes
+
+
+def png_bytes_gpu(frames_u8) -> list:
+    """encode_png_gpu, copied to the host: one bytes object (a complete PNG file) per frame."""
+    files, sizes = encode_png_gpu(frames_u8)
+    sz = sizes.cpu().tolist()
+    host = files.cpu().numpy()
+    return [host[j, :sz[j]].tobytes() for j in range(len(sz))]

@@ -277,7 +277,7 @@ def test_inference_res_lanczos_cli(tmp_path):
 
 
 @pytest.mark.parametrize("gpus,extra", [(2, []), (3, ["--mask", "MASK", "--smooth_chroma"]),
-                                        (2, ["--no-smooth_lightness"])])
+                                        (2, ["--no-smooth_lightness"]), (2, ["--png_writer", "gpu"])])
 def test_multi_gpu_orchestration_gloo_matches_single(tmp_path, monkeypatch, gpus, extra):
     """The --gpus N orchestration (pipeline.py main -> one spawned process per rank, round-robin frames; the LAB
     planes of every frame to rank 0, the ordered EMA there, the smoothed planes back to each frame's owner, which
@@ -399,7 +399,7 @@ def test_input_dir_staging_in_memory_jpeg_exif_png(tmp_path):
         staged.append(np.array(up))
     outs = {}
     for tag, extra in (("mem", []), ("keep", ["--keep_staged", "--png_compress_level", "1"]),
-                       ("pil", ["--png_writer", "pil"])):
+                       ("pil", ["--png_writer", "pil"]), ("gpu", ["--png_writer", "gpu"])):
         d_out = tmp_path / f"out_{tag}"
         assert P.main(["--input_dir", str(d_in), "--output_dir", str(d_out), "--model", ck, "--io_preset", "imagenet_255",
                        "--pattern", "frame_*", "--no-smooth_lightness", "--batch", "1", "--work_dir",
@@ -413,6 +413,7 @@ def test_input_dir_staging_in_memory_jpeg_exif_png(tmp_path):
         assert d.max() <= 1
         assert np.array_equal(outs["mem"][i], outs["keep"][i])
         assert np.array_equal(outs["mem"][i], outs["pil"][i])
+        assert np.array_equal(outs["mem"][i], outs["gpu"][i])  # the GPU-built file (csrc/png_enc.hip)
     kept = sorted((tmp_path / "w_keep").rglob("frame_*"))
     assert len(kept) == 3
     for i, p in enumerate(kept):

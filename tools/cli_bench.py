@@ -13,7 +13,7 @@ Default CLI settings (bf16, --batch 8, --blend 0.9, --smooth_alpha 0.65, staged/
 --jpeg_quality 85 from quality-95 source files, PNG through the default fast writer) on synthetic frames (smooth gradients + shapes + ~5 LSB
 noise, neuralstyletransferv1_amd/synthetic.py).  The timed run excludes the model load (a warm-up run first).
 
-  python tools/cli_bench.py [--frames 240] [--threads 16] [--png_writer fast|pil]
+  python tools/cli_bench.py [--frames 240] [--threads 16] [--png_writer fast|pil|gpu]
 """
 from __future__ import annotations
 
@@ -78,7 +78,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=240)
     ap.add_argument("--threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    ap.add_argument("--png_writer", default="fast", choices=["fast", "pil"])
+    ap.add_argument("--png_writer", default="fast", choices=["fast", "pil", "gpu"],
+                    help="the CLI's PNG writer; the host-only encode rate beside it uses pngio's writer for fast/gpu")
     ap.add_argument("--formats", default="jpg,png")
     ap.add_argument("--paths", default="frames_dir,input_dir")
     ap.add_argument("--gpus", type=int, default=1,
@@ -118,7 +119,7 @@ def main():
             p = os.path.join(d_enc, f"o_{i:04d}.{ext}")
             if ext == "jpg":
                 Image.fromarray(frames[i % len(frames)]).save(p, format="JPEG", quality=95)
-            elif args.png_writer == "fast":
+            elif args.png_writer in ("fast", "gpu"):
                 pngio.write_png(p, frames[i % len(frames)])
             else:
                 Image.fromarray(frames[i % len(frames)]).save(p)
