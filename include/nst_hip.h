@@ -536,7 +536,7 @@ int nst_motion_alpha(const float* flow, int h, int w, float motion_norm, double 
  * block (dynamic Huffman codes built per frame from that frame's run-length tokens, or a stored block where that is
  * smaller), the zlib stream's Adler-32 and the chunks' CRC-32 computed on the device.  Lossless: decoders return
  * the frames' bytes exactly, as from Pillow's file.  out_stride >= nst_png_bound; workspace per
- * nst_png_workspace_bytes; w*c + 1 <= 65535. */
+ * nst_png_workspace_bytes; out and out_stride 16-byte aligned; w*c + 1 <= 65535. */
 int nst_png_bound(int h, int w, int c, size_t* out_stride);
 int nst_png_workspace_bytes(int n, int h, int w, int c, size_t* out);
 int nst_png_encode_u8(const uint8_t* frames, int n, int h, int w, int c, uint8_t* out, size_t out_stride,
