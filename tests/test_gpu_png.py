@@ -87,6 +87,8 @@ def test_png_bound_and_workspace_validate_without_gpu():
     ("synthetic", 1, 20, 36, 4),
     ("flat", 1, 1, 1, 3),
     ("noise", 1, 130, 7, 1),          # the header alone outweighs every scanline
+    ("noise", 1, 2, 65534, 1),        # the widest scanline: a 65,535-byte stored block (LEN = 0xffff)
+    ("synthetic", 1, 2160, 3840, 3),  # 4K (configs[3])
 ])
 def test_gpu_png_decodes_to_the_frames(kind, n, h, w, c):
     fr = _frames(kind, n, h, w, c, seed=h * w + c)
@@ -133,3 +135,20 @@ def test_gpu_png_styled_output_through_the_engine():
     host = out.cpu().numpy()
     for j, data in enumerate(files):
         assert np.array_equal(np.asarray(Image.open(io.BytesIO(data))), host[j])
+
+
+@pytest.mark.gpu
+def test_gpu_png_rejects_small_workspace_and_stride():
+    x = torch.zeros((1, 8, 8, 3), dtype=torch.uint8, device="cuda")
+    L = _lib.lib()
+    bound, wsb = ctypes.c_size_t(), ctypes.c_size_t()
+    assert L.nst_png_bound(8, 8, 3, ctypes.byref(bound)) == 0
+    assert L.nst_png_workspace_bytes(1, 8, 8, 3, ctypes.byref(wsb)) == 0
+    out = torch.empty(bound.value, dtype=torch.uint8, device="cuda")
+    sizes = torch.empty(1, dtype=torch.int64, device="cuda")
+    ws = torch.empty(wsb.value, dtype=torch.uint8, device="cuda")
+    args = (x.data_ptr(), 1, 8, 8, 3, out.data_ptr())
+    assert L.nst_png_encode_u8(*args, bound.value, sizes.data_ptr(), ws.data_ptr(), wsb.value - 1, None) == -5
+    assert L.nst_png_encode_u8(*args, bound.value - 16, sizes.data_ptr(), ws.data_ptr(), wsb.value, None) == -1
+    assert L.nst_png_encode_u8(*args, bound.value, sizes.data_ptr(), ws.data_ptr(), wsb.value, None) == 0
+    torch.cuda.synchronize()
