@@ -917,16 +917,15 @@ hipError_t launch_seg_gauss_u8(const uint8_t* m, int n, int h, int w, float sigm
 // ---------------------------------------------------------------------------------------
 // Mask composite (pipeline.py:2040-2043) + uniform blend with the original (pipeline.py:2087-2092)
 // + ToPILImage truncation.  S = styled/255, O = original/255 (to_tensor).
-__global__ __launch_bounds__(256) void blend_kernel(const uint8_t* __restrict__ s, const uint8_t* __restrict__ o,
-                                                    const float* __restrict__ mask,
-                                                    const uint8_t* __restrict__ mask8, int mode, float b, float omb,
-                                                    uint8_t* out, size_t npix) {
-  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npix) return;
-#pragma unroll
-  for (int ch = 0; ch < 3; ++ch) {
-    const float S = (float)s[p * 3 + ch] / 255.0f;
-    const float O = (float)o[p * 3 + ch] / 255.0f;
+struct BlendOp {
+  const float* mask;
+  const uint8_t* mask8;
+  int mode;
+  float b, omb;
+  // one channel value of pixel p: styled byte sv, original byte ov -> output byte
+  __device__ __forceinline__ uint32_t operator()(uint32_t sv, uint32_t ov, size_t p) const {
+    const float S = (float)sv / 255.0f;
+    const float O = (float)ov / 255.0f;
     float C = S;
     if (mask || mask8) {  // alpha = the fp32 mask, or an 8-bit mask read as m / 255 (pipeline.py:353)
       const float al = mask ? mask[p] : (float)mask8[p] / 255.0f;
@@ -940,15 +939,52 @@ __global__ __launch_bounds__(256) void blend_kernel(const uint8_t* __restrict__ 
       const float t1 = omb * O;
       v = fminf(fmaxf(t0 + t1, 0.f), 1.f);
     }
-    out[p * 3 + ch] = (uint8_t)(v * 255.0f);
+    return (uint32_t)(uint8_t)(v * 255.0f);
   }
+};
+
+__global__ __launch_bounds__(256) void blend1_kernel(const uint8_t* __restrict__ s, const uint8_t* __restrict__ o,
+                                                     BlendOp op, uint8_t* out, size_t npix) {
+  const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) out[p * 3 + ch] = (uint8_t)op(s[p * 3 + ch], o[p * 3 + ch], p);
+}
+
+// 4 pixels (12 bytes: three aligned dwords of each frame buffer) per thread; the last ragged pixels one at a time
+// (the same per-channel arithmetic either way)
+__global__ __launch_bounds__(256) void blend_kernel(const uint8_t* __restrict__ s, const uint8_t* __restrict__ o,
+                                                    BlendOp op, uint8_t* out, size_t npix) {
+  const size_t p0 = 4 * ((size_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (p0 >= npix) return;
+  if (p0 + 4 <= npix) {
+    const uint32_t* s4 = (const uint32_t*)(s + p0 * 3);
+    const uint32_t* o4 = (const uint32_t*)(o + p0 * 3);
+    const uint32_t sw[3] = {s4[0], s4[1], s4[2]}, ow[3] = {o4[0], o4[1], o4[2]};
+    uint32_t r[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const uint32_t v = op((sw[i >> 2] >> (8 * (i & 3))) & 0xffu, (ow[i >> 2] >> (8 * (i & 3))) & 0xffu, p0 + i / 3);
+      r[i >> 2] |= v << (8 * (i & 3));
+    }
+    uint32_t* d4 = (uint32_t*)(out + p0 * 3);
+    d4[0] = r[0]; d4[1] = r[1]; d4[2] = r[2];
+    return;
+  }
+  for (size_t p = p0; p < npix; ++p)
+    for (int ch = 0; ch < 3; ++ch) out[p * 3 + ch] = (uint8_t)op(s[p * 3 + ch], o[p * 3 + ch], p);
 }
 
 hipError_t launch_blend(const uint8_t* s, const uint8_t* o, const float* mask, int mode, float b, float omb,
                         uint8_t* out, int n, int hw, hipStream_t st, const uint8_t* mask8) {
   const size_t npix = (size_t)n * hw;
-  hipLaunchKernelGGL(blend_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, s, o, mask, mask8, mode, b,
-                     omb, out, npix);
+  const BlendOp op{mask, mask8, mode, b, omb};
+  if (((uintptr_t)s | (uintptr_t)o | (uintptr_t)out) & 3) {  // unaligned buffers: one pixel per thread
+    hipLaunchKernelGGL(blend1_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, s, o, op, out, npix);
+    return hipGetLastError();
+  }
+  const size_t threads = (npix + 3) / 4;
+  hipLaunchKernelGGL(blend_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, s, o, op, out, npix);
   return hipGetLastError();
 }
 
