@@ -461,6 +461,14 @@ def main():
     def chain_step():
         return blend_frames(chain_ema(eng.stylize_u8(frames, PRESET)), frames, 0.9)
     chain_s = time_steps(chain_step, max(3, min(args.steps, 10))) if world == 1 else None
+    # the save leg on the GPU (--png_writer gpu, csrc/png_enc.hip): the chain's output as 8 complete PNG files
+    png_s, png_ratio = None, None
+    if world == 1:
+        from neuralstyletransferv1_amd.pngio import encode_png_gpu
+        chain_out = chain_step()
+        png_s = time_steps(lambda: encode_png_gpu(chain_out), max(3, min(args.steps, 10)))
+        _, png_sizes = encode_png_gpu(chain_out)
+        png_ratio = float(png_sizes.double().mean().item()) / (H * (W * 3 + 1))
 
     # the other precision modes, same step: fp16 (NST_DT_F16: the bench kernels with fp16 operands) and
     # split-fp16 (NST_DT_F32S: fp32 activations, fp16 hi/lo operand pairs -- the fp32 parity bars)
@@ -628,6 +636,12 @@ def main():
             "what": "forward (bf16) + LAB lightness EMA (alpha 0.65, frames in order) + blend 0.9 with the original "
                     "(run_videos.py defaults), one GPU, frames in HBM",
         }
+    if png_s is not None:
+        result["gpu_png_encode"] = {
+            "frames_per_s": round(nloc / png_s, 1), "ms_per_step": round(png_s * 1e3, 4),
+            "size_over_raw": round(png_ratio, 4),
+            "what": "the chain's output frames as complete PNG files on the GPU (Up filter, per-scanline dynamic-Huffman "
+                    "deflate, Adler-32 / CRC-32; csrc/png_enc.hip, --png_writer gpu); lossless"}
     for key, (_, info) in alt_modes.items():
         result[key] = info
     if args.graph and not args.gather:  # the replayed graph's output is the eager forward's, bit for bit

@@ -13,7 +13,7 @@ for k in ("fp32_parity_frames_per_s", "ssim_vs_cpu", "max_abs_lsb_vs_cpu", "with
         print(k, d[k])
 if d.get("cpu_baseline"):
     print("cpu", json.dumps(d["cpu_baseline"]))
-for k in ("fp16_mode", "fp16m_mode", "fp32s_mode", "gpu_full_chain"):
+for k in ("fp16_mode", "fp16m_mode", "fp32s_mode", "gpu_full_chain", "gpu_png_encode"):
     if d.get(k):
         print(k, json.dumps(d[k]))
 if "measured_peak" in d["roofline"]:
