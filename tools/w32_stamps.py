@@ -1,4 +1,4 @@
-"""Cycle breakdown of the 32x32x16 trunk kernel from its s_memtime intervals (diagnostic library: `make stamp`,
+"""Cycle breakdown of the trunk kernel (conv_wst16.hip, or conv_wst32.hip) from its s_memtime intervals (diagnostic library: `make stamp`,
 then NST_HIP_LIB=.../libnst_hip_stamp.so python tools/w32_stamps.py).  The last trunk launch of the step
 (res5.conv2, a plain conv) leaves the sums per wave.  Scratch measurement."""
 import ctypes
@@ -25,7 +25,9 @@ torch.cuda.synchronize()
 PT = 16
 n = 256 * 4 * PT
 buf = (ctypes.c_longlong * n)()
-got = _lib.lib().nst_debug_w32_stamps(buf, n)
+L = _lib.lib()
+fn = getattr(L, "nst_debug_w16_stamps", None) or getattr(L, "nst_debug_w32_stamps")
+got = fn(buf, n)
 a = np.frombuffer(buf, dtype=np.int64).reshape(256 * 4, PT).astype(np.float64)
 tiles = a[:, 6]
 ok = tiles > 0
