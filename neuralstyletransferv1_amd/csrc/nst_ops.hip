@@ -93,47 +93,49 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restr
   out[(size_t)n * cstride + c] = make_float2((float)scale, (float)((double)beta[c] - mean * scale));
 }
 
-// One-launch form for layers with few tiles per frame (the 270x480 trunk: ~1k): grid (n, cstride/16), block
-// 1024 = 16 channels x 64 tile phases, each thread sums tiles phase, phase + 64, ... in fp64 (<= 32 loads,
-// all in flight), a wave's 4 phases by xor shuffles, the 16 waves through LDS in wave order, then the finalize.
+// One-launch form for layers with few tiles per frame (the 270x480 trunk: ~1k): grid (n, cstride/CH), block
+// 1024 = CH channels x 1024/CH tile phases, each thread sums tiles phase, phase + 1024/CH, ... in fp64 (all its loads
+// in flight), a wave's phases by xor shuffles, the 16 waves through LDS in wave order, then the finalize.
 // Deterministic; half the launches of the two-stage form, whose second launch is pure latency at this size.
-constexpr int IN_ONE_PH = 64, IN_ONE_CH = 16, IN_ONE_MAX_TILES = 2048;
+constexpr int IN_ONE_MAX_TILES = 2048;
+template <int CH>
 __global__ __launch_bounds__(1024) void in_stats_kernel(const float* __restrict__ partial, int tiles, int cstride,
                                                         double count, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps, int frn,
                                                         float2* __restrict__ out) {
-  __shared__ double red[IN_ONE_PH / 4][IN_ONE_CH][2];
+  constexpr int PH = 1024 / CH, NL = IN_ONE_MAX_TILES / PH;
+  __shared__ double red[16][CH][2];
   const int n = blockIdx.x;
-  const int cl = threadIdx.x & (IN_ONE_CH - 1), q = threadIdx.x / IN_ONE_CH;
-  const int c = min(blockIdx.y * IN_ONE_CH + cl, cstride - 1);
+  const int cl = threadIdx.x & (CH - 1), q = threadIdx.x / CH;
+  const int c = min(blockIdx.y * CH + cl, cstride - 1);
   const float2* p = (const float2*)partial + (size_t)n * tiles * cstride + c;
   // every load in flight at once: indices clamped into range (always a valid address), the extra ones zeroed after
-  float2 v[IN_ONE_MAX_TILES / IN_ONE_PH];
+  float2 v[NL];
 #pragma unroll
-  for (int k = 0; k < IN_ONE_MAX_TILES / IN_ONE_PH; ++k) v[k] = p[(size_t)min(q + k * IN_ONE_PH, tiles - 1) * cstride];
+  for (int k = 0; k < NL; ++k) v[k] = p[(size_t)min(q + k * PH, tiles - 1) * cstride];
   double s1 = 0.0, s2 = 0.0;
 #pragma unroll
-  for (int k = 0; k < IN_ONE_MAX_TILES / IN_ONE_PH; ++k) {
-    const bool in = q + k * IN_ONE_PH < tiles;
+  for (int k = 0; k < NL; ++k) {
+    const bool in = q + k * PH < tiles;
     s1 += in ? (double)v[k].x : 0.0;
     s2 += in ? (double)v[k].y : 0.0;
   }
-  // the wave's 4 tile phases (lanes cl, cl + 16, cl + 32, cl + 48), then the 16 waves in LDS, fixed order
+  // the wave's 64 / CH tile phases (lanes cl, cl + CH, ...), then the 16 waves in LDS, fixed order
 #pragma unroll
-  for (int o = 16; o <= 32; o <<= 1) {
+  for (int o = CH; o < 64; o <<= 1) {
     s1 += __shfl_xor(s1, o);
     s2 += __shfl_xor(s2, o);
   }
   const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) < IN_ONE_CH) {
+  if ((threadIdx.x & 63) < CH) {
     red[wv][cl][0] = s1;
     red[wv][cl][1] = s2;
   }
   __syncthreads();
-  if (threadIdx.x >= IN_ONE_CH || blockIdx.y * IN_ONE_CH + cl >= cstride) return;
+  if (threadIdx.x >= CH || blockIdx.y * CH + cl >= cstride) return;
   s1 = red[0][cl][0];
   s2 = red[0][cl][1];
-  for (int w = 1; w < IN_ONE_PH / 4; ++w) {
+  for (int w = 1; w < 16; ++w) {
     s1 += red[w][cl][0];
     s2 += red[w][cl][1];
   }
@@ -143,6 +145,17 @@ __global__ __launch_bounds__(1024) void in_stats_kernel(const float* __restrict_
   const double rstd = 1.0 / sqrt(var + (double)eps);
   const double scale = (double)gamma[c] * rstd;
   out[(size_t)n * cstride + c] = make_float2((float)scale, (float)((double)beta[c] - mean * scale));
+}
+
+// channels per block of the one-launch form: 4 (r06: 9.2 -> 5.9 µs per trunk layer against 16, four times the
+// blocks in flight; `profiles/r06_in_one_ab.txt`); NST_IN_ONE_CH = 2, 8 or 16 for A/B runs
+static int in_one_ch() {
+  static const int v = [] {
+    const char* e = std::getenv("NST_IN_ONE_CH");
+    const int x = e ? std::atoi(e) : 4;
+    return (x == 2 || x == 8 || x == 16) ? x : 4;
+  }();
+  return v;
 }
 
 int in_finalize_segments(int tiles) { return max(1, min(IN_MAX_SEGMENTS, tiles / 64)); }
@@ -166,8 +179,16 @@ hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstrid
                               const float* gamma, const float* beta, float eps, int frn, float2* out,
                               void* seg_ws, hipStream_t st) {
   if (tiles <= IN_ONE_MAX_TILES) {
-    hipLaunchKernelGGL(in_stats_kernel, dim3(n, (cstride + IN_ONE_CH - 1) / IN_ONE_CH), dim3(1024), 0, st, partial,
-                       tiles, cstride, count, gamma, beta, eps, frn, out);
+    const int ch = in_one_ch();
+    const dim3 grid(n, (cstride + ch - 1) / ch);
+    if (ch == 2)
+      hipLaunchKernelGGL(in_stats_kernel<2>, grid, dim3(1024), 0, st, partial, tiles, cstride, count, gamma, beta, eps, frn, out);
+    else if (ch == 4)
+      hipLaunchKernelGGL(in_stats_kernel<4>, grid, dim3(1024), 0, st, partial, tiles, cstride, count, gamma, beta, eps, frn, out);
+    else if (ch == 8)
+      hipLaunchKernelGGL(in_stats_kernel<8>, grid, dim3(1024), 0, st, partial, tiles, cstride, count, gamma, beta, eps, frn, out);
+    else
+      hipLaunchKernelGGL(in_stats_kernel<16>, grid, dim3(1024), 0, st, partial, tiles, cstride, count, gamma, beta, eps, frn, out);
     return hipGetLastError();
   }
   const int nseg = in_finalize_segments(tiles);
