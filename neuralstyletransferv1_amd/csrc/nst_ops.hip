@@ -23,65 +23,88 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // in fp64 and emits the affine {scale, shift} the consumer's prologue applies:
 //   y = x*scale + shift, scale = gamma/sqrt(var+eps), shift = beta - mean*scale.
 // Two deterministic stages (fixed summation order, no atomics):
-//   stage 1  grid (n, cstride/64, nseg), block 256 = 64 channels x 4 tile phases: each block
+//   stage 1  grid (n, cstride/CH, nseg), block 256 = CH channels x 256/CH tile phases: each block
 //            sums a contiguous segment of tiles in fp64 -> seg[n][s][c] (double2)
-//   stage 2  grid (n, cstride/64), 64 threads: sums the nseg segments, emits {scale, shift}.
+//   stage 2  grid (n, cstride/CH), block 256: sums the nseg segments, emits {scale, shift}.
+//   (r06: blocks of CH channels x 256/CH phases -- stage 1 CH = 16, stage 2 CH = 4 -- instead of 64 x 4: the 32- and
+//   64-channel full-resolution layers kept half of their lanes idle and ran few blocks; the phases of a wave are
+//   combined by xor shuffles, the four waves through LDS in wave order: deterministic)
+template <int CH>
 __global__ __launch_bounds__(256) void in_partial_reduce_kernel(const float* __restrict__ partial, int tiles,
                                                                 int cstride, int per_seg,
                                                                 double2* __restrict__ seg) {
-  __shared__ double red[4][64][2];
+  constexpr int PH = 256 / CH;
+  __shared__ double red[4][CH][2];
   const int n = blockIdx.x, s = blockIdx.z;
-  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.y * 64 + cl;
+  const int cl = threadIdx.x & (CH - 1), q = threadIdx.x / CH;
+  const int c = blockIdx.y * CH + cl;
   const int t0 = s * per_seg, t1 = min(tiles, t0 + per_seg);
   double s1 = 0.0, s2 = 0.0;
   if (c < cstride) {
     const float2* p = (const float2*)partial + (size_t)n * tiles * cstride + c;
     int t = t0 + q;
-    for (; t + 12 < t1; t += 16) {
-      const float2 a = p[(size_t)t * cstride], b = p[(size_t)(t + 4) * cstride];
-      const float2 d = p[(size_t)(t + 8) * cstride], e = p[(size_t)(t + 12) * cstride];
+    for (; t + 3 * PH < t1; t += 4 * PH) {
+      const float2 a = p[(size_t)t * cstride], b = p[(size_t)(t + PH) * cstride];
+      const float2 d = p[(size_t)(t + 2 * PH) * cstride], e = p[(size_t)(t + 3 * PH) * cstride];
       s1 += (double)a.x + (double)b.x + (double)d.x + (double)e.x;
       s2 += (double)a.y + (double)b.y + (double)d.y + (double)e.y;
     }
-    for (; t < t1; t += 4) {
+    for (; t < t1; t += PH) {
       const float2 a = p[(size_t)t * cstride];
       s1 += a.x;
       s2 += a.y;
     }
   }
-  red[q][cl][0] = s1;
-  red[q][cl][1] = s2;
+#pragma unroll
+  for (int o = CH; o < 64; o <<= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < CH) {
+    red[wv][cl][0] = s1;
+    red[wv][cl][1] = s2;
+  }
   __syncthreads();
-  if (q == 0 && c < cstride) {
+  if (threadIdx.x < CH && c < cstride) {
     s1 = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
     s2 = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
     seg[((size_t)n * gridDim.z + s) * cstride + c] = make_double2(s1, s2);
   }
 }
 
+template <int CH>
 __global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restrict__ seg, int nseg, int cstride,
                                                           double count, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps, int frn,
                                                           float2* __restrict__ out) {
-  // 64 channels x 4 segment phases per block (the segments' loads in flight together), then a
-  // fixed-order LDS combine: deterministic
-  __shared__ double red[4][64][2];
+  // CH channels x 256/CH segment phases per block (the segments' loads in flight together), the wave's phases by
+  // xor shuffles, then a fixed-order LDS combine: deterministic
+  constexpr int PH = 256 / CH;
+  __shared__ double red[4][CH][2];
   const int n = blockIdx.x;
-  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.y * 64 + cl;
+  const int cl = threadIdx.x & (CH - 1), q = threadIdx.x / CH;
+  const int c = blockIdx.y * CH + cl;
   double s1 = 0.0, s2 = 0.0;
   if (c < cstride) {
-    for (int s = q; s < nseg; s += 4) {
+    for (int s = q; s < nseg; s += PH) {
       const double2 v = seg[((size_t)n * nseg + s) * cstride + c];
       s1 += v.x;
       s2 += v.y;
     }
   }
-  red[q][cl][0] = s1;
-  red[q][cl][1] = s2;
+#pragma unroll
+  for (int o = CH; o < 64; o <<= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < CH) {
+    red[wv][cl][0] = s1;
+    red[wv][cl][1] = s2;
+  }
   __syncthreads();
-  if (q != 0 || c >= cstride) return;
+  if (threadIdx.x >= CH || c >= cstride) return;
   s1 = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
   s2 = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
   // FRN (frn.py:71-74): nu2 = mean(x^2), x * rsqrt(nu2 + |eps|), then weight * x + bias
@@ -92,6 +115,7 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(const double2* __restr
   const double scale = (double)gamma[c] * rstd;
   out[(size_t)n * cstride + c] = make_float2((float)scale, (float)((double)beta[c] - mean * scale));
 }
+constexpr int IN_RED_CH = 16, IN_FIN_CH = 4;
 
 // One-launch form for layers with few tiles per frame (the 270x480 trunk: ~1k): grid (n, cstride/CH), block
 // 1024 = CH channels x 1024/CH tile phases, each thread sums tiles phase, phase + 1024/CH, ... in fp64 (all its loads
@@ -193,12 +217,12 @@ hipError_t launch_in_finalize(const float* partial, int n, int tiles, int cstrid
   }
   const int nseg = in_finalize_segments(tiles);
   const int per_seg = (tiles + nseg - 1) / nseg;
-  hipLaunchKernelGGL(in_partial_reduce_kernel, dim3(n, (cstride + 63) / 64, nseg), dim3(256), 0, st, partial,
-                     tiles, cstride, per_seg, (double2*)seg_ws);
+  hipLaunchKernelGGL(in_partial_reduce_kernel<IN_RED_CH>, dim3(n, (cstride + IN_RED_CH - 1) / IN_RED_CH, nseg),
+                     dim3(256), 0, st, partial, tiles, cstride, per_seg, (double2*)seg_ws);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(in_finalize_kernel, dim3(n, (cstride + 63) / 64), dim3(256), 0, st, (const double2*)seg_ws,
-                     nseg, cstride, count, gamma, beta, eps, frn, out);
+  hipLaunchKernelGGL(in_finalize_kernel<IN_FIN_CH>, dim3(n, (cstride + IN_FIN_CH - 1) / IN_FIN_CH), dim3(256), 0, st,
+                     (const double2*)seg_ws, nseg, cstride, count, gamma, beta, eps, frn, out);
   return hipGetLastError();
 }
 
