@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of the two-stage IN reduce's channels per block (NST_IN_RED_CH): kernel times from kernel traces of a short bench
+# (profiles/r06_in_red_ab.txt; the NST_IN_RED_CH selector in nst_ops.hip launch_in_finalize was removed after it: re-add to rerun)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 mkdir -p gpurun_out
